@@ -1,0 +1,207 @@
+// device_common.hpp -- gfx950 device helpers shared by the GPAR kernels.
+//
+// Stationary kernels (Stheno Matern12/32/52, EQ) and the closed-form
+// Matern-nu state-space discretisation (TemporalGPs `to_sde`).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace gpar {
+
+enum KernelKind : int { KM12 = 0, KM32 = 1, KM52 = 2, KEQ = 3 };
+
+constexpr double kSqrt3 = 1.7320508075688772935;
+constexpr double kSqrt5 = 2.2360679774997896964;
+constexpr double kLog2Pi = 1.8378770664093454836;
+
+// Per-step gains record: A (d x d, row-major) | K (d) | rs = 1/sqrt(S) ; padded.
+template <int D> struct Rec { static constexpr int size = D == 3 ? 16 : (D == 2 ? 8 : 4); };
+// Per-step fix-up vector g_k (d), padded to 4 doubles.
+constexpr int kGStride = 4;
+// Carry / end-state vectors (d), padded to 4 doubles.
+constexpr int kSStride = 4;
+
+template <int KIND> struct Sde;
+template <> struct Sde<KM12> { static constexpr int d = 1; };
+template <> struct Sde<KM32> { static constexpr int d = 2; };
+template <> struct Sde<KM52> { static constexpr int d = 3; };
+
+// Unit-variance, unit-length kernel of the distance r >= 0.
+template <int KIND>
+__device__ __forceinline__ double kappa(double r) {
+  if constexpr (KIND == KM12) {
+    return exp(-r);
+  } else if constexpr (KIND == KM32) {
+    const double x = kSqrt3 * r;
+    return (1.0 + x) * exp(-x);
+  } else if constexpr (KIND == KM52) {
+    const double x = kSqrt5 * r;
+    return (1.0 + x + x * x * (1.0 / 3.0)) * exp(-x);
+  } else {
+    return exp(-0.5 * r * r);
+  }
+}
+
+// Kernel from a squared distance (EQ needs no sqrt).
+template <int KIND>
+__device__ __forceinline__ double kappa_sq(double d2, double inv_l) {
+  if constexpr (KIND == KEQ) {
+    return exp(-0.5 * d2 * inv_l * inv_l);
+  } else {
+    return kappa<KIND>(sqrt(d2) * inv_l);
+  }
+}
+
+__device__ __forceinline__ double kappa_rt(int kind, double r) {
+  switch (kind) {
+    case KM12: return kappa<KM12>(r);
+    case KM32: return kappa<KM32>(r);
+    case KM52: return kappa<KM52>(r);
+    default: return kappa<KEQ>(r);
+  }
+}
+
+// Stationary covariance of the unit SDE (times s gives the scaled prior: H = e1 convention).
+template <int D>
+__device__ __forceinline__ void sde_pinf(double s, double (&P)[D][D]) {
+  if constexpr (D == 1) {
+    P[0][0] = s;
+  } else if constexpr (D == 2) {
+    P[0][0] = s; P[0][1] = 0.0; P[1][0] = 0.0; P[1][1] = 3.0 * s;
+  } else {
+    P[0][0] = s;             P[0][1] = 0.0;               P[0][2] = -(5.0 / 3.0) * s;
+    P[1][0] = 0.0;           P[1][1] = (5.0 / 3.0) * s;   P[1][2] = 0.0;
+    P[2][0] = -(5.0 / 3.0) * s; P[2][1] = 0.0;            P[2][2] = 25.0 * s;
+  }
+}
+
+// A = exp(F tau): F + lambda I is nilpotent, so exp(F tau) = e^{-lambda tau} (I + tau N + tau^2/2 N^2).
+template <int D>
+__device__ __forceinline__ void sde_transition(double tau, double (&A)[D][D]) {
+  if constexpr (D == 1) {
+    A[0][0] = exp(-tau);
+  } else if constexpr (D == 2) {
+    const double lam = kSqrt3;
+    const double e = exp(-lam * tau);
+    A[0][0] = e * (1.0 + lam * tau);  A[0][1] = e * tau;
+    A[1][0] = -e * (3.0 * tau);       A[1][1] = e * (1.0 - lam * tau);
+  } else {
+    const double lam = kSqrt5, l2 = 5.0, l3 = 5.0 * kSqrt5, l4 = 25.0;
+    const double e = exp(-lam * tau);
+    const double t2 = tau * tau;
+    A[0][0] = e * (1.0 + lam * tau + 0.5 * l2 * t2);
+    A[0][1] = e * (tau + lam * t2);
+    A[0][2] = e * (0.5 * t2);
+    A[1][0] = e * (-0.5 * l3 * t2);
+    A[1][1] = e * (1.0 + lam * tau - l2 * t2);
+    A[1][2] = e * (tau - 0.5 * lam * t2);
+    A[2][0] = e * (-l3 * tau + 0.5 * l4 * t2);
+    A[2][1] = e * (-3.0 * l2 * tau + l3 * t2);
+    A[2][2] = e * (1.0 - 2.0 * lam * tau + 0.5 * l2 * t2);
+  }
+}
+
+// ---- small dense helpers (fully unrolled, registers only)
+template <int D>
+__device__ __forceinline__ void mat_mul(const double (&X)[D][D], const double (&Y)[D][D],
+                                        double (&Z)[D][D]) {
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) acc = fma(X[i][k], Y[k][j], acc);
+      Z[i][j] = acc;
+    }
+}
+
+// Z = X * Y^T
+template <int D>
+__device__ __forceinline__ void mat_mul_bt(const double (&X)[D][D], const double (&Y)[D][D],
+                                           double (&Z)[D][D]) {
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) acc = fma(X[i][k], Y[j][k], acc);
+      Z[i][j] = acc;
+    }
+}
+
+// Z = X^T * Y
+template <int D>
+__device__ __forceinline__ void mat_mul_at(const double (&X)[D][D], const double (&Y)[D][D],
+                                           double (&Z)[D][D]) {
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      double acc = 0.0;
+#pragma unroll
+      for (int k = 0; k < D; ++k) acc = fma(X[k][i], Y[k][j], acc);
+      Z[i][j] = acc;
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void mat_copy(const double (&X)[D][D], double (&Z)[D][D]) {
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) Z[i][j] = X[i][j];
+}
+
+template <int D>
+__device__ __forceinline__ void mat_eye(double (&Z)[D][D]) {
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) Z[i][j] = (i == j) ? 1.0 : 0.0;
+}
+
+template <int D>
+__device__ __forceinline__ void mat_zero(double (&Z)[D][D]) {
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) Z[i][j] = 0.0;
+}
+
+// Inverse of a small general matrix (adjugate / determinant).
+template <int D>
+__device__ __forceinline__ void mat_inv(const double (&X)[D][D], double (&Z)[D][D]) {
+  if constexpr (D == 1) {
+    Z[0][0] = 1.0 / X[0][0];
+  } else if constexpr (D == 2) {
+    const double det = X[0][0] * X[1][1] - X[0][1] * X[1][0];
+    const double id = 1.0 / det;
+    Z[0][0] = X[1][1] * id;  Z[0][1] = -X[0][1] * id;
+    Z[1][0] = -X[1][0] * id; Z[1][1] = X[0][0] * id;
+  } else {
+    const double c00 = X[1][1] * X[2][2] - X[1][2] * X[2][1];
+    const double c01 = X[1][2] * X[2][0] - X[1][0] * X[2][2];
+    const double c02 = X[1][0] * X[2][1] - X[1][1] * X[2][0];
+    const double det = X[0][0] * c00 + X[0][1] * c01 + X[0][2] * c02;
+    const double id = 1.0 / det;
+    Z[0][0] = c00 * id;
+    Z[1][0] = c01 * id;
+    Z[2][0] = c02 * id;
+    Z[0][1] = (X[0][2] * X[2][1] - X[0][1] * X[2][2]) * id;
+    Z[1][1] = (X[0][0] * X[2][2] - X[0][2] * X[2][0]) * id;
+    Z[2][1] = (X[0][1] * X[2][0] - X[0][0] * X[2][1]) * id;
+    Z[0][2] = (X[0][1] * X[1][2] - X[0][2] * X[1][1]) * id;
+    Z[1][2] = (X[0][2] * X[1][0] - X[0][0] * X[1][2]) * id;
+    Z[2][2] = (X[0][0] * X[1][1] - X[0][1] * X[1][0]) * id;
+  }
+}
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+}  // namespace gpar

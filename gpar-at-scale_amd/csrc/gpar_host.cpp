@@ -1,0 +1,697 @@
+// gpar_host.cpp -- C-ABI (include/gpar_hip.h) of the MI355X GPAR hot path.
+//
+// Host orchestration only: argument checking, device workspace, kernel sequencing, the
+// batched Nelder-Mead driver.  Every number is computed by the gfx950 kernels in
+// k_lgssm.hip / k_gram.hip / k_dense.hip / k_predict.hip; there is no CPU fallback.
+#include "gpar_hip.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <unordered_map>
+#include <vector>
+
+#include "launch.hpp"
+#include "nelder_mead.hpp"
+
+struct gpar_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  struct Buf {
+    void* p = nullptr;
+    size_t bytes = 0;
+  };
+  std::unordered_map<std::string, Buf> bufs;
+};
+
+namespace gpar {
+
+struct Error : std::runtime_error {
+  int code;
+  Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
+};
+
+#define HIPCHECK(x)                                                                    \
+  do {                                                                                 \
+    hipError_t e_ = (x);                                                               \
+    if (e_ != hipSuccess)                                                              \
+      throw ::gpar::Error(e_ == hipErrorOutOfMemory ? GPAR_ERR_OOM : GPAR_ERR_HIP,     \
+                          std::string(#x) + ": " + hipGetErrorString(e_));             \
+  } while (0)
+
+#define ARGCHECK(c, msg)                                     \
+  do {                                                       \
+    if (!(c)) throw ::gpar::Error(GPAR_ERR_ARG, (msg));      \
+  } while (0)
+
+static void check_launch(const char* what) {
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) throw Error(GPAR_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <class T>
+static T* ws(gpar_ctx* c, const std::string& name, size_t count) {
+  size_t bytes = count * sizeof(T);
+  if (bytes == 0) bytes = 16;
+  auto& b = c->bufs[name];
+  if (b.bytes < bytes) {
+    if (b.p) HIPCHECK(hipFree(b.p));
+    b.p = nullptr;
+    b.bytes = 0;
+    HIPCHECK(hipMalloc(&b.p, bytes));
+    b.bytes = bytes;
+  }
+  return reinterpret_cast<T*>(b.p);
+}
+
+template <class T>
+static void h2d(gpar_ctx* c, T* dst, const T* src, size_t count) {
+  if (count) HIPCHECK(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, c->stream));
+}
+template <class T>
+static void d2h(gpar_ctx* c, T* dst, const T* src, size_t count) {
+  if (count) HIPCHECK(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyDeviceToHost, c->stream));
+}
+static void sync(gpar_ctx* c) { HIPCHECK(hipStreamSynchronize(c->stream)); }
+
+constexpr int kChunk = 256;   // time-chunk length of the Kalman sweeps (multiple of 16)
+
+static int sde_dim(int kind) {
+  if (kind == GPAR_MATERN12) return 1;
+  if (kind == GPAR_MATERN32) return 2;
+  if (kind == GPAR_MATERN52) return 3;
+  throw Error(GPAR_ERR_UNSUPPORTED, "time kernel has no finite state-space form (EQ)");
+}
+
+static int64_t round_up(int64_t x, int64_t q) { return ((x + q - 1) / q) * q; }
+
+// --------------------------------------------------------------------------- problems on device
+struct DevProblem {
+  int64_t n, m, d, mp, mc, nch;
+  const double *t, *v, *z, *y;
+  const double* t_user;  // caller's pointer (grouping key)
+  int64_t ldv, ldz;
+  int ok, tk, sdim, kuu_noise;
+};
+
+static void check_sorted_host(const double* t, int64_t n) {
+  for (int64_t k = 1; k < n; ++k)
+    ARGCHECK(t[k] >= t[k - 1], "time locations must be ascending (dtc.jl:102 does not sort)");
+}
+
+static DevProblem prepare_problem(gpar_ctx* c, const gpar_problem& p, int idx) {
+  ARGCHECK(p.n >= 1 && p.m >= 1, "n and m must be >= 1");
+  ARGCHECK(p.d >= 1, "d must be >= 1 (use the LGSSM entry points for time-only outputs)");
+  ARGCHECK(p.ldv >= p.d && p.ldz >= p.d, "ldv/ldz must be >= d");
+  ARGCHECK(p.t && p.v && p.z && p.y, "null input pointer");
+  ARGCHECK(p.out_kernel >= 0 && p.out_kernel <= 3, "bad out_kernel");
+  ARGCHECK(p.mem == GPAR_MEM_HOST || p.mem == GPAR_MEM_DEVICE, "bad mem");
+  if (p.d > 64) throw Error(GPAR_ERR_UNSUPPORTED, "input dimension d > 64 not supported yet");
+  if (p.m > 2048) throw Error(GPAR_ERR_UNSUPPORTED, "m > 2048 not supported");
+  DevProblem d{};
+  d.n = p.n;
+  d.m = p.m;
+  d.d = p.d;
+  d.mp = round_up(p.m, kGramTile);
+  d.mc = d.mp + 1;
+  d.nch = (p.n + kChunk - 1) / kChunk;
+  d.ok = p.out_kernel;
+  d.tk = p.time_kernel;
+  d.sdim = sde_dim(p.time_kernel);
+  d.kuu_noise = p.kuu_noise;
+  d.t_user = p.t;
+  if (p.mem == GPAR_MEM_DEVICE) {
+    d.t = p.t; d.v = p.v; d.z = p.z; d.y = p.y;
+    d.ldv = p.ldv; d.ldz = p.ldz;
+    return d;
+  }
+  check_sorted_host(p.t, p.n);
+  const std::string k = "prob" + std::to_string(idx);
+  double* t = ws<double>(c, k + "_t", p.n);
+  double* v = ws<double>(c, k + "_v", (size_t)p.n * p.d);
+  double* z = ws<double>(c, k + "_z", (size_t)p.m * p.d);
+  double* y = ws<double>(c, k + "_y", p.n);
+  h2d(c, t, p.t, p.n);
+  h2d(c, y, p.y, p.n);
+  HIPCHECK(hipMemcpy2DAsync(v, p.d * sizeof(double), p.v, p.ldv * sizeof(double),
+                            p.d * sizeof(double), p.n, hipMemcpyHostToDevice, c->stream));
+  HIPCHECK(hipMemcpy2DAsync(z, p.d * sizeof(double), p.z, p.ldz * sizeof(double),
+                            p.d * sizeof(double), p.m, hipMemcpyHostToDevice, c->stream));
+  d.t = t; d.v = v; d.z = z; d.y = y;
+  d.ldv = p.d; d.ldz = p.d;
+  return d;
+}
+
+struct Theta {
+  double l_t, sv_t, l_o, sv_o, sigma;
+};
+
+// --------------------------------------------------------------------------- gains
+struct GainsOut {
+  double *rec, *g, *phi, *logs, *pf;
+  int64_t recstride, gstride, phistride;
+};
+
+// Data-independent per-step filter quantities for `nchains` chains sharing t (n steps).
+static GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
+                          const std::vector<ChainParamsHost>& cps, const double* noise,
+                          bool want_pf, const std::string& tag) {
+  const int nchains = (int)cps.size();
+  const int64_t nch = (n + kChunk - 1) / kChunk;
+  const int rs = rec_size(sdim);
+  const int d2 = sdim * sdim;
+  ChainParamsHost* dcps = ws<ChainParamsHost>(c, tag + "_cps", nchains);
+  h2d(c, dcps, cps.data(), nchains);
+  double* agg = ws<double>(c, tag + "_agg", (size_t)nchains * nch * 3 * d2);
+  double* pst = ws<double>(c, tag + "_pstart", (size_t)nchains * nch * d2);
+  GainsOut o;
+  o.recstride = n * rs;
+  o.gstride = n * 4;
+  o.phistride = nch * d2;
+  o.rec = ws<double>(c, tag + "_rec", (size_t)nchains * n * rs);
+  o.g = ws<double>(c, tag + "_g", (size_t)nchains * n * 4);
+  o.phi = ws<double>(c, tag + "_phi", (size_t)nchains * nch * d2);
+  o.logs = ws<double>(c, tag + "_logs", (size_t)nchains * nch);
+  o.pf = want_pf ? ws<double>(c, tag + "_pf", (size_t)nchains * n * d2) : nullptr;
+  launch_gains(c->stream, sdim, t, n, kChunk, nch, nchains, dcps, noise, agg, pst, o.rec, o.g,
+               o.phi, o.logs, o.pf);
+  check_launch("gains");
+  return o;
+}
+
+// --------------------------------------------------------------------------- Gram stage
+struct GramOut {
+  double *G, *r, *a2part, *logs;  // per problem
+  int64_t ldg, npart;
+};
+
+// For every problem: G = beta^T beta, r = beta^T alpha, sum alpha^2 partials, sum log S
+// partials, at hyperparameters th.  `beta_keep` (single problem) keeps the corrected beta.
+static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
+                              const std::vector<Theta>& th, bool fix_beta = false) {
+  const int np = (int)P.size();
+  int64_t mpmax = 0, n = P[0].n;
+  for (auto& p : P) mpmax = std::max(mpmax, p.mp);
+  const int64_t nch = (n + kChunk - 1) / kChunk;
+  const int64_t npart = vec_fix_blocks(n);
+  GramOut o;
+  o.ldg = mpmax;
+  o.npart = npart;
+  o.G = ws<double>(c, "G", (size_t)np * mpmax * mpmax);
+  o.r = ws<double>(c, "r", (size_t)np * mpmax);
+  o.a2part = ws<double>(c, "a2part", (size_t)np * npart);
+  o.logs = ws<double>(c, "logs_all", (size_t)np * nch);
+
+  // group problems sharing (t, n, time kernel) into one batched gains launch
+  bool shared = true;
+  for (auto& p : P)
+    if (p.t_user != P[0].t_user || p.n != n || p.sdim != P[0].sdim) shared = false;
+  std::vector<GainsOut> gains(np);
+  if (shared) {
+    std::vector<ChainParamsHost> cps(np);
+    for (int i = 0; i < np; ++i)
+      cps[i] = {1.0 / th[i].l_t, th[i].l_t, th[i].sv_t * th[i].sv_t, th[i].sigma * th[i].sigma};
+    GainsOut g = run_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fit");
+    for (int i = 0; i < np; ++i) {
+      gains[i] = g;
+      gains[i].rec = g.rec + (size_t)i * g.recstride;
+      gains[i].g = g.g + (size_t)i * g.gstride;
+      gains[i].phi = g.phi + (size_t)i * g.phistride;
+      gains[i].logs = g.logs + (size_t)i * nch;
+    }
+    HIPCHECK(hipMemcpyAsync(o.logs, g.logs, (size_t)np * nch * sizeof(double),
+                            hipMemcpyDeviceToDevice, c->stream));
+  }
+
+  double* beta = ws<double>(c, "beta", (size_t)n * mpmax);
+  double* alpha = ws<double>(c, "alpha", (size_t)n);
+  double* send = ws<double>(c, "send", (size_t)nch * (mpmax + 1) * 4);
+  double* cin = ws<double>(c, "cin", (size_t)nch * (mpmax + 1) * 4);
+  for (int i = 0; i < np; ++i) {
+    const DevProblem& p = P[i];
+    ARGCHECK(p.n == n, "all problems of one call must share n");
+    GainsOut g;
+    if (shared) {
+      g = gains[i];
+    } else {
+      std::vector<ChainParamsHost> cps(1);
+      cps[0] = {1.0 / th[i].l_t, th[i].l_t, th[i].sv_t * th[i].sv_t, th[i].sigma * th[i].sigma};
+      g = run_gains(c, p.sdim, p.t, n, cps, nullptr, false, "fit1");
+      HIPCHECK(hipMemcpyAsync(o.logs + (size_t)i * nch, g.logs, nch * sizeof(double),
+                              hipMemcpyDeviceToDevice, c->stream));
+    }
+    const double s_o = th[i].sv_o * th[i].sv_o;
+    launch_whiten_kfu(c->stream, p.tk, p.ok, g.rec, p.v, p.ldv, (int)p.d, p.z, p.ldz, p.m, p.mp,
+                      n, kChunk, nch, 1.0 / th[i].l_o, s_o, beta, p.mp, send, p.mc);
+    check_launch("whiten_kfu");
+    launch_whiten_vec(c->stream, p.sdim, g.rec, 0, p.y, 0, n, kChunk, nch, 1, alpha, 0, send, 0,
+                      p.mc, p.mp);
+    check_launch("whiten_vec");
+    launch_carry(c->stream, p.sdim, g.phi, 0, send, cin, 0, nch, p.mc, p.mc, 1);
+    check_launch("carry");
+    launch_vec_fix(c->stream, p.sdim, alpha, 0, g.g, 0, cin, 0, p.mc, p.mp, n, kChunk, 1,
+                   o.a2part + (size_t)i * npart);
+    check_launch("vec_fix");
+    GramPlan plan = gram_plan(n, p.mp);
+    double* part = ws<double>(c, "gram_part", (size_t)plan.nsplit * plan.ntiles * kGramTile * kGramTile);
+    double* rpart = ws<double>(c, "gram_rpart", (size_t)plan.nsplit * plan.ntb * kGramTile);
+    launch_gram(c->stream, p.sdim, plan, beta, p.mp, n, g.g, cin, p.mc, kChunk, alpha, part,
+                rpart, o.G + (size_t)i * mpmax * mpmax, mpmax, o.r + (size_t)i * mpmax);
+    check_launch("gram");
+    if (fix_beta) {
+      launch_beta_fix(c->stream, p.sdim, beta, p.mp, n, g.g, cin, p.mc, kChunk);
+      check_launch("beta_fix");
+    }
+  }
+  return o;
+}
+
+// --------------------------------------------------------------------------- dense tail
+struct DenseOut {
+  double *Lu, *Llam, *W;
+  int* status;
+  int64_t ld;
+};
+
+// chol(Kuu [+ sigma^2 I]) and chol(L_u^-1 G L_u^-T + I) for every problem.
+static DenseOut run_dense(gpar_ctx* c, const std::vector<DevProblem>& P,
+                          const std::vector<Theta>& th, const GramOut& go, bool qu_mode) {
+  const int np = (int)P.size();
+  const int64_t ld = go.ldg;
+  DenseOut o;
+  o.ld = ld;
+  o.Lu = ws<double>(c, "Kuu", (size_t)np * ld * ld);
+  o.W = ws<double>(c, "Wmat", (size_t)np * ld * ld);
+  o.Llam = ws<double>(c, "Lam", (size_t)np * ld * ld);
+  o.status = ws<int>(c, "status", (size_t)np * 2);
+  HIPCHECK(hipMemsetAsync(o.status, 0, np * 2 * sizeof(int), c->stream));
+  int mmax = 0;
+  std::vector<KuuJobHost> kj(np);
+  std::vector<CholJobHost> cj(np), cl(np);
+  std::vector<TrsmJobHost> t1(np), t2(np);
+  for (int i = 0; i < np; ++i) {
+    const DevProblem& p = P[i];
+    mmax = std::max<int>(mmax, (int)p.m);
+    double* Kuu = o.Lu + (size_t)i * ld * ld;
+    double* W = o.W + (size_t)i * ld * ld;
+    double* Lam = o.Llam + (size_t)i * ld * ld;
+    const double s2 = th[i].sigma * th[i].sigma;
+    kj[i] = {p.z, p.ldz, (int)p.d, p.ok, 1.0 / th[i].l_o, th[i].sv_o * th[i].sv_o,
+             (!qu_mode && p.kuu_noise) ? s2 : 0.0, Kuu, ld, (int)p.m};
+    cj[i] = {Kuu, ld, (int)p.m, 0.0, o.status + 2 * i};
+    t1[i] = {Kuu, ld, go.G + (size_t)i * ld * ld, ld, W, ld, (int)p.m, p.m, 0, 0};
+    t2[i] = {Kuu, ld, W, ld, Lam, ld, (int)p.m, p.m, 1, 0};
+    cl[i] = {Lam, ld, (int)p.m, 1.0, o.status + 2 * i + 1};
+  }
+  auto* dkj = ws<KuuJobHost>(c, "kuujobs", np);
+  auto* dcj = ws<CholJobHost>(c, "choljobs", np);
+  auto* dcl = ws<CholJobHost>(c, "choljobs2", np);
+  auto* dt1 = ws<TrsmJobHost>(c, "trsmjobs1", np);
+  auto* dt2 = ws<TrsmJobHost>(c, "trsmjobs2", np);
+  h2d(c, dkj, kj.data(), np);
+  h2d(c, dcj, cj.data(), np);
+  h2d(c, dcl, cl.data(), np);
+  h2d(c, dt1, t1.data(), np);
+  h2d(c, dt2, t2.data(), np);
+  launch_kuu(c->stream, dkj, np, mmax);
+  check_launch("kuu");
+  launch_chol(c->stream, dcj, np);
+  check_launch("chol(Kuu)");
+  launch_trsm(c->stream, dt1, np, mmax);
+  check_launch("trsm1");
+  launch_trsm(c->stream, dt2, np, mmax);
+  check_launch("trsm2");
+  launch_chol(c->stream, dcl, np);
+  check_launch("chol(Lambda)");
+  return o;
+}
+
+static std::vector<Theta> thetas_from(const double* theta, int np) {
+  std::vector<Theta> th(np);
+  for (int i = 0; i < np; ++i) {
+    const double* q = theta + 5 * i;
+    th[i] = {q[0], q[1], q[2], q[3], q[4]};
+    for (int j = 0; j < 5; ++j)
+      ARGCHECK(std::isfinite(q[j]) && q[j] > 0.0, "theta entries must be positive and finite");
+  }
+  return th;
+}
+
+// DTC objective for all problems; status_out[i] = 1 if a Cholesky failed for problem i.
+static void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<Theta>& th,
+                     double* out, std::vector<int>& status_out) {
+  const int np = (int)P.size();
+  GramOut go = run_gram_stage(c, P, th);
+  DenseOut dn = run_dense(c, P, th, go, false);
+  const int64_t nch = P[0].nch;
+  std::vector<FinishJobHost> fj(np);
+  double* dout = ws<double>(c, "dtc_out", np);
+  for (int i = 0; i < np; ++i) {
+    fj[i] = {dn.Lu + (size_t)i * dn.ld * dn.ld, dn.Llam + (size_t)i * dn.ld * dn.ld, dn.ld,
+             (int)P[i].m, go.r + (size_t)i * go.ldg, go.logs + (size_t)i * nch, nch,
+             go.a2part + (size_t)i * go.npart, go.npart, P[i].n, dn.status + 2 * i, dout + i,
+             nullptr};
+  }
+  auto* dfj = ws<FinishJobHost>(c, "finishjobs", np);
+  h2d(c, dfj, fj.data(), np);
+  launch_finish(c->stream, dfj, np);
+  check_launch("finish");
+  std::vector<int> st(2 * np);
+  d2h(c, out, dout, np);
+  d2h(c, st.data(), dn.status, 2 * np);
+  sync(c);
+  status_out.assign(np, 0);
+  for (int i = 0; i < np; ++i) status_out[i] = st[2 * i] || st[2 * i + 1];
+}
+
+
+struct QuOut {
+  double *me, *cov, *Ucol;
+  int64_t ld;
+};
+
+// compute_q_u (gpar_scaled_inference.jl:141-196): Cuu without noise, D = L_u^-1 G L_u^-T + I,
+// m_e = D^-1 L_u^-1 r, cov = inv(D) = L_D^-T L_D^-1, U_u = chol(Cuu).U.
+static QuOut run_q_u(gpar_ctx* c, const DevProblem& p, const Theta& th) {
+  std::vector<DevProblem> P{p};
+  std::vector<Theta> T{th};
+  GramOut go = run_gram_stage(c, P, T);
+  DenseOut dn = run_dense(c, P, T, go, /*qu_mode=*/true);
+  QuOut q;
+  q.ld = dn.ld;
+  q.me = ws<double>(c, "qu_me", p.m);
+  FinishJobHost fj{dn.Lu, dn.Llam, dn.ld, (int)p.m, go.r, go.logs, p.nch, go.a2part, go.npart,
+                   p.n, dn.status, ws<double>(c, "dtc_out", 1), q.me};
+  auto* dfj = ws<FinishJobHost>(c, "finishjobs", 1);
+  h2d(c, dfj, &fj, 1);
+  launch_finish(c->stream, dfj, 1);
+  check_launch("finish(q_u)");
+  // X = L_D^{-1} I ; cov = X^T X
+  double* I = ws<double>(c, "qu_eye", (size_t)dn.ld * dn.ld);
+  double* X = ws<double>(c, "qu_X", (size_t)dn.ld * dn.ld);
+  q.cov = ws<double>(c, "qu_cov", (size_t)dn.ld * dn.ld);
+  launch_eye(c->stream, I, dn.ld, (int)p.m);
+  TrsmJobHost tj{dn.Llam, dn.ld, I, dn.ld, X, dn.ld, (int)p.m, p.m, 0, 0};
+  auto* dtj = ws<TrsmJobHost>(c, "trsmjobsQ", 1);
+  h2d(c, dtj, &tj, 1);
+  launch_trsm(c->stream, dtj, 1, p.m);
+  launch_gram_small(c->stream, X, dn.ld, (int)p.m, q.cov, dn.ld);
+  q.Ucol = ws<double>(c, "qu_U", (size_t)p.m * p.m);
+  launch_lower_to_upper_colmajor(c->stream, dn.Lu, dn.ld, (int)p.m, q.Ucol);
+  check_launch("q_u tail");
+  int st[2];
+  d2h(c, st, dn.status, 2);
+  sync(c);
+  if (st[0]) throw Error(GPAR_ERR_NOT_PD, "PosDefException: cholesky(Symmetric(Cuu)) failed (gpar_scaled_inference.jl:159)");
+  if (st[1]) throw Error(GPAR_ERR_NOT_PD, "PosDefException: cholesky(Symmetric(D)) failed (gpar_scaled_inference.jl:188)");
+  return q;
+}
+
+// logpdf of independent LGSSM chains sharing t (device pointers).
+static void chains_logpdf(gpar_ctx* c, int nchains, int64_t n, const double* t, const double* y,
+                          int64_t ldy, int kernel, int sdim, const double* theta, double* lml) {
+  std::vector<ChainParamsHost> cps(nchains);
+  for (int i = 0; i < nchains; ++i) {
+    const double l = theta[3 * i], pv = theta[3 * i + 1], ns = theta[3 * i + 2];
+    ARGCHECK(l > 0 && pv > 0 && ns > 0, "theta entries must be positive");
+    cps[i] = {1.0 / l, l, pv * pv, ns * ns};
+  }
+  const int64_t nch = (n + kChunk - 1) / kChunk;
+  GainsOut g = run_gains(c, sdim, t, n, cps, nullptr, false, "chain");
+  double* alpha = ws<double>(c, "chain_alpha", (size_t)nchains * n);
+  double* send = ws<double>(c, "chain_send", (size_t)nchains * nch * 4);
+  double* cin = ws<double>(c, "chain_cin", (size_t)nchains * nch * 4);
+  const int64_t npart = vec_fix_blocks(n);
+  double* a2 = ws<double>(c, "chain_a2", (size_t)nchains * npart);
+  double* dl = ws<double>(c, "chain_lml", nchains);
+  launch_whiten_vec(c->stream, sdim, g.rec, g.recstride, y, ldy, n, kChunk, nch, nchains, alpha, n,
+                    send, nch * 4, 1, 0);
+  launch_carry(c->stream, sdim, g.phi, g.phistride, send, cin, nch * 4, nch, 1, 1, nchains);
+  launch_vec_fix(c->stream, sdim, alpha, n, g.g, g.gstride, cin, nch * 4, 1, 0, n, kChunk, nchains, a2);
+  launch_chain_lml(c->stream, g.logs, nch, a2, npart, n, nchains, dl);
+  check_launch("chains_logpdf");
+  d2h(c, lml, dl, nchains);
+  sync(c);
+}
+
+static double unpack(double p) { return std::exp(p) + 1e-3; }
+
+}  // namespace gpar
+
+using namespace gpar;
+
+#define API_BEGIN(ctx)                                          \
+  if (!(ctx)) return GPAR_ERR_STATE;                            \
+  try {                                                         \
+    (ctx)->err.clear();                                         \
+    HIPCHECK(hipSetDevice((ctx)->device));
+
+#define API_END(ctx)                                            \
+  }                                                             \
+  catch (const gpar::Error& e) {                                \
+    (ctx)->err = e.what();                                      \
+    return e.code;                                              \
+  }                                                             \
+  catch (const std::exception& e) {                             \
+    (ctx)->err = e.what();                                      \
+    return GPAR_ERR_HIP;                                        \
+  }                                                             \
+  return GPAR_OK;
+
+extern "C" {
+
+int32_t gpar_abi_version(void) { return GPAR_ABI_VERSION; }
+
+int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
+  if (!out) return GPAR_ERR_ARG;
+  *out = nullptr;
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return GPAR_ERR_HIP;
+  if (device < 0 || device >= n) return GPAR_ERR_ARG;
+  if (hipSetDevice(device) != hipSuccess) return GPAR_ERR_HIP;
+  auto* c = new gpar_ctx();
+  c->device = device;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return GPAR_ERR_HIP;
+  }
+  *out = c;
+  return GPAR_OK;
+}
+
+int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
+  if (!ctx) return GPAR_ERR_STATE;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  for (auto& kv : ctx->bufs)
+    if (kv.second.p) (void)hipFree(kv.second.p);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return GPAR_OK;
+}
+
+const char* gpar_last_error(const gpar_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int64_t gpar_ctx_workspace_bytes(const gpar_ctx* ctx) {
+  if (!ctx) return 0;
+  int64_t s = 0;
+  for (auto& kv : ctx->bufs) s += (int64_t)kv.second.bytes;
+  return s;
+}
+
+int32_t gpar_ctx_trim(gpar_ctx* ctx) {
+  API_BEGIN(ctx)
+  HIPCHECK(hipStreamSynchronize(ctx->stream));
+  for (auto& kv : ctx->bufs)
+    if (kv.second.p) HIPCHECK(hipFree(kv.second.p));
+  ctx->bufs.clear();
+  API_END(ctx)
+}
+
+int32_t gpar_dtc_objective(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                           const double* theta, double* dtc_out) {
+  API_BEGIN(ctx)
+  ARGCHECK(probs && nprob >= 1 && theta && dtc_out, "null argument");
+  std::vector<DevProblem> P;
+  for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
+  std::vector<Theta> th = thetas_from(theta, nprob);
+  std::vector<int> st;
+  eval_dtc(ctx, P, th, dtc_out, st);
+  for (int i = 0; i < nprob; ++i)
+    if (st[i])
+      throw Error(GPAR_ERR_NOT_PD, "PosDefException: Cholesky failed for output " + std::to_string(i));
+  API_END(ctx)
+}
+
+int32_t gpar_fit(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                 const double* log_theta0, const gpar_fit_options* opts, double* theta_out,
+                 double* nlml_out, int32_t* evals_out) {
+  API_BEGIN(ctx)
+  ARGCHECK(probs && nprob >= 1 && log_theta0 && theta_out, "null argument");
+  gpar_fit_options o{0, 1000, 1e-8, 0.0};
+  if (opts) o = *opts;
+  std::vector<DevProblem> P;
+  for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
+  std::vector<NelderMead> nm;
+  nm.reserve(nprob);
+  for (int i = 0; i < nprob; ++i)
+    nm.emplace_back(std::vector<double>(log_theta0 + 5 * i, log_theta0 + 5 * i + 5), o.max_evals,
+                    o.max_iterations, o.g_tol, o.time_limit);
+  std::vector<double> vals;
+  while (true) {
+    std::vector<int> act;
+    for (int i = 0; i < nprob; ++i)
+      if (!nm[i].done()) act.push_back(i);
+    if (act.empty()) break;
+    std::vector<DevProblem> sub;
+    std::vector<Theta> th;
+    for (int i : act) {
+      sub.push_back(P[i]);
+      const auto& x = nm[i].ask();
+      th.push_back({unpack(x[0]), unpack(x[1]), unpack(x[2]), unpack(x[3]), unpack(x[4])});
+    }
+    vals.assign(act.size(), 0.0);
+    std::vector<int> st;
+    eval_dtc(ctx, sub, th, vals.data(), st);
+    for (size_t a = 0; a < act.size(); ++a) {
+      double f = -vals[a];
+      if (st[a] || !std::isfinite(f)) f = INFINITY;  // PosDefException -> reject the point
+      nm[act[a]].tell(f);
+    }
+  }
+  for (int i = 0; i < nprob; ++i) {
+    const auto& x = nm[i].x_min();
+    for (int j = 0; j < 5; ++j) theta_out[5 * i + j] = unpack(x[j]);
+    if (nlml_out) nlml_out[i] = nm[i].f_min();
+    if (evals_out) evals_out[i] = nm[i].evals();
+  }
+  API_END(ctx)
+}
+
+int32_t gpar_dtc_objective_A(gpar_ctx* ctx, const gpar_problem* prob, const double* theta,
+                             double* dtc_out, double* A_out) {
+  API_BEGIN(ctx)
+  ARGCHECK(prob && theta && dtc_out && A_out, "null argument");
+  std::vector<DevProblem> P{prepare_problem(ctx, *prob, 0)};
+  std::vector<Theta> th = thetas_from(theta, 1);
+  GramOut go = run_gram_stage(ctx, P, th, /*fix_beta=*/true);
+  DenseOut dn = run_dense(ctx, P, th, go, false);
+  const DevProblem& p = P[0];
+  const int64_t nch = p.nch;
+  FinishJobHost fj{dn.Lu, dn.Llam, dn.ld, (int)p.m, go.r, go.logs, nch, go.a2part, go.npart,
+                   p.n, dn.status, ws<double>(ctx, "dtc_out", 1), nullptr};
+  auto* dfj = ws<FinishJobHost>(ctx, "finishjobs", 1);
+  h2d(ctx, dfj, &fj, 1);
+  launch_finish(ctx->stream, dfj, 1);
+  check_launch("finish");
+  // A = L_u^{-1} beta^T (M x N), written column-major: A[i + j*m] -> transX with ldx = m
+  double* A = ws<double>(ctx, "A_out", (size_t)p.m * p.n);
+  TrsmJobHost tj{dn.Lu, dn.ld, ws<double>(ctx, "beta", 1), p.mp, A, p.m, (int)p.m, p.n, 1, 1};
+  auto* dtj = ws<TrsmJobHost>(ctx, "trsmjobsA", 1);
+  h2d(ctx, dtj, &tj, 1);
+  launch_trsm(ctx->stream, dtj, 1, p.n);
+  check_launch("trsm(A)");
+  int st[2];
+  d2h(ctx, st, dn.status, 2);
+  d2h(ctx, dtc_out, fj.out, 1);
+  if (prob->mem == GPAR_MEM_DEVICE)
+    HIPCHECK(hipMemcpyAsync(A_out, A, (size_t)p.m * p.n * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+  else
+    d2h(ctx, A_out, A, (size_t)p.m * p.n);
+  sync(ctx);
+  if (st[0] || st[1]) throw Error(GPAR_ERR_NOT_PD, "PosDefException: Cholesky failed");
+  API_END(ctx)
+}
+
+int32_t gpar_q_u(gpar_ctx* ctx, const gpar_problem* prob, const double* theta, double* m_e,
+                 double* cov, double* U_u) {
+  API_BEGIN(ctx)
+  ARGCHECK(prob && theta && m_e && cov && U_u, "null argument");
+  std::vector<DevProblem> P{prepare_problem(ctx, *prob, 0)};
+  std::vector<Theta> th = thetas_from(theta, 1);
+  QuOut q = run_q_u(ctx, P[0], th[0]);
+  const int64_t m = P[0].m;
+  if (prob->mem == GPAR_MEM_DEVICE) {
+    HIPCHECK(hipMemcpyAsync(m_e, q.me, m * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHECK(hipMemcpy2DAsync(cov, m * sizeof(double), q.cov, q.ld * sizeof(double), m * sizeof(double), m, hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHECK(hipMemcpyAsync(U_u, q.Ucol, m * m * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+  } else {
+    d2h(ctx, m_e, q.me, m);
+    HIPCHECK(hipMemcpy2DAsync(cov, m * sizeof(double), q.cov, q.ld * sizeof(double), m * sizeof(double), m, hipMemcpyDeviceToHost, ctx->stream));
+    d2h(ctx, U_u, q.Ucol, (size_t)m * m);
+  }
+  sync(ctx);
+  API_END(ctx)
+}
+
+int32_t gpar_lgssm_logpdf(gpar_ctx* ctx, int32_t nchains, int64_t n, const double* t,
+                          const double* y, int64_t ldy, int32_t kernel, const double* theta,
+                          int32_t mem, double* lml_out) {
+  API_BEGIN(ctx)
+  ARGCHECK(nchains >= 1 && n >= 1 && t && y && theta && lml_out, "bad argument");
+  ARGCHECK(ldy >= n, "ldy must be >= n");
+  const int sdim = sde_dim(kernel);
+  const double* dt = t;
+  const double* dy = y;
+  if (mem == GPAR_MEM_HOST) {
+    check_sorted_host(t, n);
+    double* tt = ws<double>(ctx, "lg_t", n);
+    double* yy = ws<double>(ctx, "lg_y", (size_t)nchains * n);
+    h2d(ctx, tt, t, n);
+    HIPCHECK(hipMemcpy2DAsync(yy, n * sizeof(double), y, ldy * sizeof(double), n * sizeof(double), nchains, hipMemcpyHostToDevice, ctx->stream));
+    dt = tt;
+    dy = yy;
+    ldy = n;
+  }
+  std::vector<double> lml(nchains);
+  chains_logpdf(ctx, nchains, n, dt, dy, ldy, kernel, sdim, theta, lml.data());
+  for (int i = 0; i < nchains; ++i) lml_out[i] = lml[i];
+  API_END(ctx)
+}
+
+static int32_t not_yet(gpar_ctx* ctx, const char* what) {
+  if (!ctx) return GPAR_ERR_STATE;
+  ctx->err = std::string(what) + ": not implemented in this build";
+  return GPAR_ERR_UNSUPPORTED;
+}
+
+int32_t gpar_predict(gpar_ctx* ctx, const gpar_problem* prob, const double* theta,
+                     int64_t n_star, const double* t_star, const double* v_star, int64_t ldvs,
+                     int32_t mode, int32_t samples, uint64_t seed, double* mean, double* std) {
+  return not_yet(ctx, "gpar_predict");
+}
+
+int32_t gpar_lgssm_smooth(gpar_ctx* ctx, int32_t nchains, int64_t n, const double* t,
+                          const double* y, int64_t ldy, const double* noise, int32_t kernel,
+                          const double* theta, int32_t mem, double* mean, double* var) {
+  return not_yet(ctx, "gpar_lgssm_smooth");
+}
+
+int32_t gpar_sde_predictions(gpar_ctx* ctx, int32_t nchains, int64_t n, const double* t,
+                             const double* y, int64_t ldy, int64_t n_star, const double* t_star,
+                             int32_t kernel, const double* log_theta0,
+                             const gpar_fit_options* opts, int32_t mem, double* theta_out,
+                             double* mean, double* var) {
+  return not_yet(ctx, "gpar_sde_predictions");
+}
+
+int32_t gpar_exact_logpdf(gpar_ctx* ctx, int64_t n, int64_t dx, const double* x, int64_t ldx,
+                          const double* y, int32_t time_kernel, int32_t out_kernel,
+                          const double* theta, int32_t mem, double* lml_out) {
+  return not_yet(ctx, "gpar_exact_logpdf");
+}
+
+int32_t gpar_exact_posterior(gpar_ctx* ctx, int64_t n, int64_t dx, const double* x, int64_t ldx,
+                             const double* y, int64_t n_star, const double* x_star,
+                             int64_t ldxs, int32_t time_kernel, int32_t out_kernel,
+                             const double* theta, int32_t mem, double* mean, double* var) {
+  return not_yet(ctx, "gpar_exact_posterior");
+}
+
+}  // extern "C"

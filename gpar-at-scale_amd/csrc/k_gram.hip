@@ -1,0 +1,247 @@
+// k_gram.hip -- the dominant contraction of the DTC objective on fp64 MFMA.
+//
+// G = beta^T beta (M x M) and r = beta^T alpha over N time steps, where
+// beta[k, c] = beta_loc[k, c] + g_k . cin[chunk(k)][c] applies the chunk fix-up of the
+// time-chunked Kalman whitening on the fly (k_lgssm.hip), so the corrected beta is never
+// written to HBM.  In the reference this is the M x M x N trsm + gemm of dtc.jl:119-120
+// (A = L_u^{-1} beta^T; Lambda = A A^T + I), which the build reassociates as
+// Lambda = L_u^{-1} (beta^T beta) L_u^{-T} + I.
+//
+// Tiling: one 256-thread workgroup = one 128 x 128 lower-triangle tile of G over one
+// split of the time axis (split-K).  4 waves as 2 x 2, each 64 x 64 = 4 x 4 MFMA tiles of
+// v_mfma_f64_16x16x4_f64 (C/D: col = lane & 15, row = (lane >> 4) + 4 * reg).
+// K-step = 16 time rows staged global -> VGPR (fix-up) -> LDS, double buffered.
+// Blocks of one split run on one XCD group (blockIdx % 8) so the split's rows are
+// shared through that XCD's L2 by its tiles.
+#include "device_common.hpp"
+
+namespace gpar {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+constexpr int kGT = 128;          // tile edge
+constexpr int kBK = 16;           // time rows per K-step
+constexpr int kLdsStride = 144;   // padded LDS row (doubles): rows r and r+1 hit opposite bank halves
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void gram_kernel(
+    const double* __restrict__ beta, int64_t ldb, int64_t n, const double* __restrict__ g,
+    const double* __restrict__ cin, int64_t mc, int L, const double* __restrict__ alpha,
+    int ntb, int ntiles, int nsplit, int64_t rows_per_split, double* __restrict__ part,
+    double* __restrict__ rpart) {
+  __shared__ __attribute__((aligned(16))) double lds[2][2][kBK * kLdsStride];
+  __shared__ double rred[128];
+
+  // XCD-aware decode: blocks b and b+8 share an XCD; give each XCD group whole splits.
+  const int b = blockIdx.x;
+  const int xg = b & 7;
+  const int q = b >> 3;
+  const int split = (q / ntiles) * 8 + xg;
+  const int tile = q % ntiles;
+  if (split >= nsplit) return;
+  int ti = 0;
+  while ((ti + 1) * (ti + 2) / 2 <= tile) ++ti;
+  const int tj = tile - ti * (ti + 1) / 2;
+  const bool diag = (ti == tj);
+  const int64_t i0 = (int64_t)ti * kGT, j0 = (int64_t)tj * kGT;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int sc = tid & 127;   // staging column
+  const int rg = tid >> 7;    // staging row group (wave-uniform)
+
+  const int64_t kb = (int64_t)split * rows_per_split;
+  int64_t ke = kb + rows_per_split;
+  if (ke > n) ke = n;
+
+  d4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[a][c] = d4{0.0, 0.0, 0.0, 0.0};
+
+  double racc = 0.0;
+  double cI[D], cJ[D];
+  int64_t cur_chunk = -1;
+  double sI[8], sJ[8];
+
+  auto stage_load = [&](int64_t k0) {
+    const int64_t ch = k0 / L;
+    if (ch != cur_chunk) {
+      cur_chunk = ch;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        cI[i] = cin[(ch * mc + i0 + sc) * kSStride + i];
+        cJ[i] = cin[(ch * mc + j0 + sc) * kSStride + i];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      const int64_t k = k0 + rg + 2 * r;
+      double vi = 0.0, vj = 0.0;
+      if (k < ke) {
+        vi = beta[k * ldb + i0 + sc];
+        if (!diag) vj = beta[k * ldb + j0 + sc];
+        const double* gk = g + k * kGStride;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          vi = fma(gk[i], cI[i], vi);
+          if (!diag) vj = fma(gk[i], cJ[i], vj);
+        }
+        if (diag) racc = fma(alpha[k], vi, racc);
+      }
+      sI[r] = vi;
+      sJ[r] = vj;
+    }
+  };
+  auto stage_store = [&](int buf) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) {
+      lds[buf][0][(rg + 2 * r) * kLdsStride + sc] = sI[r];
+      if (!diag) lds[buf][1][(rg + 2 * r) * kLdsStride + sc] = sJ[r];
+    }
+  };
+
+  const int nsteps = (int)((ke - kb + kBK - 1) / kBK);
+  if (nsteps > 0) {
+    stage_load(kb);
+    stage_store(0);
+  }
+  __syncthreads();
+  const int opB = diag ? 0 : 1;
+  const int frow = lane >> 4, fcol = lane & 15;
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    const bool more = (s + 1) < nsteps;
+    if (more) stage_load(kb + (int64_t)(s + 1) * kBK);
+    const double* la = &lds[buf][0][0];
+    const double* lb = &lds[buf][opB][0];
+#pragma unroll
+    for (int ks = 0; ks < kBK / 4; ++ks) {
+      double fa[4], fb[4];
+      const int row = ks * 4 + frow;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) fa[a] = la[row * kLdsStride + wr * 64 + a * 16 + fcol];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) fb[c] = lb[row * kLdsStride + wc * 64 + c * 16 + fcol];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[c], acc[a][c], 0, 0, 0);
+    }
+    if (more) stage_store(buf ^ 1);
+    __syncthreads();
+  }
+
+  double* pt = part + ((int64_t)split * ntiles + tile) * (kGT * kGT);
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wr * 64 + a * 16 + frow + 4 * r;
+        const int col = wc * 64 + c * 16 + fcol;
+        pt[row * kGT + col] = acc[a][c][r];
+      }
+  if (diag) {
+    if (rg == 1) rred[sc] = racc;
+    __syncthreads();
+    if (rg == 0) rpart[((int64_t)split * ntb + ti) * kGT + sc] = racc + rred[sc];
+  }
+}
+
+// Sum split partials in split order (deterministic) into the full symmetric G (ldg) and r.
+__global__ __launch_bounds__(256) void gram_reduce(const double* __restrict__ part,
+                                                   const double* __restrict__ rpart, int ntb,
+                                                   int ntiles, int nsplit, double* __restrict__ G,
+                                                   int64_t ldg, double* __restrict__ r) {
+  const int tile = blockIdx.y;
+  const int e = blockIdx.x * 256 + threadIdx.x;   // element within the tile
+  int ti = 0;
+  while ((ti + 1) * (ti + 2) / 2 <= tile) ++ti;
+  const int tj = tile - ti * (ti + 1) / 2;
+  if (e < kGT * kGT && !(ti == tj && e / kGT < e % kGT)) {
+    double s = 0.0;
+    for (int sp = 0; sp < nsplit; ++sp) s += part[((int64_t)sp * ntiles + tile) * (kGT * kGT) + e];
+    const int64_t row = (int64_t)ti * kGT + e / kGT, col = (int64_t)tj * kGT + e % kGT;
+    G[row * ldg + col] = s;
+    G[col * ldg + row] = s;
+  }
+  if (ti == tj && blockIdx.x == 0 && threadIdx.x < kGT) {
+    double s = 0.0;
+    for (int sp = 0; sp < nsplit; ++sp) s += rpart[((int64_t)sp * ntb + ti) * kGT + threadIdx.x];
+    r[(int64_t)ti * kGT + threadIdx.x] = s;
+  }
+}
+
+// Materialise the corrected beta (only for the (dtc, A) parity entry point).
+template <int D>
+__global__ __launch_bounds__(256) void beta_fix_kernel(double* __restrict__ beta, int64_t ldb,
+                                                       int64_t n, const double* __restrict__ g,
+                                                       const double* __restrict__ cin, int64_t mc,
+                                                       int L) {
+  const int64_t e = blockIdx.x * (int64_t)256 + threadIdx.x;
+  if (e >= n * ldb) return;
+  const int64_t k = e / ldb, c = e % ldb;
+  const int64_t ch = k / L;
+  double v = beta[e];
+#pragma unroll
+  for (int i = 0; i < D; ++i) v = fma(g[k * kGStride + i], cin[(ch * mc + c) * kSStride + i], v);
+  beta[e] = v;
+}
+
+}  // namespace gpar
+
+// ============================================================================ launch wrappers
+#include "launch.hpp"
+
+namespace gpar {
+
+GramPlan gram_plan(int64_t n, int64_t mp) {
+  GramPlan p;
+  p.ntb = (int)(mp / kGT);
+  p.ntiles = p.ntb * (p.ntb + 1) / 2;
+  int ns = 512 / p.ntiles;
+  ns = (ns / 8) * 8;
+  if (ns < 8) ns = 8;
+  int64_t maxs = (n + 255) / 256;          // keep >= 256 rows per split
+  if (maxs < 8) maxs = 8;
+  if (ns > maxs) ns = (int)((maxs / 8) * 8);
+  if (ns < 8) ns = 8;
+  p.nsplit = ns;
+  int64_t rps = (n + ns - 1) / ns;
+  rps = ((rps + kBK - 1) / kBK) * kBK;
+  p.rows_per_split = rps;
+  return p;
+}
+
+void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* beta,
+                 int64_t ldb, int64_t n, const double* g, const double* cin, int64_t mc, int L,
+                 const double* alpha, double* part, double* rpart, double* G, int64_t ldg,
+                 double* r) {
+  const int nblk = plan.ntiles * plan.nsplit;
+
+  switch (sdim) {
+    case 1: gram_kernel<1><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.ntb, plan.ntiles, plan.nsplit, plan.rows_per_split, part, rpart); break;
+    case 2: gram_kernel<2><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.ntb, plan.ntiles, plan.nsplit, plan.rows_per_split, part, rpart); break;
+    default: gram_kernel<3><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.ntb, plan.ntiles, plan.nsplit, plan.rows_per_split, part, rpart); break;
+  }
+  dim3 rgrid((kGT * kGT + 255) / 256, plan.ntiles);
+  gram_reduce<<<rgrid, 256, 0, st>>>(part, rpart, plan.ntb, plan.ntiles, plan.nsplit, G, ldg, r);
+}
+
+void launch_beta_fix(hipStream_t st, int sdim, double* beta, int64_t ldb, int64_t n,
+                     const double* g, const double* cin, int64_t mc, int L) {
+  const unsigned nb = (unsigned)((n * ldb + 255) / 256);
+  switch (sdim) {
+    case 1: beta_fix_kernel<1><<<nb, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L); break;
+    case 2: beta_fix_kernel<2><<<nb, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L); break;
+    default: beta_fix_kernel<3><<<nb, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L); break;
+  }
+}
+
+}  // namespace gpar

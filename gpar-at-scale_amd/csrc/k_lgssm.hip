@@ -1,0 +1,635 @@
+// k_lgssm.hip -- state-space (Kalman) sweeps of the time GP on gfx950.
+//
+// Replaces the sequential TemporalGPs `decorrelate`/`logpdf` calls of the reference
+// (dtc.jl:106-117, gpar_scaled_inference.jl:170-183, temporal_gp_inference.jl:295) with a
+// time-chunked formulation whose every sequential dependency is short:
+//
+//  gains (data-independent, per chain = per output or temporal chain):
+//    phase 1  per chunk: fold the chunk's covariance elements (A, C, J) of the parallel
+//             Kalman filter (Sarkka & Garcia-Fernandez 2021, covariance part only);
+//    phase 2  per chain: exclusive scan of the chunk aggregates -> filtered covariance at
+//             every chunk start;
+//    phase 3  per chunk: ordinary Riccati recursion from that covariance, emitting the
+//             per-step record {A_k, K_k, 1/sqrt(S_k)}, the fix-up vectors
+//             g_k = -rs_k (A_k Phi_{k-1})[0,:], the chunk transition Phi_j and sum log S_k.
+//  columns (data): the filter is affine in the data with data-independent coefficients,
+//    m_k = (I - K_k h) A_k m_{k-1} + K_k x_k, so each chunk is filtered from a zero state
+//    (whiten_*), the true chunk-start states follow from a short carry recursion over chunks
+//    (carry_kernel), and alpha_k(true) = alpha_k(local) + g_k . c_chunk (applied by the
+//    consumer: vec_fix_kernel here, the Gram loader in k_gram.hip).
+#include "device_common.hpp"
+
+namespace gpar {
+
+struct ChainParams {
+  double inv_l;   // 1 / time lengthscale
+  double l;       // time lengthscale
+  double s;       // time-kernel variance (time_var^2)
+  double r;       // observation noise variance (sigma^2), used when no noise vector
+};
+
+template <int D>
+struct Elem {
+  double A[D][D];
+  double C[D][D];
+  double J[D][D];
+};
+
+template <int D>
+__device__ __forceinline__ void elem_identity(Elem<D>& e) {
+  mat_eye(e.A);
+  mat_zero(e.C);
+  mat_zero(e.J);
+}
+
+// e = e1 (earlier) (x) e2 (later)
+template <int D>
+__device__ __forceinline__ void elem_combine(const Elem<D>& e1, const Elem<D>& e2, Elem<D>& out) {
+  double Mi[D][D], M[D][D], T[D][D], X[D][D], V[D][D], U[D][D];
+  mat_mul(e1.C, e2.J, Mi);
+#pragma unroll
+  for (int i = 0; i < D; ++i) Mi[i][i] += 1.0;
+  mat_inv(Mi, M);
+  mat_mul(e2.A, M, T);                 // T = A2 M
+  Elem<D> r;
+  mat_mul(T, e1.A, r.A);               // A = A2 M A1
+  mat_mul(T, e1.C, X);                 // X = A2 M C1
+  mat_mul_bt(X, e2.A, r.C);            // C = A2 M C1 A2^T + C2
+  mat_mul(M, e1.A, V);                 // V = M A1
+  mat_mul(e2.J, e1.A, U);              // U = J2 A1
+  mat_mul_at(V, U, r.J);               // J = A1^T M^T J2 A1 + J1
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      r.C[i][j] += e2.C[i][j];
+      r.J[i][j] += e1.J[i][j];
+    }
+  // keep the covariance parts exactly symmetric
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      const double c = 0.5 * (r.C[i][j] + r.C[j][i]);
+      r.C[i][j] = c; r.C[j][i] = c;
+      const double q = 0.5 * (r.J[i][j] + r.J[j][i]);
+      r.J[i][j] = q; r.J[j][i] = q;
+    }
+  out = r;
+}
+
+// Transition + process noise for step k of chain p (stationary start: tau_0 = 1).
+template <int D>
+__device__ __forceinline__ void step_model(const double* __restrict__ t, int64_t k,
+                                           const ChainParams& cp, double (&A)[D][D],
+                                           double (&Q)[D][D]) {
+  const double tau = (k == 0) ? 1.0 : (t[k] - t[k - 1]) / cp.l;
+  sde_transition<D>(tau, A);
+  double Pinf[D][D], X[D][D];
+  sde_pinf<D>(cp.s, Pinf);
+  mat_mul(A, Pinf, X);
+  mat_mul_bt(X, A, Q);
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) Q[i][j] = Pinf[i][j] - Q[i][j];
+}
+
+// Covariance element of step k (Sarkka & Garcia-Fernandez, Lemma 7 without the data parts).
+template <int D>
+__device__ __forceinline__ void step_elem(const double* __restrict__ t, int64_t k,
+                                          const ChainParams& cp, double R, Elem<D>& e) {
+  double A[D][D], Q[D][D];
+  step_model<D>(t, k, cp, A, Q);
+  if (k == 0) {
+    double P0[D][D], X[D][D], Pm[D][D];
+    sde_pinf<D>(cp.s, P0);
+    mat_mul(A, P0, X);
+    mat_mul_bt(X, A, Pm);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int j = 0; j < D; ++j) Pm[i][j] += Q[i][j];
+    const double S = Pm[0][0] + R;
+    mat_zero(e.A);
+    mat_zero(e.J);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int j = 0; j < D; ++j) e.C[i][j] = Pm[i][j] - (Pm[i][0] / S) * Pm[0][j];
+  } else {
+    const double S = Q[0][0] + R;
+    const double iS = 1.0 / S;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const double kk = Q[i][0] * iS;
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        e.A[i][j] = A[i][j] - kk * A[0][j];
+        e.C[i][j] = Q[i][j] - kk * Q[0][j];
+        e.J[i][j] = A[0][i] * A[0][j] * iS;
+      }
+    }
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void elem_store(double* __restrict__ p, const Elem<D>& e) {
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      p[i * D + j] = e.A[i][j];
+      p[D * D + i * D + j] = e.C[i][j];
+      p[2 * D * D + i * D + j] = e.J[i][j];
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void elem_load(const double* __restrict__ p, Elem<D>& e) {
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      e.A[i][j] = p[i * D + j];
+      e.C[i][j] = p[D * D + i * D + j];
+      e.J[i][j] = p[2 * D * D + i * D + j];
+    }
+}
+
+// ---------------------------------------------------------------------------- phase 1
+template <int D>
+__global__ __launch_bounds__(256) void gains_phase1(const double* __restrict__ t, int64_t n,
+                                                    int L, int64_t nch,
+                                                    const ChainParams* __restrict__ cps,
+                                                    const double* __restrict__ noise,
+                                                    double* __restrict__ agg) {
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (j >= nch) return;
+  const ChainParams cp = cps[p];
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  Elem<D> acc, e;
+  step_elem<D>(t, k0, cp, noise ? noise[k0] : cp.r, acc);
+  for (int64_t k = k0 + 1; k < k1; ++k) {
+    step_elem<D>(t, k, cp, noise ? noise[k] : cp.r, e);
+    elem_combine<D>(acc, e, acc);
+  }
+  elem_store<D>(agg + ((int64_t)p * nch + j) * (3 * D * D), acc);
+}
+
+// ---------------------------------------------------------------------------- phase 2
+// One workgroup per chain: exclusive scan over chunk aggregates; writes the filtered
+// covariance at the end of chunk j-1 into pstart[j] (j >= 1).
+template <int D>
+__global__ __launch_bounds__(256) void gains_phase2(int64_t nch, const double* __restrict__ agg,
+                                                    double* __restrict__ pstart) {
+  constexpr int E = 3 * D * D;
+  __shared__ double buf[2][256 * E];
+  const int p = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t per = (nch + 255) / 256;
+  const int64_t j0 = tid * per;
+  const int64_t j1 = (j0 + per < nch) ? j0 + per : nch;
+  const double* a = agg + (int64_t)p * nch * E;
+  Elem<D> loc, e;
+  elem_identity(loc);
+  for (int64_t j = j0; j < j1; ++j) {
+    elem_load<D>(a + j * E, e);
+    elem_combine<D>(loc, e, loc);
+  }
+  elem_store<D>(&buf[0][tid * E], loc);
+  __syncthreads();
+  int cur = 0;
+  for (int off = 1; off < 256; off <<= 1) {
+    Elem<D> mine;
+    elem_load<D>(&buf[cur][tid * E], mine);
+    if (tid >= off) {
+      Elem<D> prev;
+      elem_load<D>(&buf[cur][(tid - off) * E], prev);
+      elem_combine<D>(prev, mine, mine);
+    }
+    elem_store<D>(&buf[cur ^ 1][tid * E], mine);
+    __syncthreads();
+    cur ^= 1;
+  }
+  Elem<D> pre;
+  if (tid == 0) {
+    elem_identity(pre);
+  } else {
+    elem_load<D>(&buf[cur][(tid - 1) * E], pre);
+  }
+  double* ps = pstart + (int64_t)p * nch * (D * D);
+  for (int64_t j = j0; j < j1; ++j) {
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) ps[j * D * D + i * D + q] = pre.C[i][q];
+    elem_load<D>(a + j * E, e);
+    elem_combine<D>(pre, e, pre);
+  }
+}
+
+// ---------------------------------------------------------------------------- phase 3
+// Riccati recursion inside each chunk from the scanned start covariance.
+//   rec[k]   = {A_k (row-major), K_k, rs_k = 1/sqrt(S_k)}
+//   g[k]     = -rs_k * (A_k Phi_{j,k-1})[0, :]
+//   phi[j]   = prod_{k in chunk} (I - K_k e1^T) A_k   (D x D)
+//   logs[j]  = sum_{k in chunk} log S_k
+// With `smooth` output (prediction): pf[k] = filtered covariance (D x D), used by the RTS pass.
+template <int D>
+__global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t, int64_t n,
+                                                    int L, int64_t nch,
+                                                    const ChainParams* __restrict__ cps,
+                                                    const double* __restrict__ noise,
+                                                    const double* __restrict__ pstart,
+                                                    double* __restrict__ rec,
+                                                    double* __restrict__ g,
+                                                    double* __restrict__ phi,
+                                                    double* __restrict__ logs,
+                                                    double* __restrict__ pf) {
+  constexpr int RS = Rec<D>::size;
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (j >= nch) return;
+  const ChainParams cp = cps[p];
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  double P[D][D];
+  if (j == 0) {
+    sde_pinf<D>(cp.s, P);
+  } else {
+    const double* ps = pstart + ((int64_t)p * nch + j) * (D * D);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) P[i][q] = ps[i * D + q];
+  }
+  double Phi[D][D];
+  mat_eye(Phi);
+  double lsum = 0.0;
+  double* rp = rec + (int64_t)p * n * RS;
+  double* gp = g + (int64_t)p * n * kGStride;
+  double* pfp = pf ? pf + (int64_t)p * n * (D * D) : nullptr;
+  for (int64_t k = k0; k < k1; ++k) {
+    double A[D][D], Q[D][D], X[D][D], Pm[D][D];
+    step_model<D>(t, k, cp, A, Q);
+    mat_mul(A, P, X);
+    mat_mul_bt(X, A, Pm);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) Pm[i][q] += Q[i][q];
+    const double R = noise ? noise[k] : cp.r;
+    const double S = Pm[0][0] + R;
+    const double rs = 1.0 / sqrt(S);
+    double Kg[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) Kg[i] = Pm[i][0] / S;
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) P[i][q] = Pm[i][q] - Kg[i] * Pm[0][q];
+    double* r = rp + k * RS;
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) r[i * D + q] = A[i][q];
+#pragma unroll
+    for (int i = 0; i < D; ++i) r[D * D + i] = Kg[i];
+    r[D * D + D] = rs;
+    // g_k = -rs (A Phi)[0, :]
+    double AP[D][D];
+    mat_mul(A, Phi, AP);
+#pragma unroll
+    for (int q = 0; q < D; ++q) gp[k * kGStride + q] = -rs * AP[0][q];
+    // Phi <- (I - K e1^T) A Phi
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) Phi[i][q] = AP[i][q] - Kg[i] * AP[0][q];
+    lsum += log(S);
+    if (pfp) {
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) pfp[k * D * D + i * D + q] = P[i][q];
+    }
+  }
+  double* ph = phi + ((int64_t)p * nch + j) * (D * D);
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) ph[i * D + q] = Phi[i][q];
+  logs[(int64_t)p * nch + j] = lsum;
+}
+
+// ---------------------------------------------------------------------------- whitening of Kfu columns
+// beta_loc[k, c] = chunk-local whitened Kfu[k, c] with Kfu computed on the fly:
+// Kfu[k, c] = s_o kappa(||v_k - z_c|| / l_o)   (Stheno pairwise, dtc.jl:104).
+// grid: (nch, ceil(mp / 256)); block 256, one column per thread.
+// send[(j * mc + c) * 4 + i] = local end state of chunk j.
+constexpr int kVTile = 32;
+
+template <int TK, int OK, int DP>
+__global__ __launch_bounds__(256) void whiten_kfu(
+    const double* __restrict__ rec, const double* __restrict__ v, int64_t ldv, int d,
+    const double* __restrict__ z, int64_t ldz, int64_t m, int64_t mp, int64_t n, int L,
+    double inv_lo, double s_o, double* __restrict__ beta, int64_t ldb, double* __restrict__ send,
+    int64_t mc) {
+  constexpr int D = Sde<TK>::d;
+  constexpr int RS = Rec<D>::size;
+  __shared__ __attribute__((aligned(16))) double vs[kVTile][DP];
+  const int64_t j = blockIdx.x;
+  const int64_t c = (int64_t)blockIdx.y * 256 + threadIdx.x;
+  const bool valid = c < m;
+  const bool active = c < mp;
+  double zr[DP];
+#pragma unroll
+  for (int i = 0; i < DP; ++i) zr[i] = (valid && i < d) ? z[c * ldz + i] : 0.0;
+  double mst[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) mst[i] = 0.0;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  for (int64_t kt = k0; kt < k1; kt += kVTile) {
+    const int nt = (kt + kVTile <= k1) ? kVTile : (int)(k1 - kt);
+    __syncthreads();
+    for (int e = threadIdx.x; e < kVTile * DP; e += 256) {
+      const int kk = e / DP, i = e % DP;
+      vs[kk][i] = (kk < nt && i < d) ? v[(kt + kk) * ldv + i] : 0.0;
+    }
+    __syncthreads();
+    for (int kk = 0; kk < nt; ++kk) {
+      const int64_t k = kt + kk;
+      double d2a = 0.0, d2b = 0.0;
+#pragma unroll
+      for (int i = 0; i < DP; i += 2) {
+        const double a0 = vs[kk][i] - zr[i];
+        d2a = fma(a0, a0, d2a);
+        if (i + 1 < DP) {
+          const double a1 = vs[kk][i + 1] - zr[i + 1];
+          d2b = fma(a1, a1, d2b);
+        }
+      }
+      const double x = valid ? s_o * kappa_sq<OK>(d2a + d2b, inv_lo) : 0.0;
+      const double* r = rec + k * RS;
+      double mm[D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < D; ++q) acc = fma(r[i * D + q], mst[q], acc);
+        mm[i] = acc;
+      }
+      const double ev = x - mm[0];
+      const double al = ev * r[D * D + D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) mst[i] = fma(r[D * D + i], ev, mm[i]);
+      if (active) beta[k * ldb + c] = al;
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) send[(j * mc + c) * kSStride + i] = mst[i];
+  }
+}
+
+// ---------------------------------------------------------------------------- whitening of a vector per chain
+// One thread per (chunk, chain).  x_c[k] = y[c * ldy + k]; writes alpha_loc[c * lda + k]
+// and the local end state to send[(j * mc + col) * 4] for column `col` of chain c
+// (col = col0 + c * colstride).
+template <int D>
+__global__ __launch_bounds__(256) void whiten_vec(const double* __restrict__ rec, int64_t recstride,
+                                                  const double* __restrict__ y, int64_t ldy,
+                                                  int64_t n, int L, int64_t nch,
+                                                  double* __restrict__ alpha, int64_t lda,
+                                                  double* __restrict__ send, int64_t sendstride,
+                                                  int64_t mc, int64_t col) {
+  constexpr int RS = Rec<D>::size;
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int c = blockIdx.y;
+  if (j >= nch) return;
+  const double* rp = rec + (int64_t)c * recstride;
+  const double* yp = y + (int64_t)c * ldy;
+  double* ap = alpha + (int64_t)c * lda;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  double mst[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) mst[i] = 0.0;
+  for (int64_t k = k0; k < k1; ++k) {
+    const double* r = rp + k * RS;
+    double mm[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < D; ++q) acc = fma(r[i * D + q], mst[q], acc);
+      mm[i] = acc;
+    }
+    const double ev = yp[k] - mm[0];
+    ap[k] = ev * r[D * D + D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) mst[i] = fma(r[D * D + i], ev, mm[i]);
+  }
+  double* sp = send + (int64_t)c * sendstride;
+#pragma unroll
+  for (int i = 0; i < D; ++i) sp[(j * mc + col) * kSStride + i] = mst[i];
+}
+
+// ---------------------------------------------------------------------------- carry over chunks
+// For each column c (and chain b = blockIdx.y): cin[j][c] = true state at the start of chunk j,
+// cin[0] = 0, cin[j+1] = Phi_j cin[j] + send[j].
+template <int D>
+__global__ __launch_bounds__(256) void carry_kernel(const double* __restrict__ phi, int64_t phistride,
+                                                    const double* __restrict__ send,
+                                                    double* __restrict__ cin, int64_t sstride,
+                                                    int64_t nch, int64_t mc, int64_t ncols) {
+  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (c >= ncols) return;
+  const double* ph = phi + (int64_t)b * phistride;
+  const double* sp = send + (int64_t)b * sstride;
+  double* cp = cin + (int64_t)b * sstride;
+  double st[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) st[i] = 0.0;
+  for (int64_t j = 0; j < nch; ++j) {
+    const int64_t o = (j * mc + c) * kSStride;
+#pragma unroll
+    for (int i = 0; i < D; ++i) cp[o + i] = st[i];
+    double nx[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc = sp[o + i];
+#pragma unroll
+      for (int q = 0; q < D; ++q) acc = fma(ph[j * D * D + i * D + q], st[q], acc);
+      nx[i] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) st[i] = nx[i];
+  }
+}
+
+// ---------------------------------------------------------------------------- fix-up of a vector
+// alpha[k] += g_k . cin[chunk(k)][col]; per-block partial sums of alpha^2 into part[b][blk].
+template <int D>
+__global__ __launch_bounds__(256) void vec_fix(double* __restrict__ alpha, int64_t lda,
+                                               const double* __restrict__ g, int64_t gstride,
+                                               const double* __restrict__ cin, int64_t sstride,
+                                               int64_t mc, int64_t col, int64_t n, int L,
+                                               double* __restrict__ part) {
+  __shared__ double red[4];
+  const int b = blockIdx.y;
+  const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  double a2 = 0.0;
+  if (k < n) {
+    const int64_t j = k / L;
+    const double* gp = g + (int64_t)b * gstride + k * kGStride;
+    const double* cp = cin + (int64_t)b * sstride + (j * mc + col) * kSStride;
+    double a = alpha[(int64_t)b * lda + k];
+#pragma unroll
+    for (int i = 0; i < D; ++i) a = fma(gp[i], cp[i], a);
+    alpha[(int64_t)b * lda + k] = a;
+    a2 = a * a;
+  }
+  a2 = wave_sum(a2);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a2;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    part[(int64_t)b * gridDim.x + blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+}
+
+// ---------------------------------------------------------------------------- chain log-likelihood
+// lml[b] = -0.5 (n log 2pi + sum logS + sum alpha^2), partials summed in a fixed order.
+__global__ void chain_lml(const double* __restrict__ logs, int64_t nch,
+                          const double* __restrict__ a2part, int64_t npart, int64_t n,
+                          double* __restrict__ lml) {
+  const int b = blockIdx.x;
+  __shared__ double red[2][256];
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t j = threadIdx.x; j < nch; j += 256) s1 += logs[(int64_t)b * nch + j];
+  for (int64_t j = threadIdx.x; j < npart; j += 256) s2 += a2part[(int64_t)b * npart + j];
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = s2;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + off];
+      red[1][threadIdx.x] += red[1][threadIdx.x + off];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) lml[b] = -0.5 * ((double)n * kLog2Pi + red[0][0] + red[1][0]);
+}
+
+}  // namespace gpar
+
+// ============================================================================ launch wrappers
+#include "launch.hpp"
+
+namespace gpar {
+
+#define GPAR_DISPATCH_D(D, ...)                                   \
+  switch (D) {                                                    \
+    case 1: { constexpr int DD = 1; __VA_ARGS__; } break;         \
+    case 2: { constexpr int DD = 2; __VA_ARGS__; } break;         \
+    default: { constexpr int DD = 3; __VA_ARGS__; } break;        \
+  }
+
+void launch_gains(hipStream_t st, int sdim, const double* t, int64_t n, int L, int64_t nch,
+                  int nchains, const ChainParamsHost* cps_dev, const double* noise,
+                  double* agg, double* pstart, double* rec, double* g, double* phi,
+                  double* logs, double* pf) {
+  const ChainParams* cps = reinterpret_cast<const ChainParams*>(cps_dev);
+  dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, {
+    gains_phase1<DD><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, agg);
+    gains_phase2<DD><<<nchains, 256, 0, st>>>(nch, agg, pstart);
+    gains_phase3<DD><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, pstart, rec, g, phi, logs, pf);
+  });
+}
+
+template <int TK, int OK>
+static void launch_whiten_kfu_k(hipStream_t st, int dp, dim3 grid, const double* rec,
+                                const double* v, int64_t ldv, int d, const double* z,
+                                int64_t ldz, int64_t m, int64_t mp, int64_t n, int L,
+                                double inv_lo, double s_o, double* beta, int64_t ldb,
+                                double* send, int64_t mc) {
+  switch (dp) {
+    case 4: whiten_kfu<TK, OK, 4><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case 8: whiten_kfu<TK, OK, 8><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case 16: whiten_kfu<TK, OK, 16><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case 32: whiten_kfu<TK, OK, 32><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    default: whiten_kfu<TK, OK, 64><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+  }
+}
+
+template <int TK>
+static void launch_whiten_kfu_t(hipStream_t st, int ok, int dp, dim3 grid, const double* rec,
+                                const double* v, int64_t ldv, int d, const double* z,
+                                int64_t ldz, int64_t m, int64_t mp, int64_t n, int L,
+                                double inv_lo, double s_o, double* beta, int64_t ldb,
+                                double* send, int64_t mc) {
+  switch (ok) {
+    case KM12: launch_whiten_kfu_k<TK, KM12>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case KM32: launch_whiten_kfu_k<TK, KM32>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case KM52: launch_whiten_kfu_k<TK, KM52>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    default: launch_whiten_kfu_k<TK, KEQ>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+  }
+}
+
+int dp_bucket(int d) {
+  if (d <= 4) return 4;
+  if (d <= 8) return 8;
+  if (d <= 16) return 16;
+  if (d <= 32) return 32;
+  if (d <= 64) return 64;
+  return -1;
+}
+
+void launch_whiten_kfu(hipStream_t st, int time_kind, int out_kind, const double* rec,
+                       const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
+                       int64_t m, int64_t mp, int64_t n, int L, int64_t nch, double inv_lo,
+                       double s_o, double* beta, int64_t ldb, double* send, int64_t mc) {
+  dim3 grid((unsigned)nch, (unsigned)((mp + 255) / 256));
+  const int dp = dp_bucket(d);
+  switch (time_kind) {
+    case KM12: launch_whiten_kfu_t<KM12>(st, out_kind, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case KM32: launch_whiten_kfu_t<KM32>(st, out_kind, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    default: launch_whiten_kfu_t<KM52>(st, out_kind, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+  }
+}
+
+void launch_whiten_vec(hipStream_t st, int sdim, const double* rec, int64_t recstride,
+                       const double* y, int64_t ldy, int64_t n, int L, int64_t nch, int nchains,
+                       double* alpha, int64_t lda, double* send, int64_t sendstride, int64_t mc,
+                       int64_t col) {
+  dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, whiten_vec<DD><<<grid, 256, 0, st>>>(rec, recstride, y, ldy, n, L, nch, alpha, lda, send, sendstride, mc, col));
+}
+
+void launch_carry(hipStream_t st, int sdim, const double* phi, int64_t phistride,
+                  const double* send, double* cin, int64_t sstride, int64_t nch, int64_t mc,
+                  int64_t ncols, int nchains) {
+  dim3 grid((unsigned)((ncols + 255) / 256), (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, carry_kernel<DD><<<grid, 256, 0, st>>>(phi, phistride, send, cin, sstride, nch, mc, ncols));
+}
+
+int64_t vec_fix_blocks(int64_t n) { return (n + 255) / 256; }
+
+void launch_vec_fix(hipStream_t st, int sdim, double* alpha, int64_t lda, const double* g,
+                    int64_t gstride, const double* cin, int64_t sstride, int64_t mc,
+                    int64_t col, int64_t n, int L, int nchains, double* part) {
+  dim3 grid((unsigned)vec_fix_blocks(n), (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, vec_fix<DD><<<grid, 256, 0, st>>>(alpha, lda, g, gstride, cin, sstride, mc, col, n, L, part));
+}
+
+void launch_chain_lml(hipStream_t st, const double* logs, int64_t nch, const double* a2part,
+                      int64_t npart, int64_t n, int nchains, double* lml) {
+  chain_lml<<<nchains, 256, 0, st>>>(logs, nch, a2part, npart, n, lml);
+}
+
+}  // namespace gpar

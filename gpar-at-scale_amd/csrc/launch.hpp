@@ -1,0 +1,111 @@
+// launch.hpp -- host-callable launch wrappers of the gfx950 kernels (one per .hip file).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace gpar {
+
+// Mirrors of the device job structs (identical layout).
+struct ChainParamsHost {
+  double inv_l, l, s, r;
+};
+struct KuuJobHost {
+  const double* z;
+  int64_t ldz;
+  int d;
+  int kind;
+  double inv_l, s, diag_add;
+  double* K;
+  int64_t ldk;
+  int m;
+};
+struct CholJobHost {
+  double* A;
+  int64_t ld;
+  int m;
+  double diag_add;
+  int* status;
+};
+struct TrsmJobHost {
+  const double* L;
+  int64_t ldl;
+  const double* B;
+  int64_t ldb;
+  double* X;
+  int64_t ldx;
+  int m;
+  int64_t ncols;
+  int transB;
+  int transX;
+};
+struct FinishJobHost {
+  const double* Lu;
+  const double* Llam;
+  int64_t ld;
+  int m;
+  const double* r;
+  const double* logs;
+  int64_t nch;
+  const double* a2part;
+  int64_t npart;
+  int64_t n;
+  const int* status;
+  double* out;
+  double* me;
+};
+
+struct GramPlan {
+  int ntb = 0, ntiles = 0, nsplit = 0;
+  int64_t rows_per_split = 0;
+};
+
+constexpr int kGramTile = 128;
+constexpr int kRecStride3 = 16;
+
+inline int rec_size(int sdim) { return sdim == 3 ? 16 : (sdim == 2 ? 8 : 4); }
+
+// k_lgssm.hip
+void launch_gains(hipStream_t st, int sdim, const double* t, int64_t n, int L, int64_t nch,
+                  int nchains, const ChainParamsHost* cps_dev, const double* noise,
+                  double* agg, double* pstart, double* rec, double* g, double* phi,
+                  double* logs, double* pf);
+int dp_bucket(int d);
+void launch_whiten_kfu(hipStream_t st, int time_kind, int out_kind, const double* rec,
+                       const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
+                       int64_t m, int64_t mp, int64_t n, int L, int64_t nch, double inv_lo,
+                       double s_o, double* beta, int64_t ldb, double* send, int64_t mc);
+void launch_whiten_vec(hipStream_t st, int sdim, const double* rec, int64_t recstride,
+                       const double* y, int64_t ldy, int64_t n, int L, int64_t nch, int nchains,
+                       double* alpha, int64_t lda, double* send, int64_t sendstride, int64_t mc,
+                       int64_t col);
+void launch_carry(hipStream_t st, int sdim, const double* phi, int64_t phistride,
+                  const double* send, double* cin, int64_t sstride, int64_t nch, int64_t mc,
+                  int64_t ncols, int nchains);
+int64_t vec_fix_blocks(int64_t n);
+void launch_vec_fix(hipStream_t st, int sdim, double* alpha, int64_t lda, const double* g,
+                    int64_t gstride, const double* cin, int64_t sstride, int64_t mc,
+                    int64_t col, int64_t n, int L, int nchains, double* part);
+void launch_chain_lml(hipStream_t st, const double* logs, int64_t nch, const double* a2part,
+                      int64_t npart, int64_t n, int nchains, double* lml);
+
+// k_gram.hip
+GramPlan gram_plan(int64_t n, int64_t mp);
+void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* beta,
+                 int64_t ldb, int64_t n, const double* g, const double* cin, int64_t mc, int L,
+                 const double* alpha, double* part, double* rpart, double* G, int64_t ldg,
+                 double* r);
+void launch_beta_fix(hipStream_t st, int sdim, double* beta, int64_t ldb, int64_t n,
+                     const double* g, const double* cin, int64_t mc, int L);
+
+// k_dense.hip
+void launch_kuu(hipStream_t st, const KuuJobHost* jobs_dev, int njobs, int mmax);
+void launch_chol(hipStream_t st, const CholJobHost* jobs_dev, int njobs);
+void launch_trsm(hipStream_t st, const TrsmJobHost* jobs_dev, int njobs, int64_t ncols_max);
+void launch_finish(hipStream_t st, const FinishJobHost* jobs_dev, int njobs);
+void launch_gram_small(hipStream_t st, const double* X, int64_t ldx, int m, double* C,
+                       int64_t ldc);
+void launch_lower_to_upper_colmajor(hipStream_t st, const double* L, int64_t ldl, int m,
+                                    double* U);
+void launch_eye(hipStream_t st, double* A, int64_t ld, int m);
+
+}  // namespace gpar

@@ -1,0 +1,164 @@
+"""ctypes binding of include/gpar_hip.h (libgparhip.so, built in-tree for gfx950).
+
+The product path: every numeric result comes from the gfx950 kernels behind this C-ABI.
+If the shared library is missing or no GPU is visible, calls raise -- there is no CPU
+fallback.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "libgparhip.so"))
+
+GPAR_OK, GPAR_ERR_ARG, GPAR_ERR_NOT_PD, GPAR_ERR_HIP, GPAR_ERR_OOM, GPAR_ERR_UNSUPPORTED, GPAR_ERR_STATE = range(7)
+GPAR_MEM_HOST, GPAR_MEM_DEVICE = 0, 1
+GPAR_PREDICT_ANALYTIC, GPAR_PREDICT_MC = 0, 1
+KERNEL_ID = {"matern12": 0, "matern32": 1, "matern52": 2, "eq": 3}
+
+# Every entry point include/gpar_hip.h declares (tests check the library exports them all).
+EXPORTED = (
+    "gpar_abi_version", "gpar_ctx_create", "gpar_ctx_destroy", "gpar_last_error",
+    "gpar_ctx_workspace_bytes", "gpar_ctx_trim", "gpar_dtc_objective", "gpar_dtc_objective_A",
+    "gpar_fit", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
+    "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
+)
+
+
+class GparError(RuntimeError):
+    """Generic failure of the native library (HIP error, OOM, ...)."""
+
+    def __init__(self, code, msg):
+        super().__init__(f"[gpar status {code}] {msg}")
+        self.code = code
+
+
+class PosDefException(GparError):
+    """Mirrors Julia's LinearAlgebra.PosDefException thrown by `cholesky`
+    (dtc.jl:119-120, gpar_scaled_inference.jl:159,188)."""
+
+
+class DomainError(GparError, ValueError):
+    """Mirrors Julia's DomainError / ArgumentError on malformed inputs (util.jl:127-133)."""
+
+
+class Unsupported(GparError):
+    pass
+
+
+class GparProblem(C.Structure):
+    _fields_ = [
+        ("n", C.c_int64), ("m", C.c_int64), ("d", C.c_int64),
+        ("t", C.c_void_p), ("v", C.c_void_p), ("ldv", C.c_int64),
+        ("z", C.c_void_p), ("ldz", C.c_int64), ("y", C.c_void_p),
+        ("out_kernel", C.c_int32), ("time_kernel", C.c_int32), ("kuu_noise", C.c_int32),
+        ("mem", C.c_int32),
+    ]
+
+
+class GparFitOptions(C.Structure):
+    _fields_ = [("max_evals", C.c_int32), ("max_iterations", C.c_int32),
+                ("g_tol", C.c_double), ("time_limit", C.c_double)]
+
+
+_lib = None
+_lock = threading.Lock()
+
+
+def load(path: str | None = None):
+    """Load libgparhip.so (raises OSError if it has not been built)."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        p = path or os.environ.get("GPAR_HIP_LIB", LIB_PATH)
+        if not os.path.exists(p):
+            raise OSError(f"libgparhip.so not found at {p}: run `make -C gpar-at-scale_amd` "
+                          "(or __graft_entry__.build())")
+        lib = C.CDLL(p)
+        vp, i32, i64, dp = C.c_void_p, C.c_int32, C.c_int64, C.c_void_p
+        sig = {
+            "gpar_abi_version": (i32, []),
+            "gpar_ctx_create": (i32, [i32, C.POINTER(vp)]),
+            "gpar_ctx_destroy": (i32, [vp]),
+            "gpar_last_error": (C.c_char_p, [vp]),
+            "gpar_ctx_workspace_bytes": (i64, [vp]),
+            "gpar_ctx_trim": (i32, [vp]),
+            "gpar_dtc_objective": (i32, [vp, C.POINTER(GparProblem), i32, dp, dp]),
+            "gpar_dtc_objective_A": (i32, [vp, C.POINTER(GparProblem), dp, dp, dp]),
+            "gpar_fit": (i32, [vp, C.POINTER(GparProblem), i32, dp, C.POINTER(GparFitOptions),
+                               dp, dp, dp]),
+            "gpar_q_u": (i32, [vp, C.POINTER(GparProblem), dp, dp, dp, dp]),
+            "gpar_predict": (i32, [vp, C.POINTER(GparProblem), dp, i64, dp, dp, i64, i32, i32,
+                                   C.c_uint64, dp, dp]),
+            "gpar_lgssm_logpdf": (i32, [vp, i32, i64, dp, dp, i64, i32, dp, i32, dp]),
+            "gpar_lgssm_smooth": (i32, [vp, i32, i64, dp, dp, i64, dp, i32, dp, i32, dp, dp]),
+            "gpar_sde_predictions": (i32, [vp, i32, i64, dp, dp, i64, i64, dp, i32, dp,
+                                           C.POINTER(GparFitOptions), i32, dp, dp, dp]),
+            "gpar_exact_logpdf": (i32, [vp, i64, i64, dp, i64, dp, i32, i32, dp, i32, dp]),
+            "gpar_exact_posterior": (i32, [vp, i64, i64, dp, i64, dp, i64, dp, i64, i32, i32,
+                                           dp, i32, dp, dp]),
+        }
+        for name, (res, args) in sig.items():
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = lib
+        return lib
+
+
+def raise_for(ctx, code):
+    if code == GPAR_OK:
+        return
+    msg = load().gpar_last_error(ctx)
+    msg = msg.decode() if msg else ""
+    if code == GPAR_ERR_NOT_PD:
+        raise PosDefException(code, msg)
+    if code == GPAR_ERR_ARG:
+        raise DomainError(code, msg)
+    if code == GPAR_ERR_UNSUPPORTED:
+        raise Unsupported(code, msg)
+    raise GparError(code, msg)
+
+
+class Context:
+    """One gpar_ctx (one GPU, one host thread)."""
+
+    def __init__(self, device: int = 0):
+        lib = load()
+        h = C.c_void_p()
+        code = lib.gpar_ctx_create(device, C.byref(h))
+        if code != GPAR_OK:
+            raise GparError(code, f"gpar_ctx_create(device={device}) failed (no GPU visible?)")
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if self.h:
+            load().gpar_ctx_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def check(self, code):
+        raise_for(self.h, code)
+
+    def workspace_bytes(self):
+        return int(load().gpar_ctx_workspace_bytes(self.h))
+
+
+_ctx: dict[int, Context] = {}
+
+
+def context(device: int = 0) -> Context:
+    c = _ctx.get(device)
+    if c is None:
+        c = Context(device)
+        _ctx[device] = c
+    return c

@@ -1,0 +1,279 @@
+"""Python mirror of the reference's Julia API for the hot path (same names, argument
+meaning and error behaviour), on top of the C-ABI in include/gpar_hip.h.
+
+Reference functions mirrored (TudorParas/GPAR-at-scale):
+  compute_gpar_dtc_objective     src/gp/dtc.jl:83-128
+  get_optim_scaled_gpar_params   src/gp/dtc.jl:11-77
+  compute_q_u                    src/gp/gpar_scaled_inference.jl:141-196
+  get_gpar_scaled_predictions    src/gp/gpar_scaled_inference.jl:20-136
+  create_lgssm / logpdf          src/gp/temporal_gp_inference.jl:15-39, :286-296
+  get_sde_predictions            src/gp/temporal_gp_inference.jl:45-114
+  create_optim_gp[_post] / create_optim_gpar[_post] logpdf / marginals  src/gp/optimized.jl
+
+Inputs follow the reference's conventions: V / Z are ColVecs-like D x N matrices (or a list of
+D length-N vectors, util.jl:16-31); theta in natural units (unpack_gpar, util.jl:61-71);
+initial values are log-params (i_log_*), missing ones drawn U(0,1) like util.jl:144-150.
+Host numpy arrays go through GPAR_MEM_HOST; torch CUDA tensors (rows = points) through
+GPAR_MEM_DEVICE without host copies.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import GparFitOptions, GparProblem, KERNEL_ID, context
+
+DEFAULT_TIME_LIMIT = 1000.0  # dtc.jl:21
+
+
+# ----------------------------------------------------------------------------- util.jl
+def unpack_gp(params):
+    """util.jl:52-59."""
+    return tuple(float(np.exp(p) + 1e-3) for p in list(params)[:3])
+
+
+def unpack_gpar(params):
+    """util.jl:61-71."""
+    return tuple(float(np.exp(p) + 1e-3) for p in list(params)[:5])
+
+
+def get_time_mask(input_length):
+    """util.jl:118-122."""
+    m = np.zeros(input_length)
+    m[0] = 1.0
+    return m
+
+
+def get_output_mask(input_length):
+    """util.jl:127-139; DomainError for input_length <= 1."""
+    if input_length <= 1:
+        raise _lib.DomainError(_lib.GPAR_ERR_ARG, "Input length must be integer greater than 1")
+    m = np.zeros((input_length - 1, input_length))
+    for r in range(input_length - 1):
+        m[r, r + 1] = 1.0
+    return m
+
+
+def parse_initial_params(vals, rng=None):
+    """util.jl:144-185: missing initial log-params are U(0,1) draws."""
+    rng = rng if rng is not None else np.random.default_rng()
+    return np.array([rng.random() if v is None else float(v) for v in vals], dtype=np.float64)
+
+
+def to_colvecs(inputs):
+    """util.jl:32-47: list of per-dimension vectors -> D x N."""
+    if _is_torch(inputs):
+        return inputs
+    if isinstance(inputs, np.ndarray):
+        return np.atleast_2d(np.asarray(inputs, dtype=np.float64))
+    return np.vstack([np.asarray(a, dtype=np.float64) for a in inputs])
+
+
+# ----------------------------------------------------------------------------- marshalling
+def _is_torch(x):
+    return type(x).__module__.startswith("torch")
+
+
+def _kernel_id(k):
+    if isinstance(k, int):
+        return k
+    return KERNEL_ID[str(k).lower()]
+
+
+class _Keep(list):
+    pass
+
+
+def _host_vec(x, keep):
+    a = np.ascontiguousarray(np.asarray(x, dtype=np.float64).ravel())
+    keep.append(a)
+    return a.ctypes.data
+
+
+def _host_points(X, keep):
+    """D x N (ColVecs) -> point-major N x D contiguous; returns (ptr, ld, n, d)."""
+    X = to_colvecs(X)
+    P = np.ascontiguousarray(X.T)
+    keep.append(P)
+    return P.ctypes.data, P.shape[1], P.shape[0], P.shape[1]
+
+
+def _dev_points(X, keep):
+    """torch CUDA tensor with rows = points (N x D, unit column stride)."""
+    if X.dim() == 1:
+        X = X.reshape(-1, 1)
+    assert X.dtype.is_floating_point and X.element_size() == 8, "float64 tensors required"
+    if X.stride(1) != 1:
+        X = X.contiguous()
+    keep.append(X)
+    return X.data_ptr(), X.stride(0), X.shape[0], X.shape[1]
+
+
+def _dev_vec(x, keep):
+    x = x.contiguous()
+    keep.append(x)
+    return x.data_ptr()
+
+
+def make_problem(V, Z, t, y, out_kernel="matern52", time_kernel="matern52", kuu_noise=True,
+                 keep=None):
+    """Build a gpar_problem.  Host: V, Z as D x N / D x M (ColVecs).  Device: torch tensors
+    with rows = points (N x D, M x D)."""
+    keep = keep if keep is not None else _Keep()
+    p = GparProblem()
+    dev = _is_torch(t)
+    if dev:
+        p.v, p.ldv, n, d = _dev_points(V, keep)
+        p.z, p.ldz, m, dz = _dev_points(Z, keep)
+        p.t = _dev_vec(t, keep)
+        p.y = _dev_vec(y, keep)
+        p.mem = _lib.GPAR_MEM_DEVICE
+    else:
+        p.v, p.ldv, n, d = _host_points(V, keep)
+        p.z, p.ldz, m, dz = _host_points(Z, keep)
+        p.t = _host_vec(t, keep)
+        p.y = _host_vec(y, keep)
+        p.mem = _lib.GPAR_MEM_HOST
+        if len(np.asarray(t)) != n or len(np.asarray(y)) != n:
+            raise _lib.DomainError(_lib.GPAR_ERR_ARG, "t, y and V must have the same length")
+    if d != dz:
+        raise _lib.DomainError(_lib.GPAR_ERR_ARG, "V and Z must have the same dimension")
+    p.n, p.m, p.d = n, m, d
+    p.out_kernel = _kernel_id(out_kernel)
+    p.time_kernel = _kernel_id(time_kernel)
+    p.kuu_noise = 1 if kuu_noise else 0
+    return p, keep
+
+
+def _ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+# ----------------------------------------------------------------------------- DTC objective
+def compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel="matern52", time_kernel="matern52",
+                               kuu_noise=True, return_A=False, device=0):
+    """dtc.jl:83-128.  theta = (time_l, time_var, out_l, out_var, noise_sigma), natural units.
+
+    Returns the DTC log marginal likelihood; with return_A=True returns (dtc, A) like the
+    reference (A = chol(cov(u)).U' \\ beta', M x N)."""
+    ctx = context(device)
+    lib = _lib.load()
+    p, keep = make_problem(V, Z, t, y, out_kernel, time_kernel, kuu_noise)
+    th = np.ascontiguousarray(np.asarray(theta, dtype=np.float64).reshape(5))
+    out = np.zeros(1)
+    if return_A:
+        A = np.zeros((p.n, p.m))  # column-major M x N == row-major N x M
+        ctx.check(lib.gpar_dtc_objective_A(ctx.h, C.byref(p), _ptr(th), _ptr(out), _ptr(A)))
+        return float(out[0]), A.T.copy()
+    ctx.check(lib.gpar_dtc_objective(ctx.h, C.byref(p), 1, _ptr(th), _ptr(out)))
+    return float(out[0])
+
+
+def dtc_objective_batch(problems, thetas, device=0):
+    """Batched objective over independent outputs (one GPU round)."""
+    ctx = context(device)
+    lib = _lib.load()
+    arr = (GparProblem * len(problems))(*problems)
+    th = np.ascontiguousarray(np.asarray(thetas, dtype=np.float64).reshape(len(problems), 5))
+    out = np.zeros(len(problems))
+    ctx.check(lib.gpar_dtc_objective(ctx.h, arr, len(problems), _ptr(th), _ptr(out)))
+    return out
+
+
+# ----------------------------------------------------------------------------- fit
+@dataclass
+class FitResult:
+    theta: np.ndarray      # P x 5 natural units
+    nlml: np.ndarray       # P
+    evals: np.ndarray      # P
+
+
+def fit_batch(problems, log_theta0, max_evals=0, max_iterations=1000, g_tol=1e-8,
+              time_limit=0.0, device=0):
+    """Batched NelderMead over outputs (gpar_fit)."""
+    ctx = context(device)
+    lib = _lib.load()
+    P = len(problems)
+    arr = (GparProblem * P)(*problems)
+    x0 = np.ascontiguousarray(np.asarray(log_theta0, dtype=np.float64).reshape(P, 5))
+    opts = GparFitOptions(int(max_evals), int(max_iterations), float(g_tol), float(time_limit))
+    theta = np.zeros((P, 5))
+    nlml = np.zeros(P)
+    evals = np.zeros(P, dtype=np.int32)
+    ctx.check(lib.gpar_fit(ctx.h, arr, P, _ptr(x0), C.byref(opts), _ptr(theta), _ptr(nlml),
+                           _ptr(evals)))
+    return FitResult(theta, nlml, evals)
+
+
+def get_optim_scaled_gpar_params(input_locations, pseudo_input_locations, time_loc, outputs,
+                                 out_kernel="matern52", time_kernel="matern52",
+                                 i_log_time_l=None, i_log_time_var=None, i_log_out_l=None,
+                                 i_log_out_var=None, i_log_noise_sigma=None,
+                                 optimization_time_limit=DEFAULT_TIME_LIMIT, max_evals=0,
+                                 g_tol=1e-8, rng=None, device=0):
+    """dtc.jl:11-77: returns the optimised (time_l, time_var, out_l, out_var, noise_sigma)."""
+    p, keep = make_problem(input_locations, pseudo_input_locations, time_loc, outputs,
+                           out_kernel, time_kernel)
+    x0 = parse_initial_params([i_log_time_l, i_log_time_var, i_log_out_l, i_log_out_var,
+                               i_log_noise_sigma], rng)
+    r = fit_batch([p], x0[None, :], max_evals=max_evals, g_tol=g_tol,
+                  time_limit=optimization_time_limit or 0.0, device=device)
+    return tuple(float(v) for v in r.theta[0])
+
+
+# ----------------------------------------------------------------------------- q(u)
+def compute_q_u(input_locations, pseudo_input_locations, time_loc, outputs, theta,
+                out_kernel="matern52", time_kernel="matern52", device=0):
+    """gpar_scaled_inference.jl:141-196 -> (m_e, cov_e = inv(D), U_u upper)."""
+    ctx = context(device)
+    lib = _lib.load()
+    p, keep = make_problem(input_locations, pseudo_input_locations, time_loc, outputs,
+                           out_kernel, time_kernel)
+    th = np.ascontiguousarray(np.asarray(theta, dtype=np.float64).reshape(5))
+    m = p.m
+    me = np.zeros(m)
+    cov = np.zeros((m, m))
+    U = np.zeros((m, m))  # column-major -> read as transposed
+    ctx.check(lib.gpar_q_u(ctx.h, C.byref(p), _ptr(th), _ptr(me), _ptr(cov), _ptr(U)))
+    return me, cov, U.T.copy()
+
+
+# ----------------------------------------------------------------------------- temporal-only
+@dataclass
+class LGSSMSpec:
+    """create_lgssm(t, l, process_var, noise_sigma, k) (temporal_gp_inference.jl:15-39)."""
+    t: np.ndarray
+    l: float
+    process_var: float
+    noise_sigma: float
+    kernel: str = "matern52"
+
+
+def create_lgssm(latent_locations, l, process_var, noise_sigma, kernel_structure="matern52"):
+    return LGSSMSpec(np.asarray(latent_locations, dtype=np.float64), float(l), float(process_var),
+                     float(noise_sigma), kernel_structure)
+
+
+def logpdf(lgssm: LGSSMSpec, y, device=0):
+    """logpdf(lgssm, y) (temporal_gp_inference.jl:295)."""
+    return float(lgssm_logpdf_batch(lgssm.t, np.asarray(y, dtype=np.float64)[None, :],
+                                    [[lgssm.l, lgssm.process_var, lgssm.noise_sigma]],
+                                    lgssm.kernel, device)[0])
+
+
+def lgssm_logpdf_batch(t, Y, theta, kernel="matern52", device=0):
+    """Chains sharing t: Y is nchains x n; theta nchains x 3 natural (l, pv, sigma)."""
+    ctx = context(device)
+    lib = _lib.load()
+    keep = _Keep()
+    Y = np.ascontiguousarray(np.asarray(Y, dtype=np.float64))
+    nch, n = Y.shape
+    th = np.ascontiguousarray(np.asarray(theta, dtype=np.float64).reshape(nch, 3))
+    tp = _host_vec(t, keep)
+    out = np.zeros(nch)
+    ctx.check(lib.gpar_lgssm_logpdf(ctx.h, nch, n, tp, _ptr(Y), n, _kernel_id(kernel), _ptr(th),
+                                    _lib.GPAR_MEM_HOST, _ptr(out)))
+    return out

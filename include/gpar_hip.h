@@ -1,0 +1,190 @@
+/*
+ * gpar_hip.h -- C-ABI of the MI355X-native GPAR-at-scale hot path.
+ *
+ * The reference (TudorParas/GPAR-at-scale) is a Julia package whose hot path is a set
+ * of plain Julia functions.  Each entry point below replaces one of them; the Julia
+ * `ccall` binding a maintainer would add is in INTEGRATION.md, the Python ctypes
+ * mirror is gpar-at-scale_amd/python/gparatscale/.
+ *
+ * Conventions
+ *   - return value: gpar_status (0 = OK); gpar_last_error(ctx) describes the failure.
+ *     GPAR_ERR_NOT_PD mirrors Julia's PosDefException thrown by `cholesky`
+ *     (dtc.jl:119-120, gpar_scaled_inference.jl:159,188); GPAR_ERR_ARG mirrors the
+ *     DomainError of util.jl:127-133 and malformed inputs.
+ *   - fp64 only.  Sizes are int64_t.  Calls are synchronous on return.
+ *   - Pointers are borrowed: read-only inputs, never retained past return.  Inputs live
+ *     in host memory (mem = GPAR_MEM_HOST) or are already resident in device HBM
+ *     (mem = GPAR_MEM_DEVICE, e.g. torch tensors' data_ptr()).  Outputs follow the same
+ *     `mem` as the inputs of the call unless stated otherwise.
+ *   - Inputs V (one point = one column of the reference's ColVecs, util.jl:16-31): point k,
+ *     dimension i lives at v[k*ldv + i]; ldv >= d lets V be a view into an N x P
+ *     row-major output matrix (GPAR's previous outputs).
+ *   - theta in natural units, as returned by unpack_gpar (util.jl:61-71):
+ *     (time_l, time_var, out_l, out_var, noise_sigma); kernel variances are the squares
+ *     (dtc.jl:31,37).  log_theta = the reference's i_log_* initial values.
+ *   - One gpar_ctx per GPU, one host thread per ctx (not thread-safe).
+ */
+#ifndef GPAR_HIP_H
+#define GPAR_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define GPAR_ABI_VERSION 1
+
+typedef enum gpar_status {
+  GPAR_OK = 0,
+  GPAR_ERR_ARG = 1,         /* invalid argument (DomainError / malformed input)        */
+  GPAR_ERR_NOT_PD = 2,      /* Cholesky of a non positive-definite matrix              */
+  GPAR_ERR_HIP = 3,         /* HIP runtime failure                                     */
+  GPAR_ERR_OOM = 4,         /* device allocation failed                                */
+  GPAR_ERR_UNSUPPORTED = 5, /* configuration outside what the kernels implement        */
+  GPAR_ERR_STATE = 6        /* context misuse (NULL ctx, ...)                          */
+} gpar_status;
+
+typedef enum gpar_kernel {
+  GPAR_MATERN12 = 0, /* Stheno Matern12() */
+  GPAR_MATERN32 = 1, /* Stheno Matern32() */
+  GPAR_MATERN52 = 2, /* Stheno Matern52() (the reference's default everywhere) */
+  GPAR_EQ = 3        /* Stheno EQ(): output kernel only (no finite state-space form) */
+} gpar_kernel;
+
+typedef enum gpar_mem { GPAR_MEM_HOST = 0, GPAR_MEM_DEVICE = 1 } gpar_mem;
+
+typedef enum gpar_predict_mode {
+  GPAR_PREDICT_ANALYTIC = 0, /* exact S -> infinity limit of the reference's MC estimator */
+  GPAR_PREDICT_MC = 1        /* reference-faithful Monte Carlo (gpar_scaled_inference.jl:110-130) */
+} gpar_predict_mode;
+
+typedef struct gpar_ctx gpar_ctx;
+
+/* One scaled-GPAR output: the arguments of compute_gpar_dtc_objective / get_optim_scaled_gpar_params
+ * (dtc.jl:11-25, 83-91) with the FiniteGPs f = GP(k_o)(V, sigma^2), u = GP(k_o)(Z, sigma^2) unfolded. */
+typedef struct gpar_problem {
+  int64_t n;            /* training points N                                           */
+  int64_t m;            /* pseudo-points M                                             */
+  int64_t d;            /* input dimension D = number of previous outputs (>= 1)       */
+  const double* t;      /* [n] time locations, ascending (dtc.jl:102 does not sort)    */
+  const double* v;      /* inputs,        point k dim i at v[k*ldv + i]                */
+  int64_t ldv;          /* >= d                                                        */
+  const double* z;      /* pseudo-inputs, point j dim i at z[j*ldz + i]                */
+  int64_t ldz;          /* >= d                                                        */
+  const double* y;      /* [n] targets                                                 */
+  int32_t out_kernel;   /* gpar_kernel of f_x (dtc.jl:16)                              */
+  int32_t time_kernel;  /* GPAR_MATERN12/32/52 of f_t (dtc.jl:17)                      */
+  int32_t kuu_noise;    /* 1: Kuu + sigma^2 I as FiniteGP cov(u) (dtc.jl:35,119)       */
+  int32_t mem;          /* gpar_mem of t, v, z, y                                      */
+} gpar_problem;
+
+typedef struct gpar_fit_options {
+  int32_t max_evals;      /* >0: objective evaluations per output incl. the final centroid
+                             evaluation (the build's reproducible budget); 0 = unlimited   */
+  int32_t max_iterations; /* Optim.Options iterations (default 1000)                      */
+  double g_tol;           /* Optim NelderMead convergence tolerance (default 1e-8; <0 off)  */
+  double time_limit;      /* seconds of wall clock (dtc.jl:21 optimization_time_limit);
+                             <=0 = none                                                    */
+} gpar_fit_options;
+
+/* ---------------------------------------------------------------- context */
+int32_t gpar_abi_version(void);
+int32_t gpar_ctx_create(int32_t device, gpar_ctx** out);
+int32_t gpar_ctx_destroy(gpar_ctx* ctx);
+const char* gpar_last_error(const gpar_ctx* ctx);
+/* bytes of device workspace currently held by the context */
+int64_t gpar_ctx_workspace_bytes(const gpar_ctx* ctx);
+/* release cached device workspace */
+int32_t gpar_ctx_trim(gpar_ctx* ctx);
+
+/* ---------------------------------------------------------------- DTC objective
+ * Replaces compute_gpar_dtc_objective (src/gp/dtc.jl:83-128), batched over `nprob`
+ * independent outputs.  theta: nprob x 5 (natural units, row per output), host memory.
+ * dtc_out: [nprob] log marginal likelihood (DTC), host memory. */
+int32_t gpar_dtc_objective(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                           const double* theta, double* dtc_out);
+
+/* Same, for one output, also returning the reference's second tuple element
+ * A = chol(cov(u)).U' \ beta'  (M x N, column-major: A[i + j*m]), host memory.
+ * Materialises A: intended for parity checks at modest N*M. */
+int32_t gpar_dtc_objective_A(gpar_ctx* ctx, const gpar_problem* prob, const double* theta,
+                             double* dtc_out, double* A_out);
+
+/* ---------------------------------------------------------------- fit
+ * Replaces get_optim_scaled_gpar_params (src/gp/dtc.jl:11-77): Nelder-Mead over the 5
+ * log-hyperparameters maximising the DTC objective, batched over nprob outputs (one GPU
+ * evaluation round serves every output's pending simplex point).
+ * log_theta0: nprob x 5 initial log-params (host).  theta_out: nprob x 5 natural units
+ * (host).  nlml_out: [nprob] final -dtc (host, may be NULL).  evals_out: [nprob] (may be NULL). */
+int32_t gpar_fit(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                 const double* log_theta0, const gpar_fit_options* opts,
+                 double* theta_out, double* nlml_out, int32_t* evals_out);
+
+/* ---------------------------------------------------------------- q(u)
+ * Replaces compute_q_u (src/gp/gpar_scaled_inference.jl:141-196) at theta (natural units).
+ * Cuu carries NO noise here (:157); prob->kuu_noise is ignored.  Outputs (host):
+ * m_e [m], cov [m x m] = inv(D) (Symmetric), U_u [m x m] upper Cholesky factor of Cuu;
+ * matrices column-major. */
+int32_t gpar_q_u(gpar_ctx* ctx, const gpar_problem* prob, const double* theta,
+                 double* m_e, double* cov, double* U_u);
+
+/* ---------------------------------------------------------------- prediction
+ * Replaces the prediction half of get_gpar_scaled_predictions
+ * (src/gp/gpar_scaled_inference.jl:63-135) at a fitted theta: q(u), merge train+test,
+ * Cf*u, LGSSM with R = sigma^2 (train) / 1e10 (test), RTS smoothing.
+ * t_star [n_star], v_star point k dim i at v_star[k*ldvs + i]; in prob->mem.
+ * mean/std [n_star] in prob->mem.  ANALYTIC: mean and std of the latent f (the MC
+ * estimator's S -> infinity limit); MC: `samples` draws with the given seed, mean and
+ * Bessel-corrected std over samples as the reference does. */
+int32_t gpar_predict(gpar_ctx* ctx, const gpar_problem* prob, const double* theta,
+                     int64_t n_star, const double* t_star, const double* v_star, int64_t ldvs,
+                     int32_t mode, int32_t samples, uint64_t seed, double* mean, double* std);
+
+/* ---------------------------------------------------------------- temporal-only (LGSSM) chains
+ * `nchains` independent chains sharing the time grid t [n] (ascending); chain c's
+ * observations at y[c*ldy + k].  theta: nchains x 3 natural (l, process_var, noise_sigma)
+ * (unpack_gp, util.jl:52-59), host.
+ *
+ * logpdf(create_lgssm(t, l, pv, sigma, k), y)  (temporal_gp_inference.jl:286-296):
+ * lml_out [nchains] host. */
+int32_t gpar_lgssm_logpdf(gpar_ctx* ctx, int32_t nchains, int64_t n, const double* t,
+                          const double* y, int64_t ldy, int32_t kernel, const double* theta,
+                          int32_t mem, double* lml_out);
+
+/* smooth(create_lgssm(...; noise_vector), y) marginals of f (temporal_gp_inference.jl:109,
+ * gpar_scaled_inference.jl:117): noise [n] per-step observation variance shared by all
+ * chains (NULL = noise_sigma^2 everywhere).  mean/var [nchains*ldy layout like y], in mem. */
+int32_t gpar_lgssm_smooth(gpar_ctx* ctx, int32_t nchains, int64_t n, const double* t,
+                          const double* y, int64_t ldy, const double* noise, int32_t kernel,
+                          const double* theta, int32_t mem, double* mean, double* var);
+
+/* get_sde_predictions (temporal_gp_inference.jl:45-114): NM fit of (l, pv, sigma) per chain
+ * on -logpdf, then smoothing over the merged train+test grid; marginals of f at t_star.
+ * log_theta0 nchains x 3 (host); theta_out nchains x 3 (host); mean/var: chain c at
+ * [c*n_star + k], in mem. */
+int32_t gpar_sde_predictions(gpar_ctx* ctx, int32_t nchains, int64_t n, const double* t,
+                             const double* y, int64_t ldy, int64_t n_star, const double* t_star,
+                             int32_t kernel, const double* log_theta0,
+                             const gpar_fit_options* opts, int32_t mem, double* theta_out,
+                             double* mean, double* var);
+
+/* ---------------------------------------------------------------- exact GP / GPAR (config 1)
+ * logpdf(f(x, sigma^2), y) with the GPAR kernel s_t k_t(x[0]/l_t) + s_o k_o(x[1:]/l_o)
+ * (optimized.jl:132-154); x point k dim i at x[k*ldx + i], dx = 1 + #previous outputs
+ * (dx == 1: plain GP on time, optimized.jl:28-36, theta = (l, pv, sigma, -, -) uses
+ * entries 0, 1 and 4).  theta: 5 natural (host).  lml_out host. */
+int32_t gpar_exact_logpdf(gpar_ctx* ctx, int64_t n, int64_t dx, const double* x, int64_t ldx,
+                          const double* y, int32_t time_kernel, int32_t out_kernel,
+                          const double* theta, int32_t mem, double* lml_out);
+
+/* Posterior marginals of f at x_star (optimized.jl:94,236 + marginals): mean/var [n_star]. */
+int32_t gpar_exact_posterior(gpar_ctx* ctx, int64_t n, int64_t dx, const double* x, int64_t ldx,
+                             const double* y, int64_t n_star, const double* x_star,
+                             int64_t ldxs, int32_t time_kernel, int32_t out_kernel,
+                             const double* theta, int32_t mem, double* mean, double* var);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPAR_HIP_H */
