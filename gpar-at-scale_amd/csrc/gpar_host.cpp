@@ -91,6 +91,19 @@ static int sde_dim(int kind) {
 
 static int64_t round_up(int64_t x, int64_t q) { return ((x + q - 1) / q) * q; }
 
+// Two-level carry over chunks (k_lgssm.hip launch_carry) with context workspace.
+static void run_carry(gpar_ctx* c, int sdim, const double* phi, int64_t phistride,
+                      const double* send, double* cin, int64_t sstride, int64_t nch, int64_t mc,
+                      int64_t ncols, int nchains, const std::string& tag, bool rev = false) {
+  const int gs = carry_group_size(nch);
+  const int64_t ng = (nch + gs - 1) / gs;
+  double* gend = ws<double>(c, tag + "_gend", (size_t)nchains * ng * mc * 4);
+  double* gin = ws<double>(c, tag + "_gin", (size_t)nchains * ng * mc * 4);
+  double* psi = ws<double>(c, tag + "_psi", (size_t)nchains * ng * sdim * sdim);
+  launch_carry(c->stream, sdim, phi, phistride, send, cin, sstride, nch, mc, ncols, nchains, gend,
+               gin, psi, rev);
+}
+
 // --------------------------------------------------------------------------- problems on device
 struct DevProblem {
   int64_t n, m, d, mp, mc, nch;
@@ -253,7 +266,7 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     launch_whiten_vec(c->stream, p.sdim, g.rec, 0, p.y, 0, n, kChunk, nch, 1, alpha, 0, send, 0,
                       p.mc, p.mp);
     check_launch("whiten_vec");
-    launch_carry(c->stream, p.sdim, g.phi, 0, send, cin, 0, nch, p.mc, p.mc, 1);
+    run_carry(c, p.sdim, g.phi, 0, send, cin, 0, nch, p.mc, p.mc, 1, "fitc");
     check_launch("carry");
     launch_vec_fix(c->stream, p.sdim, alpha, 0, g.g, 0, cin, 0, p.mc, p.mp, n, kChunk, 1,
                    o.a2part + (size_t)i * npart);
@@ -432,12 +445,146 @@ static void chains_logpdf(gpar_ctx* c, int nchains, int64_t n, const double* t, 
   double* dl = ws<double>(c, "chain_lml", nchains);
   launch_whiten_vec(c->stream, sdim, g.rec, g.recstride, y, ldy, n, kChunk, nch, nchains, alpha, n,
                     send, nch * 4, 1, 0);
-  launch_carry(c->stream, sdim, g.phi, g.phistride, send, cin, nch * 4, nch, 1, 1, nchains);
+  run_carry(c, sdim, g.phi, g.phistride, send, cin, nch * 4, nch, 1, 1, nchains, "chainc");
   launch_vec_fix(c->stream, sdim, alpha, n, g.g, g.gstride, cin, nch * 4, 1, 0, n, kChunk, nchains, a2);
   launch_chain_lml(c->stream, g.logs, nch, a2, npart, n, nchains, dl);
   check_launch("chains_logpdf");
   d2h(c, lml, dl, nchains);
   sync(c);
+}
+
+
+// --------------------------------------------------------------------------- prediction
+// Prediction half of get_gpar_scaled_predictions (gpar_scaled_inference.jl:63-135); see the
+// header of k_predict.hip for the algebra.
+static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
+                         int64_t n_star, const double* t_star_in, const double* v_star_in,
+                         int64_t ldvs, int mode, int samples, uint64_t seed, double* mean_out,
+                         double* std_out) {
+  const int64_t n = P.n, m = P.m, d = P.d, mp = P.mp, mc = P.mc;
+  // ---- test inputs on device, ascending (host inputs are stably sorted here, outputs
+  //      un-permuted at the end; device inputs must already be ascending)
+  std::vector<int64_t> perm;
+  const double* ts = t_star_in;
+  const double* vs = v_star_in;
+  int64_t ldv_s = ldvs;
+  if (mem == GPAR_MEM_HOST) {
+    perm.resize(n_star);
+    for (int64_t i = 0; i < n_star; ++i) perm[i] = i;
+    std::stable_sort(perm.begin(), perm.end(),
+                     [&](int64_t a, int64_t b) { return t_star_in[a] < t_star_in[b]; });
+    std::vector<double> tsh(n_star), vsh((size_t)n_star * d);
+    for (int64_t i = 0; i < n_star; ++i) {
+      tsh[i] = t_star_in[perm[i]];
+      for (int64_t q = 0; q < d; ++q) vsh[i * d + q] = v_star_in[perm[i] * ldvs + q];
+    }
+    double* dts = ws<double>(c, "pr_ts", n_star);
+    double* dvs = ws<double>(c, "pr_vs", (size_t)n_star * d);
+    h2d(c, dts, tsh.data(), n_star);
+    h2d(c, dvs, vsh.data(), (size_t)n_star * d);
+    sync(c);
+    ts = dts;
+    vs = dvs;
+    ldv_s = d;
+  }
+  // ---- q(u): m_e, L_u = chol(Cuu), L_D = chol(D)
+  QuOut q = run_q_u(c, P, th);
+  const double* Lu = ws<double>(c, "Kuu", 1);
+  const double* LD = ws<double>(c, "Lam", 1);
+  const int64_t ld = q.ld;
+  // w = L_u^{-T} m_e
+  double* w = ws<double>(c, "pr_w", m);
+  TrsvJobHost tv{Lu, ld, (int)m, q.me, w, 1};
+  auto* dtv = ws<TrsvJobHost>(c, "pr_trsv", 1);
+  h2d(c, dtv, &tv, 1);
+  launch_trsv(c->stream, dtv, 1);
+  // V = L_D^{-1} L_u^{-1}
+  double* I = ws<double>(c, "qu_eye", (size_t)ld * ld);
+  double* X1 = ws<double>(c, "pr_X1", (size_t)ld * ld);
+  double* Vm = ws<double>(c, "pr_V", (size_t)ld * ld);
+  launch_eye(c->stream, I, ld, (int)m);
+  TrsmJobHost tj[2] = {{Lu, ld, I, ld, X1, ld, (int)m, m, 0, 0}, {LD, ld, X1, ld, Vm, ld, (int)m, m, 0, 0}};
+  auto* dtj = ws<TrsmJobHost>(c, "pr_trsm", 2);
+  h2d(c, dtj, tj, 2);
+  launch_trsm(c->stream, dtj, 1, m);
+  launch_trsm(c->stream, dtj + 1, 1, m);
+  check_launch("predict: q(u) tail");
+  // ---- merged grid
+  const int64_t nt = n + n_star;
+  const int64_t nch = (nt + kChunk - 1) / kChunk;
+  double* tm = ws<double>(c, "pr_tm", nt);
+  double* ym = ws<double>(c, "pr_ym", nt);
+  double* rm = ws<double>(c, "pr_rm", nt);
+  double* vm = ws<double>(c, "pr_vm", (size_t)nt * d);
+  int64_t* pos = ws<int64_t>(c, "pr_pos", n_star);
+  const double s2 = th.sigma * th.sigma;
+  launch_merge_side(c->stream, P.t, n, ts, n_star, 0, P.y, s2, P.v, P.ldv, (int)d, tm, ym, rm, vm, d, nullptr);
+  launch_merge_side(c->stream, ts, n_star, P.t, n, 1, nullptr, 1e10, vs, ldv_s, (int)d, tm, ym, rm, vm, d, pos);
+  check_launch("predict: merge");
+  // ---- gains on the merged grid (noise sigma^2 train / 1e10 test)
+  std::vector<ChainParamsHost> cps{{1.0 / th.l_t, th.l_t, th.sv_t * th.sv_t, s2}};
+  GainsOut g = run_gains(c, P.sdim, tm, nt, cps, rm, false, "pred");
+  // ---- whiten Cf*u columns (on the fly) and y* into X, forward carry
+  const int64_t ldx = mp + 64;
+  double* X = ws<double>(c, "pr_X", (size_t)nt * ldx);
+  double* send = ws<double>(c, "pr_send", (size_t)nch * mc * 4);
+  double* cin = ws<double>(c, "pr_cin", (size_t)nch * mc * 4);
+  double* bend = ws<double>(c, "pr_bend", (size_t)nch * mc * 4);
+  double* chat = ws<double>(c, "pr_chat", (size_t)nch * mc * 4);
+  double* h = ws<double>(c, "pr_h", (size_t)nt * 4);
+  launch_whiten_kfu(c->stream, P.tk, P.ok, g.rec, vm, d, (int)d, P.z, P.ldz, m, mp, nt, kChunk,
+                    nch, 1.0 / th.l_o, th.sv_o * th.sv_o, X, ldx, send, mc);
+  launch_whiten_vec(c->stream, P.sdim, g.rec, 0, ym, 0, nt, kChunk, nch, 1, X + mp, 0, send, 0,
+                    mc, mp, ldx);
+  check_launch("predict: whiten");
+  run_carry(c, P.sdim, g.phi, 0, send, cin, 0, nch, mc, mc, 1, "predf");
+  // ---- adjoint: Sigma^{-1} x = W^T (W x)
+  launch_gains_adjoint(c->stream, P.sdim, g.rec, nt, kChunk, nch, 1, h);
+  launch_adjoint_local(c->stream, P.sdim, X, ldx, mc, g.rec, g.g, cin, mc, nt, kChunk, nch, bend);
+  check_launch("predict: adjoint");
+  run_carry(c, P.sdim, g.phi, 0, bend, chat, 0, nch, mc, mc, 1, "predb", /*rev=*/true);
+  // ---- per test row: Q = R Sigma^{-1} Cf*u, mean
+  double* Q = ws<double>(c, "pr_Q", (size_t)n_star * mp);
+  double* dmean = ws<double>(c, "pr_mean", n_star);
+  double* dstd = ws<double>(c, "pr_std", n_star);
+  launch_predict_rows(c->stream, P.sdim, X, ldx, h, chat, mc, mp, m, kChunk, pos, n_star, rm, ym, w,
+                      Q, mp, dmean);
+  check_launch("predict: rows");
+  // ---- Z = Q V^T;  ANALYTIC: std = |Z_i|;  MC: f_s = mean + Z xi_s, mean/std over samples
+  const int ncb = (int)((m + 127) / 128);
+  if (mode == GPAR_PREDICT_ANALYTIC) {
+    double* rowsq = ws<double>(c, "pr_rowsq", (size_t)ncb * n_star);
+    launch_gemm_nt(c->stream, Q, mp, Vm, ld, n_star, m, m, 0, nullptr, 0, rowsq, 0, nullptr,
+                   nullptr, nullptr);
+    launch_rowsq_finish(c->stream, rowsq, n_star, ncb, dstd);
+  } else {
+    double* Z = ws<double>(c, "pr_Z", (size_t)n_star * mp);
+    double* rowsq = ws<double>(c, "pr_rowsq", (size_t)ncb * n_star);
+    double* xi = ws<double>(c, "pr_xi", (size_t)samples * mp);
+    double* mmc = ws<double>(c, "pr_mmc", n_star);
+    launch_gemm_nt(c->stream, Q, mp, Vm, ld, n_star, m, m, 0, Z, mp, rowsq, 0, nullptr, nullptr,
+                   nullptr);
+    launch_normal(c->stream, xi, mp, samples, m, samples, seed);
+    launch_gemm_nt(c->stream, Z, mp, xi, mp, n_star, samples, m, 1, nullptr, 0, nullptr, samples,
+                   dmean, mmc, dstd);
+    dmean = mmc;
+  }
+  check_launch("predict: gemm");
+  // ---- outputs
+  if (mem == GPAR_MEM_DEVICE) {
+    HIPCHECK(hipMemcpyAsync(mean_out, dmean, n_star * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    HIPCHECK(hipMemcpyAsync(std_out, dstd, n_star * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    sync(c);
+  } else {
+    std::vector<double> hm(n_star), hs(n_star);
+    d2h(c, hm.data(), dmean, n_star);
+    d2h(c, hs.data(), dstd, n_star);
+    sync(c);
+    for (int64_t i = 0; i < n_star; ++i) {
+      mean_out[perm[i]] = hm[i];
+      std_out[perm[i]] = hs[i];
+    }
+  }
 }
 
 static double unpack(double p) { return std::exp(p) + 1e-3; }
@@ -664,7 +811,17 @@ static int32_t not_yet(gpar_ctx* ctx, const char* what) {
 int32_t gpar_predict(gpar_ctx* ctx, const gpar_problem* prob, const double* theta,
                      int64_t n_star, const double* t_star, const double* v_star, int64_t ldvs,
                      int32_t mode, int32_t samples, uint64_t seed, double* mean, double* std) {
-  return not_yet(ctx, "gpar_predict");
+  API_BEGIN(ctx)
+  ARGCHECK(prob && theta && t_star && v_star && mean && std, "null argument");
+  ARGCHECK(n_star >= 1, "n_star must be >= 1");
+  ARGCHECK(ldvs >= prob->d, "ldvs must be >= d");
+  ARGCHECK(mode == GPAR_PREDICT_ANALYTIC || mode == GPAR_PREDICT_MC, "bad mode");
+  if (mode == GPAR_PREDICT_MC)
+    ARGCHECK(samples >= 2 && samples <= 128, "MC mode supports 2..128 samples");
+  DevProblem P = prepare_problem(ctx, *prob, 0);
+  std::vector<Theta> th = thetas_from(theta, 1);
+  predict_impl(ctx, P, th[0], prob->mem, n_star, t_star, v_star, ldvs, mode, samples, seed, mean, std);
+  API_END(ctx)
 }
 
 int32_t gpar_lgssm_smooth(gpar_ctx* ctx, int32_t nchains, int64_t n, const double* t,

@@ -225,6 +225,8 @@ __global__ __launch_bounds__(256) void trsm_kernel(const TrsmJob* __restrict__ j
   }
 }
 
+constexpr int kMaxMTrsv = 2048;
+
 // ---------------------------------------------------------------------------- single-wave vector solves
 // x = L^{-1} b (forward) into LDS array x (length m); one wave.
 __device__ void wave_forward(const double* __restrict__ L, int64_t ld, int m,
@@ -250,6 +252,29 @@ __device__ void wave_backward_t(const double* __restrict__ L, int64_t ld, int m,
     __builtin_amdgcn_s_waitcnt(0);
     __builtin_amdgcn_wave_barrier();
   }
+}
+
+// x = L^{-1} b (trans = 0) or x = L^{-T} b (trans = 1); one wave, batched over blockIdx.
+struct TrsvJob {
+  const double* L;
+  int64_t ld;
+  int m;
+  const double* b;
+  double* x;
+  int trans;
+};
+
+__global__ __launch_bounds__(64) void trsv_kernel(const TrsvJob* __restrict__ jobs) {
+  const TrsvJob jb = jobs[blockIdx.x];
+  __shared__ double xs[kMaxMTrsv], bs[kMaxMTrsv];
+  for (int i = threadIdx.x; i < jb.m; i += 64) bs[i] = jb.b[i];
+  __syncthreads();
+  if (jb.trans)
+    wave_backward_t(jb.L, jb.ld, jb.m, bs, xs, threadIdx.x);
+  else
+    wave_forward(jb.L, jb.ld, jb.m, bs, xs, threadIdx.x);
+  __syncthreads();
+  for (int i = threadIdx.x; i < jb.m; i += 64) jb.x[i] = xs[i];
 }
 
 struct FinishJob {
@@ -375,6 +400,10 @@ void launch_lower_to_upper_colmajor(hipStream_t st, const double* L, int64_t ldl
 void launch_eye(hipStream_t st, double* A, int64_t ld, int m) {
   dim3 grid((m + 15) / 16, (m + 15) / 16);
   eye_kernel<<<grid, 256, 0, st>>>(A, ld, m);
+}
+
+void launch_trsv(hipStream_t st, const TrsvJobHost* jobs_dev, int njobs) {
+  trsv_kernel<<<njobs, 64, 0, st>>>(reinterpret_cast<const TrsvJob*>(jobs_dev));
 }
 
 }  // namespace gpar

@@ -29,8 +29,11 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
     const double* __restrict__ cin, int64_t mc, int L, const double* __restrict__ alpha,
     int ntb, int ntiles, int nsplit, int64_t rows_per_split, double* __restrict__ part,
     double* __restrict__ rpart) {
-  __shared__ __attribute__((aligned(16))) double lds[2][2][kBK * kLdsStride];
-  __shared__ double rred[128];
+  // one LDS array: [2 buf][2 operand][kBK rows x kLdsStride] | g/alpha ring [2][kBK][4 + 1] | r reduce [128]
+  constexpr int kTileD = kBK * kLdsStride;
+  constexpr int kGRing = kBK * 5;
+  __shared__ __attribute__((aligned(16))) double smem[4 * kTileD + 2 * kGRing + 128];
+  double* rred = smem + 4 * kTileD + 2 * kGRing;
 
   // XCD-aware decode: blocks b and b+8 share an XCD; give each XCD group whole splits.
   const int b = blockIdx.x;
@@ -51,6 +54,7 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
   const int wr = wave >> 1, wc = wave & 1;
   const int sc = tid & 127;   // staging column
   const int rg = tid >> 7;    // staging row group (wave-uniform)
+  const int rgu = __builtin_amdgcn_readfirstlane(rg);
 
   const int64_t kb = (int64_t)split * rows_per_split;
   int64_t ke = kb + rows_per_split;
@@ -63,61 +67,86 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
     for (int c = 0; c < 4; ++c) acc[a][c] = d4{0.0, 0.0, 0.0, 0.0};
 
   double racc = 0.0;
-  double cI[D], cJ[D];
-  int64_t cur_chunk = -1;
-  double sI[8], sJ[8];
+  double bI[8], bJ[8], cI[D], cJ[D];
+  double gpre = 0.0;
 
+  // Pipeline (one barrier per K-step):
+  //   stage_load(s+1)  raw beta / carry loads, issued before the MFMAs of step s
+  //   gload(s+2)       the K-step's g_k rows + alpha_k (80 doubles, one per thread) two steps ahead
+  //   MFMAs(s)         from lds[s & 1]
+  //   stage_store(s+1) fix-up beta += g_k . c_chunk (g from the LDS ring) -> lds[(s+1) & 1]
+  //   gstore(s+2)      ring slot (s+2) & 1 == s & 1, last read by stage_store(s) one barrier ago
+  // Consuming a global load right after issuing it makes hipcc wait vmcnt(0) per row, so all
+  // global loads are consumed one MFMA phase later.  Rows past the split are clamped + masked.
   auto stage_load = [&](int64_t k0) {
     const int64_t ch = k0 / L;
-    if (ch != cur_chunk) {
-      cur_chunk = ch;
 #pragma unroll
-      for (int i = 0; i < D; ++i) {
-        cI[i] = cin[(ch * mc + i0 + sc) * kSStride + i];
-        cJ[i] = cin[(ch * mc + j0 + sc) * kSStride + i];
-      }
+    for (int i = 0; i < D; ++i) {
+      cI[i] = cin[(ch * mc + i0 + sc) * kSStride + i];
+      cJ[i] = cin[(ch * mc + j0 + sc) * kSStride + i];
     }
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      const int64_t k = k0 + rg + 2 * r;
-      double vi = 0.0, vj = 0.0;
-      if (k < ke) {
-        vi = beta[k * ldb + i0 + sc];
-        if (!diag) vj = beta[k * ldb + j0 + sc];
-        const double* gk = g + k * kGStride;
-#pragma unroll
-        for (int i = 0; i < D; ++i) {
-          vi = fma(gk[i], cI[i], vi);
-          if (!diag) vj = fma(gk[i], cJ[i], vj);
-        }
-        if (diag) racc = fma(alpha[k], vi, racc);
-      }
-      sI[r] = vi;
-      sJ[r] = vj;
+      const int64_t k = k0 + rgu + 2 * r;
+      const int64_t kc = (k < n) ? k : n - 1;
+      bI[r] = beta[kc * ldb + i0 + sc];
+      bJ[r] = beta[kc * ldb + j0 + sc];
     }
   };
-  auto stage_store = [&](int buf) {
+  auto gload = [&](int64_t k0) {
+    if (tid < kBK * 5) {
+      const int row = tid / 5, col = tid % 5;
+      const int64_t k = k0 + row;
+      const int64_t kc = (k < n) ? k : n - 1;
+      gpre = (col < 4) ? g[kc * kGStride + col] : alpha[kc];
+    }
+  };
+  auto gstore = [&](int slot) {
+    if (tid < kBK * 5) smem[4 * kTileD + slot * kGRing + tid] = gpre;
+  };
+  auto stage_store = [&](int64_t k0, int buf) {
+    const double* gr = smem + 4 * kTileD + buf * kGRing;
+    double* ldsI = smem + (buf * 2 + 0) * kTileD;
+    double* ldsJ = smem + (buf * 2 + 1) * kTileD;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
-      lds[buf][0][(rg + 2 * r) * kLdsStride + sc] = sI[r];
-      if (!diag) lds[buf][1][(rg + 2 * r) * kLdsStride + sc] = sJ[r];
+      const int row = rgu + 2 * r;
+      const int64_t k = k0 + row;
+      const double msk = (k < ke) ? 1.0 : 0.0;
+      double vi = bI[r], vj = bJ[r];
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        const double gi = gr[row * 5 + i];
+        vi = fma(gi, cI[i], vi);
+        vj = fma(gi, cJ[i], vj);
+      }
+      vi *= msk;
+      racc = fma(gr[row * 5 + 4], vi, racc);
+      ldsI[row * kLdsStride + sc] = vi;
+      ldsJ[row * kLdsStride + sc] = vj * msk;
     }
   };
 
   const int nsteps = (int)((ke - kb + kBK - 1) / kBK);
   if (nsteps > 0) {
+    gload(kb);
     stage_load(kb);
-    stage_store(0);
+    gstore(0);
+    if (nsteps > 1) gload(kb + kBK);
+    __syncthreads();
+    stage_store(kb, 0);
+    if (nsteps > 1) gstore(1);
   }
   __syncthreads();
-  const int opB = diag ? 0 : 1;
   const int frow = lane >> 4, fcol = lane & 15;
   for (int s = 0; s < nsteps; ++s) {
     const int buf = s & 1;
     const bool more = (s + 1) < nsteps;
+    const bool more2 = (s + 2) < nsteps;
     if (more) stage_load(kb + (int64_t)(s + 1) * kBK);
-    const double* la = &lds[buf][0][0];
-    const double* lb = &lds[buf][opB][0];
+    if (more2) gload(kb + (int64_t)(s + 2) * kBK);
+    const double* la = smem + (buf * 2 + 0) * kTileD;
+    const double* lb = smem + (buf * 2 + 1) * kTileD;
 #pragma unroll
     for (int ks = 0; ks < kBK / 4; ++ks) {
       double fa[4], fb[4];
@@ -132,7 +161,8 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
         for (int c = 0; c < 4; ++c)
           acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[c], acc[a][c], 0, 0, 0);
     }
-    if (more) stage_store(buf ^ 1);
+    if (more) stage_store(kb + (int64_t)(s + 1) * kBK, buf ^ 1);
+    if (more2) gstore(buf);
     __syncthreads();
   }
 

@@ -397,79 +397,299 @@ __global__ __launch_bounds__(256) void whiten_kfu(
 }
 
 // ---------------------------------------------------------------------------- whitening of a vector per chain
-// One thread per (chunk, chain).  x_c[k] = y[c * ldy + k]; writes alpha_loc[c * lda + k]
-// and the local end state to send[(j * mc + col) * 4] for column `col` of chain c
-// (col = col0 + c * colstride).
+// One 64-thread block per (chunk, chain): the chunk's gains records and data are staged into
+// LDS with coalesced loads, lane 0 runs the recursion out of LDS, and the block writes the
+// whitened chunk back coalesced.  x_c[k] = y[c * ldy + k]; alpha_loc[c * lda + k]; local end
+// state -> send[c * sendstride + (j * mc + col) * 4].
+constexpr int kVecL = 256;   // == host chunk length
+
 template <int D>
-__global__ __launch_bounds__(256) void whiten_vec(const double* __restrict__ rec, int64_t recstride,
-                                                  const double* __restrict__ y, int64_t ldy,
-                                                  int64_t n, int L, int64_t nch,
-                                                  double* __restrict__ alpha, int64_t lda,
-                                                  double* __restrict__ send, int64_t sendstride,
-                                                  int64_t mc, int64_t col) {
+__global__ __launch_bounds__(64) void whiten_vec(const double* __restrict__ rec, int64_t recstride,
+                                                 const double* __restrict__ y, int64_t ldy,
+                                                 int64_t n, int L, int64_t nch,
+                                                 double* __restrict__ alpha, int64_t lda,
+                                                 double* __restrict__ send, int64_t sendstride,
+                                                 int64_t mc, int64_t col, int64_t astride) {
   constexpr int RS = Rec<D>::size;
-  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  __shared__ __attribute__((aligned(16))) double rl[kVecL * RS];
+  __shared__ double yl[kVecL];
+  const int64_t j = blockIdx.x;
   const int c = blockIdx.y;
-  if (j >= nch) return;
+  const int lane = threadIdx.x;
   const double* rp = rec + (int64_t)c * recstride;
   const double* yp = y + (int64_t)c * ldy;
-  double* ap = alpha + (int64_t)c * lda;
   const int64_t k0 = j * L;
-  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
-  double mst[D];
+  const int nk = (int)(((k0 + L < n) ? k0 + L : n) - k0);
+  for (int e = lane; e < nk * RS; e += 64) rl[e] = rp[k0 * RS + e];
+  for (int e = lane; e < nk; e += 64) yl[e] = yp[k0 + e];
+  __syncthreads();
+  if (lane == 0) {
+    double mst[D];
 #pragma unroll
-  for (int i = 0; i < D; ++i) mst[i] = 0.0;
-  for (int64_t k = k0; k < k1; ++k) {
-    const double* r = rp + k * RS;
-    double mm[D];
+    for (int i = 0; i < D; ++i) mst[i] = 0.0;
+    for (int kk = 0; kk < nk; ++kk) {
+      const double* r = rl + kk * RS;
+      double mm[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) {
-      double acc = 0.0;
+      for (int i = 0; i < D; ++i) {
+        double acc = 0.0;
 #pragma unroll
-      for (int q = 0; q < D; ++q) acc = fma(r[i * D + q], mst[q], acc);
-      mm[i] = acc;
+        for (int q = 0; q < D; ++q) acc = fma(r[i * D + q], mst[q], acc);
+        mm[i] = acc;
+      }
+      const double ev = yl[kk] - mm[0];
+      yl[kk] = ev * r[D * D + D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) mst[i] = fma(r[D * D + i], ev, mm[i]);
     }
-    const double ev = yp[k] - mm[0];
-    ap[k] = ev * r[D * D + D];
+    double* sp = send + (int64_t)c * sendstride;
 #pragma unroll
-    for (int i = 0; i < D; ++i) mst[i] = fma(r[D * D + i], ev, mm[i]);
+    for (int i = 0; i < D; ++i) sp[(j * mc + col) * kSStride + i] = mst[i];
   }
-  double* sp = send + (int64_t)c * sendstride;
-#pragma unroll
-  for (int i = 0; i < D; ++i) sp[(j * mc + col) * kSStride + i] = mst[i];
+  __syncthreads();
+  double* ap = alpha + (int64_t)c * lda;
+  for (int e = lane; e < nk; e += 64) ap[(k0 + e) * astride] = yl[e];
 }
 
 // ---------------------------------------------------------------------------- carry over chunks
-// For each column c (and chain b = blockIdx.y): cin[j][c] = true state at the start of chunk j,
-// cin[0] = 0, cin[j+1] = Phi_j cin[j] + send[j].
-template <int D>
-__global__ __launch_bounds__(256) void carry_kernel(const double* __restrict__ phi, int64_t phistride,
-                                                    const double* __restrict__ send,
-                                                    double* __restrict__ cin, int64_t sstride,
-                                                    int64_t nch, int64_t mc, int64_t ncols) {
+// cin[j][c] = true filter state at the start of chunk j: cin[0] = 0,
+// cin[j+1] = Phi_j cin[j] + send[j].  Two-level: groups of GS chunks.
+//   a) per (group, column): group end state from zero            -> gend
+//   b) per group: Psi_g = prod Phi_j over the group               -> psi
+//   c) per column: sequential over groups                          -> gin
+//   d) per (group, column): re-propagate inside the group          -> cin
+// Chains (blockIdx.z) are independent; per-chain strides: phistride, sstride (send/cin),
+// gstride_ (gend/gin), psistride.
+// REV: the adjoint's backward carry (chunks visited last to first, Phi transposed):
+// out[J-1] = 0, out[j] = Phi_{j+1}^T out[j+1] + b_{j+1}.
+template <int D, bool REV>
+__device__ __forceinline__ void carry_step(const double* __restrict__ ph, int64_t r,
+                                           const double* __restrict__ sv, double (&st)[D]) {
+  double nx[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    double acc = sv[i];
+#pragma unroll
+    for (int q = 0; q < D; ++q)
+      acc = fma(REV ? ph[r * D * D + q * D + i] : ph[r * D * D + i * D + q], st[q], acc);
+    nx[i] = acc;
+  }
+#pragma unroll
+  for (int i = 0; i < D; ++i) st[i] = nx[i];
+}
+
+template <int D, bool REV>
+__global__ __launch_bounds__(256) void carry_group_local(const double* __restrict__ phi, int64_t phistride,
+                                                         const double* __restrict__ send, int64_t sstride,
+                                                         int64_t nch, int64_t mc, int64_t ncols, int GS,
+                                                         double* __restrict__ gend, int64_t gstride_) {
   const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  const int b = blockIdx.y;
+  const int64_t gidx = blockIdx.y;
+  const int b = blockIdx.z;
   if (c >= ncols) return;
   const double* ph = phi + (int64_t)b * phistride;
   const double* sp = send + (int64_t)b * sstride;
-  double* cp = cin + (int64_t)b * sstride;
+  const int64_t j0 = gidx * GS;
+  const int64_t j1 = (j0 + GS < nch) ? j0 + GS : nch;
   double st[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) st[i] = 0.0;
-  for (int64_t j = 0; j < nch; ++j) {
-    const int64_t o = (j * mc + c) * kSStride;
+#pragma unroll 4
+  for (int64_t j = j0; j < j1; ++j) {
+    const int64_t r = REV ? nch - 1 - j : j;
+    carry_step<D, REV>(ph, r, sp + (r * mc + c) * kSStride, st);
+  }
+  double* ge = gend + (int64_t)b * gstride_ + (gidx * mc + c) * kSStride;
 #pragma unroll
-    for (int i = 0; i < D; ++i) cp[o + i] = st[i];
+  for (int i = 0; i < D; ++i) ge[i] = st[i];
+}
+
+template <int D, bool REV>
+__global__ __launch_bounds__(256) void carry_group_phi(const double* __restrict__ phi, int64_t phistride,
+                                                       int64_t nch, int GS, int64_t ngroups,
+                                                       double* __restrict__ psi, int64_t psistride) {
+  const int64_t gidx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (gidx >= ngroups) return;
+  const double* ph = phi + (int64_t)b * phistride;
+  const int64_t j0 = gidx * GS;
+  const int64_t j1 = (j0 + GS < nch) ? j0 + GS : nch;
+  double P[D][D], X[D][D], F[D][D];
+  mat_eye(P);
+  for (int64_t j = j0; j < j1; ++j) {
+    const int64_t r = REV ? nch - 1 - j : j;
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q)
+        F[i][q] = REV ? ph[r * D * D + q * D + i] : ph[r * D * D + i * D + q];
+    mat_mul(F, P, X);
+    mat_copy(X, P);
+  }
+  double* ps = psi + (int64_t)b * psistride + gidx * D * D;
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) ps[i * D + q] = P[i][q];
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void carry_group_scan(const double* __restrict__ psi, int64_t psistride,
+                                                        const double* __restrict__ gend,
+                                                        double* __restrict__ gin, int64_t gstride_,
+                                                        int64_t ngroups, int64_t mc, int64_t ncols) {
+  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (c >= ncols) return;
+  const double* ps = psi + (int64_t)b * psistride;
+  const double* ge = gend + (int64_t)b * gstride_;
+  double* gi = gin + (int64_t)b * gstride_;
+  double st[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) st[i] = 0.0;
+  for (int64_t g = 0; g < ngroups; ++g) {
+    const int64_t o = (g * mc + c) * kSStride;
+#pragma unroll
+    for (int i = 0; i < D; ++i) gi[o + i] = st[i];
     double nx[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-      double acc = sp[o + i];
+      double acc = ge[o + i];
 #pragma unroll
-      for (int q = 0; q < D; ++q) acc = fma(ph[j * D * D + i * D + q], st[q], acc);
+      for (int q = 0; q < D; ++q) acc = fma(ps[g * D * D + i * D + q], st[q], acc);
       nx[i] = acc;
     }
 #pragma unroll
     for (int i = 0; i < D; ++i) st[i] = nx[i];
+  }
+}
+
+template <int D, bool REV>
+__global__ __launch_bounds__(256) void carry_group_apply(const double* __restrict__ phi, int64_t phistride,
+                                                         const double* __restrict__ send,
+                                                         double* __restrict__ cin, int64_t sstride,
+                                                         const double* __restrict__ gin, int64_t gstride_,
+                                                         int64_t nch, int64_t mc, int64_t ncols, int GS) {
+  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t gidx = blockIdx.y;
+  const int b = blockIdx.z;
+  if (c >= ncols) return;
+  const double* ph = phi + (int64_t)b * phistride;
+  const double* sp = send + (int64_t)b * sstride;
+  double* cp = cin + (int64_t)b * sstride;
+  const double* gi = gin + (int64_t)b * gstride_ + (gidx * mc + c) * kSStride;
+  const int64_t j0 = gidx * GS;
+  const int64_t j1 = (j0 + GS < nch) ? j0 + GS : nch;
+  double st[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) st[i] = gi[i];
+#pragma unroll 4
+  for (int64_t j = j0; j < j1; ++j) {
+    const int64_t r = REV ? nch - 1 - j : j;
+    const int64_t o = (r * mc + c) * kSStride;
+#pragma unroll
+    for (int i = 0; i < D; ++i) cp[o + i] = st[i];
+    carry_step<D, REV>(ph, r, sp + o, st);
+  }
+}
+
+// ---------------------------------------------------------------------------- adjoint (Sigma^{-1} = W^T W)
+// The whitening alpha = W x is lower triangular; its adjoint u = W^T w runs backwards with the
+// same gains records:  u_k = rs_k w_k + K_k . lambda_k,  lambda_{k-1} = A_k^T (lambda_k - u_k e1),
+// lambda_{N-1} = 0.  Chunked like the forward pass: from lambda = 0 at each chunk end, then
+// u_k(true) = u_k(local) + h_k . chat_j with h_k = Gamma_{j,k}^T K_k,
+// Gamma_{j,k1-1} = I, Gamma_{j,k-1} = Abar_k^T Gamma_{j,k}, and the backward carry chat over
+// chunks with Phi_j^T (carry kernels, REV = true).
+template <int D>
+__global__ __launch_bounds__(256) void gains_adjoint(const double* __restrict__ rec, int64_t n,
+                                                     int L, int64_t nch, double* __restrict__ h) {
+  constexpr int RS = Rec<D>::size;
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (j >= nch) return;
+  const double* rp = rec + (int64_t)p * n * RS;
+  double* hp = h + (int64_t)p * n * kGStride;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  double Gm[D][D];
+  mat_eye(Gm);
+  for (int64_t k = k1 - 1; k >= k0; --k) {
+    const double* r = rp + k * RS;
+    double A[D][D], K[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      K[i] = r[D * D + i];
+#pragma unroll
+      for (int q = 0; q < D; ++q) A[i][q] = r[i * D + q];
+    }
+    // h_k = Gamma^T K
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) acc = fma(Gm[i][q], K[i], acc);
+      hp[k * kGStride + q] = acc;
+    }
+    // Gamma <- Abar^T Gamma,  Abar = A - K A[0,:]
+    double Ab[D][D], X[D][D];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) Ab[i][q] = A[i][q] - K[i] * A[0][q];
+    mat_mul_at(Ab, Gm, X);
+    mat_copy(X, Gm);
+  }
+}
+
+// Backward local pass over a column-major-in-rows matrix X (row k, column c at X[k*ldx + c]):
+// reads w = X[k][c] + g_k . cin[j][c] (forward fix-up applied on the fly), writes u_loc in place,
+// and the chunk's backward end state (lambda before its first step) to bend[(j*mc + c)*4].
+// grid: (nch, ceil(ncols / 64)); block 64 (one column per lane).
+template <int D>
+__global__ __launch_bounds__(64) void adjoint_local(double* __restrict__ X, int64_t ldx,
+                                                    int64_t ncols, const double* __restrict__ rec,
+                                                    const double* __restrict__ g,
+                                                    const double* __restrict__ cin, int64_t mc,
+                                                    int64_t n, int L, double* __restrict__ bend) {
+  constexpr int RS = Rec<D>::size;
+  const int64_t j = blockIdx.x;
+  const int64_t c = (int64_t)blockIdx.y * 64 + threadIdx.x;
+  const bool act = c < ncols;
+  const int64_t cc = act ? c : 0;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  double cf[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) cf[i] = cin[(j * mc + cc) * kSStride + i];
+  double lam[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) lam[i] = 0.0;
+#pragma unroll 4
+  for (int64_t k = k1 - 1; k >= k0; --k) {
+    const double* r = rec + k * RS;
+    const double* gk = g + k * kGStride;
+    double w = X[k * ldx + cc];
+#pragma unroll
+    for (int i = 0; i < D; ++i) w = fma(gk[i], cf[i], w);
+    double u = w * r[D * D + D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) u = fma(r[D * D + i], lam[i], u);
+    lam[0] -= u;
+    double nl[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) acc = fma(r[i * D + q], lam[i], acc);
+      nl[q] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) lam[i] = nl[i];
+    if (act) X[k * ldx + c] = u;
+  }
+  if (act) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) bend[(j * mc + c) * kSStride + i] = lam[i];
   }
 }
 
@@ -606,16 +826,53 @@ void launch_whiten_kfu(hipStream_t st, int time_kind, int out_kind, const double
 void launch_whiten_vec(hipStream_t st, int sdim, const double* rec, int64_t recstride,
                        const double* y, int64_t ldy, int64_t n, int L, int64_t nch, int nchains,
                        double* alpha, int64_t lda, double* send, int64_t sendstride, int64_t mc,
-                       int64_t col) {
-  dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
-  GPAR_DISPATCH_D(sdim, whiten_vec<DD><<<grid, 256, 0, st>>>(rec, recstride, y, ldy, n, L, nch, alpha, lda, send, sendstride, mc, col));
+                       int64_t col, int64_t astride) {
+  dim3 grid((unsigned)nch, (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, whiten_vec<DD><<<grid, 64, 0, st>>>(rec, recstride, y, ldy, n, L, nch, alpha, lda, send, sendstride, mc, col, astride));
+}
+
+int carry_group_size(int64_t nch) {
+  int gs = 1;
+  while ((int64_t)gs * gs < nch) ++gs;
+  return gs;
 }
 
 void launch_carry(hipStream_t st, int sdim, const double* phi, int64_t phistride,
                   const double* send, double* cin, int64_t sstride, int64_t nch, int64_t mc,
-                  int64_t ncols, int nchains) {
-  dim3 grid((unsigned)((ncols + 255) / 256), (unsigned)nchains);
-  GPAR_DISPATCH_D(sdim, carry_kernel<DD><<<grid, 256, 0, st>>>(phi, phistride, send, cin, sstride, nch, mc, ncols));
+                  int64_t ncols, int nchains, double* gend, double* gin, double* psi, bool rev) {
+  const int GS = carry_group_size(nch);
+  const int64_t ng = (nch + GS - 1) / GS;
+  const int64_t gstride_ = ng * mc * kSStride;
+  const int64_t psistride = ng * sdim * sdim;
+  dim3 g3((unsigned)((ncols + 255) / 256), (unsigned)ng, (unsigned)nchains);
+  dim3 gp((unsigned)((ng + 255) / 256), (unsigned)nchains);
+  dim3 gc((unsigned)((ncols + 255) / 256), (unsigned)nchains);
+#define GPAR_CARRY_LAUNCH(RV)                                                                       \
+  GPAR_DISPATCH_D(sdim, {                                                                          \
+    carry_group_local<DD, RV><<<g3, 256, 0, st>>>(phi, phistride, send, sstride, nch, mc, ncols, GS, gend, gstride_); \
+    carry_group_phi<DD, RV><<<gp, 256, 0, st>>>(phi, phistride, nch, GS, ng, psi, psistride);      \
+    carry_group_scan<DD><<<gc, 256, 0, st>>>(psi, psistride, gend, gin, gstride_, ng, mc, ncols);   \
+    carry_group_apply<DD, RV><<<g3, 256, 0, st>>>(phi, phistride, send, cin, sstride, gin, gstride_, nch, mc, ncols, GS); \
+  })
+  if (rev) {
+    GPAR_CARRY_LAUNCH(true);
+  } else {
+    GPAR_CARRY_LAUNCH(false);
+  }
+#undef GPAR_CARRY_LAUNCH
+}
+
+void launch_gains_adjoint(hipStream_t st, int sdim, const double* rec, int64_t n, int L,
+                          int64_t nch, int nchains, double* h) {
+  dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, gains_adjoint<DD><<<grid, 256, 0, st>>>(rec, n, L, nch, h));
+}
+
+void launch_adjoint_local(hipStream_t st, int sdim, double* X, int64_t ldx, int64_t ncols,
+                          const double* rec, const double* g, const double* cin, int64_t mc,
+                          int64_t n, int L, int64_t nch, double* bend) {
+  dim3 grid((unsigned)nch, (unsigned)((ncols + 63) / 64));
+  GPAR_DISPATCH_D(sdim, adjoint_local<DD><<<grid, 64, 0, st>>>(X, ldx, ncols, rec, g, cin, mc, n, L, bend));
 }
 
 int64_t vec_fix_blocks(int64_t n) { return (n + 255) / 256; }

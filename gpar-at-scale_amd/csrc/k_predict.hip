@@ -1,0 +1,322 @@
+// k_predict.hip -- scaled-GPAR prediction (gpar_scaled_inference.jl:63-135) on gfx950.
+//
+// The reference draws e ~ q(u), forms f_x = Cf*u U_u^{-1} e and RTS-smooths y* - f_x 100 times.
+// The build uses the same model through linear algebra on the merged (train + test) grid:
+//   S x = x - R Sigma^{-1} x,   Sigma^{-1} = W^T W  (whitening + adjoint, k_lgssm.hip)
+//   f*_e = S y* + (I - S) Cf*u U_u^{-1} e = S y* + Q U_u^{-1} e,   Q = R Sigma^{-1} Cf*u
+// so with V = L_D^{-1} L_u^{-1} (q(u) = N(m_e, D^{-1}), D = L_D L_D^T):
+//   mean_i = (S y*)_i + Q_i w,  w = U_u^{-1} m_e
+//   f*_{i,s} = mean_i + Z_i xi_s,  Z = Q V^T,  xi_s ~ N(0, I)      (MC, reference-faithful)
+//   var_i = |Z_i|^2                                                 (ANALYTIC, S -> infinity)
+#include "device_common.hpp"
+
+namespace gpar {
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// ---------------------------------------------------------------------------- merge train + test
+// Stable sortperm of vcat(train, test) (gpar_scaled_inference.jl:75-87) for ascending inputs:
+// train k -> k + #{test < t_k};  test i -> i + #{train <= t*_i}.
+__device__ __forceinline__ int64_t lower_bound(const double* a, int64_t n, double x) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] < x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+__device__ __forceinline__ int64_t upper_bound(const double* a, int64_t n, double x) {
+  int64_t lo = 0, hi = n;
+  while (lo < hi) {
+    const int64_t mid = (lo + hi) >> 1;
+    if (a[mid] <= x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+// Scatter one side (train or test) into the merged arrays.  V rows are copied (d values).
+__global__ __launch_bounds__(256) void merge_side(const double* __restrict__ ts, int64_t ns,
+                                                  const double* __restrict__ other, int64_t no,
+                                                  int is_test, const double* __restrict__ ys,
+                                                  double rval, const double* __restrict__ vs,
+                                                  int64_t ldvs, int d,
+                                                  double* __restrict__ tm, double* __restrict__ ym,
+                                                  double* __restrict__ rm, double* __restrict__ vm,
+                                                  int64_t ldvm, int64_t* __restrict__ pos_out) {
+  const int64_t k = blockIdx.x * (int64_t)256 + threadIdx.x;
+  if (k >= ns) return;
+  const double tk = ts[k];
+  const int64_t pos = k + (is_test ? upper_bound(other, no, tk) : lower_bound(other, no, tk));
+  tm[pos] = tk;
+  ym[pos] = ys ? ys[k] : 0.0;
+  rm[pos] = rval;
+  for (int i = 0; i < d; ++i) vm[pos * ldvm + i] = vs[k * ldvs + i];
+  if (pos_out) pos_out[k] = pos;
+}
+
+// ---------------------------------------------------------------------------- per test row
+// X: merged grid rows of local adjoint outputs (columns 0..m-1 = Cf*u columns, column mp = y*),
+// h: adjoint fix-up vectors, chat: backward carries [nch][mc][4].  One wave per test point:
+//   Q[i][c] = R_k u_{k,c}, mean_i = y*_k - R_k u_{k,y} + Q_i . w.
+template <int D>
+__global__ __launch_bounds__(256) void predict_rows(const double* __restrict__ X, int64_t ldx,
+                                                    const double* __restrict__ h,
+                                                    const double* __restrict__ chat, int64_t mc,
+                                                    int64_t mp, int64_t m, int L,
+                                                    const int64_t* __restrict__ pos,
+                                                    int64_t nstar, const double* __restrict__ rm,
+                                                    const double* __restrict__ ym,
+                                                    const double* __restrict__ w,
+                                                    double* __restrict__ Q, int64_t ldq,
+                                                    double* __restrict__ mean) {
+  const int64_t i = blockIdx.x * (int64_t)4 + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (i >= nstar) return;
+  const int64_t k = pos[i];
+  const int64_t j = k / L;
+  const double R = rm[k];
+  double hk[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) hk[q] = h[k * kGStride + q];
+  double dot = 0.0;
+  for (int64_t c = lane; c < mp; c += 64) {
+    const double* ch = chat + (j * mc + c) * kSStride;
+    double u = X[k * ldx + c];
+#pragma unroll
+    for (int q = 0; q < D; ++q) u = fma(hk[q], ch[q], u);
+    const double qv = (c < m) ? R * u : 0.0;
+    Q[i * ldq + c] = qv;
+    if (c < m) dot = fma(qv, w[c], dot);
+  }
+  dot = wave_sum(dot);
+  if (lane == 0) {
+    const double* ch = chat + (j * mc + mp) * kSStride;
+    double u = X[k * ldx + mp];
+#pragma unroll
+    for (int q = 0; q < D; ++q) u = fma(hk[q], ch[q], u);
+    mean[i] = ym[k] - R * u + dot;
+  }
+}
+
+// ---------------------------------------------------------------------------- GEMM  C = A B^T
+// A: rows x K (row-major, lda), B: cols x K (row-major, ldb); 128 x 128 tile per 256-thread
+// block (2 x 2 waves of 4 x 4 v_mfma_f64_16x16x4_f64), K-step 16 through LDS (k-major,
+// padded rows: conflict-free fragment reads, see k_gram.hip).
+// Epilogues: mode 0: C written (ldc) + rowsq[colblock][row] = sum_c C^2 over the tile;
+//            mode 1: MC statistics over the tile's first `valid_cols` columns:
+//                    out0[row] = base[row] + mean_c C, out1[row] = Bessel std_c C.
+constexpr int kPT = 128, kPBK = 16, kPLds = 144;
+
+__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
+    const double* __restrict__ A, int64_t lda, const double* __restrict__ B, int64_t ldb,
+    int64_t rows, int64_t cols, int64_t K, int mode, double* __restrict__ C, int64_t ldc,
+    double* __restrict__ rowsq, int64_t valid_cols, const double* __restrict__ base,
+    double* __restrict__ out0, double* __restrict__ out1) {
+  __shared__ __attribute__((aligned(16))) double smem[2 * 2 * kPBK * kPLds + 2 * 128 * 2];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+  const int64_t r0 = (int64_t)blockIdx.x * kPT, c0 = (int64_t)blockIdx.y * kPT;
+  // staging: thread t loads row (t >> 1) of the A / B tile, k offset (t & 1) * 8, 8 doubles
+  const int srow = tid >> 1, sk = (tid & 1) * 8;
+  const int64_t arow = r0 + srow, brow = c0 + srow;
+  const bool av = arow < rows, bv = brow < cols;
+  double ra[8], rb[8];
+  // branch-free loads: indices clamped, out-of-range elements masked after the load
+  const int64_t arc = av ? arow : rows - 1, brc = bv ? brow : cols - 1;
+  auto load = [&](int64_t k0) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const int64_t kk = k0 + sk + q;
+      const int64_t kc = kk < K ? kk : K - 1;
+      ra[q] = A[arc * lda + kc] * ((av && kk < K) ? 1.0 : 0.0);
+      rb[q] = B[brc * ldb + kc] * ((bv && kk < K) ? 1.0 : 0.0);
+    }
+  };
+  auto store = [&](int buf) {
+    double* la = smem + (buf * 2 + 0) * kPBK * kPLds;
+    double* lb = smem + (buf * 2 + 1) * kPBK * kPLds;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      la[(sk + q) * kPLds + srow] = ra[q];
+      lb[(sk + q) * kPLds + srow] = rb[q];
+    }
+  };
+  d4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[a][c] = d4{0.0, 0.0, 0.0, 0.0};
+  const int nsteps = (int)((K + kPBK - 1) / kPBK);
+  load(0);
+  store(0);
+  __syncthreads();
+  const int frow = lane >> 4, fcol = lane & 15;
+  for (int s = 0; s < nsteps; ++s) {
+    const int buf = s & 1;
+    const bool more = s + 1 < nsteps;
+    if (more) load((int64_t)(s + 1) * kPBK);
+    const double* la = smem + (buf * 2 + 0) * kPBK * kPLds;
+    const double* lb = smem + (buf * 2 + 1) * kPBK * kPLds;
+#pragma unroll
+    for (int ks = 0; ks < kPBK / 4; ++ks) {
+      double fa[4], fb[4];
+      const int kr = ks * 4 + frow;
+#pragma unroll
+      for (int a = 0; a < 4; ++a) fa[a] = la[kr * kPLds + wr * 64 + a * 16 + fcol];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) fb[c] = lb[kr * kPLds + wc * 64 + c * 16 + fcol];
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[c], acc[a][c], 0, 0, 0);
+    }
+    if (more) store(buf ^ 1);
+    __syncthreads();
+  }
+  // epilogue: per-lane partial row reductions over this wave's 64 columns
+  double* red = smem + 2 * 2 * kPBK * kPLds;   // [2 (wc)][128 rows] x 2 quantities
+  double s1[4][4], s2[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double p = 0.0, p2 = 0.0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int64_t col = c0 + wc * 64 + c * 16 + fcol;
+        const double v = acc[a][c][r];
+        const bool ok = (mode == 0) ? (col < cols) : (col - c0 < valid_cols);
+        if (ok) { p += v; p2 = fma(v, v, p2); }
+        if (mode == 0) {
+          const int64_t row = r0 + wr * 64 + a * 16 + frow + 4 * r;
+          if (C && row < rows && col < cols) C[row * ldc + col] = v;
+        }
+      }
+      s1[a][r] = p;
+      s2[a][r] = p2;
+    }
+  // reduce across the 16 lanes sharing a row (fcol)
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) {
+        s1[a][r] += __shfl_xor(s1[a][r], off, 64);
+        s2[a][r] += __shfl_xor(s2[a][r], off, 64);
+      }
+    }
+  if (fcol == 0) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rl = wr * 64 + a * 16 + frow + 4 * r;
+        red[(wc * 128 + rl) * 2 + 0] = s1[a][r];
+        red[(wc * 128 + rl) * 2 + 1] = s2[a][r];
+      }
+  }
+  __syncthreads();
+  if (tid < 128) {
+    const int64_t row = r0 + tid;
+    if (row < rows) {
+      const double t1 = red[(0 * 128 + tid) * 2 + 0] + red[(1 * 128 + tid) * 2 + 0];
+      const double t2 = red[(0 * 128 + tid) * 2 + 1] + red[(1 * 128 + tid) * 2 + 1];
+      if (mode == 0) {
+        rowsq[(int64_t)blockIdx.y * rows + row] = t2;
+      } else {
+        // MC: f_s = base + F_s; Bessel-corrected std over the valid_cols samples
+        const double S = (double)valid_cols;
+        const double mu = t1 / S;
+        const double var = (t2 - S * mu * mu) / (S - 1.0);
+        out0[row] = base[row] + mu;
+        out1[row] = sqrt(var > 0.0 ? var : 0.0);
+      }
+    }
+  }
+}
+
+// var_i = sum over column blocks of rowsq; std = sqrt(var)
+__global__ void rowsq_finish(const double* __restrict__ rowsq, int64_t rows, int nblk,
+                             double* __restrict__ std_out) {
+  const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
+  if (i >= rows) return;
+  double s = 0.0;
+  for (int b = 0; b < nblk; ++b) s += rowsq[(int64_t)b * rows + i];
+  std_out[i] = sqrt(s);
+}
+
+// ---------------------------------------------------------------------------- normal draws
+// xi[s * ld + m] ~ N(0, 1) for s < S, m < M (zero beyond), from a counter-based hash
+// (splitmix64) + Box-Muller: reproducible for a given seed, independent of launch geometry.
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__global__ void normal_kernel(double* __restrict__ xi, int64_t ld, int64_t S, int64_t M,
+                              int64_t Sp, uint64_t seed) {
+  const int64_t e = blockIdx.x * (int64_t)256 + threadIdx.x;
+  if (e >= Sp * ld) return;
+  const int64_t s = e / ld, m = e % ld;
+  double v = 0.0;
+  if (s < S && m < M) {
+    const uint64_t a = splitmix64(seed ^ splitmix64((uint64_t)e * 2 + 1));
+    const uint64_t b = splitmix64(a ^ 0xD1B54A32D192ED03ull);
+    const double u1 = ((double)(a >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+    const double u2 = ((double)(b >> 11)) * (1.0 / 9007199254740992.0);
+    v = sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
+  }
+  xi[e] = v;
+}
+
+}  // namespace gpar
+
+// ============================================================================ launch wrappers
+#include "launch.hpp"
+
+namespace gpar {
+
+void launch_merge_side(hipStream_t st, const double* ts, int64_t ns, const double* other,
+                       int64_t no, int is_test, const double* ys, double rval, const double* vs,
+                       int64_t ldvs, int d, double* tm, double* ym, double* rm, double* vm,
+                       int64_t ldvm, int64_t* pos_out) {
+  if (ns <= 0) return;
+  merge_side<<<(unsigned)((ns + 255) / 256), 256, 0, st>>>(ts, ns, other, no, is_test, ys, rval, vs,
+                                                           ldvs, d, tm, ym, rm, vm, ldvm, pos_out);
+}
+
+void launch_predict_rows(hipStream_t st, int sdim, const double* X, int64_t ldx, const double* h,
+                         const double* chat, int64_t mc, int64_t mp, int64_t m, int L,
+                         const int64_t* pos, int64_t nstar, const double* rm, const double* ym,
+                         const double* w, double* Q, int64_t ldq, double* mean) {
+  const unsigned nb = (unsigned)((nstar + 3) / 4);
+  switch (sdim) {
+    case 1: predict_rows<1><<<nb, 256, 0, st>>>(X, ldx, h, chat, mc, mp, m, L, pos, nstar, rm, ym, w, Q, ldq, mean); break;
+    case 2: predict_rows<2><<<nb, 256, 0, st>>>(X, ldx, h, chat, mc, mp, m, L, pos, nstar, rm, ym, w, Q, ldq, mean); break;
+    default: predict_rows<3><<<nb, 256, 0, st>>>(X, ldx, h, chat, mc, mp, m, L, pos, nstar, rm, ym, w, Q, ldq, mean); break;
+  }
+}
+
+void launch_gemm_nt(hipStream_t st, const double* A, int64_t lda, const double* B, int64_t ldb,
+                    int64_t rows, int64_t cols, int64_t K, int mode, double* C, int64_t ldc,
+                    double* rowsq, int64_t valid_cols, const double* base, double* out0,
+                    double* out1) {
+  dim3 grid((unsigned)((rows + kPT - 1) / kPT), (unsigned)((cols + kPT - 1) / kPT));
+  gemm_nt_kernel<<<grid, 256, 0, st>>>(A, lda, B, ldb, rows, cols, K, mode, C, ldc, rowsq,
+                                       valid_cols, base, out0, out1);
+}
+
+void launch_rowsq_finish(hipStream_t st, const double* rowsq, int64_t rows, int nblk,
+                         double* std_out) {
+  rowsq_finish<<<(unsigned)((rows + 255) / 256), 256, 0, st>>>(rowsq, rows, nblk, std_out);
+}
+
+void launch_normal(hipStream_t st, double* xi, int64_t ld, int64_t S, int64_t M, int64_t Sp,
+                   uint64_t seed) {
+  normal_kernel<<<(unsigned)((Sp * ld + 255) / 256), 256, 0, st>>>(xi, ld, S, M, Sp, seed);
+}
+
+}  // namespace gpar

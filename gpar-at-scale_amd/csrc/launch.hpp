@@ -54,6 +54,15 @@ struct FinishJobHost {
   double* me;
 };
 
+struct TrsvJobHost {
+  const double* L;
+  int64_t ld;
+  int m;
+  const double* b;
+  double* x;
+  int trans;
+};
+
 struct GramPlan {
   int ntb = 0, ntiles = 0, nsplit = 0;
   int64_t rows_per_split = 0;
@@ -77,10 +86,19 @@ void launch_whiten_kfu(hipStream_t st, int time_kind, int out_kind, const double
 void launch_whiten_vec(hipStream_t st, int sdim, const double* rec, int64_t recstride,
                        const double* y, int64_t ldy, int64_t n, int L, int64_t nch, int nchains,
                        double* alpha, int64_t lda, double* send, int64_t sendstride, int64_t mc,
-                       int64_t col);
+                       int64_t col, int64_t astride = 1);
+int carry_group_size(int64_t nch);
+// gend/gin: nchains * ngroups * mc * 4 doubles; psi: nchains * ngroups * sdim^2 doubles
 void launch_carry(hipStream_t st, int sdim, const double* phi, int64_t phistride,
                   const double* send, double* cin, int64_t sstride, int64_t nch, int64_t mc,
-                  int64_t ncols, int nchains);
+                  int64_t ncols, int nchains, double* gend, double* gin, double* psi,
+                  bool rev = false);
+// adjoint (backward) pass helpers
+void launch_gains_adjoint(hipStream_t st, int sdim, const double* rec, int64_t n, int L,
+                          int64_t nch, int nchains, double* h);
+void launch_adjoint_local(hipStream_t st, int sdim, double* X, int64_t ldx, int64_t ncols,
+                          const double* rec, const double* g, const double* cin, int64_t mc,
+                          int64_t n, int L, int64_t nch, double* bend);
 int64_t vec_fix_blocks(int64_t n);
 void launch_vec_fix(hipStream_t st, int sdim, double* alpha, int64_t lda, const double* g,
                     int64_t gstride, const double* cin, int64_t sstride, int64_t mc,
@@ -107,5 +125,24 @@ void launch_gram_small(hipStream_t st, const double* X, int64_t ldx, int m, doub
 void launch_lower_to_upper_colmajor(hipStream_t st, const double* L, int64_t ldl, int m,
                                     double* U);
 void launch_eye(hipStream_t st, double* A, int64_t ld, int m);
+void launch_trsv(hipStream_t st, const TrsvJobHost* jobs_dev, int njobs);
+
+// k_predict.hip
+void launch_merge_side(hipStream_t st, const double* ts, int64_t ns, const double* other,
+                       int64_t no, int is_test, const double* ys, double rval, const double* vs,
+                       int64_t ldvs, int d, double* tm, double* ym, double* rm, double* vm,
+                       int64_t ldvm, int64_t* pos_out);
+void launch_predict_rows(hipStream_t st, int sdim, const double* X, int64_t ldx, const double* h,
+                         const double* chat, int64_t mc, int64_t mp, int64_t m, int L,
+                         const int64_t* pos, int64_t nstar, const double* rm, const double* ym,
+                         const double* w, double* Q, int64_t ldq, double* mean);
+void launch_gemm_nt(hipStream_t st, const double* A, int64_t lda, const double* B, int64_t ldb,
+                    int64_t rows, int64_t cols, int64_t K, int mode, double* C, int64_t ldc,
+                    double* rowsq, int64_t valid_cols, const double* base, double* out0,
+                    double* out1);
+void launch_rowsq_finish(hipStream_t st, const double* rowsq, int64_t rows, int nblk,
+                         double* std_out);
+void launch_normal(hipStream_t st, double* xi, int64_t ld, int64_t S, int64_t M, int64_t Sp,
+                   uint64_t seed);
 
 }  // namespace gpar

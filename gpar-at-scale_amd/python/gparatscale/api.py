@@ -277,3 +277,55 @@ def lgssm_logpdf_batch(t, Y, theta, kernel="matern52", device=0):
     ctx.check(lib.gpar_lgssm_logpdf(ctx.h, nch, n, tp, _ptr(Y), n, _kernel_id(kernel), _ptr(th),
                                     _lib.GPAR_MEM_HOST, _ptr(out)))
     return out
+
+
+# ----------------------------------------------------------------------------- prediction
+def predict_scaled(input_locations, pseudo_input_locations, time_loc, outputs, theta,
+                   inference_time_loc, inference_input_locations, out_kernel="matern52",
+                   time_kernel="matern52", mode="analytic", samples=100, seed=0, device=0):
+    """Prediction half of get_gpar_scaled_predictions (gpar_scaled_inference.jl:63-135) at a
+    given theta.  Returns (mean, std) at the inference locations, in their input order.
+    mode="mc" reproduces the reference's 100-sample Monte Carlo estimator; "analytic" is its
+    S -> infinity limit."""
+    ctx = context(device)
+    lib = _lib.load()
+    p, keep = make_problem(input_locations, pseudo_input_locations, time_loc, outputs,
+                           out_kernel, time_kernel)
+    th = np.ascontiguousarray(np.asarray(theta, dtype=np.float64).reshape(5))
+    md = _lib.GPAR_PREDICT_MC if mode == "mc" else _lib.GPAR_PREDICT_ANALYTIC
+    if p.mem == _lib.GPAR_MEM_DEVICE:
+        import torch
+        vsp, ldvs, ns, ds = _dev_points(inference_input_locations, keep)
+        tsp = _dev_vec(inference_time_loc, keep)
+        mean = torch.empty(ns, dtype=torch.float64, device=inference_time_loc.device)
+        std = torch.empty(ns, dtype=torch.float64, device=inference_time_loc.device)
+        ctx.check(lib.gpar_predict(ctx.h, C.byref(p), _ptr(th), ns, tsp, vsp, ldvs, md,
+                                   int(samples), int(seed), mean.data_ptr(), std.data_ptr()))
+        return mean, std
+    vsp, ldvs, ns, ds = _host_points(inference_input_locations, keep)
+    tsp = _host_vec(inference_time_loc, keep)
+    if ds != p.d:
+        raise _lib.DomainError(_lib.GPAR_ERR_ARG, "inference inputs must have the training dimension")
+    mean = np.zeros(ns)
+    std = np.zeros(ns)
+    ctx.check(lib.gpar_predict(ctx.h, C.byref(p), _ptr(th), ns, tsp, vsp, ldvs, md, int(samples),
+                               int(seed), _ptr(mean), _ptr(std)))
+    return mean, std
+
+
+def get_gpar_scaled_predictions(input_locations, pseudo_input_locations, time_loc, outputs,
+                                inference_time_loc, inference_input_locations,
+                                out_kernel_structure="matern52", time_kernel_structure="matern52",
+                                i_log_time_l=None, i_log_time_var=None, i_log_out_l=None,
+                                i_log_out_var=None, i_log_noise_sigma=None,
+                                optimization_time_limit=DEFAULT_TIME_LIMIT, max_evals=0,
+                                mode="mc", samples=100, seed=0, rng=None, device=0):
+    """gpar_scaled_inference.jl:20-136: fit theta (Matern52 hard-coded for the fit, :48-49),
+    then predict; returns (mean, std) like the reference."""
+    theta = get_optim_scaled_gpar_params(
+        input_locations, pseudo_input_locations, time_loc, outputs, "matern52", "matern52",
+        i_log_time_l, i_log_time_var, i_log_out_l, i_log_out_var, i_log_noise_sigma,
+        optimization_time_limit, max_evals, rng=rng, device=device)
+    return predict_scaled(input_locations, pseudo_input_locations, time_loc, outputs, theta,
+                          inference_time_loc, inference_input_locations, out_kernel_structure,
+                          time_kernel_structure, mode, samples, seed, device)

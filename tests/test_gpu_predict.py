@@ -1,0 +1,77 @@
+"""GPU parity of scaled-GPAR prediction (gpar_scaled_inference.jl:63-135) and of the
+Nelder-Mead fit (dtc.jl:11-77) against the oracle."""
+import numpy as np
+import pytest
+
+from oracle import gpar_oracle as O
+
+pytestmark = pytest.mark.gpu
+G = pytest.importorskip("gparatscale")
+
+
+def _data(n, P, M, seed, n_star, gaps=0):
+    t, Y = O.synthetic_gpar(n, P, seed=seed, noise=0.3, gaps=gaps, gap_len=max(1, n // 25))
+    V = Y[:, : P - 1].T
+    y = Y[:, P - 1]
+    Z = O.pick_pseudo_inputs(V, M, seed + 3)
+    rng = np.random.default_rng(seed + 11)
+    ts = np.sort(rng.uniform(t[0] - 1.0, t[-1] + 2.0, n_star))
+    Vs = np.vstack([np.interp(ts, t, V[q]) for q in range(P - 1)])
+    return t, V, Z, y, ts, Vs
+
+
+# q(u) factors Cuu with no jitter (gpar_scaled_inference.jl:157-159), so agreement between
+# any two fp64 implementations is limited by cond(Cuu) * eps; the cases below keep
+# cond(Cuu) <= ~1e7 so the 1e-8 / 1e-7 tolerances are meaningful.
+@pytest.mark.parametrize("n,P,M,kernels,l_o", [(400, 3, 30, ("matern52", "matern52"), 1.2),
+                                               (700, 4, 140, ("eq", "matern32"), 0.25),
+                                               (300, 2, 20, ("matern32", "matern12"), 0.3)])
+def test_predict_analytic_matches_oracle(n, P, M, kernels, l_o):
+    t, V, Z, y, ts, Vs = _data(n, P, M, 5, 150, gaps=2)
+    theta = (1.4, 0.9, l_o, 1.1, 0.3)
+    ok, tk = kernels
+    m_ref, s_ref = O.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, ok, tk, "analytic")
+    m, s = G.predict_scaled(V, Z, t, y, theta, ts, Vs, ok, tk, mode="analytic")
+    np.testing.assert_allclose(m, m_ref, rtol=1e-8, atol=1e-9 * np.abs(m_ref).max())
+    np.testing.assert_allclose(s, s_ref, rtol=1e-7, atol=1e-9 * np.abs(s_ref).max())
+
+
+def test_predict_unsorted_and_coincident_test_points():
+    t, V, Z, y, ts, Vs = _data(350, 3, 25, 9, 120)
+    ts = np.concatenate([ts, t[::37]])            # test times coinciding with train times
+    Vs = np.hstack([Vs, V[:, ::37]])
+    perm = np.random.default_rng(1).permutation(len(ts))
+    ts, Vs = ts[perm], Vs[:, perm]
+    theta = (0.9, 1.1, 0.8, 1.3, 0.25)
+    m_ref, s_ref = O.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, mode="analytic")
+    m, s = G.predict_scaled(V, Z, t, y, theta, ts, Vs, mode="analytic")
+    np.testing.assert_allclose(m, m_ref, rtol=1e-8, atol=1e-9 * np.abs(m_ref).max())
+    np.testing.assert_allclose(s, s_ref, rtol=1e-7, atol=1e-9 * np.abs(s_ref).max())
+
+
+def test_predict_mc_statistically_matches_analytic():
+    """MC mode (reference-faithful, 100 samples): |mean_mc - mean| <= 5 std / sqrt(S)."""
+    t, V, Z, y, ts, Vs = _data(500, 3, 40, 13, 200)
+    theta = (1.2, 1.0, 1.0, 1.2, 0.3)
+    m, s = G.predict_scaled(V, Z, t, y, theta, ts, Vs, mode="analytic")
+    mm, sm = G.predict_scaled(V, Z, t, y, theta, ts, Vs, mode="mc", samples=100, seed=7)
+    S = 100
+    assert np.all(np.abs(mm - m) <= 5.0 * s / np.sqrt(S) + 1e-12)
+    # sample std within chi-distribution tolerance of the analytic std
+    ratio = sm / np.maximum(s, 1e-300)
+    assert np.median(np.abs(ratio - 1.0)) < 0.15
+    mm2, sm2 = G.predict_scaled(V, Z, t, y, theta, ts, Vs, mode="mc", samples=100, seed=7)
+    np.testing.assert_array_equal(mm, mm2)    # seeded -> reproducible
+
+
+def test_fit_matches_oracle_nelder_mead():
+    """Same NM state machine on both sides: identical trajectories up to fp64 ties."""
+    t, V, Z, y, _, _ = _data(300, 3, 25, 17, 1)
+    x0 = [0.1, 0.2, 0.0, 0.1, -1.5]
+    th_ref, nm = O.get_optim_scaled_gpar_params(V, Z, t, y, log_theta0=x0, max_evals=40,
+                                                return_nm=True)
+    th = G.get_optim_scaled_gpar_params(V, Z, t, y, i_log_time_l=x0[0], i_log_time_var=x0[1],
+                                        i_log_out_l=x0[2], i_log_out_var=x0[3],
+                                        i_log_noise_sigma=x0[4], max_evals=40,
+                                        optimization_time_limit=0)
+    np.testing.assert_allclose(th, th_ref, rtol=1e-6)
