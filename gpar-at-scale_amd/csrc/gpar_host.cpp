@@ -587,6 +587,53 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
   }
 }
 
+
+// --------------------------------------------------------------------------- temporal chains: smoothing
+// Smoothed marginals of f for chains sharing the grid t (device pointers): mean = y - R Sigma^-1 y,
+// var = RTS P^s[0,0].  noise: per-step observation variance (negative = chain sigma^2) or null.
+static void chains_smooth(gpar_ctx* c, int nchains, int64_t n, const double* t, const double* y,
+                          int64_t ldy, const double* noise, int sdim,
+                          const std::vector<ChainParamsHost>& cps, double* mean, double* var,
+                          int64_t ldo) {
+  const int64_t nch = (n + kChunk - 1) / kChunk;
+  GainsOut g = run_gains(c, sdim, t, n, cps, noise, /*want_pf=*/true, "sm");
+  double* u = ws<double>(c, "sm_u", (size_t)nchains * n);
+  double* send = ws<double>(c, "sm_send", (size_t)nchains * nch * 4);
+  double* cin = ws<double>(c, "sm_cin", (size_t)nchains * nch * 4);
+  double* bend = ws<double>(c, "sm_bend", (size_t)nchains * nch * 4);
+  double* chat = ws<double>(c, "sm_chat", (size_t)nchains * nch * 4);
+  double* h = ws<double>(c, "sm_h", (size_t)nchains * n * 4);
+  const int64_t ss = nch * 4;
+  launch_whiten_vec(c->stream, sdim, g.rec, g.recstride, y, ldy, n, kChunk, nch, nchains, u, n,
+                    send, ss, 1, 0);
+  run_carry(c, sdim, g.phi, g.phistride, send, cin, ss, nch, 1, 1, nchains, "smf");
+  launch_gains_adjoint(c->stream, sdim, g.rec, n, kChunk, nch, nchains, h);
+  launch_adjoint_local(c->stream, sdim, u, 1, 1, g.rec, g.g, cin, 1, n, kChunk, nch, bend, nchains,
+                       n, ss);
+  run_carry(c, sdim, g.phi, g.phistride, bend, chat, ss, nch, 1, 1, nchains, "smb", true);
+  auto* dcps = ws<ChainParamsHost>(c, "sm_cps2", nchains);
+  h2d(c, dcps, cps.data(), nchains);
+  launch_smooth_mean(c->stream, sdim, u, h, chat, ss, y, ldy, noise, dcps, n, kChunk, nchains, mean,
+                     ldo);
+  double* vloc = ws<double>(c, "sm_vloc", (size_t)nchains * n);
+  double* gam = ws<double>(c, "sm_gam", (size_t)nchains * n * 4);
+  double* agg = ws<double>(c, "sm_agg", (size_t)nchains * nch * 2 * sdim * sdim);
+  double* phat = ws<double>(c, "sm_phat", (size_t)nchains * nch * sdim * sdim);
+  launch_cov_smooth(c->stream, sdim, t, g.rec, g.pf, dcps, n, kChunk, nch, nchains, vloc, gam, agg,
+                    phat, var, ldo);
+  check_launch("chains_smooth");
+}
+
+static std::vector<ChainParamsHost> chain_params(const double* theta, int nchains) {
+  std::vector<ChainParamsHost> cps(nchains);
+  for (int i = 0; i < nchains; ++i) {
+    const double l = theta[3 * i], pv = theta[3 * i + 1], ns = theta[3 * i + 2];
+    ARGCHECK(l > 0 && pv > 0 && ns > 0 && std::isfinite(l + pv + ns), "theta entries must be positive");
+    cps[i] = {1.0 / l, l, pv * pv, ns * ns};
+  }
+  return cps;
+}
+
 static double unpack(double p) { return std::exp(p) + 1e-3; }
 
 }  // namespace gpar
@@ -827,7 +874,37 @@ int32_t gpar_predict(gpar_ctx* ctx, const gpar_problem* prob, const double* thet
 int32_t gpar_lgssm_smooth(gpar_ctx* ctx, int32_t nchains, int64_t n, const double* t,
                           const double* y, int64_t ldy, const double* noise, int32_t kernel,
                           const double* theta, int32_t mem, double* mean, double* var) {
-  return not_yet(ctx, "gpar_lgssm_smooth");
+  API_BEGIN(ctx)
+  ARGCHECK(nchains >= 1 && n >= 1 && t && y && theta && mean && var, "bad argument");
+  ARGCHECK(ldy >= n, "ldy must be >= n");
+  const int sdim = sde_dim(kernel);
+  std::vector<ChainParamsHost> cps = chain_params(theta, nchains);
+  const double *dt = t, *dy = y, *dn = noise;
+  double *dm = mean, *dv = var;
+  if (mem == GPAR_MEM_HOST) {
+    check_sorted_host(t, n);
+    double* tt = ws<double>(ctx, "ls_t", n);
+    double* yy = ws<double>(ctx, "ls_y", (size_t)nchains * n);
+    h2d(ctx, tt, t, n);
+    HIPCHECK(hipMemcpy2DAsync(yy, n * sizeof(double), y, ldy * sizeof(double), n * sizeof(double), nchains, hipMemcpyHostToDevice, ctx->stream));
+    if (noise) {
+      double* nn = ws<double>(ctx, "ls_noise", n);
+      h2d(ctx, nn, noise, n);
+      dn = nn;
+    }
+    dt = tt;
+    dy = yy;
+    dm = ws<double>(ctx, "ls_mean", (size_t)nchains * n);
+    dv = ws<double>(ctx, "ls_var", (size_t)nchains * n);
+  }
+  chains_smooth(ctx, nchains, n, dt, dy, mem == GPAR_MEM_HOST ? n : ldy, dn, sdim, cps, dm, dv,
+                mem == GPAR_MEM_HOST ? n : ldy);
+  if (mem == GPAR_MEM_HOST) {
+    HIPCHECK(hipMemcpy2DAsync(mean, ldy * sizeof(double), dm, n * sizeof(double), n * sizeof(double), nchains, hipMemcpyDeviceToHost, ctx->stream));
+    HIPCHECK(hipMemcpy2DAsync(var, ldy * sizeof(double), dv, n * sizeof(double), n * sizeof(double), nchains, hipMemcpyDeviceToHost, ctx->stream));
+  }
+  sync(ctx);
+  API_END(ctx)
 }
 
 int32_t gpar_sde_predictions(gpar_ctx* ctx, int32_t nchains, int64_t n, const double* t,
@@ -835,7 +912,98 @@ int32_t gpar_sde_predictions(gpar_ctx* ctx, int32_t nchains, int64_t n, const do
                              int32_t kernel, const double* log_theta0,
                              const gpar_fit_options* opts, int32_t mem, double* theta_out,
                              double* mean, double* var) {
-  return not_yet(ctx, "gpar_sde_predictions");
+  API_BEGIN(ctx)
+  ARGCHECK(nchains >= 1 && n >= 1 && n_star >= 1 && t && y && t_star && log_theta0 && theta_out &&
+               mean && var, "bad argument");
+  ARGCHECK(ldy >= n, "ldy must be >= n");
+  const int sdim = sde_dim(kernel);
+  gpar_fit_options o{0, 1000, 1e-8, 0.0};
+  if (opts) o = *opts;
+  // ---- inputs on device; test times ascending (host: stable-sorted here, un-permuted after)
+  const double *dt = t, *dy = y, *dts = t_star;
+  int64_t ldyd = ldy;
+  std::vector<int64_t> perm;
+  if (mem == GPAR_MEM_HOST) {
+    check_sorted_host(t, n);
+    double* tt = ws<double>(ctx, "sp_t", n);
+    double* yy = ws<double>(ctx, "sp_y", (size_t)nchains * n);
+    h2d(ctx, tt, t, n);
+    HIPCHECK(hipMemcpy2DAsync(yy, n * sizeof(double), y, ldy * sizeof(double), n * sizeof(double), nchains, hipMemcpyHostToDevice, ctx->stream));
+    perm.resize(n_star);
+    for (int64_t i = 0; i < n_star; ++i) perm[i] = i;
+    std::stable_sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) { return t_star[a] < t_star[b]; });
+    std::vector<double> tsh(n_star);
+    for (int64_t i = 0; i < n_star; ++i) tsh[i] = t_star[perm[i]];
+    double* ts = ws<double>(ctx, "sp_ts", n_star);
+    h2d(ctx, ts, tsh.data(), n_star);
+    sync(ctx);
+    dt = tt; dy = yy; dts = ts; ldyd = n;
+  }
+  // ---- NM fit of (l, process_var, noise_sigma) per chain on -logpdf (temporal_gp_inference.jl:286-300)
+  std::vector<NelderMead> nm;
+  nm.reserve(nchains);
+  for (int i = 0; i < nchains; ++i)
+    nm.emplace_back(std::vector<double>(log_theta0 + 3 * i, log_theta0 + 3 * i + 3), o.max_evals,
+                    o.max_iterations, o.g_tol, o.time_limit);
+  double* ysub = ws<double>(ctx, "sp_ysub", (size_t)nchains * n);
+  while (true) {
+    std::vector<int> act;
+    for (int i = 0; i < nchains; ++i)
+      if (!nm[i].done()) act.push_back(i);
+    if (act.empty()) break;
+    std::vector<double> th(3 * act.size());
+    for (size_t a = 0; a < act.size(); ++a) {
+      const auto& x = nm[act[a]].ask();
+      for (int q = 0; q < 3; ++q) th[3 * a + q] = unpack(x[q]);
+      HIPCHECK(hipMemcpyAsync(ysub + a * n, dy + (size_t)act[a] * ldyd, n * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    std::vector<double> lml(act.size());
+    chains_logpdf(ctx, (int)act.size(), n, dt, ysub, n, kernel, sdim, th.data(), lml.data());
+    for (size_t a = 0; a < act.size(); ++a) {
+      double f = -lml[a];
+      if (!std::isfinite(f)) f = INFINITY;
+      nm[act[a]].tell(f);
+    }
+  }
+  std::vector<double> theta(3 * nchains);
+  for (int i = 0; i < nchains; ++i)
+    for (int q = 0; q < 3; ++q) theta[3 * i + q] = theta_out[3 * i + q] = unpack(nm[i].x_min()[q]);
+  // ---- merged grid: y* = y (train) / 0 (test), R = sigma_c^2 (train, -1 flag) / 1e10 (test)
+  const int64_t nt = n + n_star;
+  double* tm = ws<double>(ctx, "sp_tm", nt);
+  double* ym = ws<double>(ctx, "sp_ym", (size_t)nchains * nt);
+  double* rm = ws<double>(ctx, "sp_rm", nt);
+  double* dummy = ws<double>(ctx, "sp_dummy", nt);
+  int64_t* ptr = ws<int64_t>(ctx, "sp_ptr", n);
+  int64_t* pts = ws<int64_t>(ctx, "sp_pts", n_star);
+  launch_merge_side(ctx->stream, dt, n, dts, n_star, 0, nullptr, -1.0, dt, 1, 0, tm, dummy, rm, dummy, 1, ptr);
+  launch_merge_side(ctx->stream, dts, n_star, dt, n, 1, nullptr, 1e10, dts, 1, 0, tm, dummy, rm, dummy, 1, pts);
+  HIPCHECK(hipMemsetAsync(ym, 0, (size_t)nchains * nt * sizeof(double), ctx->stream));
+  launch_scatter_chains(ctx->stream, dy, ldyd, n, ptr, ym, nt, nchains);
+  double* mm = ws<double>(ctx, "sp_mean", (size_t)nchains * nt);
+  double* vv = ws<double>(ctx, "sp_var", (size_t)nchains * nt);
+  chains_smooth(ctx, nchains, nt, tm, ym, nt, rm, sdim, chain_params(theta.data(), nchains), mm, vv, nt);
+  double* om = ws<double>(ctx, "sp_om", (size_t)nchains * n_star);
+  double* ov = ws<double>(ctx, "sp_ov", (size_t)nchains * n_star);
+  launch_gather_chains(ctx->stream, mm, nt, n_star, pts, om, n_star, nchains);
+  launch_gather_chains(ctx->stream, vv, nt, n_star, pts, ov, n_star, nchains);
+  check_launch("sde_predictions");
+  if (mem == GPAR_MEM_DEVICE) {
+    HIPCHECK(hipMemcpyAsync(mean, om, (size_t)nchains * n_star * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    HIPCHECK(hipMemcpyAsync(var, ov, (size_t)nchains * n_star * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    sync(ctx);
+  } else {
+    std::vector<double> hm((size_t)nchains * n_star), hv((size_t)nchains * n_star);
+    d2h(ctx, hm.data(), om, hm.size());
+    d2h(ctx, hv.data(), ov, hv.size());
+    sync(ctx);
+    for (int b = 0; b < nchains; ++b)
+      for (int64_t i = 0; i < n_star; ++i) {
+        mean[(size_t)b * n_star + perm[i]] = hm[(size_t)b * n_star + i];
+        var[(size_t)b * n_star + perm[i]] = hv[(size_t)b * n_star + i];
+      }
+  }
+  API_END(ctx)
 }
 
 int32_t gpar_exact_logpdf(gpar_ctx* ctx, int64_t n, int64_t dx, const double* x, int64_t ldx,

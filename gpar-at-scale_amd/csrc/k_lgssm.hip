@@ -78,6 +78,16 @@ __device__ __forceinline__ void elem_combine(const Elem<D>& e1, const Elem<D>& e
   out = r;
 }
 
+// Observation noise of step k: the shared per-step vector when given (prediction grids: 1e10 at
+// test points, gpar_scaled_inference.jl:100-107), where a negative entry means "this chain's
+// own sigma^2" (train points of chains with different sigma, temporal_gp_inference.jl:310-313).
+__device__ __forceinline__ double step_noise(const double* __restrict__ noise, int64_t k,
+                                            const ChainParams& cp) {
+  if (!noise) return cp.r;
+  const double v = noise[k];
+  return v < 0.0 ? cp.r : v;
+}
+
 // Transition + process noise for step k of chain p (stationary start: tau_0 = 1).
 template <int D>
 __device__ __forceinline__ void step_model(const double* __restrict__ t, int64_t k,
@@ -171,9 +181,9 @@ __global__ __launch_bounds__(256) void gains_phase1(const double* __restrict__ t
   const int64_t k0 = j * L;
   const int64_t k1 = (k0 + L < n) ? k0 + L : n;
   Elem<D> acc, e;
-  step_elem<D>(t, k0, cp, noise ? noise[k0] : cp.r, acc);
+  step_elem<D>(t, k0, cp, step_noise(noise, k0, cp), acc);
   for (int64_t k = k0 + 1; k < k1; ++k) {
-    step_elem<D>(t, k, cp, noise ? noise[k] : cp.r, e);
+    step_elem<D>(t, k, cp, step_noise(noise, k, cp), e);
     elem_combine<D>(acc, e, acc);
   }
   elem_store<D>(agg + ((int64_t)p * nch + j) * (3 * D * D), acc);
@@ -281,7 +291,7 @@ __global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t
     for (int i = 0; i < D; ++i)
 #pragma unroll
       for (int q = 0; q < D; ++q) Pm[i][q] += Q[i][q];
-    const double R = noise ? noise[k] : cp.r;
+    const double R = step_noise(noise, k, cp);
     const double S = Pm[0][0] + R;
     const double rs = 1.0 / sqrt(S);
     double Kg[D];
@@ -650,9 +660,18 @@ __global__ __launch_bounds__(64) void adjoint_local(double* __restrict__ X, int6
                                                     int64_t ncols, const double* __restrict__ rec,
                                                     const double* __restrict__ g,
                                                     const double* __restrict__ cin, int64_t mc,
-                                                    int64_t n, int L, double* __restrict__ bend) {
+                                                    int64_t n, int L, double* __restrict__ bend,
+                                                    int64_t xstride, int64_t sstride) {
   constexpr int RS = Rec<D>::size;
   const int64_t j = blockIdx.x;
+  {
+    const int b = blockIdx.z;   // chain: gains (rec, g) are per chain, X / cin / bend strided
+    X += (int64_t)b * xstride;
+    rec += (int64_t)b * n * RS;
+    g += (int64_t)b * n * kGStride;
+    cin += (int64_t)b * sstride;
+    bend += (int64_t)b * sstride;
+  }
   const int64_t c = (int64_t)blockIdx.y * 64 + threadIdx.x;
   const bool act = c < ncols;
   const int64_t cc = act ? c : 0;
@@ -691,6 +710,170 @@ __global__ __launch_bounds__(64) void adjoint_local(double* __restrict__ X, int6
 #pragma unroll
     for (int i = 0; i < D; ++i) bend[(j * mc + c) * kSStride + i] = lam[i];
   }
+}
+
+// ---------------------------------------------------------------------------- smoothed mean of f
+// f_k = y_k - R_k (Sigma^{-1} y)_k   (S y = y - R Sigma^{-1} y), with
+// (Sigma^{-1} y)_k = u_loc_k + h_k . chat_{chunk(k)};  u_loc: adjoint output (contiguous per chain).
+template <int D>
+__global__ __launch_bounds__(256) void smooth_mean(const double* __restrict__ u,
+                                                   const double* __restrict__ h,
+                                                   const double* __restrict__ chat, int64_t sstride,
+                                                   const double* __restrict__ y, int64_t ldy,
+                                                   const double* __restrict__ noise,
+                                                   const ChainParams* __restrict__ cps, int64_t n,
+                                                   int L, double* __restrict__ mean, int64_t ldm) {
+  const int64_t k = blockIdx.x * (int64_t)256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (k >= n) return;
+  const int64_t j = k / L;
+  const double* hk = h + ((int64_t)b * n + k) * kGStride;
+  const double* ch = chat + (int64_t)b * sstride + j * kSStride;
+  double uu = u[(int64_t)b * n + k];
+#pragma unroll
+  for (int i = 0; i < D; ++i) uu = fma(hk[i], ch[i], uu);
+  const double R = step_noise(noise, k, cps[b]);
+  mean[(int64_t)b * ldm + k] = y[(int64_t)b * ldy + k] - R * uu;
+}
+
+// ---------------------------------------------------------------------------- smoothed covariance
+// RTS: P^s_k = G_k P^s_{k+1} G_k^T + C_k,  G_k = P_k A_{k+1}^T (P^-_{k+1})^{-1},
+// C_k = P_k - G_k P^-_{k+1} G_k^T  (G_{N-1} = 0, C_{N-1} = P_{N-1}).  Chunked: local from 0 at
+// each chunk end, P^s_k = local + Gamma_k Phat_j Gamma_k^T with Gamma_k = G_k ... G_{k1-1};
+// the per-chunk aggregate (local P^s at the chunk start, Gamma_{k0}) feeds a backward carry.
+// Only var_k = P^s_k[0,0] (the latent f, H = e1) is emitted.
+template <int D>
+__global__ __launch_bounds__(256) void cov_local(const double* __restrict__ t,
+                                                 const double* __restrict__ rec,
+                                                 const double* __restrict__ pf,
+                                                 const ChainParams* __restrict__ cps, int64_t n,
+                                                 int L, int64_t nch, double* __restrict__ vloc,
+                                                 double* __restrict__ gam,
+                                                 double* __restrict__ agg) {
+  constexpr int RS = Rec<D>::size;
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (j >= nch) return;
+  const ChainParams cp = cps[b];
+  const double* rp = rec + (int64_t)b * n * RS;
+  const double* pp = pf + (int64_t)b * n * D * D;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  double Ps[D][D], Gm[D][D];
+  mat_zero(Ps);
+  mat_eye(Gm);
+  for (int64_t k = k1 - 1; k >= k0; --k) {
+    double P[D][D];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) P[i][q] = pp[k * D * D + i * D + q];
+    double G[D][D], C[D][D];
+    if (k == n - 1) {
+      mat_zero(G);
+      mat_copy(P, C);
+    } else {
+      double A1[D][D], Q1[D][D], X[D][D], Pm[D][D], Pmi[D][D];
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) A1[i][q] = rp[(k + 1) * RS + i * D + q];
+      // Q_{k+1} = s Pinf - A Pinf A^T (same construction as step_model)
+      double Pinf[D][D];
+      sde_pinf<D>(cp.s, Pinf);
+      mat_mul(A1, Pinf, X);
+      mat_mul_bt(X, A1, Q1);
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) Q1[i][q] = Pinf[i][q] - Q1[i][q];
+      mat_mul(A1, P, X);
+      mat_mul_bt(X, A1, Pm);
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) Pm[i][q] += Q1[i][q];
+      mat_inv(Pm, Pmi);
+      mat_mul_bt(P, A1, X);        // P A^T
+      mat_mul(X, Pmi, G);          // G = P A^T Pm^{-1}
+      double GP[D][D], GPG[D][D];
+      mat_mul(G, Pm, GP);
+      mat_mul_bt(GP, G, GPG);
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) C[i][q] = P[i][q] - GPG[i][q];
+    }
+    double T[D][D], U[D][D];
+    mat_mul(G, Ps, T);
+    mat_mul_bt(T, G, U);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) Ps[i][q] = U[i][q] + C[i][q];
+    mat_mul(G, Gm, T);
+    mat_copy(T, Gm);
+    vloc[(int64_t)b * n + k] = Ps[0][0];
+#pragma unroll
+    for (int q = 0; q < D; ++q) gam[((int64_t)b * n + k) * kGStride + q] = Gm[0][q];
+  }
+  double* ag = agg + ((int64_t)b * nch + j) * (2 * D * D);
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      ag[i * D + q] = Ps[i][q];
+      ag[D * D + i * D + q] = Gm[i][q];
+    }
+}
+
+// Backward carry over chunks (one thread per chain): Phat_{J-1} = 0,
+// Phat_{j-1} = Ps_loc(j) + Gamma_j Phat_j Gamma_j^T.
+template <int D>
+__global__ void cov_carry(const double* __restrict__ agg, int64_t nch, int nchains,
+                          double* __restrict__ phat) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nchains) return;
+  double Ph[D][D];
+  mat_zero(Ph);
+  for (int64_t j = nch - 1; j >= 0; --j) {
+    double* o = phat + ((int64_t)b * nch + j) * (D * D);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) o[i * D + q] = Ph[i][q];
+    const double* ag = agg + ((int64_t)b * nch + j) * (2 * D * D);
+    double Gm[D][D], T[D][D], U[D][D];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) Gm[i][q] = ag[D * D + i * D + q];
+    mat_mul(Gm, Ph, T);
+    mat_mul_bt(T, Gm, U);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) Ph[i][q] = ag[i * D + q] + U[i][q];
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void cov_out(const double* __restrict__ vloc,
+                                               const double* __restrict__ gam,
+                                               const double* __restrict__ phat, int64_t n, int L,
+                                               int64_t nch, double* __restrict__ var, int64_t ldv) {
+  const int64_t k = blockIdx.x * (int64_t)256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (k >= n) return;
+  const int64_t j = k / L;
+  const double* gk = gam + ((int64_t)b * n + k) * kGStride;
+  const double* P = phat + ((int64_t)b * nch + j) * (D * D);
+  double v = vloc[(int64_t)b * n + k];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) v = fma(gk[i] * P[i * D + q], gk[q], v);
+  var[(int64_t)b * ldv + k] = v;
 }
 
 // ---------------------------------------------------------------------------- fix-up of a vector
@@ -870,9 +1053,32 @@ void launch_gains_adjoint(hipStream_t st, int sdim, const double* rec, int64_t n
 
 void launch_adjoint_local(hipStream_t st, int sdim, double* X, int64_t ldx, int64_t ncols,
                           const double* rec, const double* g, const double* cin, int64_t mc,
-                          int64_t n, int L, int64_t nch, double* bend) {
-  dim3 grid((unsigned)nch, (unsigned)((ncols + 63) / 64));
-  GPAR_DISPATCH_D(sdim, adjoint_local<DD><<<grid, 64, 0, st>>>(X, ldx, ncols, rec, g, cin, mc, n, L, bend));
+                          int64_t n, int L, int64_t nch, double* bend, int nchains,
+                          int64_t xstride, int64_t sstride) {
+  dim3 grid((unsigned)nch, (unsigned)((ncols + 63) / 64), (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, adjoint_local<DD><<<grid, 64, 0, st>>>(X, ldx, ncols, rec, g, cin, mc, n, L, bend, xstride, sstride));
+}
+
+void launch_smooth_mean(hipStream_t st, int sdim, const double* u, const double* h,
+                        const double* chat, int64_t sstride, const double* y, int64_t ldy,
+                        const double* noise, const ChainParamsHost* cps, int64_t n, int L,
+                        int nchains, double* mean, int64_t ldm) {
+  dim3 grid((unsigned)((n + 255) / 256), (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, smooth_mean<DD><<<grid, 256, 0, st>>>(u, h, chat, sstride, y, ldy, noise, reinterpret_cast<const ChainParams*>(cps), n, L, mean, ldm));
+}
+
+void launch_cov_smooth(hipStream_t st, int sdim, const double* t, const double* rec,
+                       const double* pf, const ChainParamsHost* cps, int64_t n, int L,
+                       int64_t nch, int nchains, double* vloc, double* gam, double* agg,
+                       double* phat, double* var, int64_t ldv) {
+  dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
+  dim3 gout((unsigned)((n + 255) / 256), (unsigned)nchains);
+  const ChainParams* c = reinterpret_cast<const ChainParams*>(cps);
+  GPAR_DISPATCH_D(sdim, {
+    cov_local<DD><<<grid, 256, 0, st>>>(t, rec, pf, c, n, L, nch, vloc, gam, agg);
+    cov_carry<DD><<<(nchains + 63) / 64, 64, 0, st>>>(agg, nch, nchains, phat);
+    cov_out<DD><<<gout, 256, 0, st>>>(vloc, gam, phat, n, L, nch, var, ldv);
+  });
 }
 
 int64_t vec_fix_blocks(int64_t n) { return (n + 255) / 256; }

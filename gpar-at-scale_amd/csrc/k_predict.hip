@@ -272,6 +272,27 @@ __global__ void normal_kernel(double* __restrict__ xi, int64_t ld, int64_t S, in
   xi[e] = v;
 }
 
+// ---------------------------------------------------------------------------- chain scatter / gather
+// dst[b * ldd + pos[k]] = src[b * lds + k]   (train observations of every chain onto the merged grid)
+__global__ void scatter_chains(const double* __restrict__ src, int64_t lds, int64_t ns,
+                               const int64_t* __restrict__ pos, double* __restrict__ dst,
+                               int64_t ldd) {
+  const int64_t k = blockIdx.x * (int64_t)256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (k >= ns) return;
+  dst[(int64_t)b * ldd + pos[k]] = src[(int64_t)b * lds + k];
+}
+
+// dst[b * ldd + i] = src[b * lds + pos[i]]   (test-point marginals back in input order)
+__global__ void gather_chains(const double* __restrict__ src, int64_t lds, int64_t ns,
+                              const int64_t* __restrict__ pos, double* __restrict__ dst,
+                              int64_t ldd) {
+  const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (i >= ns) return;
+  dst[(int64_t)b * ldd + i] = src[(int64_t)b * lds + pos[i]];
+}
+
 }  // namespace gpar
 
 // ============================================================================ launch wrappers
@@ -317,6 +338,18 @@ void launch_rowsq_finish(hipStream_t st, const double* rowsq, int64_t rows, int 
 void launch_normal(hipStream_t st, double* xi, int64_t ld, int64_t S, int64_t M, int64_t Sp,
                    uint64_t seed) {
   normal_kernel<<<(unsigned)((Sp * ld + 255) / 256), 256, 0, st>>>(xi, ld, S, M, Sp, seed);
+}
+
+void launch_scatter_chains(hipStream_t st, const double* src, int64_t lds, int64_t ns,
+                           const int64_t* pos, double* dst, int64_t ldd, int nchains) {
+  dim3 grid((unsigned)((ns + 255) / 256), (unsigned)nchains);
+  scatter_chains<<<grid, 256, 0, st>>>(src, lds, ns, pos, dst, ldd);
+}
+
+void launch_gather_chains(hipStream_t st, const double* src, int64_t lds, int64_t ns,
+                          const int64_t* pos, double* dst, int64_t ldd, int nchains) {
+  dim3 grid((unsigned)((ns + 255) / 256), (unsigned)nchains);
+  gather_chains<<<grid, 256, 0, st>>>(src, lds, ns, pos, dst, ldd);
 }
 
 }  // namespace gpar

@@ -98,7 +98,18 @@ void launch_gains_adjoint(hipStream_t st, int sdim, const double* rec, int64_t n
                           int64_t nch, int nchains, double* h);
 void launch_adjoint_local(hipStream_t st, int sdim, double* X, int64_t ldx, int64_t ncols,
                           const double* rec, const double* g, const double* cin, int64_t mc,
-                          int64_t n, int L, int64_t nch, double* bend);
+                          int64_t n, int L, int64_t nch, double* bend, int nchains = 1,
+                          int64_t xstride = 0, int64_t sstride = 0);
+// temporal chains: smoothed mean f = y - R Sigma^{-1} y, smoothed variance of f (RTS)
+void launch_smooth_mean(hipStream_t st, int sdim, const double* u, const double* h,
+                        const double* chat, int64_t sstride, const double* y, int64_t ldy,
+                        const double* noise, const ChainParamsHost* cps, int64_t n, int L,
+                        int nchains, double* mean, int64_t ldm);
+// vloc/var: nchains * n; gam: nchains * n * 4; agg: nchains * nch * 2 sdim^2; phat: nchains * nch * sdim^2
+void launch_cov_smooth(hipStream_t st, int sdim, const double* t, const double* rec,
+                       const double* pf, const ChainParamsHost* cps, int64_t n, int L,
+                       int64_t nch, int nchains, double* vloc, double* gam, double* agg,
+                       double* phat, double* var, int64_t ldv);
 int64_t vec_fix_blocks(int64_t n);
 void launch_vec_fix(hipStream_t st, int sdim, double* alpha, int64_t lda, const double* g,
                     int64_t gstride, const double* cin, int64_t sstride, int64_t mc,
@@ -144,5 +155,9 @@ void launch_rowsq_finish(hipStream_t st, const double* rowsq, int64_t rows, int 
                          double* std_out);
 void launch_normal(hipStream_t st, double* xi, int64_t ld, int64_t S, int64_t M, int64_t Sp,
                    uint64_t seed);
+void launch_scatter_chains(hipStream_t st, const double* src, int64_t lds, int64_t ns,
+                           const int64_t* pos, double* dst, int64_t ldd, int nchains);
+void launch_gather_chains(hipStream_t st, const double* src, int64_t lds, int64_t ns,
+                          const int64_t* pos, double* dst, int64_t ldd, int nchains);
 
 }  // namespace gpar

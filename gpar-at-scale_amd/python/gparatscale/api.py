@@ -329,3 +329,53 @@ def get_gpar_scaled_predictions(input_locations, pseudo_input_locations, time_lo
     return predict_scaled(input_locations, pseudo_input_locations, time_loc, outputs, theta,
                           inference_time_loc, inference_input_locations, out_kernel_structure,
                           time_kernel_structure, mode, samples, seed, device)
+
+
+def lgssm_smooth_batch(t, Y, theta, kernel="matern52", noise=None, device=0):
+    """smooth(create_lgssm(...; noise_vector), y) marginals of f for chains sharing t
+    (temporal_gp_inference.jl:109): returns (mean, var), nchains x n."""
+    ctx = context(device)
+    lib = _lib.load()
+    keep = _Keep()
+    Y = np.ascontiguousarray(np.atleast_2d(np.asarray(Y, dtype=np.float64)))
+    nch, n = Y.shape
+    th = np.ascontiguousarray(np.asarray(theta, dtype=np.float64).reshape(nch, 3))
+    tp = _host_vec(t, keep)
+    npp = _host_vec(noise, keep) if noise is not None else None
+    mean = np.zeros((nch, n))
+    var = np.zeros((nch, n))
+    ctx.check(lib.gpar_lgssm_smooth(ctx.h, nch, n, tp, _ptr(Y), n, npp, _kernel_id(kernel),
+                                    _ptr(th), _lib.GPAR_MEM_HOST, _ptr(mean), _ptr(var)))
+    return mean, var
+
+
+def get_sde_predictions(data_locations, data_outputs, output_locations,
+                        kernel_structure="matern52", i_log_time_l=None, i_log_time_var=None,
+                        i_log_noise_sigma=None, max_evals=0, g_tol=1e-8, time_limit=0.0,
+                        rng=None, device=0):
+    """temporal_gp_inference.jl:45-114 for one or several chains sharing the time grid.
+
+    data_outputs: n (one chain) or nchains x n.  Returns (theta, mean, var) with the
+    marginals of f at output_locations (the reference returns their Gaussians; its
+    `.m[1]` / `.P[1]` are mean / variance)."""
+    ctx = context(device)
+    lib = _lib.load()
+    keep = _Keep()
+    Y = np.ascontiguousarray(np.atleast_2d(np.asarray(data_outputs, dtype=np.float64)))
+    nch, n = Y.shape
+    x0 = np.vstack([parse_initial_params([i_log_time_l, i_log_time_var, i_log_noise_sigma], rng)
+                    for _ in range(nch)])
+    x0 = np.ascontiguousarray(x0)
+    ts = np.asarray(output_locations, dtype=np.float64)
+    tp = _host_vec(data_locations, keep)
+    tsp = _host_vec(ts, keep)
+    opts = GparFitOptions(int(max_evals), 1000, float(g_tol), float(time_limit))
+    theta = np.zeros((nch, 3))
+    mean = np.zeros((nch, len(ts)))
+    var = np.zeros((nch, len(ts)))
+    ctx.check(lib.gpar_sde_predictions(ctx.h, nch, n, tp, _ptr(Y), n, len(ts), tsp,
+                                       _kernel_id(kernel_structure), _ptr(x0), C.byref(opts),
+                                       _lib.GPAR_MEM_HOST, _ptr(theta), _ptr(mean), _ptr(var)))
+    if nch == 1:
+        return tuple(theta[0]), mean[0], var[0]
+    return theta, mean, var

@@ -75,3 +75,29 @@ def test_fit_matches_oracle_nelder_mead():
                                         i_log_noise_sigma=x0[4], max_evals=40,
                                         optimization_time_limit=0)
     np.testing.assert_allclose(th, th_ref, rtol=1e-6)
+
+
+@pytest.mark.parametrize("kernel", ["matern12", "matern32", "matern52"])
+def test_lgssm_smooth_matches_oracle(kernel):
+    t, Y = O.synthetic_gpar(1200, 2, seed=4, noise=0.4, gaps=3, gap_len=80)
+    th = [(0.7, 1.3, 0.2), (4.0, 0.8, 0.5)]
+    rng = np.random.default_rng(3)
+    noise = np.where(rng.random(len(t)) < 0.2, 1e10, -1.0)   # some 'test' points, rest chain sigma^2
+    mean, var = G.lgssm_smooth_batch(t, Y.T, th, kernel, noise=noise)
+    for c in range(2):
+        R = np.where(noise < 0, th[c][2] ** 2, noise)
+        lg = O.create_lgssm(t, *th[c], kind=kernel, noise_vector=R)
+        ms, Ps = O.rts_smooth(lg, Y[:, c])
+        np.testing.assert_allclose(mean[c], ms[:, 0], rtol=1e-9, atol=1e-10 * np.abs(ms[:, 0]).max())
+        np.testing.assert_allclose(var[c], Ps[:, 0, 0], rtol=1e-8, atol=1e-12)
+
+
+def test_sde_predictions_match_oracle():
+    t, Y = O.synthetic_gpar(600, 2, seed=6, noise=0.4, gaps=2, gap_len=40)
+    ts = np.sort(np.random.default_rng(2).uniform(-1, t[-1] + 1, 90))
+    x0 = (-1.0, 0.2, -1.5)
+    th_ref, m_ref, v_ref = O.get_sde_predictions(t, Y[:, 0], ts, "matern52", x0, max_evals=30)
+    th, m, v = G.get_sde_predictions(t, Y[:, 0], ts, "matern52", *x0, max_evals=30)
+    np.testing.assert_allclose(th, th_ref, rtol=1e-6)
+    np.testing.assert_allclose(m, m_ref, rtol=1e-6, atol=1e-8)
+    np.testing.assert_allclose(v, v_ref, rtol=1e-6, atol=1e-10)
