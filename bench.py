@@ -1,0 +1,244 @@
+#!/usr/bin/env python3
+"""bench.py -- GPAR-at-scale fit+predict throughput on MI355X (BASELINE.json metric).
+
+One *step* = the whole GPAR job of BASELINE.json's north star (N=1e6 time points, M=512
+pseudo-points, P=64 outputs), the per-output driver of examples/GPAR_scaled_examples.jl:86-175:
+  * output 1: get_sde_predictions (temporal-only LGSSM: NM fit + RTS smoothing at t*),
+  * outputs 2..P: get_optim_scaled_gpar_params (DTC objective, Nelder-Mead with exactly
+    `--evals` objective evaluations per output, fixed init log theta = (0, 0, 0, 0, -2)) and the
+    prediction half of get_gpar_scaled_predictions (analytic mode) at N* = N test times with the
+    noiseless previous outputs as inference inputs (GPAR_scaled_examples.jl:139 style).
+Inputs (t, Y, pseudo-inputs, test grid) are resident in HBM before the timed region.
+Multi-GPU: one process per GPU (torch.distributed, RCCL); outputs are sharded round-robin,
+shared inputs are broadcast from rank 0 once (untimed); per step the fitted thetas are
+all-gathered.  value = N * P / wall-clock per step (pts*outputs/s, whole job).
+
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config north|eeg|dtc|small]
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "gpar-at-scale_amd", "python"))
+
+import numpy as np  # noqa: E402
+
+CONFIGS = {
+    # BASELINE.json metric / north star: N=1e6, M=512, P=64
+    "north": dict(N=1_000_000, M=512, P=64, evals=50, out_kernel="matern52"),
+    # configs[3]: EEG-shaped N~1e5, M=512, P=64
+    "eeg": dict(N=100_000, M=512, P=64, evals=50, out_kernel="matern52"),
+    # configs[1]: DTC sparse GPAR N=1e5, M=256, P=8, RBF (EQ) output kernel
+    "dtc": dict(N=100_000, M=256, P=8, evals=50, out_kernel="eq"),
+    "small": dict(N=20_000, M=128, P=4, evals=20, out_kernel="matern52"),
+}
+FP64_MFMA_PEAK_TFLOPS = 78.6   # MI355X dense fp64 matrix (AMD spec; measured 74 on v_mfma_f64_16x16x4)
+HBM_PEAK_GBS = 8000.0
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="north", choices=sorted(CONFIGS))
+    ap.add_argument("--evals", type=int, default=None)
+    ap.add_argument("--predict", default="analytic", choices=["analytic", "mc"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    import gparatscale as G
+    from gparatscale import data as D
+
+    cfg = dict(CONFIGS[args.config])
+    if args.evals:
+        cfg["evals"] = args.evals
+    N, M, P, EV = cfg["N"], cfg["M"], cfg["P"], cfg["evals"]
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", device_id=dev)
+
+    # ---------------------------------------------------------------- inputs (untimed)
+    t0 = time.perf_counter()
+    if rank == 0:
+        ds = D.gpar_dataset(N, P, seed=0, observation_noise=0.8)
+        t_h, Y_h, ts_h, Fs_h = ds["t"], ds["Y"], ds["t_star"], ds["F_star"]
+        n_eff, ns_eff = len(t_h), len(ts_h)
+    else:
+        n_eff = ns_eff = 0
+    if world > 1:
+        sz = torch.tensor([n_eff, ns_eff], device=dev)
+        dist.broadcast(sz, 0)
+        n_eff, ns_eff = int(sz[0]), int(sz[1])
+    t_d = torch.empty(n_eff, dtype=torch.float64, device=dev)
+    Y_d = torch.empty((n_eff, P), dtype=torch.float64, device=dev)
+    ts_d = torch.empty(ns_eff, dtype=torch.float64, device=dev)
+    Fs_d = torch.empty((ns_eff, P), dtype=torch.float64, device=dev)
+    if rank == 0:
+        t_d.copy_(torch.from_numpy(t_h)); Y_d.copy_(torch.from_numpy(Y_h))
+        ts_d.copy_(torch.from_numpy(ts_h)); Fs_d.copy_(torch.from_numpy(Fs_h))
+    if world > 1:   # RCCL broadcast of the shared inputs over xGMI
+        for x in (t_d, Y_d, ts_d, Fs_d):
+            dist.broadcast(x, 0)
+    mine = [p for p in range(1, P + 1) if (p - 1) % world == rank]
+    gpar_out = [p for p in mine if p >= 2]
+    Yh = Y_d.cpu().numpy() if gpar_out else None
+    # q(u) with Kuu + sigma^2 I (qu_kuu_noise): the reference's jitter-free Cuu
+    # (gpar_scaled_inference.jl:157) is numerically singular for M=512 pseudo-inputs drawn from
+    # the data at fitted lengthscales; the objective itself is unchanged (dtc.jl:35,119).
+    problems, keep, ycols, Zs = [], [], {}, {}
+    for p in gpar_out:
+        ycols[p] = Y_d[:, p - 1].contiguous()
+        Zs[p] = torch.from_numpy(D.pseudo_inputs(Yh[:, : p - 1], M, seed=p)).to(dev)
+        pr, k = G.make_problem(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], cfg["out_kernel"], "matern52")
+        problems.append(pr)
+        keep.append(k)
+    y1 = Y_d[:, 0].contiguous() if 1 in mine else None
+    x0 = np.tile(np.array([0.0, 0.0, 0.0, 0.0, -2.0]), (len(problems), 1))
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] inputs ready in {time.perf_counter() - t0:.1f}s: N={n_eff} N*={ns_eff} "
+        f"M={M} P={P} outputs={mine}")
+
+    ctx = G.context(local)
+
+    def step():
+        res = {}
+        if problems:
+            fr = G.fit_batch(problems, x0, max_evals=EV, g_tol=-1.0, device=local)
+            for i, p in enumerate(gpar_out):
+                res[p] = fr.theta[i]
+        if y1 is not None:
+            th1, m1, v1 = G.get_sde_predictions_device(t_d, y1, ts_d, "matern52", (0.0, 0.0, -2.0),
+                                                       max_evals=EV, device=local)
+            res[1] = np.array(list(th1) + [0.0, 0.0])
+        for i, p in enumerate(gpar_out):
+            G.predict_scaled(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], res[p], ts_d, Fs_d[:, : p - 1],
+                             cfg["out_kernel"], "matern52", mode=args.predict, samples=100,
+                             seed=p, device=local, qu_kuu_noise=True)
+        th = np.zeros((P, 5))
+        for p, v in res.items():
+            th[p - 1] = v
+        if world > 1:   # gather fitted hyperparameters (tiny)
+            tt = torch.from_numpy(th).to(dev)
+            dist.all_reduce(tt)
+            th = tt.cpu().numpy()
+        return th
+
+    for _ in range(args.warmup):
+        step()
+    ctx.set_profiling(True)
+    ctx.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ts0 = time.perf_counter()
+    for _ in range(args.steps):
+        theta = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = (time.perf_counter() - ts0) * 1e3 / args.steps
+    if world > 1:
+        e = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e[0])
+    gram_n, gram_ms = ctx.kernel_stats("gram")
+    wh_n, wh_ms = ctx.kernel_stats("whiten")
+
+    out = None
+    if rank == 0:
+        value = n_eff * P / (el / 1e3)
+        flops = float(n_eff) * M * (M + 1)       # N*M*(M+1) per Gram launch
+        avg = gram_ms / max(gram_n, 1)
+        achieved = flops / (avg * 1e-3) / 1e12 if gram_n else None
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "gram_pmc_r01.json")
+        if os.path.exists(pmc):
+            with open(pmc) as f:
+                traffic = json.load(f).get("hbm_bytes_per_launch")
+        out = {
+            "metric": "GPAR fit+predict wall-clock (ms) and pts*outputs/sec, N=1e6 M=512 P=64",
+            "value": value,
+            "unit": "pts*outputs/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": el,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (toy_data.jl big-set functions, P outputs, seed 0)",
+            "config": {"workload": f"GPAR-DTC fit+predict ({args.config})", "N": n_eff, "N_star": ns_eff,
+                       "M": M, "P": P, "evals_per_output": EV, "predict": args.predict,
+                       "out_kernel": cfg["out_kernel"], "time_kernel": "matern52",
+                       "parallelism": f"outputs sharded over {world} GPU(s)"},
+            "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
+                         "traffic": traffic, "kernel": "gram_kernel (beta^T beta, fp64 MFMA)",
+                         "launches": gram_n, "avg_ms": avg, "flops_per_launch": flops},
+            "kernels": {"gram_ms_per_step": gram_ms / args.steps, "whiten_ms_per_step": wh_ms / args.steps,
+                        "whiten_launches": wh_n},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(n_eff, ns_eff, M, P, EV, cfg["out_kernel"])
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def cpu_baseline(N, NS, M, P, EV, out_kernel, n_sample=20_000, d_sample=32):
+    """Time the numpy oracle (oracle/gpar_oracle.py, the CPU restatement of the reference;
+    "port") on a bounded sample -- one DTC objective evaluation and one analytic prediction at
+    n_sample points, D = d_sample -- and scale linearly in N (every piece is O(N)) to the job:
+    (P-1) outputs x EV evaluations + (P-1) predictions (+ the temporal output, negligible)."""
+    sys.path.insert(0, ROOT)
+    from oracle import gpar_oracle as O
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([x.get("num_threads", 1) for x in threadpool_info()] + [1])
+    except Exception:
+        cores = os.cpu_count() or 1
+    t, Y = O.synthetic_gpar(n_sample, d_sample + 1, seed=1, noise=0.8)
+    V = Y[:, :d_sample].T
+    y = Y[:, d_sample]
+    Z = O.pick_pseudo_inputs(V, M, 3)
+    theta = (2.0, 2.0, 2.0, 2.0, float(np.exp(-2.0) + 1e-3))
+    t0 = time.perf_counter()
+    O.compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel, "matern52")
+    t_eval = time.perf_counter() - t0
+    ns = n_sample // 4
+    ts = np.sort(np.random.default_rng(2).uniform(t[0], t[-1], ns))
+    Vs = np.vstack([np.interp(ts, t, V[q]) for q in range(d_sample)])
+    t0 = time.perf_counter()
+    O.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, out_kernel, "matern52", "analytic")
+    t_pred = time.perf_counter() - t0
+    scale = N / n_sample
+    pred_scale = (N + NS) / (n_sample + ns)
+    t_job = (P - 1) * (EV * t_eval * scale + t_pred * pred_scale)
+    return {"value": N * P / t_job, "unit": "pts*outputs/s", "cores": int(cores), "kind": "port",
+            "sample": f"numpy oracle: 1 DTC objective eval (N={n_sample}, M={M}, D={d_sample}) = {t_eval:.2f}s "
+                      f"+ 1 analytic predict (N={n_sample}, N*={ns}) = {t_pred:.2f}s, scaled linearly in N "
+                      f"to {P - 1} outputs x {EV} evals + {P - 1} predicts: est {t_job:.0f}s per job"}
+
+
+if __name__ == "__main__":
+    main()

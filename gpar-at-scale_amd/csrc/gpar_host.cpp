@@ -28,6 +28,14 @@ struct gpar_ctx {
     size_t bytes = 0;
   };
   std::unordered_map<std::string, Buf> bufs;
+  // event-based kernel timing (gpar_ctx_set_profiling)
+  bool profiling = false;
+  struct Stat {
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    int64_t launches = 0;
+    double ms = 0.0;
+  };
+  std::unordered_map<std::string, Stat> stats;
 };
 
 namespace gpar {
@@ -53,6 +61,40 @@ struct Error : std::runtime_error {
 static void check_launch(const char* what) {
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) throw Error(GPAR_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+// RAII timing scope: records HIP events around the enclosed launches on the ctx stream.
+struct Timed {
+  gpar_ctx* c;
+  const char* name;
+  hipEvent_t e1 = nullptr;
+  Timed(gpar_ctx* c_, const char* n) : c(c_), name(n) {
+    if (!c->profiling) return;
+    hipEvent_t e0;
+    (void)hipEventCreate(&e0);
+    (void)hipEventCreate(&e1);
+    (void)hipEventRecord(e0, c->stream);
+    c->stats[name].pending.push_back({e0, e1});
+  }
+  ~Timed() {
+    if (e1) (void)hipEventRecord(e1, c->stream);
+  }
+};
+
+static void flush_stats(gpar_ctx* c) {
+  (void)hipStreamSynchronize(c->stream);
+  for (auto& kv : c->stats) {
+    for (auto& pr : kv.second.pending) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) {
+        kv.second.ms += ms;
+        kv.second.launches += 1;
+      }
+      (void)hipEventDestroy(pr.first);
+      (void)hipEventDestroy(pr.second);
+    }
+    kv.second.pending.clear();
+  }
 }
 
 template <class T>
@@ -110,7 +152,7 @@ struct DevProblem {
   const double *t, *v, *z, *y;
   const double* t_user;  // caller's pointer (grouping key)
   int64_t ldv, ldz;
-  int ok, tk, sdim, kuu_noise;
+  int ok, tk, sdim, kuu_noise, qu_noise;
 };
 
 static void check_sorted_host(const double* t, int64_t n) {
@@ -138,6 +180,7 @@ static DevProblem prepare_problem(gpar_ctx* c, const gpar_problem& p, int idx) {
   d.tk = p.time_kernel;
   d.sdim = sde_dim(p.time_kernel);
   d.kuu_noise = p.kuu_noise;
+  d.qu_noise = p.qu_kuu_noise;
   d.t_user = p.t;
   if (p.mem == GPAR_MEM_DEVICE) {
     d.t = p.t; d.v = p.v; d.z = p.z; d.y = p.y;
@@ -192,8 +235,11 @@ static GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
   o.phi = ws<double>(c, tag + "_phi", (size_t)nchains * nch * d2);
   o.logs = ws<double>(c, tag + "_logs", (size_t)nchains * nch);
   o.pf = want_pf ? ws<double>(c, tag + "_pf", (size_t)nchains * n * d2) : nullptr;
-  launch_gains(c->stream, sdim, t, n, kChunk, nch, nchains, dcps, noise, agg, pst, o.rec, o.g,
-               o.phi, o.logs, o.pf);
+  {
+    Timed tm_(c, "gains");
+    launch_gains(c->stream, sdim, t, n, kChunk, nch, nchains, dcps, noise, agg, pst, o.rec, o.g,
+                 o.phi, o.logs, o.pf);
+  }
   check_launch("gains");
   return o;
 }
@@ -260,8 +306,11 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
                               hipMemcpyDeviceToDevice, c->stream));
     }
     const double s_o = th[i].sv_o * th[i].sv_o;
-    launch_whiten_kfu(c->stream, p.tk, p.ok, g.rec, p.v, p.ldv, (int)p.d, p.z, p.ldz, p.m, p.mp,
-                      n, kChunk, nch, 1.0 / th[i].l_o, s_o, beta, p.mp, send, p.mc);
+    {
+      Timed tm_(c, "whiten");
+      launch_whiten_kfu(c->stream, p.tk, p.ok, g.rec, p.v, p.ldv, (int)p.d, p.z, p.ldz, p.m, p.mp,
+                        n, kChunk, nch, 1.0 / th[i].l_o, s_o, beta, p.mp, send, p.mc);
+    }
     check_launch("whiten_kfu");
     launch_whiten_vec(c->stream, p.sdim, g.rec, 0, p.y, 0, n, kChunk, nch, 1, alpha, 0, send, 0,
                       p.mc, p.mp);
@@ -274,8 +323,11 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     GramPlan plan = gram_plan(n, p.mp);
     double* part = ws<double>(c, "gram_part", (size_t)plan.nsplit * plan.ntiles * kGramTile * kGramTile);
     double* rpart = ws<double>(c, "gram_rpart", (size_t)plan.nsplit * plan.ntb * kGramTile);
-    launch_gram(c->stream, p.sdim, plan, beta, p.mp, n, g.g, cin, p.mc, kChunk, alpha, part,
-                rpart, o.G + (size_t)i * mpmax * mpmax, mpmax, o.r + (size_t)i * mpmax);
+    {
+      Timed tm_(c, "gram");
+      launch_gram(c->stream, p.sdim, plan, beta, p.mp, n, g.g, cin, p.mc, kChunk, alpha, part,
+                  rpart, o.G + (size_t)i * mpmax * mpmax, mpmax, o.r + (size_t)i * mpmax);
+    }
     check_launch("gram");
     if (fix_beta) {
       launch_beta_fix(c->stream, p.sdim, beta, p.mp, n, g.g, cin, p.mc, kChunk);
@@ -316,7 +368,7 @@ static DenseOut run_dense(gpar_ctx* c, const std::vector<DevProblem>& P,
     double* Lam = o.Llam + (size_t)i * ld * ld;
     const double s2 = th[i].sigma * th[i].sigma;
     kj[i] = {p.z, p.ldz, (int)p.d, p.ok, 1.0 / th[i].l_o, th[i].sv_o * th[i].sv_o,
-             (!qu_mode && p.kuu_noise) ? s2 : 0.0, Kuu, ld, (int)p.m};
+             (qu_mode ? p.qu_noise : p.kuu_noise) ? s2 : 0.0, Kuu, ld, (int)p.m};
     cj[i] = {Kuu, ld, (int)p.m, 0.0, o.status + 2 * i};
     t1[i] = {Kuu, ld, go.G + (size_t)i * ld * ld, ld, W, ld, (int)p.m, p.m, 0, 0};
     t2[i] = {Kuu, ld, W, ld, Lam, ld, (int)p.m, p.m, 1, 0};
@@ -332,6 +384,7 @@ static DenseOut run_dense(gpar_ctx* c, const std::vector<DevProblem>& P,
   h2d(c, dcl, cl.data(), np);
   h2d(c, dt1, t1.data(), np);
   h2d(c, dt2, t2.data(), np);
+  Timed tm_(c, "dense");
   launch_kuu(c->stream, dkj, np, mmax);
   check_launch("kuu");
   launch_chol(c->stream, dcj, np);
@@ -705,6 +758,29 @@ int32_t gpar_ctx_trim(gpar_ctx* ctx) {
   for (auto& kv : ctx->bufs)
     if (kv.second.p) HIPCHECK(hipFree(kv.second.p));
   ctx->bufs.clear();
+  API_END(ctx)
+}
+
+int32_t gpar_ctx_set_profiling(gpar_ctx* ctx, int32_t on) {
+  API_BEGIN(ctx)
+  ctx->profiling = on != 0;
+  API_END(ctx)
+}
+
+int32_t gpar_ctx_kernel_stats(gpar_ctx* ctx, const char* name, int64_t* launches, double* total_ms) {
+  API_BEGIN(ctx)
+  ARGCHECK(name && launches && total_ms, "null argument");
+  flush_stats(ctx);
+  auto it = ctx->stats.find(name);
+  *launches = it == ctx->stats.end() ? 0 : it->second.launches;
+  *total_ms = it == ctx->stats.end() ? 0.0 : it->second.ms;
+  API_END(ctx)
+}
+
+int32_t gpar_ctx_reset_stats(gpar_ctx* ctx) {
+  API_BEGIN(ctx)
+  flush_stats(ctx);
+  ctx->stats.clear();
   API_END(ctx)
 }
 

@@ -24,6 +24,7 @@ EXPORTED = (
     "gpar_ctx_workspace_bytes", "gpar_ctx_trim", "gpar_dtc_objective", "gpar_dtc_objective_A",
     "gpar_fit", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
+    "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_reset_stats",
 )
 
 
@@ -54,7 +55,7 @@ class GparProblem(C.Structure):
         ("t", C.c_void_p), ("v", C.c_void_p), ("ldv", C.c_int64),
         ("z", C.c_void_p), ("ldz", C.c_int64), ("y", C.c_void_p),
         ("out_kernel", C.c_int32), ("time_kernel", C.c_int32), ("kuu_noise", C.c_int32),
-        ("mem", C.c_int32),
+        ("mem", C.c_int32), ("qu_kuu_noise", C.c_int32),
     ]
 
 
@@ -86,6 +87,9 @@ def load(path: str | None = None):
             "gpar_last_error": (C.c_char_p, [vp]),
             "gpar_ctx_workspace_bytes": (i64, [vp]),
             "gpar_ctx_trim": (i32, [vp]),
+            "gpar_ctx_set_profiling": (i32, [vp, i32]),
+            "gpar_ctx_kernel_stats": (i32, [vp, C.c_char_p, C.POINTER(i64), C.POINTER(C.c_double)]),
+            "gpar_ctx_reset_stats": (i32, [vp]),
             "gpar_dtc_objective": (i32, [vp, C.POINTER(GparProblem), i32, dp, dp]),
             "gpar_dtc_objective_A": (i32, [vp, C.POINTER(GparProblem), dp, dp, dp]),
             "gpar_fit": (i32, [vp, C.POINTER(GparProblem), i32, dp, C.POINTER(GparFitOptions),
@@ -151,6 +155,20 @@ class Context:
 
     def workspace_bytes(self):
         return int(load().gpar_ctx_workspace_bytes(self.h))
+
+    def set_profiling(self, on=True):
+        self.check(load().gpar_ctx_set_profiling(self.h, 1 if on else 0))
+
+    def kernel_stats(self, name):
+        """(launches, total_ms) of a kernel family since the last reset (HIP events on the
+        context stream)."""
+        n = C.c_int64()
+        ms = C.c_double()
+        self.check(load().gpar_ctx_kernel_stats(self.h, name.encode(), C.byref(n), C.byref(ms)))
+        return int(n.value), float(ms.value)
+
+    def reset_stats(self):
+        self.check(load().gpar_ctx_reset_stats(self.h))
 
 
 _ctx: dict[int, Context] = {}

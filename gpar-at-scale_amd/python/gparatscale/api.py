@@ -119,7 +119,7 @@ def _dev_vec(x, keep):
 
 
 def make_problem(V, Z, t, y, out_kernel="matern52", time_kernel="matern52", kuu_noise=True,
-                 keep=None):
+                 keep=None, qu_kuu_noise=False):
     """Build a gpar_problem.  Host: V, Z as D x N / D x M (ColVecs).  Device: torch tensors
     with rows = points (N x D, M x D)."""
     keep = keep if keep is not None else _Keep()
@@ -145,6 +145,7 @@ def make_problem(V, Z, t, y, out_kernel="matern52", time_kernel="matern52", kuu_
     p.out_kernel = _kernel_id(out_kernel)
     p.time_kernel = _kernel_id(time_kernel)
     p.kuu_noise = 1 if kuu_noise else 0
+    p.qu_kuu_noise = 1 if qu_kuu_noise else 0
     return p, keep
 
 
@@ -282,7 +283,8 @@ def lgssm_logpdf_batch(t, Y, theta, kernel="matern52", device=0):
 # ----------------------------------------------------------------------------- prediction
 def predict_scaled(input_locations, pseudo_input_locations, time_loc, outputs, theta,
                    inference_time_loc, inference_input_locations, out_kernel="matern52",
-                   time_kernel="matern52", mode="analytic", samples=100, seed=0, device=0):
+                   time_kernel="matern52", mode="analytic", samples=100, seed=0, device=0,
+                   qu_kuu_noise=False):
     """Prediction half of get_gpar_scaled_predictions (gpar_scaled_inference.jl:63-135) at a
     given theta.  Returns (mean, std) at the inference locations, in their input order.
     mode="mc" reproduces the reference's 100-sample Monte Carlo estimator; "analytic" is its
@@ -290,7 +292,7 @@ def predict_scaled(input_locations, pseudo_input_locations, time_loc, outputs, t
     ctx = context(device)
     lib = _lib.load()
     p, keep = make_problem(input_locations, pseudo_input_locations, time_loc, outputs,
-                           out_kernel, time_kernel)
+                           out_kernel, time_kernel, qu_kuu_noise=qu_kuu_noise)
     th = np.ascontiguousarray(np.asarray(theta, dtype=np.float64).reshape(5))
     md = _lib.GPAR_PREDICT_MC if mode == "mc" else _lib.GPAR_PREDICT_ANALYTIC
     if p.mem == _lib.GPAR_MEM_DEVICE:
@@ -376,6 +378,32 @@ def get_sde_predictions(data_locations, data_outputs, output_locations,
     ctx.check(lib.gpar_sde_predictions(ctx.h, nch, n, tp, _ptr(Y), n, len(ts), tsp,
                                        _kernel_id(kernel_structure), _ptr(x0), C.byref(opts),
                                        _lib.GPAR_MEM_HOST, _ptr(theta), _ptr(mean), _ptr(var)))
+    if nch == 1:
+        return tuple(theta[0]), mean[0], var[0]
+    return theta, mean, var
+
+
+def get_sde_predictions_device(t, Y, t_star, kernel_structure="matern52", log_theta0=(0.0, 0.0, -2.0),
+                               max_evals=0, g_tol=-1.0, time_limit=0.0, device=0):
+    """get_sde_predictions with HBM-resident torch inputs: t (n), Y (n) or (nchains x n,
+    contiguous rows), t_star (n_star, ascending).  Returns (theta, mean, var) on the device."""
+    import torch
+    ctx = context(device)
+    lib = _lib.load()
+    keep = _Keep()
+    Y2 = Y.reshape(1, -1) if Y.dim() == 1 else Y
+    Y2 = Y2.contiguous()
+    nch, n = Y2.shape
+    x0 = np.ascontiguousarray(np.tile(np.asarray(log_theta0, dtype=np.float64), (nch, 1)))
+    opts = GparFitOptions(int(max_evals), 1000, float(g_tol), float(time_limit))
+    theta = np.zeros((nch, 3))
+    ns = t_star.shape[0]
+    mean = torch.empty((nch, ns), dtype=torch.float64, device=t.device)
+    var = torch.empty((nch, ns), dtype=torch.float64, device=t.device)
+    ctx.check(lib.gpar_sde_predictions(ctx.h, nch, n, _dev_vec(t, keep), Y2.data_ptr(), n, ns,
+                                       _dev_vec(t_star, keep), _kernel_id(kernel_structure),
+                                       _ptr(x0), C.byref(opts), _lib.GPAR_MEM_DEVICE, _ptr(theta),
+                                       mean.data_ptr(), var.data_ptr()))
     if nch == 1:
         return tuple(theta[0]), mean[0], var[0]
     return theta, mean, var

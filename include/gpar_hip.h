@@ -77,6 +77,9 @@ typedef struct gpar_problem {
   int32_t time_kernel;  /* GPAR_MATERN12/32/52 of f_t (dtc.jl:17)                      */
   int32_t kuu_noise;    /* 1: Kuu + sigma^2 I as FiniteGP cov(u) (dtc.jl:35,119)       */
   int32_t mem;          /* gpar_mem of t, v, z, y                                      */
+  int32_t qu_kuu_noise; /* q(u)/prediction: 0 = Cuu without noise as the reference
+                           (gpar_scaled_inference.jl:157); 1 = Cuu + sigma^2 I like the
+                           objective (opt-in: robust when pseudo-inputs nearly coincide)     */
 } gpar_problem;
 
 typedef struct gpar_fit_options {
@@ -97,6 +100,13 @@ const char* gpar_last_error(const gpar_ctx* ctx);
 int64_t gpar_ctx_workspace_bytes(const gpar_ctx* ctx);
 /* release cached device workspace */
 int32_t gpar_ctx_trim(gpar_ctx* ctx);
+/* Kernel timing with HIP events on the context's stream (bench / roofline support).
+ * name: "gram" (the fp64 MFMA Gram contraction), "whiten" (Kfu assembly + Kalman whitening),
+ * "gains" (parallel Riccati scan), "dense" (M x M Cholesky / solves).  total_ms accumulates
+ * over launches since the last reset. */
+int32_t gpar_ctx_set_profiling(gpar_ctx* ctx, int32_t on);
+int32_t gpar_ctx_kernel_stats(gpar_ctx* ctx, const char* name, int64_t* launches, double* total_ms);
+int32_t gpar_ctx_reset_stats(gpar_ctx* ctx);
 
 /* ---------------------------------------------------------------- DTC objective
  * Replaces compute_gpar_dtc_objective (src/gp/dtc.jl:83-128), batched over `nprob`
