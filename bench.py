@@ -9,7 +9,7 @@ pseudo-points, P=64 outputs), the per-output driver of examples/GPAR_scaled_exam
     prediction half of get_gpar_scaled_predictions (analytic mode) at N* = N test times with the
     noiseless previous outputs as inference inputs (GPAR_scaled_examples.jl:139 style).
 Inputs (t, Y, pseudo-inputs, test grid) are resident in HBM before the timed region.
-Multi-GPU: one process per GPU (torch.distributed, RCCL); outputs are sharded round-robin,
+Multi-GPU: one process per GPU (torch.distributed, RCCL); outputs are sharded by cost-balanced assignment (gparatscale.shard),
 shared inputs are broadcast from rank 0 once (untimed); per step the fitted thetas are
 all-gathered.  value = N * P / wall-clock per step (pts*outputs/s, whole job).
 
@@ -60,6 +60,7 @@ def main():
     import torch.distributed as dist
     import gparatscale as G
     from gparatscale import data as D
+    from gparatscale import shard as S
 
     cfg = dict(CONFIGS[args.config])
     if args.evals:
@@ -94,10 +95,8 @@ def main():
     if rank == 0:
         t_d.copy_(torch.from_numpy(t_h)); Y_d.copy_(torch.from_numpy(Y_h))
         ts_d.copy_(torch.from_numpy(ts_h)); Fs_d.copy_(torch.from_numpy(Fs_h))
-    if world > 1:   # RCCL broadcast of the shared inputs over xGMI
-        for x in (t_d, Y_d, ts_d, Fs_d):
-            dist.broadcast(x, 0)
-    mine = [p for p in range(1, P + 1) if (p - 1) % world == rank]
+    S.broadcast_inputs((t_d, Y_d, ts_d, Fs_d))   # RCCL broadcast of the shared inputs over xGMI
+    mine = S.assign_outputs(P, world)[rank]
     gpar_out = [p for p in mine if p >= 2]
     Yh = Y_d.cpu().numpy() if gpar_out else None
     # q(u) with Kuu + sigma^2 I (qu_kuu_noise): the reference's jitter-free Cuu
@@ -132,14 +131,7 @@ def main():
             G.predict_scaled(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], res[p], ts_d, Fs_d[:, : p - 1],
                              cfg["out_kernel"], "matern52", mode=args.predict, samples=100,
                              seed=p, device=local, qu_kuu_noise=True)
-        th = np.zeros((P, 5))
-        for p, v in res.items():
-            th[p - 1] = v
-        if world > 1:   # gather fitted hyperparameters (tiny)
-            tt = torch.from_numpy(th).to(dev)
-            dist.all_reduce(tt)
-            th = tt.cpu().numpy()
-        return th
+        return S.gather_thetas(res, P, dev)   # fitted hyperparameters, P x 5 (tiny)
 
     for _ in range(args.warmup):
         step()

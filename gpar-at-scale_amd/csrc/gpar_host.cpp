@@ -244,6 +244,23 @@ static GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
   return o;
 }
 
+
+// Kfu assembly + chunk-local whitening: fp64-MFMA Gram-form kernel for the smooth output
+// kernels, direct-difference kernel for Matern-1/2 (kappa not smooth in d^2 at 0).
+static void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const double* rec, const double* v,
+                           int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
+                           int64_t ldb, double* send) {
+  const double s_o = th.sv_o * th.sv_o;
+  if (p.ok == GPAR_MATERN12) {
+    launch_whiten_kfu(c->stream, p.tk, p.ok, rec, v, ldv, (int)p.d, p.z, p.ldz, p.m, p.mp, n,
+                      kChunk, nch, 1.0 / th.l_o, s_o, beta, ldb, send, p.mc);
+  } else {
+    double* zc = ws<double>(c, "zcenter", (size_t)((p.mp + 255) / 256) * 64);
+    launch_whiten_kfu_mfma(c->stream, p.tk, p.ok, rec, v, ldv, (int)p.d, p.z, p.ldz, zc, p.m, p.mp,
+                           n, kChunk, nch, 1.0 / th.l_o, s_o, beta, ldb, send, p.mc);
+  }
+}
+
 // --------------------------------------------------------------------------- Gram stage
 struct GramOut {
   double *G, *r, *a2part, *logs;  // per problem
@@ -308,8 +325,7 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     const double s_o = th[i].sv_o * th[i].sv_o;
     {
       Timed tm_(c, "whiten");
-      launch_whiten_kfu(c->stream, p.tk, p.ok, g.rec, p.v, p.ldv, (int)p.d, p.z, p.ldz, p.m, p.mp,
-                        n, kChunk, nch, 1.0 / th[i].l_o, s_o, beta, p.mp, send, p.mc);
+      whiten_kfu_any(c, p, g.rec, p.v, p.ldv, n, nch, th[i], beta, p.mp, send);
     }
     check_launch("whiten_kfu");
     launch_whiten_vec(c->stream, p.sdim, g.rec, 0, p.y, 0, n, kChunk, nch, 1, alpha, 0, send, 0,
@@ -585,8 +601,7 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
   double* bend = ws<double>(c, "pr_bend", (size_t)nch * mc * 4);
   double* chat = ws<double>(c, "pr_chat", (size_t)nch * mc * 4);
   double* h = ws<double>(c, "pr_h", (size_t)nt * 4);
-  launch_whiten_kfu(c->stream, P.tk, P.ok, g.rec, vm, d, (int)d, P.z, P.ldz, m, mp, nt, kChunk,
-                    nch, 1.0 / th.l_o, th.sv_o * th.sv_o, X, ldx, send, mc);
+  whiten_kfu_any(c, P, g.rec, vm, d, nt, nch, th, X, ldx, send);
   launch_whiten_vec(c->stream, P.sdim, g.rec, 0, ym, 0, nt, kChunk, nch, 1, X + mp, 0, send, 0,
                     mc, mp, ldx);
   check_launch("predict: whiten");
@@ -1093,6 +1108,50 @@ int32_t gpar_exact_posterior(gpar_ctx* ctx, int64_t n, int64_t dx, const double*
                              int64_t ldxs, int32_t time_kernel, int32_t out_kernel,
                              const double* theta, int32_t mem, double* mean, double* var) {
   return not_yet(ctx, "gpar_exact_posterior");
+}
+
+// ---------------------------------------------------------------- host-only Nelder-Mead
+struct gpar_nm {
+  gpar::NelderMead nm;
+};
+
+int32_t gpar_nm_create(int32_t n, const double* x0, const gpar_fit_options* opts, gpar_nm** out) {
+  if (!out || !x0 || n < 1) return GPAR_ERR_ARG;
+  gpar_fit_options o{0, 1000, 1e-8, 0.0};
+  if (opts) o = *opts;
+  *out = new gpar_nm{gpar::NelderMead(std::vector<double>(x0, x0 + n), o.max_evals,
+                                      o.max_iterations, o.g_tol, o.time_limit)};
+  return GPAR_OK;
+}
+
+int32_t gpar_nm_destroy(gpar_nm* nm) {
+  delete nm;
+  return GPAR_OK;
+}
+
+int32_t gpar_nm_ask(gpar_nm* nm, double* x) {
+  if (!nm || !x) return -1;
+  if (nm->nm.done()) return 0;
+  const auto& p = nm->nm.ask();
+  std::copy(p.begin(), p.end(), x);
+  return 1;
+}
+
+int32_t gpar_nm_tell(gpar_nm* nm, double f) {
+  if (!nm || nm->nm.done()) return GPAR_ERR_STATE;
+  nm->nm.tell(f);
+  return GPAR_OK;
+}
+
+int32_t gpar_nm_result(const gpar_nm* nm, double* x_min, double* f_min, int32_t* evals,
+                       int32_t* iterations) {
+  if (!nm) return GPAR_ERR_STATE;
+  const auto& x = nm->nm.x_min();
+  if (x_min) std::copy(x.begin(), x.end(), x_min);
+  if (f_min) *f_min = nm->nm.f_min();
+  if (evals) *evals = nm->nm.evals();
+  if (iterations) *iterations = nm->nm.iterations();
+  return GPAR_OK;
 }
 
 }  // extern "C"

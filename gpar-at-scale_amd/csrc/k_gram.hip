@@ -22,6 +22,9 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int kGT = 128;          // tile edge
 constexpr int kBK = 16;           // time rows per K-step
 constexpr int kLdsStride = 144;   // padded LDS row (doubles): rows r and r+1 hit opposite bank halves
+#ifndef GRAM_VARIANT
+#define GRAM_VARIANT 0   // ablation builds only (scratch/gram_bench): 1 no fix-up, 2 no beta loads, 3 no MFMA, 4 no staging
+#endif
 
 template <int D>
 __global__ __launch_bounds__(256, 2) void gram_kernel(
@@ -67,30 +70,39 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
     for (int c = 0; c < 4; ++c) acc[a][c] = d4{0.0, 0.0, 0.0, 0.0};
 
   double racc = 0.0;
-  double bI[8], bJ[8], cI[D], cJ[D];
   double gpre = 0.0;
+  struct Regs {
+    double bI[8], bJ[8], cI[D], cJ[D];
+  };
+  Regs RA, RB;
 
-  // Pipeline (one barrier per K-step):
-  //   stage_load(s+1)  raw beta / carry loads, issued before the MFMAs of step s
-  //   gload(s+2)       the K-step's g_k rows + alpha_k (80 doubles, one per thread) two steps ahead
-  //   MFMAs(s)         from lds[s & 1]
-  //   stage_store(s+1) fix-up beta += g_k . c_chunk (g from the LDS ring) -> lds[(s+1) & 1]
-  //   gstore(s+2)      ring slot (s+2) & 1 == s & 1, last read by stage_store(s) one barrier ago
-  // Consuming a global load right after issuing it makes hipcc wait vmcnt(0) per row, so all
-  // global loads are consumed one MFMA phase later.  Rows past the split are clamped + masked.
-  auto stage_load = [&](int64_t k0) {
+  // Pipeline (one barrier per K-step, beta loads two K-steps ahead):
+  //   load(s+2)          raw beta / carry loads into the free register set
+  //   gload(s+2)         the K-step's g_k rows + alpha_k (80 doubles, one per thread)
+  //   MFMAs(s)           from lds[s & 1], interleaved with
+  //   store_rows(s+1)    fix-up beta += g_k . c_chunk (g from the LDS ring) -> lds[(s+1) & 1]
+  //   gstore(s+2)        ring slot (s+2) & 1 == s & 1, last read by store_rows(s) a barrier ago
+  // A global load consumed soon after issue stalls the wave (hipcc waits vmcnt), so every
+  // beta load has one full MFMA phase plus one barrier to land.  Rows past the split are
+  // clamped + masked (branch-free).
+  auto load = [&](Regs& R, int64_t k0) {
     const int64_t ch = k0 / L;
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-      cI[i] = cin[(ch * mc + i0 + sc) * kSStride + i];
-      cJ[i] = cin[(ch * mc + j0 + sc) * kSStride + i];
+      R.cI[i] = cin[(ch * mc + i0 + sc) * kSStride + i];
+      R.cJ[i] = cin[(ch * mc + j0 + sc) * kSStride + i];
     }
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
       const int64_t k = k0 + rgu + 2 * r;
       const int64_t kc = (k < n) ? k : n - 1;
-      bI[r] = beta[kc * ldb + i0 + sc];
-      bJ[r] = beta[kc * ldb + j0 + sc];
+#if GRAM_VARIANT == 2
+      R.bI[r] = (double)kc;
+      R.bJ[r] = (double)kc;
+#else
+      R.bI[r] = beta[kc * ldb + i0 + sc];
+      R.bJ[r] = beta[kc * ldb + j0 + sc];
+#endif
     }
   };
   auto gload = [&](int64_t k0) {
@@ -104,22 +116,25 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
   auto gstore = [&](int slot) {
     if (tid < kBK * 5) smem[4 * kTileD + slot * kGRing + tid] = gpre;
   };
-  auto stage_store = [&](int64_t k0, int buf) {
+  auto store_rows = [&](const Regs& R, int64_t k0, int buf, int r0, int nr) {
     const double* gr = smem + 4 * kTileD + buf * kGRing;
     double* ldsI = smem + (buf * 2 + 0) * kTileD;
     double* ldsJ = smem + (buf * 2 + 1) * kTileD;
 #pragma unroll
     for (int r = 0; r < 8; ++r) {
+      if (r < r0 || r >= r0 + nr) continue;
       const int row = rgu + 2 * r;
       const int64_t k = k0 + row;
       const double msk = (k < ke) ? 1.0 : 0.0;
-      double vi = bI[r], vj = bJ[r];
+      double vi = R.bI[r], vj = R.bJ[r];
+#if GRAM_VARIANT != 1
 #pragma unroll
       for (int i = 0; i < D; ++i) {
         const double gi = gr[row * 5 + i];
-        vi = fma(gi, cI[i], vi);
-        vj = fma(gi, cJ[i], vj);
+        vi = fma(gi, R.cI[i], vi);
+        vj = fma(gi, R.cJ[i], vj);
       }
+#endif
       vi *= msk;
       racc = fma(gr[row * 5 + 4], vi, racc);
       ldsI[row * kLdsStride + sc] = vi;
@@ -128,25 +143,32 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
   };
 
   const int nsteps = (int)((ke - kb + kBK - 1) / kBK);
+  const int frow = lane >> 4, fcol = lane & 15;
   if (nsteps > 0) {
     gload(kb);
-    stage_load(kb);
+    load(RA, kb);
     gstore(0);
-    if (nsteps > 1) gload(kb + kBK);
+    if (nsteps > 1) {
+      gload(kb + kBK);
+      load(RB, kb + kBK);
+    }
     __syncthreads();
-    stage_store(kb, 0);
+    store_rows(RA, kb, 0, 0, 8);
     if (nsteps > 1) gstore(1);
   }
   __syncthreads();
-  const int frow = lane >> 4, fcol = lane & 15;
-  for (int s = 0; s < nsteps; ++s) {
+  // one K-step: Rcur holds step s+1 (staged during the MFMAs), Rnxt receives step s+2
+  auto kstep = [&](int s, const Regs& Rcur, Regs& Rnxt) {
     const int buf = s & 1;
     const bool more = (s + 1) < nsteps;
     const bool more2 = (s + 2) < nsteps;
-    if (more) stage_load(kb + (int64_t)(s + 1) * kBK);
+#if GRAM_VARIANT != 4
+    if (more2) load(Rnxt, kb + (int64_t)(s + 2) * kBK);
+#endif
     if (more2) gload(kb + (int64_t)(s + 2) * kBK);
     const double* la = smem + (buf * 2 + 0) * kTileD;
     const double* lb = smem + (buf * 2 + 1) * kTileD;
+    const int64_t kn = kb + (int64_t)(s + 1) * kBK;
 #pragma unroll
     for (int ks = 0; ks < kBK / 4; ++ks) {
       double fa[4], fb[4];
@@ -155,15 +177,28 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
       for (int a = 0; a < 4; ++a) fa[a] = la[row * kLdsStride + wr * 64 + a * 16 + fcol];
 #pragma unroll
       for (int c = 0; c < 4; ++c) fb[c] = lb[row * kLdsStride + wc * 64 + c * 16 + fcol];
+#if GRAM_VARIANT == 3
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) acc[a][c][0] += fa[a] * fb[c];
+#else
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int c = 0; c < 4; ++c)
           acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[c], acc[a][c], 0, 0, 0);
+#endif
+#if GRAM_VARIANT != 4
+      if (more) store_rows(Rcur, kn, buf ^ 1, 2 * ks, 2);
+#endif
     }
-    if (more) stage_store(kb + (int64_t)(s + 1) * kBK, buf ^ 1);
     if (more2) gstore(buf);
     __syncthreads();
+  };
+  for (int s = 0; s < nsteps; s += 2) {
+    kstep(s, RB, RA);
+    if (s + 1 < nsteps) kstep(s + 1, RA, RB);
   }
 
   double* pt = part + ((int64_t)split * ntiles + tile) * (kGT * kGT);

@@ -406,6 +406,167 @@ __global__ __launch_bounds__(256) void whiten_kfu(
   }
 }
 
+// ---------------------------------------------------------------------------- whitening of Kfu columns, MFMA form
+// Same output as whiten_kfu, with Kfu built by v_mfma_f64_16x16x4_f64 in the Gram form
+// |v - z|^2 = |v - c|^2 + |z - c|^2 - 2 (v - c).(z - c)  (Distances.jl's pairwise form as used by
+// Stheno), centred to limit
+// cancellation (c = mean of the block's 256 pseudo-inputs).  Per 16-step sub-tile and wave (64 columns): DP/4 x 4 MFMAs give the 16 x 64
+// cross products in the C layout (lane: column ct*16 + (l&15), steps (l>>4) + 4r), the kernel
+// values are evaluated there (16 per lane, independent -> ILP), transposed through LDS, and the
+// lane of column c then runs the 16 filter steps.  Used for the smooth kernels (Matern-3/2,
+// Matern-5/2, EQ: a d^2 error of eps |v - c| |z - c| is harmless); Matern-1/2 keeps the direct
+// form (its kappa is not smooth in d^2 at 0).
+constexpr int kMT = 16;   // steps per sub-tile
+
+template <int TK, int OK, int DP>
+__global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
+    const double* __restrict__ rec, const double* __restrict__ v, int64_t ldv, int d,
+    const double* __restrict__ z, int64_t ldz, const double* __restrict__ zc, int64_t m,
+    int64_t mp, int64_t n, int L, double inv_lo, double s_o, double* __restrict__ beta,
+    int64_t ldb, double* __restrict__ send, int64_t mc) {
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  constexpr int SD = Sde<TK>::d;
+  constexpr int RS = Rec<SD>::size;
+  constexpr int VS = DP + 2;      // V tile row stride: conflict-free A-fragment reads
+  constexpr int NKS = DP / 4;
+  __shared__ __attribute__((aligned(16))) double vs[kMT * VS];
+  __shared__ __attribute__((aligned(16))) double xt[4][kMT][65];
+  __shared__ __attribute__((aligned(16))) double rl[kMT * RS];   // the sub-tile's gains records
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t j = blockIdx.x;
+  const int64_t cw0 = (int64_t)blockIdx.y * 256 + wave * 64;   // wave's first column
+  const int64_t col = cw0 + lane;                               // recursion column of this lane
+  const int fr = lane & 15, fq = lane >> 4;
+  // centre of this block's 256 pseudo-inputs (subtracted from V while staging, from Z here)
+  const double* cg = zc + (int64_t)blockIdx.y * DP;
+  // B fragments (z - c) and |z - c|^2 of the C-layout columns ct*16 + fr
+  double bf[4][NKS];
+  double zn[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    const int64_t zcol = cw0 + ct * 16 + fr;
+    const bool zv = zcol < m;
+    const int64_t zcc = zv ? zcol : 0;
+    double part = 0.0;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int dim = 4 * ks + fq;
+      const double zz = (zv && dim < d) ? z[zcc * ldz + dim] - cg[dim] : 0.0;
+      bf[ct][ks] = zz;
+      part = fma(zz, zz, part);
+    }
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+    zn[ct] = part;   // full |z - c|^2 of column ct*16 + fr (dims padded with zeros)
+  }
+  const int nks = (d + 3) / 4;
+  double mst[SD];
+#pragma unroll
+  for (int i = 0; i < SD; ++i) mst[i] = 0.0;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  const bool colv = col < m, cola = col < mp;
+  // next sub-tile's V rows and gains records are prefetched into registers (one MFMA /
+  // kernel-evaluation phase ahead) and written to LDS between the two barriers.
+  constexpr int VPT = (kMT * DP + 255) / 256;   // V elements per thread
+  double pv[VPT], pr;
+  auto prefetch = [&](int64_t kt_) {
+    const int nt_ = (kt_ + kMT <= k1) ? kMT : (int)(k1 - kt_);
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      const int e = tid + q * 256;
+      const int kk = e / DP, i = e % DP;
+      const bool ok_ = e < kMT * DP && kk < nt_ && i < d;
+      const int64_t kr = ok_ ? kt_ + kk : kt_;
+      pv[q] = ok_ ? v[kr * ldv + (ok_ ? i : 0)] - cg[i < DP ? i : 0] : 0.0;
+    }
+    pr = (tid < nt_ * RS) ? rec[kt_ * RS + tid] : 0.0;
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      const int e = tid + q * 256;
+      if (e < kMT * DP) vs[(e / DP) * VS + e % DP] = pv[q];
+    }
+    if (tid < kMT * RS) rl[tid] = pr;
+  };
+  if (k0 < k1) prefetch(k0);
+  for (int64_t kt = k0; kt < k1; kt += kMT) {
+    const int nt = (kt + kMT <= k1) ? kMT : (int)(k1 - kt);
+    __syncthreads();
+    commit();
+    __syncthreads();
+    if (kt + kMT < k1) prefetch(kt + kMT);
+    // cross products (v - c).(z - c) and the step norms |v - c|^2
+    d4 acc[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) acc[ct] = d4{0.0, 0.0, 0.0, 0.0};
+    double vnp = 0.0;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      if (ks < nks) {
+        const double a = vs[fr * VS + 4 * ks + fq];
+        vnp = fma(a, a, vnp);
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+          acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bf[ct][ks], acc[ct], 0, 0, 0);
+      }
+    }
+    vnp += __shfl_xor(vnp, 16, 64);
+    vnp += __shfl_xor(vnp, 32, 64);   // lanes fr, fr+16, fr+32, fr+48 hold |v_fr - c|^2
+    // kernel values in the C layout: step fq + 4 r, column ct*16 + fr
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double vn = __shfl(vnp, fq + 4 * r, 64);
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        double d2 = vn + zn[ct] - 2.0 * acc[ct][r];
+        d2 = d2 > 0.0 ? d2 : 0.0;
+        xt[wave][fq + 4 * r][ct * 16 + fr] = s_o * kappa_sq<OK>(d2, inv_lo);
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    for (int kk = 0; kk < nt; ++kk) {
+      const int64_t k = kt + kk;
+      const double x = colv ? xt[wave][kk][lane] : 0.0;
+      const double* rr = rl + kk * RS;
+      double mm[SD];
+#pragma unroll
+      for (int i = 0; i < SD; ++i) {
+        double a2 = 0.0;
+#pragma unroll
+        for (int q = 0; q < SD; ++q) a2 = fma(rr[i * SD + q], mst[q], a2);
+        mm[i] = a2;
+      }
+      const double ev = x - mm[0];
+      const double al = ev * rr[SD * SD + SD];
+#pragma unroll
+      for (int i = 0; i < SD; ++i) mst[i] = fma(rr[SD * SD + i], ev, mm[i]);
+      if (cola) beta[k * ldb + col] = al;
+    }
+  }
+  if (cola) {
+#pragma unroll
+    for (int i = 0; i < SD; ++i) send[(j * mc + col) * kSStride + i] = mst[i];
+  }
+}
+
+// Centres of the pseudo-input column groups (256 columns each): zc[g][i] = mean_c z[c][i].
+__global__ void zcenter_kernel(const double* __restrict__ z, int64_t ldz, int d, int64_t m,
+                               int dp, double* __restrict__ zc) {
+  const int64_t g = blockIdx.x;
+  const int i = threadIdx.x;
+  if (i >= dp) return;
+  double s = 0.0;
+  int cnt = 0;
+  for (int64_t c = g * 256; c < g * 256 + 256 && c < m; ++c) {
+    if (i < d) s += z[c * ldz + i];
+    ++cnt;
+  }
+  zc[g * dp + i] = (cnt > 0 && i < d) ? s / cnt : 0.0;
+}
+
 // ---------------------------------------------------------------------------- whitening of a vector per chain
 // One 64-thread block per (chunk, chain): the chunk's gains records and data are staged into
 // LDS with coalesced loads, lane 0 runs the recursion out of LDS, and the block writes the
@@ -991,6 +1152,56 @@ int dp_bucket(int d) {
   if (d <= 32) return 32;
   if (d <= 64) return 64;
   return -1;
+}
+
+template <int TK, int OK>
+static void launch_whiten_mfma_k(hipStream_t st, int dp, dim3 grid, const double* rec,
+                                 const double* v, int64_t ldv, int d, const double* z,
+                                 int64_t ldz, const double* zc, int64_t m, int64_t mp, int64_t n,
+                                 int L, double inv_lo, double s_o, double* beta, int64_t ldb,
+                                 double* send, int64_t mc) {
+  switch (dp) {
+    case 16: whiten_kfu_mfma<TK, OK, 16><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case 32: whiten_kfu_mfma<TK, OK, 32><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case 48: whiten_kfu_mfma<TK, OK, 48><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    default: whiten_kfu_mfma<TK, OK, 64><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+  }
+}
+
+template <int TK>
+static void launch_whiten_mfma_t(hipStream_t st, int dp, dim3 grid, const double* rec,
+                                 const double* v, int64_t ldv, int d, const double* z,
+                                 int64_t ldz, const double* zc, int64_t m, int64_t mp, int64_t n,
+                                 int L, int ok, double inv_lo, double s_o, double* beta,
+                                 int64_t ldb, double* send, int64_t mc) {
+  switch (ok) {
+    case KM32: launch_whiten_mfma_k<TK, KM32>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case KEQ: launch_whiten_mfma_k<TK, KEQ>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    default: launch_whiten_mfma_k<TK, KM52>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+  }
+}
+
+int mfma_dp_bucket(int d) {
+  if (d <= 16) return 16;
+  if (d <= 32) return 32;
+  if (d <= 48) return 48;
+  if (d <= 64) return 64;
+  return -1;
+}
+
+void launch_whiten_kfu_mfma(hipStream_t st, int time_kind, int out_kind, const double* rec,
+                            const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
+                            double* zc, int64_t m, int64_t mp, int64_t n, int L, int64_t nch,
+                            double inv_lo, double s_o, double* beta, int64_t ldb, double* send,
+                            int64_t mc) {
+  const int dp = mfma_dp_bucket(d);
+  zcenter_kernel<<<(unsigned)((mp + 255) / 256), 64, 0, st>>>(z, ldz, d, m, dp, zc);
+  dim3 grid((unsigned)nch, (unsigned)((mp + 255) / 256));
+  switch (time_kind) {
+    case KM12: launch_whiten_mfma_t<KM12>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc); break;
+    case KM32: launch_whiten_mfma_t<KM32>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc); break;
+    default: launch_whiten_mfma_t<KM52>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc); break;
+  }
 }
 
 void launch_whiten_kfu(hipStream_t st, int time_kind, int out_kind, const double* rec,

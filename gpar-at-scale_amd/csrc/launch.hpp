@@ -83,6 +83,13 @@ void launch_whiten_kfu(hipStream_t st, int time_kind, int out_kind, const double
                        const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
                        int64_t m, int64_t mp, int64_t n, int L, int64_t nch, double inv_lo,
                        double s_o, double* beta, int64_t ldb, double* send, int64_t mc);
+// MFMA Gram-form Kfu (smooth out kernels: Matern-3/2, Matern-5/2, EQ); zc: (mp/64) x 64 workspace
+int mfma_dp_bucket(int d);
+void launch_whiten_kfu_mfma(hipStream_t st, int time_kind, int out_kind, const double* rec,
+                            const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
+                            double* zc, int64_t m, int64_t mp, int64_t n, int L, int64_t nch,
+                            double inv_lo, double s_o, double* beta, int64_t ldb, double* send,
+                            int64_t mc);
 void launch_whiten_vec(hipStream_t st, int sdim, const double* rec, int64_t recstride,
                        const double* y, int64_t ldy, int64_t n, int L, int64_t nch, int nchains,
                        double* alpha, int64_t lda, double* send, int64_t sendstride, int64_t mc,

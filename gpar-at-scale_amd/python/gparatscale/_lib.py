@@ -25,6 +25,7 @@ EXPORTED = (
     "gpar_fit", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
     "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_reset_stats",
+    "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
 )
 
 
@@ -105,6 +106,13 @@ def load(path: str | None = None):
             "gpar_exact_posterior": (i32, [vp, i64, i64, dp, i64, dp, i64, dp, i64, i32, i32,
                                            dp, i32, dp, dp]),
         }
+        sig.update({
+            "gpar_nm_create": (i32, [i32, dp, C.POINTER(GparFitOptions), C.POINTER(vp)]),
+            "gpar_nm_destroy": (i32, [vp]),
+            "gpar_nm_ask": (i32, [vp, dp]),
+            "gpar_nm_tell": (i32, [vp, C.c_double]),
+            "gpar_nm_result": (i32, [vp, dp, C.POINTER(C.c_double), C.POINTER(i32), C.POINTER(i32)]),
+        })
         for name, (res, args) in sig.items():
             f = getattr(lib, name)
             f.restype = res
@@ -180,3 +188,57 @@ def context(device: int = 0) -> Context:
         c = Context(device)
         _ctx[device] = c
     return c
+
+
+class NelderMead:
+    """The library's Nelder-Mead (Optim.jl NelderMead restated, nelder_mead.hpp) as an
+    ask/tell object; host only, usable without a GPU."""
+
+    def __init__(self, x0, max_evals=0, max_iterations=1000, g_tol=1e-8, time_limit=0.0):
+        import numpy as np
+        self._np = np
+        lib = load()
+        self.n = len(x0)
+        x = np.ascontiguousarray(np.asarray(x0, dtype=np.float64))
+        opts = GparFitOptions(int(max_evals), int(max_iterations), float(g_tol), float(time_limit))
+        h = C.c_void_p()
+        code = lib.gpar_nm_create(self.n, x.ctypes.data_as(C.c_void_p), C.byref(opts), C.byref(h))
+        if code != GPAR_OK:
+            raise GparError(code, "gpar_nm_create failed")
+        self.h = h
+
+    def ask(self):
+        x = self._np.zeros(self.n)
+        r = load().gpar_nm_ask(self.h, x.ctypes.data_as(C.c_void_p))
+        return x if r == 1 else None
+
+    def tell(self, f):
+        code = load().gpar_nm_tell(self.h, float(f))
+        if code != GPAR_OK:
+            raise GparError(code, "gpar_nm_tell: optimiser already finished")
+
+    def result(self):
+        x = self._np.zeros(self.n)
+        f = C.c_double()
+        ev = C.c_int32()
+        it = C.c_int32()
+        load().gpar_nm_result(self.h, x.ctypes.data_as(C.c_void_p), C.byref(f), C.byref(ev), C.byref(it))
+        return x, float(f.value), int(ev.value), int(it.value)
+
+    def __del__(self):
+        try:
+            if self.h:
+                load().gpar_nm_destroy(self.h)
+                self.h = None
+        except Exception:
+            pass
+
+
+def nelder_mead(f, x0, **kw):
+    nm = NelderMead(x0, **kw)
+    while True:
+        x = nm.ask()
+        if x is None:
+            break
+        nm.tell(f(x))
+    return nm.result()

@@ -1,0 +1,68 @@
+"""Output sharding across GPUs (one process per GPU, torch.distributed over RCCL / gloo).
+
+The reference fits GPAR outputs one after another in a serial loop
+(examples/GPAR_scaled_examples.jl:132-175, gpar_scaled_inference.jl:20-136 per output).  Output p
+only needs the *observed* previous outputs y_1..y_{p-1} as inputs, never a fitted model of them,
+so outputs are independent work units: each rank fits and predicts its own outputs with no
+data-path collective.  Shared inputs (t, Y, t*) are broadcast from rank 0 once; the fitted
+hyperparameters (P x 5 doubles) are gathered with one small all-reduce per step.
+"""
+from __future__ import annotations
+
+import heapq
+
+import numpy as np
+
+# Per-objective-evaluation cost model of output p (ms at N=1e6, M=512 on one MI355X, profiles/):
+# the Gram beta^T beta is independent of the input dimension D = p - 1, the whitening grows with
+# it, the temporal-only output 1 is ~20x cheaper.  Only relative sizes matter.
+GRAM_MS = 6.9
+WHITEN_MS0, WHITEN_MS_PER_D = 1.3, 0.033
+SDE_MS = 0.4
+
+
+def output_cost(p: int) -> float:
+    if p == 1:
+        return SDE_MS
+    return GRAM_MS + WHITEN_MS0 + WHITEN_MS_PER_D * (p - 1)
+
+
+def assign_outputs(P: int, world: int) -> list[list[int]]:
+    """Longest-processing-time-first assignment of outputs 1..P to `world` ranks.
+
+    Deterministic (ties broken by rank), every output owned by exactly one rank."""
+    heap = [(0.0, r) for r in range(world)]
+    owned: list[list[int]] = [[] for _ in range(world)]
+    for p in sorted(range(1, P + 1), key=lambda q: (-output_cost(q), q)):
+        load, r = heapq.heappop(heap)
+        owned[r].append(p)
+        heapq.heappush(heap, (load + output_cost(p), r))
+    return [sorted(o) for o in owned]
+
+
+def broadcast_inputs(tensors, src: int = 0):
+    """Broadcast already-allocated tensors from rank `src` (no-op without a process group)."""
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return
+    for x in tensors:
+        dist.broadcast(x, src)
+
+
+def gather_thetas(local: dict, P: int, device=None) -> np.ndarray:
+    """All ranks' fitted hyperparameters as a P x 5 array (row p-1 = output p).
+
+    Each output is owned by exactly one rank, so a sum all-reduce of zero-padded rows is a gather."""
+    import torch
+    import torch.distributed as dist
+    th = np.zeros((P, 5))
+    for p, v in local.items():
+        v = np.asarray(v, dtype=np.float64)
+        th[p - 1, : v.shape[0]] = v
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        tt = torch.from_numpy(th)
+        if device is not None:
+            tt = tt.to(device)
+        dist.all_reduce(tt)
+        th = tt.cpu().numpy()
+    return th

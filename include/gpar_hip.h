@@ -194,6 +194,22 @@ int32_t gpar_exact_posterior(gpar_ctx* ctx, int64_t n, int64_t dx, const double*
                              int64_t ldxs, int32_t time_kernel, int32_t out_kernel,
                              const double* theta, int32_t mem, double* mean, double* var);
 
+/* ---------------------------------------------------------------- Nelder-Mead (host only)
+ * The optimiser gpar_fit / gpar_sde_predictions run (Optim.jl NelderMead restated:
+ * AffineSimplexer(0.025, 0.5), adaptive parameters, g_tol, iterations, time_limit, and the final
+ * centroid evaluation of Optim's after_while!), exposed as an ask/tell state machine so a
+ * host-language driver (the reference's Julia, a test) can step it with its own objective.
+ * No GPU involved. */
+typedef struct gpar_nm gpar_nm;
+int32_t gpar_nm_create(int32_t n, const double* x0, const gpar_fit_options* opts, gpar_nm** out);
+int32_t gpar_nm_destroy(gpar_nm* nm);
+/* 1 while the optimiser wants more evaluations; x receives the next point (n doubles) */
+int32_t gpar_nm_ask(gpar_nm* nm, double* x);
+int32_t gpar_nm_tell(gpar_nm* nm, double f);
+/* minimiser (n doubles), its value and the number of evaluations / iterations so far */
+int32_t gpar_nm_result(const gpar_nm* nm, double* x_min, double* f_min, int32_t* evals,
+                       int32_t* iterations);
+
 #ifdef __cplusplus
 }
 #endif

@@ -10,3 +10,11 @@ for p in (ROOT, os.path.join(ROOT, "gpar-at-scale_amd", "python")):
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the gfx950 kernels)")
+
+
+def pytest_sessionstart(session):
+    """Build libgparhip.so in-tree if it is missing (the ABI / host tests load it)."""
+    lib = os.path.join(ROOT, "gpar-at-scale_amd", "libgparhip.so")
+    if not os.path.exists(lib):
+        import subprocess
+        subprocess.run(["make", "-C", os.path.join(ROOT, "gpar-at-scale_amd"), "-j8"], check=False)

@@ -1,0 +1,80 @@
+"""CPU, world_size 2 over gloo: the multi-GPU path of bench.py (gparatscale.shard).
+
+Rank 0 builds the GPAR dataset and broadcasts it; each rank fits only the outputs
+assign_outputs() gives it (the per-output fit of dtc.jl:11-77, here with the oracle objective
+as the stand-in worker since there is no GPU); gather_thetas() must return exactly what a
+serial loop over all outputs (GPAR_scaled_examples.jl:132-175) produces.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import gpar_oracle as O
+
+P, N, M, EV = 5, 160, 10, 12
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _fit(t, Y, p):
+    if p == 1:
+        th, _, _ = O.get_sde_predictions(t, Y[:, 0], t[:3], log_theta0=(0.0, 0.0, -2.0), max_evals=EV)
+        return np.array(list(th))
+    V = Y[:, : p - 1].T
+    Z = O.pick_pseudo_inputs(V, M, p)
+    nm = O.nelder_mead(lambda x: -O.compute_gpar_dtc_objective(V, Z, t, Y[:, p - 1], O.unpack_gpar(x))[0],
+                       np.array([0.0, 0.0, 0.0, 0.0, -2.0]), max_evals=EV)
+    return np.array(O.unpack_gpar(nm.x_min))
+
+
+def _worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "gpar-at-scale_amd", "python"))
+    from gparatscale import shard as S
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t_d = torch.zeros(N, dtype=torch.float64)
+        Y_d = torch.zeros((N, P), dtype=torch.float64)
+        if rank == 0:
+            t, Y = O.synthetic_gpar(N, P, seed=4, noise=0.3)
+            t_d.copy_(torch.from_numpy(t))
+            Y_d.copy_(torch.from_numpy(Y))
+        S.broadcast_inputs((t_d, Y_d))
+        t, Y = t_d.numpy(), Y_d.numpy()
+        mine = S.assign_outputs(P, world)[rank]
+        th = S.gather_thetas({p: _fit(t, Y, p) for p in mine}, P)
+        if rank == 0:
+            np.save(out, th)
+    finally:
+        dist.destroy_process_group()
+
+
+def test_assign_outputs_partitions():
+    from gparatscale import shard as S
+    for world in (1, 2, 3, 8):
+        owned = S.assign_outputs(64, world)
+        flat = sorted(p for o in owned for p in o)
+        assert flat == list(range(1, 65))
+        loads = [sum(S.output_cost(p) for p in o) for o in owned]
+        assert max(loads) <= 1.05 * sum(loads) / world
+
+
+def test_sharded_fit_equals_serial(tmp_path):
+    out = str(tmp_path / "theta.npy")
+    mp.start_processes(_worker, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    th = np.load(out)
+    t, Y = O.synthetic_gpar(N, P, seed=4, noise=0.3)
+    for p in range(1, P + 1):
+        ref = _fit(t, Y, p)
+        np.testing.assert_array_equal(th[p - 1, : ref.shape[0]], ref)
