@@ -1,0 +1,57 @@
+"""Run a few DTC objective evaluations of one north-star output (N=1e6, M=512, D inputs) on the
+GPU, for rocprofv3 counter passes and kernel timing of the Gram / whitening kernels.
+
+    rocprofv3 --pmc FETCH_SIZE --kernel-include-regex gram_kernel -d gpurun_out/pmc_fetch \
+        -o run --output-format csv -- python3 tools/gram_probe.py --evals 3
+"""
+import argparse
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "gpar-at-scale_amd", "python"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=1_000_000)
+    ap.add_argument("--m", type=int, default=512)
+    ap.add_argument("--d", type=int, default=32)
+    ap.add_argument("--evals", type=int, default=3)
+    ap.add_argument("--kernel", default="matern52")
+    a = ap.parse_args()
+    import numpy as np
+    import torch
+    import gparatscale as G
+    from gparatscale import data as D
+
+    P = a.d + 1
+    ds = D.gpar_dataset(a.n, P, seed=0, observation_noise=0.8)
+    dev = torch.device("cuda", 0)
+    t = torch.from_numpy(ds["t"]).to(dev)
+    Y = torch.from_numpy(ds["Y"]).to(dev)
+    y = Y[:, P - 1].contiguous()
+    Z = torch.from_numpy(D.pseudo_inputs(ds["Y"][:, : P - 1], a.m, seed=P)).to(dev)
+    pr, keep = G.make_problem(Y[:, : P - 1], Z, t, y, a.kernel, "matern52")
+    ctx = G.context(0)
+    theta = np.array([[1.0, 1.0, 1.0, 1.0, 0.2]])
+    G.dtc_objective_batch([pr], theta)
+    ctx.set_profiling(True)
+    ctx.reset_stats()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(a.evals):
+        v = G.dtc_objective_batch([pr], theta * (1.0 + 0.01 * i))
+    torch.cuda.synchronize()
+    el = (time.perf_counter() - t0) * 1e3 / a.evals
+    out = [f"N={a.n} M={a.m} D={a.d} ms/eval={el:.3f} dtc={v[0]:.6f}"]
+    for k in ("gram", "whiten", "gains", "dense"):
+        n, ms = ctx.kernel_stats(k)
+        if n:
+            out.append(f"{k}: {n} launches avg {ms / n:.4f} ms")
+    print("; ".join(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()
