@@ -940,12 +940,6 @@ int32_t gpar_lgssm_logpdf(gpar_ctx* ctx, int32_t nchains, int64_t n, const doubl
   API_END(ctx)
 }
 
-static int32_t not_yet(gpar_ctx* ctx, const char* what) {
-  if (!ctx) return GPAR_ERR_STATE;
-  ctx->err = std::string(what) + ": not implemented in this build";
-  return GPAR_ERR_UNSUPPORTED;
-}
-
 int32_t gpar_predict(gpar_ctx* ctx, const gpar_problem* prob, const double* theta,
                      int64_t n_star, const double* t_star, const double* v_star, int64_t ldvs,
                      int32_t mode, int32_t samples, uint64_t seed, double* mean, double* std) {
@@ -1097,17 +1091,145 @@ int32_t gpar_sde_predictions(gpar_ctx* ctx, int32_t nchains, int64_t n, const do
   API_END(ctx)
 }
 
+// ---------------------------------------------------------------- exact GP / GPAR (a10)
+namespace gpar {
+struct ExactIn {
+  const double* x;   // device, point-major, ld dx
+  const double* y;   // device
+  double inv_lt, s_t, inv_lo, s_o, s2;
+};
+
+// theta: (l_t, time_var, l_o, out_var, sigma); dx == 1 uses entries 0, 1, 4 (optimized.jl:28-36).
+static ExactIn exact_prepare(gpar_ctx* c, int64_t n, int64_t dx, const double* x, int64_t ldx,
+                             const double* y, int32_t tk, int32_t ok, const double* theta,
+                             int32_t mem, const char* tag) {
+  ARGCHECK(n >= 1 && n <= 2048, "exact GP supports 1 <= n <= 2048");
+  ARGCHECK(dx >= 1 && ldx >= dx && x && y && theta, "bad argument");
+  ARGCHECK(tk >= GPAR_MATERN12 && tk <= GPAR_EQ && ok >= GPAR_MATERN12 && ok <= GPAR_EQ,
+           "unknown kernel");
+  ARGCHECK(mem == GPAR_MEM_HOST || mem == GPAR_MEM_DEVICE, "bad mem");
+  const int used[3] = {0, 1, 4};
+  for (int q : used) ARGCHECK(std::isfinite(theta[q]) && theta[q] > 0.0, "theta entries must be positive");
+  if (dx > 1)
+    for (int q = 2; q < 4; ++q) ARGCHECK(std::isfinite(theta[q]) && theta[q] > 0.0, "theta entries must be positive");
+  ExactIn e;
+  e.inv_lt = 1.0 / theta[0];
+  e.s_t = theta[1] * theta[1];
+  e.inv_lo = dx > 1 ? 1.0 / theta[2] : 0.0;
+  e.s_o = dx > 1 ? theta[3] * theta[3] : 0.0;
+  e.s2 = theta[4] * theta[4];
+  if (mem == GPAR_MEM_HOST) {
+    double* xx = ws<double>(c, std::string(tag) + "_x", (size_t)n * dx);
+    double* yy = ws<double>(c, std::string(tag) + "_y", (size_t)n);
+    HIPCHECK(hipMemcpy2DAsync(xx, dx * sizeof(double), x, ldx * sizeof(double), dx * sizeof(double),
+                              n, hipMemcpyHostToDevice, c->stream));
+    h2d(c, yy, y, n);
+    e.x = xx;
+    e.y = yy;
+  } else {
+    ARGCHECK(ldx == dx, "device inputs must be dense (ldx == dx)");
+    e.x = x;
+    e.y = y;
+  }
+  return e;
+}
+
+// L = chol(K(x, x) + s2 I) (row-major n x n in ws "ex_L"), w = L^{-1} y.
+static void exact_factor(gpar_ctx* c, const ExactIn& e, int64_t n, int64_t dx, int32_t tk,
+                         int32_t ok, double** L_out, double** w_out, int** status_out) {
+  double* L = ws<double>(c, "ex_L", (size_t)n * n);
+  double* w = ws<double>(c, "ex_w", (size_t)n);
+  int* status = ws<int>(c, "ex_status", 1);
+  HIPCHECK(hipMemsetAsync(status, 0, sizeof(int), c->stream));
+  Timed tm_(c, "exact");
+  launch_exact_cov(c->stream, e.x, dx, n, e.x, dx, n, (int)dx, tk, ok, e.inv_lt, e.s_t, e.inv_lo,
+                   e.s_o, e.s2, L, n);
+  check_launch("exact_cov");
+  CholJobHost cj{L, n, (int)n, 0.0, status};
+  auto* dcj = ws<CholJobHost>(c, "ex_chol", 1);
+  h2d(c, dcj, &cj, 1);
+  launch_chol(c->stream, dcj, 1);
+  check_launch("exact chol");
+  TrsvJobHost tj{L, n, (int)n, e.y, w, 0};
+  auto* dtj = ws<TrsvJobHost>(c, "ex_trsv", 1);
+  h2d(c, dtj, &tj, 1);
+  launch_trsv(c->stream, dtj, 1);
+  check_launch("exact trsv");
+  *L_out = L;
+  *w_out = w;
+  *status_out = status;
+}
+
+static void exact_check_pd(gpar_ctx* c, const int* status) {
+  int st = 0;
+  d2h(c, &st, status, 1);
+  sync(c);
+  if (st) throw Error(GPAR_ERR_NOT_PD, "cholesky: K + sigma^2 I is not positive definite");
+}
+}  // namespace gpar
+
 int32_t gpar_exact_logpdf(gpar_ctx* ctx, int64_t n, int64_t dx, const double* x, int64_t ldx,
                           const double* y, int32_t time_kernel, int32_t out_kernel,
                           const double* theta, int32_t mem, double* lml_out) {
-  return not_yet(ctx, "gpar_exact_logpdf");
+  API_BEGIN(ctx)
+  ARGCHECK(lml_out, "null output");
+  ExactIn e = exact_prepare(ctx, n, dx, x, ldx, y, time_kernel, out_kernel, theta, mem, "exl");
+  double *L, *w;
+  int* status;
+  exact_factor(ctx, e, n, dx, time_kernel, out_kernel, &L, &w, &status);
+  double* dout = ws<double>(ctx, "ex_out", 1);
+  launch_exact_logpdf_finish(ctx->stream, L, n, (int)n, w, status, dout);
+  check_launch("exact finish");
+  exact_check_pd(ctx, status);
+  d2h(ctx, lml_out, dout, 1);
+  sync(ctx);
+  API_END(ctx)
 }
 
 int32_t gpar_exact_posterior(gpar_ctx* ctx, int64_t n, int64_t dx, const double* x, int64_t ldx,
                              const double* y, int64_t n_star, const double* x_star,
                              int64_t ldxs, int32_t time_kernel, int32_t out_kernel,
                              const double* theta, int32_t mem, double* mean, double* var) {
-  return not_yet(ctx, "gpar_exact_posterior");
+  API_BEGIN(ctx)
+  ARGCHECK(n_star >= 1 && x_star && ldxs >= dx && mean && var, "bad argument");
+  ExactIn e = exact_prepare(ctx, n, dx, x, ldx, y, time_kernel, out_kernel, theta, mem, "exp");
+  const double* xs = x_star;
+  if (mem == GPAR_MEM_HOST) {
+    double* xx = ws<double>(ctx, "exp_xs", (size_t)n_star * dx);
+    HIPCHECK(hipMemcpy2DAsync(xx, dx * sizeof(double), x_star, ldxs * sizeof(double),
+                              dx * sizeof(double), n_star, hipMemcpyHostToDevice, ctx->stream));
+    xs = xx;
+  } else {
+    ARGCHECK(ldxs == dx, "device inputs must be dense (ldxs == dx)");
+  }
+  double *L, *w;
+  int* status;
+  exact_factor(ctx, e, n, dx, time_kernel, out_kernel, &L, &w, &status);
+  double* Ks = ws<double>(ctx, "ex_Ks", (size_t)n * n_star);
+  double* W = ws<double>(ctx, "ex_W", (size_t)n * n_star);
+  launch_exact_cov(ctx->stream, e.x, dx, n, xs, dx, n_star, (int)dx, time_kernel, out_kernel,
+                   e.inv_lt, e.s_t, e.inv_lo, e.s_o, 0.0, Ks, n_star);
+  check_launch("exact cross cov");
+  TrsmJobHost tj{L, n, Ks, n_star, W, n_star, (int)n, n_star, 0, 0};
+  auto* dtj = ws<TrsmJobHost>(ctx, "ex_trsm", 1);
+  h2d(ctx, dtj, &tj, 1);
+  launch_trsm(ctx->stream, dtj, 1, n_star);
+  check_launch("exact trsm");
+  double* dm = mean;
+  double* dv = var;
+  if (mem == GPAR_MEM_HOST) {
+    dm = ws<double>(ctx, "exp_mean", n_star);
+    dv = ws<double>(ctx, "exp_var", n_star);
+  }
+  launch_exact_post(ctx->stream, W, n_star, (int)n, n_star, w, e.s_t + e.s_o, dm, dv);
+  check_launch("exact posterior");
+  exact_check_pd(ctx, status);
+  if (mem == GPAR_MEM_HOST) {
+    d2h(ctx, mean, dm, n_star);
+    d2h(ctx, var, dv, n_star);
+  }
+  sync(ctx);
+  API_END(ctx)
 }
 
 // ---------------------------------------------------------------- host-only Nelder-Mead

@@ -167,4 +167,13 @@ void launch_scatter_chains(hipStream_t st, const double* src, int64_t lds, int64
 void launch_gather_chains(hipStream_t st, const double* src, int64_t lds, int64_t ns,
                           const int64_t* pos, double* dst, int64_t ldd, int nchains);
 
+// k_exact.hip
+void launch_exact_cov(hipStream_t st, const double* x, int64_t ldx, int64_t n, const double* x2,
+                      int64_t ldx2, int64_t n2, int dx, int tk, int ok, double inv_lt, double s_t,
+                      double inv_lo, double s_o, double diag, double* K, int64_t ldk);
+void launch_exact_logpdf_finish(hipStream_t st, const double* L, int64_t ld, int n, const double* w,
+                                const int* status, double* out);
+void launch_exact_post(hipStream_t st, const double* W, int64_t ldw, int n, int64_t n_star,
+                       const double* w, double kss, double* mean, double* var);
+
 }  // namespace gpar

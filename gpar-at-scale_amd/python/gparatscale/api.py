@@ -407,3 +407,116 @@ def get_sde_predictions_device(t, Y, t_star, kernel_structure="matern52", log_th
     if nch == 1:
         return tuple(theta[0]), mean[0], var[0]
     return theta, mean, var
+
+
+# ----------------------------------------------------------------------------- exact GP / GPAR
+def _theta5(theta, dx):
+    th = np.asarray(theta, dtype=np.float64).ravel()
+    if dx == 1 and th.shape[0] == 3:        # unpack_gp order (l, process_var, noise_sigma)
+        th = np.array([th[0], th[1], 1.0, 1.0, th[2]])
+    return np.ascontiguousarray(th.reshape(5))
+
+
+def exact_logpdf(X, y, theta, time_kernel="eq", out_kernel="eq", device=0):
+    """logpdf(f(x, sigma^2), y) of the exact GP (dx == 1, optimized.jl:28-36, theta =
+    (l, process_var, noise_sigma)) or GPAR (optimized.jl:132-154, theta = unpack_gpar order).
+    X: 1-D times or ColVecs dx x n with row 0 = time."""
+    ctx = context(device)
+    keep = _Keep()
+    xp, ldx, n, dx = _host_points(X, keep)
+    th = _theta5(theta, dx)
+    out = np.zeros(1)
+    ctx.check(_lib.load().gpar_exact_logpdf(ctx.h, n, dx, xp, ldx, _host_vec(y, keep),
+                                            _kernel_id(time_kernel), _kernel_id(out_kernel),
+                                            _ptr(th), _lib.GPAR_MEM_HOST, _ptr(out)))
+    return float(out[0])
+
+
+def exact_posterior(X, y, X_star, theta, time_kernel="eq", out_kernel="eq", device=0):
+    """Marginals (mean, var) of f at X_star under the exact posterior
+    gp | (gp(x, sigma^2) <- y)  (optimized.jl:94,236)."""
+    ctx = context(device)
+    keep = _Keep()
+    xp, ldx, n, dx = _host_points(X, keep)
+    sp, ldxs, ns, dxs = _host_points(X_star, keep)
+    if dxs != dx:
+        raise _lib.DomainError(_lib.GPAR_ERR_ARG, "X_star must have the dimension of X")
+    th = _theta5(theta, dx)
+    mean = np.zeros(ns)
+    var = np.zeros(ns)
+    ctx.check(_lib.load().gpar_exact_posterior(ctx.h, n, dx, xp, ldx, _host_vec(y, keep), ns, sp,
+                                               ldxs, _kernel_id(time_kernel), _kernel_id(out_kernel),
+                                               _ptr(th), _lib.GPAR_MEM_HOST, _ptr(mean), _ptr(var)))
+    return mean, var
+
+
+@dataclass
+class ExactGP:
+    """Result of create_optim_gp[ar]: the fitted kernel (the reference returns the Stheno GP
+    and opt_params)."""
+    X: np.ndarray
+    y: np.ndarray
+    theta: tuple
+    time_kernel: str
+    out_kernel: str
+    device: int = 0
+
+    def logpdf(self):
+        return exact_logpdf(self.X, self.y, self.theta, self.time_kernel, self.out_kernel, self.device)
+
+    def marginals(self, X_star):
+        """Posterior marginals (mean, var) at X_star: the create_optim_gp[ar]_post posterior."""
+        return exact_posterior(self.X, self.y, X_star, self.theta, self.time_kernel,
+                               self.out_kernel, self.device)
+
+
+def _nm_fit(nlml, x0, max_evals):
+    nm = _lib.NelderMead(x0, max_evals=max_evals)
+    while (x := nm.ask()) is not None:
+        try:
+            f = nlml(x)
+        except _lib.PosDefException:
+            f = np.inf
+        nm.tell(f)
+    return nm.result()[0]
+
+
+def create_optim_gp(input_locations, outputs, kernel_structure="eq", i_log_l=None,
+                    i_log_process_var=None, i_log_noise_sigma=None, max_evals=0, rng=None, device=0):
+    """optimized.jl:19-59: NelderMead on -logpdf over (l, process_var, noise_sigma);
+    returns (ExactGP, opt_params)."""
+    x = np.asarray(input_locations, dtype=np.float64).ravel()
+    y = np.asarray(outputs, dtype=np.float64)
+    x0 = parse_initial_params([i_log_l, i_log_process_var, i_log_noise_sigma], rng)
+    xm = _nm_fit(lambda p: -exact_logpdf(x, y, unpack_gp(p), kernel_structure, device=device),
+                 x0, max_evals)
+    th = unpack_gp(xm)
+    return ExactGP(x, y, th, kernel_structure, kernel_structure, device), th
+
+
+def create_optim_gpar(input_locations, outputs, time_kernel="eq", out_kernel="eq",
+                      i_log_time_l=None, i_log_time_var=None, i_log_out_l=None,
+                      i_log_out_var=None, i_log_noise_sigma=None, multi_input=True, max_evals=0,
+                      rng=None, device=0):
+    """optimized.jl:106-183 (multi_input=False falls back to create_optim_gp, :118-127)."""
+    if not multi_input:
+        return create_optim_gp(input_locations, outputs, time_kernel, i_log_time_l, i_log_time_var,
+                               i_log_noise_sigma, max_evals, rng, device)
+    X = to_colvecs(input_locations)
+    y = np.asarray(outputs, dtype=np.float64)
+    x0 = parse_initial_params([i_log_time_l, i_log_time_var, i_log_out_l, i_log_out_var,
+                               i_log_noise_sigma], rng)
+    xm = _nm_fit(lambda p: -exact_logpdf(X, y, unpack_gpar(p), time_kernel, out_kernel, device),
+                 x0, max_evals)
+    th = unpack_gpar(xm)
+    return ExactGP(X, y, th, time_kernel, out_kernel, device), th
+
+
+def create_optim_gp_post(input_locations, outputs, kernel_structure="eq", **kw):
+    """optimized.jl:76-97: the fitted GP conditioned on the data (use .marginals(x_star))."""
+    return create_optim_gp(input_locations, outputs, kernel_structure, **kw)[0]
+
+
+def create_optim_gpar_post(input_locations, outputs, time_kernel="eq", out_kernel="eq", **kw):
+    """optimized.jl:201-239."""
+    return create_optim_gpar(input_locations, outputs, time_kernel, out_kernel, **kw)[0]

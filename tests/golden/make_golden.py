@@ -87,9 +87,17 @@ def main():
     Ks = O.exact_gpar_kernel(X, Xs, theta)
     kss = np.diag(O.exact_gpar_kernel(Xs, Xs, theta))
     mean, var = O.exact_posterior(K, Ks, kss, Y[:, 2], theta[4])
+    # plain GP on time with a Matern-3/2 kernel (optimized.jl:28-36), theta = (l, pv, sigma)
+    th1 = (0.7, 1.4, 0.3)
+    K1 = O.exact_gp_kernel(t, t, th1, "matern32")
+    ts = t[::3] + 0.01
+    m1, v1 = O.exact_posterior(K1, O.exact_gp_kernel(t, ts, th1, "matern32"),
+                               np.full(len(ts), th1[1] ** 2), Y[:, 0], th1[2])
     np.savez_compressed(os.path.join(HERE, "exact.npz"), X=X, y=Y[:, 2], X_star=Xs,
                         theta=np.array(theta), logpdf=O.exact_logpdf(K, Y[:, 2], theta[4]),
-                        post_mean=mean, post_var=var)
+                        post_mean=mean, post_var=var, gp_t=t, gp_y=Y[:, 0], gp_t_star=ts,
+                        gp_theta=np.array(th1), gp_logpdf=O.exact_logpdf(K1, Y[:, 0], th1[2]),
+                        gp_mean=m1, gp_var=v1)
     print("golden fixtures written to", HERE)
 
 
