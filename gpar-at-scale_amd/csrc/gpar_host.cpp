@@ -122,7 +122,7 @@ static void d2h(gpar_ctx* c, T* dst, const T* src, size_t count) {
 }
 static void sync(gpar_ctx* c) { HIPCHECK(hipStreamSynchronize(c->stream)); }
 
-constexpr int kChunk = 256;   // time-chunk length of the Kalman sweeps (multiple of 16)
+constexpr int kChunk = 256;   // time-chunk length of the Kalman sweeps (power of two, multiple of 16)
 
 static int sde_dim(int kind) {
   if (kind == GPAR_MATERN12) return 1;
@@ -305,7 +305,9 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
                             hipMemcpyDeviceToDevice, c->stream));
   }
 
-  double* beta = ws<double>(c, "beta", (size_t)n * mpmax);
+  // beta carries 16 zero rows past n: the Gram kernel's LDS-DMA reads whole 16-row K-steps
+  // (zeroed right before each Gram launch: the whitening may write its last chunk's tail rows)
+  double* beta = ws<double>(c, "beta", (size_t)(n + 16) * mpmax);
   double* alpha = ws<double>(c, "alpha", (size_t)n);
   double* send = ws<double>(c, "send", (size_t)nch * (mpmax + 1) * 4);
   double* cin = ws<double>(c, "cin", (size_t)nch * (mpmax + 1) * 4);
@@ -337,8 +339,9 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
                    o.a2part + (size_t)i * npart);
     check_launch("vec_fix");
     GramPlan plan = gram_plan(n, p.mp);
-    double* part = ws<double>(c, "gram_part", (size_t)plan.nsplit * plan.ntiles * kGramTile * kGramTile);
-    double* rpart = ws<double>(c, "gram_rpart", (size_t)plan.nsplit * plan.ntb * kGramTile);
+    double* part = ws<double>(c, "gram_part", (size_t)plan.part_doubles);
+    double* rpart = ws<double>(c, "gram_rpart", (size_t)plan.rpart_doubles);
+    HIPCHECK(hipMemsetAsync(beta + (size_t)n * p.mp, 0, (size_t)16 * p.mp * sizeof(double), c->stream));
     {
       Timed tm_(c, "gram");
       launch_gram(c->stream, p.sdim, plan, beta, p.mp, n, g.g, cin, p.mc, kChunk, alpha, part,

@@ -7,240 +7,273 @@
 // (A = L_u^{-1} beta^T; Lambda = A A^T + I), which the build reassociates as
 // Lambda = L_u^{-1} (beta^T beta) L_u^{-T} + I.
 //
-// Tiling: one 256-thread workgroup = one 128 x 128 lower-triangle tile of G over one
-// split of the time axis (split-K).  4 waves as 2 x 2, each 64 x 64 = 4 x 4 MFMA tiles of
-// v_mfma_f64_16x16x4_f64 (C/D: col = lane & 15, row = (lane >> 4) + 4 * reg).
-// K-step = 16 time rows staged global -> VGPR (fix-up) -> LDS, double buffered.
-// Blocks of one split run on one XCD group (blockIdx % 8) so the split's rows are
-// shared through that XCD's L2 by its tiles.
+// Tiling: split-K over the time axis; one 256-thread workgroup = 4 waves, each owning one
+// 64 x 64 lower-triangle sub-tile of G = 4 x 4 MFMA tiles of v_mfma_f64_16x16x4_f64
+// (C/D: col = lane & 15, row = (lane >> 4) + 4 * reg).  K-step = 16 time rows staged
+// global -> VGPR (fix-up) -> LDS, double buffered; each wave stages one 64-column panel.
 #include "device_common.hpp"
 
 namespace gpar {
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
-constexpr int kGT = 128;          // tile edge
-constexpr int kBK = 16;           // time rows per K-step
-constexpr int kLdsStride = 144;   // padded LDS row (doubles): rows r and r+1 hit opposite bank halves
-#ifndef GRAM_VARIANT
-#define GRAM_VARIANT 0   // ablation builds only (scratch/gram_bench): 1 no fix-up, 2 no beta loads, 3 no MFMA, 4 no staging
-#endif
+constexpr int kPW = 64;               // panel width (columns of beta / of G)
+constexpr int kBK = 16;               // time rows per K-step
+constexpr int kPanelD = kBK * kPW;    // doubles per staged panel
+constexpr int kRing = kBK * 4;        // g_k (3, zero-padded) + alpha_k per row
+
+// Work decomposition.  G's lower triangle is cut into 64 x 64 sub-tiles (p_i >= p_j over
+// npan = Mp / 64 panels).  A workgroup = 4 waves = up to 4 sub-tiles whose operands come from
+// at most 4 distinct panels, staged once per K-step and shared through LDS:
+//   * "off" groups: the 2 x 2 sub-tiles of an off-diagonal 128 x 128 block (panels 2a, 2a+1 |
+//     2b, 2b+1), nb (nb - 1) / 2 of them (nb = npan / 2);
+//   * "diag" groups: the 3 sub-tiles (2a,2a), (2a+1,2a), (2a+1,2a+1) of every diagonal block,
+//     chained in order and cut into groups of 4 -- a group spans <= 4 consecutive panels.
+// No sub-tile is computed twice (the old 128-tile design recomputed the upper half of the
+// diagonal tiles: 20 % of the MFMA work at M = 512).  Diag groups also own r = beta^T alpha for
+// the panels they stage first.
+struct WaveInfo {
+  int nsub;     // sub-tiles in the group (waves >= nsub have no MFMA work)
+  int sa, sb;   // LDS panel slots of this wave's row (A) / column (B) operand
+  int pa, pb;   // panel indices of this wave's sub-tile (pa >= pb)
+  int stage;    // panel this wave stages into slot `wave` (-1: slot unused)
+  int rown;     // 1 if this group accumulates r for that panel
+};
+
+__device__ __forceinline__ void diag_sub(int qd, int& pi, int& pj) {
+  const int a = qd / 3, w = qd - 3 * a;
+  pi = 2 * a + (w >= 1);
+  pj = 2 * a + (w == 2);
+}
+
+// Pure scalar arithmetic (no per-wave arrays: dynamically indexed arrays go to scratch).
+__device__ __forceinline__ WaveInfo decode_wave(int gid, int npan, int w) {
+  WaveInfo g;
+  const int nb = npan >> 1;
+  const int noff = nb * (nb - 1) / 2;
+  if (gid < noff) {
+    int a = 1;
+    while (a * (a + 1) / 2 <= gid) ++a;
+    const int b = gid - a * (a - 1) / 2;
+    g.nsub = 4;
+    g.sa = w >> 1;
+    g.sb = 2 + (w & 1);
+    g.pa = 2 * a + (w >> 1);
+    g.pb = 2 * b + (w & 1);
+    g.stage = (w < 2) ? 2 * a + w : 2 * b + (w - 2);
+    g.rown = 0;
+    return g;
+  }
+  const int h = gid - noff;
+  const int nq = 3 * nb;
+  const int last = (4 * h + 3 < nq) ? 4 * h + 3 : nq - 1;
+  int t, pmin, pmax, prev = -1;
+  diag_sub(4 * h, t, pmin);
+  diag_sub(last, pmax, t);
+  if (h > 0) diag_sub(4 * h - 1, prev, t);
+  g.nsub = last - 4 * h + 1;
+  const int qd = 4 * h + w;
+  if (qd <= last) {
+    diag_sub(qd, g.pa, g.pb);
+  } else {
+    g.pa = g.pb = pmin;
+  }
+  g.sa = g.pa - pmin;
+  g.sb = g.pb - pmin;
+  const int p = pmin + w;
+  g.stage = (p <= pmax) ? p : -1;
+  g.rown = (p <= pmax && p > prev) ? 1 : 0;
+  return g;
+}
 
 template <int D>
 __global__ __launch_bounds__(256, 2) void gram_kernel(
     const double* __restrict__ beta, int64_t ldb, int64_t n, const double* __restrict__ g,
     const double* __restrict__ cin, int64_t mc, int L, const double* __restrict__ alpha,
-    int ntb, int ntiles, int nsplit, int64_t rows_per_split, double* __restrict__ part,
+    int npan, int ngroups, int nsplit, int64_t rows_per_split, double* __restrict__ part,
     double* __restrict__ rpart) {
-  // one LDS array: [2 buf][2 operand][kBK rows x kLdsStride] | g/alpha ring [2][kBK][4 + 1] | r reduce [128]
-  constexpr int kTileD = kBK * kLdsStride;
-  constexpr int kGRing = kBK * 5;
-  __shared__ __attribute__((aligned(16))) double smem[4 * kTileD + 2 * kGRing + 128];
-  double* rred = smem + 4 * kTileD + 2 * kGRing;
+  // LDS: img [2 slot][4 panel][kBK rows][64]  (raw beta lands here by LDS-DMA, is fixed up in
+  //      place and XOR-swizzled into the MFMA operand layout)
+  //      ring [2 slot][4 wave][kBK][4] g_k rows | ar [2 slot][4 wave][kBK] alpha_k  (wave-private)
+  __shared__ __attribute__((aligned(16))) double smem[8 * kPanelD + 2 * 4 * kRing + 2 * 4 * kBK];
+  double* ringg = smem + 8 * kPanelD;
+  double* ringa = ringg + 2 * 4 * kRing;
 
-  // XCD-aware decode: blocks b and b+8 share an XCD; give each XCD group whole splits.
+  // XCD-aware decode: blocks b and b+8 share an XCD; each XCD group takes whole splits, so
+  // the groups of one split (which read the same beta rows) share that XCD's L2.
   const int b = blockIdx.x;
   const int xg = b & 7;
   const int q = b >> 3;
-  const int split = (q / ntiles) * 8 + xg;
-  const int tile = q % ntiles;
+  const int split = (q / ngroups) * 8 + xg;
+  const int gid = q % ngroups;
   if (split >= nsplit) return;
-  int ti = 0;
-  while ((ti + 1) * (ti + 2) / 2 <= tile) ++ti;
-  const int tj = tile - ti * (ti + 1) / 2;
-  const bool diag = (ti == tj);
-  const int64_t i0 = (int64_t)ti * kGT, j0 = (int64_t)tj * kGT;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
-  const int wave = tid >> 6;
-  const int wr = wave >> 1, wc = wave & 1;
-  const int sc = tid & 127;   // staging column
-  const int rg = tid >> 7;    // staging row group (wave-uniform)
-  const int rgu = __builtin_amdgcn_readfirstlane(rg);
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const WaveInfo gi = decode_wave(gid, npan, wave);
+  // A wave without a sub-tile runs dummy MFMAs (never stored); an unused slot stages a
+  // duplicate panel (never read): no divergent per-wave branches inside the K-step.
+  const int spanel = gi.stage < 0 ? gi.pa : gi.stage;
+  const bool owns_r = gi.rown != 0;
+  const bool mf = wave < gi.nsub;
+  const int lsh = __builtin_ctz(L);   // L (the Kalman chunk) is a power of two
 
   const int64_t kb = (int64_t)split * rows_per_split;
   int64_t ke = kb + rows_per_split;
   if (ke > n) ke = n;
+  const int nsteps = (int)((ke - kb + kBK - 1) / kBK);
 
   d4 acc[4][4];
 #pragma unroll
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[a][c] = d4{0.0, 0.0, 0.0, 0.0};
-
   double racc = 0.0;
-  double gpre = 0.0;
-  struct Regs {
-    double bI[8], bJ[8], cI[D], cJ[D];
-  };
-  Regs RA, RB;
+  double rstep = 0.0;   // r contribution of the rows fixed up in the current K-step
+  double cnx[D];
 
-  // Pipeline (one barrier per K-step, beta loads two K-steps ahead):
-  //   load(s+2)          raw beta / carry loads into the free register set
-  //   gload(s+2)         the K-step's g_k rows + alpha_k (80 doubles, one per thread)
-  //   MFMAs(s)           from lds[s & 1], interleaved with
-  //   store_rows(s+1)    fix-up beta += g_k . c_chunk (g from the LDS ring) -> lds[(s+1) & 1]
-  //   gstore(s+2)        ring slot (s+2) & 1 == s & 1, last read by store_rows(s) a barrier ago
-  // A global load consumed soon after issue stalls the wave (hipcc waits vmcnt), so every
-  // beta load has one full MFMA phase plus one barrier to land.  Rows past the split are
-  // clamped + masked (branch-free).
-  auto load = [&](Regs& R, int64_t k0) {
-    const int64_t ch = k0 / L;
+  // ---- staging of K-step `s` into LDS slot s & 1 (this wave: its panel + its ring copy)
+  // beta: 8 x global_load_lds_dwordx4, each 2 rows x 64 doubles (lane l: row 2i + l/32,
+  // columns 2(l%32), +1).  The beta workspace carries kBK zero rows past n, so no row is
+  // clamped: scalar row base + a constant per-lane byte offset.
+  const int hl = lane >> 5, cl2 = (lane & 31) * 2;
+  const uint32_t boff = (uint32_t)(((int64_t)hl * ldb + (int64_t)spanel * kPW + cl2) * 8);
+  const char* bbase = reinterpret_cast<const char*>(beta);
+  const double* zrow = beta + n * ldb;   // first of the kBK zero pad rows
+  auto issue = [&](int s) __attribute__((always_inline)) {
+    const int64_t k0 = kb + (int64_t)s * kBK;
+    const int64_t ch = k0 >> lsh;
 #pragma unroll
-    for (int i = 0; i < D; ++i) {
-      R.cI[i] = cin[(ch * mc + i0 + sc) * kSStride + i];
-      R.cJ[i] = cin[(ch * mc + j0 + sc) * kSStride + i];
-    }
+    for (int i = 0; i < D; ++i) cnx[i] = cin[(ch * mc + (int64_t)spanel * kPW + lane) * kSStride + i];
+    double* img = smem + ((s & 1) * 4 + wave) * kPanelD;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      const int64_t k = k0 + rgu + 2 * r;
-      const int64_t kc = (k < n) ? k : n - 1;
-#if GRAM_VARIANT == 2
-      R.bI[r] = (double)kc;
-      R.bJ[r] = (double)kc;
-#else
-      R.bI[r] = beta[kc * ldb + i0 + sc];
-      R.bJ[r] = beta[kc * ldb + j0 + sc];
-#endif
+    for (int i = 0; i < kBK / 2; ++i) {
+      const char* rowp = bbase + (k0 + 2 * i) * ldb * 8;
+      __builtin_amdgcn_global_load_lds(rowp + boff, img + 2 * i * kPW, 16, 0, 0);
     }
-  };
-  auto gload = [&](int64_t k0) {
-    if (tid < kBK * 5) {
-      const int row = tid / 5, col = tid % 5;
-      const int64_t k = k0 + row;
-      const int64_t kc = (k < n) ? k : n - 1;
-      gpre = (col < 4) ? g[kc * kGStride + col] : alpha[kc];
+    if (lane < 32) {
+      // rows >= n read zeros (beta's pad rows), so those rows come out exactly 0: no masks
+      const int64_t kr = k0 + (lane >> 1);
+      const bool in = kr < n;
+      const double* gs = in ? g + kr * kGStride + (lane & 1) * 2 : zrow;
+      const unsigned* as = in ? reinterpret_cast<const unsigned*>(alpha + kr) + (lane & 1)
+                              : reinterpret_cast<const unsigned*>(zrow);
+      __builtin_amdgcn_global_load_lds(gs, ringg + ((s & 1) * 4 + wave) * kRing, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(as, ringa + ((s & 1) * 4 + wave) * kBK, 4, 0, 0);
     }
   };
-  auto gstore = [&](int slot) {
-    if (tid < kBK * 5) smem[4 * kTileD + slot * kGRing + tid] = gpre;
-  };
-  auto store_rows = [&](const Regs& R, int64_t k0, int buf, int r0, int nr) {
-    const double* gr = smem + 4 * kTileD + buf * kGRing;
-    double* ldsI = smem + (buf * 2 + 0) * kTileD;
-    double* ldsJ = smem + (buf * 2 + 1) * kTileD;
+  // fix-up of rows [r0, r0 + nr) of step s in place: beta += g_k . c_chunk, r += alpha_k beta_k,
+  // swizzled store (odd rows swap their 16-column halves).
+  auto fixup = [&](int s, int r0, int nr) __attribute__((always_inline)) {
+    double* img = smem + ((s & 1) * 4 + wave) * kPanelD;
+    const double* gr = ringg + ((s & 1) * 4 + wave) * kRing;
+    const double* ar = ringa + ((s & 1) * 4 + wave) * kBK;
+    // hipcc does not order this wave's LDS-DMA writes before its own ds_reads: wait for them
+    // explicitly (the memory clobber keeps the reads below the wait).
+    if (r0 == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    double v[8];
 #pragma unroll
-    for (int r = 0; r < 8; ++r) {
-      if (r < r0 || r >= r0 + nr) continue;
-      const int row = rgu + 2 * r;
-      const int64_t k = k0 + row;
-      const double msk = (k < ke) ? 1.0 : 0.0;
-      double vi = R.bI[r], vj = R.bJ[r];
-#if GRAM_VARIANT != 1
+    for (int j = 0; j < 8; ++j)
+      if (j < nr) v[j] = img[(r0 + j) * kPW + lane];
 #pragma unroll
-      for (int i = 0; i < D; ++i) {
-        const double gi = gr[row * 5 + i];
-        vi = fma(gi, R.cI[i], vi);
-        vj = fma(gi, R.cJ[i], vj);
-      }
-#endif
-      vi *= msk;
-      racc = fma(gr[row * 5 + 4], vi, racc);
-      ldsI[row * kLdsStride + sc] = vi;
-      ldsJ[row * kLdsStride + sc] = vj * msk;
+    for (int j = 0; j < 8; ++j) {
+      if (j >= nr) continue;
+      const int r = r0 + j;
+      double x = v[j];
+#pragma unroll
+      for (int i = 0; i < D; ++i) x = fma(gr[r * 4 + i], cnx[i], x);
+      rstep = fma(ar[r], x, rstep);
+      v[j] = x;
     }
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (j < nr) img[(r0 + j) * kPW + (lane ^ (((r0 + j) & 1) << 4))] = v[j];
   };
 
-  const int nsteps = (int)((ke - kb + kBK - 1) / kBK);
   const int frow = lane >> 4, fcol = lane & 15;
+  const int par = frow & 1;
+  int offa[4], offb[4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    offa[a] = gi.sa * kPanelD + frow * kPW + ((a ^ par) << 4) + fcol;
+    offb[a] = gi.sb * kPanelD + frow * kPW + ((a ^ par) << 4) + fcol;
+  }
+
   if (nsteps > 0) {
-    gload(kb);
-    load(RA, kb);
-    gstore(0);
-    if (nsteps > 1) {
-      gload(kb + kBK);
-      load(RB, kb + kBK);
-    }
-    __syncthreads();
-    store_rows(RA, kb, 0, 0, 8);
-    if (nsteps > 1) gstore(1);
+    issue(0);
+    fixup(0, 0, 8);
+    fixup(0, 8, 8);
+    racc = rstep;
   }
   __syncthreads();
-  // one K-step: Rcur holds step s+1 (staged during the MFMAs), Rnxt receives step s+2
-  auto kstep = [&](int s, const Regs& Rcur, Regs& Rnxt) {
-    const int buf = s & 1;
-    const bool more = (s + 1) < nsteps;
-    const bool more2 = (s + 2) < nsteps;
-#if GRAM_VARIANT != 4
-    if (more2) load(Rnxt, kb + (int64_t)(s + 2) * kBK);
-#endif
-    if (more2) gload(kb + (int64_t)(s + 2) * kBK);
-    const double* la = smem + (buf * 2 + 0) * kTileD;
-    const double* lb = smem + (buf * 2 + 1) * kTileD;
-    const int64_t kn = kb + (int64_t)(s + 1) * kBK;
+  for (int s = 0; s < nsteps; ++s) {
+    const bool more = s + 1 < nsteps;
+    if (more) issue(s + 1);
+    rstep = 0.0;
+    const double* base = smem + (s & 1) * 4 * kPanelD;
 #pragma unroll
     for (int ks = 0; ks < kBK / 4; ++ks) {
       double fa[4], fb[4];
-      const int row = ks * 4 + frow;
 #pragma unroll
-      for (int a = 0; a < 4; ++a) fa[a] = la[row * kLdsStride + wr * 64 + a * 16 + fcol];
+      for (int a = 0; a < 4; ++a) fa[a] = base[offa[a] + ks * 4 * kPW];
 #pragma unroll
-      for (int c = 0; c < 4; ++c) fb[c] = lb[row * kLdsStride + wc * 64 + c * 16 + fcol];
-#if GRAM_VARIANT == 3
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) acc[a][c][0] += fa[a] * fb[c];
-#else
+      for (int c = 0; c < 4; ++c) fb[c] = base[offb[c] + ks * 4 * kPW];
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int c = 0; c < 4; ++c)
           acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[c], acc[a][c], 0, 0, 0);
-#endif
-#if GRAM_VARIANT != 4
-      if (more) store_rows(Rcur, kn, buf ^ 1, 2 * ks, 2);
-#endif
+      // the next step's rows are fixed up behind the last two MFMA groups (after the last
+      // step this rewrites a slot nobody reads again)
+      if (ks >= 2) {
+        fixup(s + 1, (ks - 2) * 8, 4);
+        fixup(s + 1, (ks - 2) * 8 + 4, 4);
+      }
     }
-    if (more2) gstore(buf);
+    racc = fma(more ? 1.0 : 0.0, rstep, racc);   // the last step's fix-up ran on a stale slot
     __syncthreads();
-  };
-  for (int s = 0; s < nsteps; s += 2) {
-    kstep(s, RB, RA);
-    if (s + 1 < nsteps) kstep(s + 1, RA, RB);
   }
 
-  double* pt = part + ((int64_t)split * ntiles + tile) * (kGT * kGT);
+  if (mf) {
+    double* pt = part + (((int64_t)split * ngroups + gid) * 4 + wave) * (kPW * kPW);
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+    for (int a = 0; a < 4; ++a)
 #pragma unroll
-    for (int c = 0; c < 4; ++c)
+      for (int c = 0; c < 4; ++c)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = wr * 64 + a * 16 + frow + 4 * r;
-        const int col = wc * 64 + c * 16 + fcol;
-        pt[row * kGT + col] = acc[a][c][r];
-      }
-  if (diag) {
-    if (rg == 1) rred[sc] = racc;
-    __syncthreads();
-    if (rg == 0) rpart[((int64_t)split * ntb + ti) * kGT + sc] = racc + rred[sc];
+        for (int r = 0; r < 4; ++r) pt[(a * 16 + frow + 4 * r) * kPW + c * 16 + fcol] = acc[a][c][r];
   }
+  if (owns_r) rpart[(int64_t)split * npan * kPW + (int64_t)spanel * kPW + lane] = racc;
 }
 
-// Sum split partials in split order (deterministic) into the full symmetric G (ldg) and r.
+// Sum split partials in split order (deterministic) into the full symmetric G (ldg); the
+// last grid row sums r.
 __global__ __launch_bounds__(256) void gram_reduce(const double* __restrict__ part,
-                                                   const double* __restrict__ rpart, int ntb,
-                                                   int ntiles, int nsplit, double* __restrict__ G,
+                                                   const double* __restrict__ rpart, int npan,
+                                                   int ngroups, int nsplit, double* __restrict__ G,
                                                    int64_t ldg, double* __restrict__ r) {
-  const int tile = blockIdx.y;
-  const int e = blockIdx.x * 256 + threadIdx.x;   // element within the tile
-  int ti = 0;
-  while ((ti + 1) * (ti + 2) / 2 <= tile) ++ti;
-  const int tj = tile - ti * (ti + 1) / 2;
-  if (e < kGT * kGT && !(ti == tj && e / kGT < e % kGT)) {
-    double s = 0.0;
-    for (int sp = 0; sp < nsplit; ++sp) s += part[((int64_t)sp * ntiles + tile) * (kGT * kGT) + e];
-    const int64_t row = (int64_t)ti * kGT + e / kGT, col = (int64_t)tj * kGT + e % kGT;
-    G[row * ldg + col] = s;
-    G[col * ldg + row] = s;
+  const int e = blockIdx.x * 256 + threadIdx.x;   // element within the sub-tile
+  if ((int)blockIdx.y == ngroups * 4) {
+    const int mp = npan * kPW;
+    for (int c = e; c < mp; c += gridDim.x * 256) {
+      double s = 0.0;
+      for (int sp = 0; sp < nsplit; ++sp) s += rpart[(int64_t)sp * mp + c];
+      r[c] = s;
+    }
+    return;
   }
-  if (ti == tj && blockIdx.x == 0 && threadIdx.x < kGT) {
-    double s = 0.0;
-    for (int sp = 0; sp < nsplit; ++sp) s += rpart[((int64_t)sp * ntb + ti) * kGT + threadIdx.x];
-    r[(int64_t)ti * kGT + threadIdx.x] = s;
-  }
+  const int gid = blockIdx.y >> 2, w = blockIdx.y & 3;
+  const WaveInfo gi = decode_wave(gid, npan, w);
+  if (w >= gi.nsub) return;
+  const int row = e / kPW, cl = e % kPW;
+  if (gi.pa == gi.pb && row < cl) return;
+  double s = 0.0;
+  for (int sp = 0; sp < nsplit; ++sp)
+    s += part[(((int64_t)sp * ngroups + gid) * 4 + w) * (kPW * kPW) + e];
+  const int64_t gr = (int64_t)gi.pa * kPW + row, gc = (int64_t)gi.pb * kPW + cl;
+  G[gr * ldg + gc] = s;
+  G[gc * ldg + gr] = s;
 }
 
 // Materialise the corrected beta (only for the (dtc, A) parity entry point).
@@ -252,7 +285,7 @@ __global__ __launch_bounds__(256) void beta_fix_kernel(double* __restrict__ beta
   const int64_t e = blockIdx.x * (int64_t)256 + threadIdx.x;
   if (e >= n * ldb) return;
   const int64_t k = e / ldb, c = e % ldb;
-  const int64_t ch = k / L;
+  const int64_t ch = k >> __builtin_ctz(L);  // L is a power of two (kChunk)
   double v = beta[e];
 #pragma unroll
   for (int i = 0; i < D; ++i) v = fma(g[k * kGStride + i], cin[(ch * mc + c) * kSStride + i], v);
@@ -268,11 +301,13 @@ namespace gpar {
 
 GramPlan gram_plan(int64_t n, int64_t mp) {
   GramPlan p;
-  p.ntb = (int)(mp / kGT);
-  p.ntiles = p.ntb * (p.ntb + 1) / 2;
-  int ns = 512 / p.ntiles;
-  ns = (ns / 8) * 8;
-  if (ns < 8) ns = 8;
+  p.npan = (int)(mp / kPW);
+  const int nb = p.npan / 2;
+  const int noff = nb * (nb - 1) / 2;
+  p.ngroups = noff + (3 * nb + 3) / 4;
+  int spx = 64 / p.ngroups;                // splits per XCD: one wave of blocks fills 8 x 64 slots
+  if (spx < 1) spx = 1;
+  int ns = 8 * spx;
   int64_t maxs = (n + 255) / 256;          // keep >= 256 rows per split
   if (maxs < 8) maxs = 8;
   if (ns > maxs) ns = (int)((maxs / 8) * 8);
@@ -281,6 +316,8 @@ GramPlan gram_plan(int64_t n, int64_t mp) {
   int64_t rps = (n + ns - 1) / ns;
   rps = ((rps + kBK - 1) / kBK) * kBK;
   p.rows_per_split = rps;
+  p.part_doubles = (int64_t)ns * p.ngroups * 4 * kPW * kPW;
+  p.rpart_doubles = (int64_t)ns * mp;
   return p;
 }
 
@@ -288,15 +325,14 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
                  int64_t ldb, int64_t n, const double* g, const double* cin, int64_t mc, int L,
                  const double* alpha, double* part, double* rpart, double* G, int64_t ldg,
                  double* r) {
-  const int nblk = plan.ntiles * plan.nsplit;
-
+  const int nblk = plan.ngroups * ((plan.nsplit + 7) / 8) * 8;
   switch (sdim) {
-    case 1: gram_kernel<1><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.ntb, plan.ntiles, plan.nsplit, plan.rows_per_split, part, rpart); break;
-    case 2: gram_kernel<2><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.ntb, plan.ntiles, plan.nsplit, plan.rows_per_split, part, rpart); break;
-    default: gram_kernel<3><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.ntb, plan.ntiles, plan.nsplit, plan.rows_per_split, part, rpart); break;
+    case 1: gram_kernel<1><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart); break;
+    case 2: gram_kernel<2><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart); break;
+    default: gram_kernel<3><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart); break;
   }
-  dim3 rgrid((kGT * kGT + 255) / 256, plan.ntiles);
-  gram_reduce<<<rgrid, 256, 0, st>>>(part, rpart, plan.ntb, plan.ntiles, plan.nsplit, G, ldg, r);
+  dim3 rgrid((kPW * kPW + 255) / 256, plan.ngroups * 4 + 1);
+  gram_reduce<<<rgrid, 256, 0, st>>>(part, rpart, plan.npan, plan.ngroups, plan.nsplit, G, ldg, r);
 }
 
 void launch_beta_fix(hipStream_t st, int sdim, double* beta, int64_t ldb, int64_t n,

@@ -887,7 +887,7 @@ __global__ __launch_bounds__(256) void smooth_mean(const double* __restrict__ u,
   const int64_t k = blockIdx.x * (int64_t)256 + threadIdx.x;
   const int b = blockIdx.y;
   if (k >= n) return;
-  const int64_t j = k / L;
+  const int64_t j = k >> __builtin_ctz(L);  // L is a power of two (kChunk)
   const double* hk = h + ((int64_t)b * n + k) * kGStride;
   const double* ch = chat + (int64_t)b * sstride + j * kSStride;
   double uu = u[(int64_t)b * n + k];
@@ -1026,7 +1026,7 @@ __global__ __launch_bounds__(256) void cov_out(const double* __restrict__ vloc,
   const int64_t k = blockIdx.x * (int64_t)256 + threadIdx.x;
   const int b = blockIdx.y;
   if (k >= n) return;
-  const int64_t j = k / L;
+  const int64_t j = k >> __builtin_ctz(L);  // L is a power of two (kChunk)
   const double* gk = gam + ((int64_t)b * n + k) * kGStride;
   const double* P = phat + ((int64_t)b * nch + j) * (D * D);
   double v = vloc[(int64_t)b * n + k];
@@ -1050,7 +1050,7 @@ __global__ __launch_bounds__(256) void vec_fix(double* __restrict__ alpha, int64
   const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   double a2 = 0.0;
   if (k < n) {
-    const int64_t j = k / L;
+    const int64_t j = k >> __builtin_ctz(L);  // L is a power of two (kChunk)
     const double* gp = g + (int64_t)b * gstride + k * kGStride;
     const double* cp = cin + (int64_t)b * sstride + (j * mc + col) * kSStride;
     double a = alpha[(int64_t)b * lda + k];

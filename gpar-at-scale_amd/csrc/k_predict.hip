@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void predict_rows(const double* __restrict__ X
   const int lane = threadIdx.x & 63;
   if (i >= nstar) return;
   const int64_t k = pos[i];
-  const int64_t j = k / L;
+  const int64_t j = k >> __builtin_ctz(L);  // L is a power of two (kChunk)
   const double R = rm[k];
   double hk[D];
 #pragma unroll

@@ -64,8 +64,9 @@ struct TrsvJobHost {
 };
 
 struct GramPlan {
-  int ntb = 0, ntiles = 0, nsplit = 0;
+  int npan = 0, ngroups = 0, nsplit = 0;   // 64-column panels, 4-sub-tile groups, time splits
   int64_t rows_per_split = 0;
+  int64_t part_doubles = 0, rpart_doubles = 0;
 };
 
 constexpr int kGramTile = 128;
