@@ -358,63 +358,78 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
 
 // --------------------------------------------------------------------------- dense tail
 struct DenseOut {
-  double *Lu, *Llam, *W;
-  int* status;
+  double *Lu, *Llam;   // chol(Kuu [+ s2 I]) and chol(Lambda), row-major lower, ld x ld per problem
+  double *Tu;          // L_u^-1 (full lower)
+  double *Tdl;         // inverses of L_lam's 64 x 64 diagonal blocks
+  int* status;         // 2 flags per problem
   int64_t ld;
+  int nb;
 };
 
-// chol(Kuu [+ sigma^2 I]) and chol(L_u^-1 G L_u^-T + I) for every problem.
+// L_u = chol(Kuu [+ s2 I]), T_u = L_u^-1, Lambda = T_u G T_u^T + I, L_lam = chol(Lambda) for
+// every problem: blocked 64 x 64 MFMA kernels (k_chol.hip), matrices padded with identity to
+// ld = Mp (padding contributes log 1 = 0 and zero right-hand sides).
 static DenseOut run_dense(gpar_ctx* c, const std::vector<DevProblem>& P,
                           const std::vector<Theta>& th, const GramOut& go, bool qu_mode) {
   const int np = (int)P.size();
   const int64_t ld = go.ldg;
+  const int nb = (int)(ld / kDenseNB);
   DenseOut o;
   o.ld = ld;
-  o.Lu = ws<double>(c, "Kuu", (size_t)np * ld * ld);
-  o.W = ws<double>(c, "Wmat", (size_t)np * ld * ld);
-  o.Llam = ws<double>(c, "Lam", (size_t)np * ld * ld);
+  o.nb = nb;
+  const size_t sq = (size_t)ld * ld;
+  o.Lu = ws<double>(c, "Kuu", (size_t)np * sq);
+  o.Llam = ws<double>(c, "Lam", (size_t)np * sq);
+  o.Tu = ws<double>(c, "Tu", (size_t)np * sq);
+  double* X = ws<double>(c, "TG", (size_t)np * sq);
+  double* Tdu = ws<double>(c, "Tdu", (size_t)np * nb * kDenseNB * kDenseNB);
+  o.Tdl = ws<double>(c, "Tdl", (size_t)np * nb * kDenseNB * kDenseNB);
   o.status = ws<int>(c, "status", (size_t)np * 2);
   HIPCHECK(hipMemsetAsync(o.status, 0, np * 2 * sizeof(int), c->stream));
-  int mmax = 0;
+  bool mixed = false;
+  for (auto& p : P) mixed |= (p.mp != ld);
+  if (mixed)   // problems narrower than ld: zero their G padding
+    for (int i = 0; i < np; ++i)
+      if (P[i].mp != ld) HIPCHECK(hipMemsetAsync(go.G + (size_t)i * sq, 0, sq * sizeof(double), c->stream));
   std::vector<KuuJobHost> kj(np);
-  std::vector<CholJobHost> cj(np), cl(np);
-  std::vector<TrsmJobHost> t1(np), t2(np);
+  std::vector<CholJob2Host> cu(np), cl(np);
+  std::vector<TgtJobHost> tj(np);
   for (int i = 0; i < np; ++i) {
     const DevProblem& p = P[i];
-    mmax = std::max<int>(mmax, (int)p.m);
-    double* Kuu = o.Lu + (size_t)i * ld * ld;
-    double* W = o.W + (size_t)i * ld * ld;
-    double* Lam = o.Llam + (size_t)i * ld * ld;
     const double s2 = th[i].sigma * th[i].sigma;
     kj[i] = {p.z, p.ldz, (int)p.d, p.ok, 1.0 / th[i].l_o, th[i].sv_o * th[i].sv_o,
-             (qu_mode ? p.qu_noise : p.kuu_noise) ? s2 : 0.0, Kuu, ld, (int)p.m};
-    cj[i] = {Kuu, ld, (int)p.m, 0.0, o.status + 2 * i};
-    t1[i] = {Kuu, ld, go.G + (size_t)i * ld * ld, ld, W, ld, (int)p.m, p.m, 0, 0};
-    t2[i] = {Kuu, ld, W, ld, Lam, ld, (int)p.m, p.m, 1, 0};
-    cl[i] = {Lam, ld, (int)p.m, 1.0, o.status + 2 * i + 1};
+             (qu_mode ? p.qu_noise : p.kuu_noise) ? s2 : 0.0, o.Lu + i * sq, ld, (int)p.m, (int)ld};
+    cu[i] = {o.Lu + i * sq, o.Tu + i * sq, Tdu + (size_t)i * nb * kDenseNB * kDenseNB, o.status + 2 * i};
+    cl[i] = {o.Llam + i * sq, nullptr, o.Tdl + (size_t)i * nb * kDenseNB * kDenseNB, o.status + 2 * i + 1};
+    tj[i] = {o.Tu + i * sq, go.G + i * sq, X + i * sq, o.Llam + i * sq};
   }
   auto* dkj = ws<KuuJobHost>(c, "kuujobs", np);
-  auto* dcj = ws<CholJobHost>(c, "choljobs", np);
-  auto* dcl = ws<CholJobHost>(c, "choljobs2", np);
-  auto* dt1 = ws<TrsmJobHost>(c, "trsmjobs1", np);
-  auto* dt2 = ws<TrsmJobHost>(c, "trsmjobs2", np);
+  auto* dcu = ws<CholJob2Host>(c, "chol2u", np);
+  auto* dcl = ws<CholJob2Host>(c, "chol2l", np);
+  auto* dtj = ws<TgtJobHost>(c, "tgtjobs", np);
   h2d(c, dkj, kj.data(), np);
-  h2d(c, dcj, cj.data(), np);
+  h2d(c, dcu, cu.data(), np);
   h2d(c, dcl, cl.data(), np);
-  h2d(c, dt1, t1.data(), np);
-  h2d(c, dt2, t2.data(), np);
+  h2d(c, dtj, tj.data(), np);
   Timed tm_(c, "dense");
-  launch_kuu(c->stream, dkj, np, mmax);
+  launch_kuu(c->stream, dkj, np, (int)ld);
   check_launch("kuu");
-  launch_chol(c->stream, dcj, np);
+  launch_chol_blocked(c->stream, dcu, np, ld, nb, /*want_t=*/true);
   check_launch("chol(Kuu)");
-  launch_trsm(c->stream, dt1, np, mmax);
-  check_launch("trsm1");
-  launch_trsm(c->stream, dt2, np, mmax);
-  check_launch("trsm2");
-  launch_chol(c->stream, dcl, np);
+  launch_tgt(c->stream, dtj, np, ld, nb);
+  check_launch("Lambda = T G T^T + I");
+  launch_chol_blocked(c->stream, dcl, np, ld, nb, /*want_t=*/false);
   check_launch("chol(Lambda)");
   return o;
+}
+
+static Finish2JobHost finish_job(const DenseOut& dn, const GramOut& go, const DevProblem& p, int i,
+                                 int64_t nch, double* out, double* me) {
+  const size_t sq = (size_t)dn.ld * dn.ld;
+  return Finish2JobHost{dn.Tu + i * sq, dn.Llam + i * sq,
+                        dn.Tdl + (size_t)i * dn.nb * kDenseNB * kDenseNB, go.r + (size_t)i * go.ldg,
+                        go.logs + (size_t)i * nch, nch, go.a2part + (size_t)i * go.npart, go.npart,
+                        p.n, dn.status + 2 * i, out, me};
 }
 
 static std::vector<Theta> thetas_from(const double* theta, int np) {
@@ -435,17 +450,12 @@ static void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::v
   GramOut go = run_gram_stage(c, P, th);
   DenseOut dn = run_dense(c, P, th, go, false);
   const int64_t nch = P[0].nch;
-  std::vector<FinishJobHost> fj(np);
+  std::vector<Finish2JobHost> fj(np);
   double* dout = ws<double>(c, "dtc_out", np);
-  for (int i = 0; i < np; ++i) {
-    fj[i] = {dn.Lu + (size_t)i * dn.ld * dn.ld, dn.Llam + (size_t)i * dn.ld * dn.ld, dn.ld,
-             (int)P[i].m, go.r + (size_t)i * go.ldg, go.logs + (size_t)i * nch, nch,
-             go.a2part + (size_t)i * go.npart, go.npart, P[i].n, dn.status + 2 * i, dout + i,
-             nullptr};
-  }
-  auto* dfj = ws<FinishJobHost>(c, "finishjobs", np);
+  for (int i = 0; i < np; ++i) fj[i] = finish_job(dn, go, P[i], i, nch, dout + i, nullptr);
+  auto* dfj = ws<Finish2JobHost>(c, "finishjobs", np);
   h2d(c, dfj, fj.data(), np);
-  launch_finish(c->stream, dfj, np);
+  launch_finish2(c->stream, dfj, np, dn.ld, dn.nb);
   check_launch("finish");
   std::vector<int> st(2 * np);
   d2h(c, out, dout, np);
@@ -470,12 +480,11 @@ static QuOut run_q_u(gpar_ctx* c, const DevProblem& p, const Theta& th) {
   DenseOut dn = run_dense(c, P, T, go, /*qu_mode=*/true);
   QuOut q;
   q.ld = dn.ld;
-  q.me = ws<double>(c, "qu_me", p.m);
-  FinishJobHost fj{dn.Lu, dn.Llam, dn.ld, (int)p.m, go.r, go.logs, p.nch, go.a2part, go.npart,
-                   p.n, dn.status, ws<double>(c, "dtc_out", 1), q.me};
-  auto* dfj = ws<FinishJobHost>(c, "finishjobs", 1);
+  q.me = ws<double>(c, "qu_me", dn.ld);
+  Finish2JobHost fj = finish_job(dn, go, p, 0, p.nch, ws<double>(c, "dtc_out", 1), q.me);
+  auto* dfj = ws<Finish2JobHost>(c, "finishjobs", 1);
   h2d(c, dfj, &fj, 1);
-  launch_finish(c->stream, dfj, 1);
+  launch_finish2(c->stream, dfj, 1, dn.ld, dn.nb);
   check_launch("finish(q_u)");
   // X = L_D^{-1} I ; cov = X^T X
   double* I = ws<double>(c, "qu_eye", (size_t)dn.ld * dn.ld);
@@ -872,11 +881,10 @@ int32_t gpar_dtc_objective_A(gpar_ctx* ctx, const gpar_problem* prob, const doub
   DenseOut dn = run_dense(ctx, P, th, go, false);
   const DevProblem& p = P[0];
   const int64_t nch = p.nch;
-  FinishJobHost fj{dn.Lu, dn.Llam, dn.ld, (int)p.m, go.r, go.logs, nch, go.a2part, go.npart,
-                   p.n, dn.status, ws<double>(ctx, "dtc_out", 1), nullptr};
-  auto* dfj = ws<FinishJobHost>(ctx, "finishjobs", 1);
+  Finish2JobHost fj = finish_job(dn, go, p, 0, nch, ws<double>(ctx, "dtc_out", 1), nullptr);
+  auto* dfj = ws<Finish2JobHost>(ctx, "finishjobs", 1);
   h2d(ctx, dfj, &fj, 1);
-  launch_finish(ctx->stream, dfj, 1);
+  launch_finish2(ctx->stream, dfj, 1, dn.ld, dn.nb);
   check_launch("finish");
   // A = L_u^{-1} beta^T (M x N), written column-major: A[i + j*m] -> transX with ldx = m
   double* A = ws<double>(ctx, "A_out", (size_t)p.m * p.n);

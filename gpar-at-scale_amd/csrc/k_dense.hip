@@ -22,6 +22,7 @@ struct KuuJob {
   double* K;
   int64_t ldk;
   int m;
+  int mpad;   // rows/columns m..mpad-1 are identity padding (blocked factorisation size)
 };
 
 struct CholJob {
@@ -50,7 +51,11 @@ __global__ __launch_bounds__(256) void kuu_kernel(const KuuJob* __restrict__ job
   const KuuJob jb = jobs[blockIdx.z];
   const int i = blockIdx.y * 16 + (threadIdx.x >> 4);
   const int j = blockIdx.x * 16 + (threadIdx.x & 15);
-  if (i >= jb.m || j >= jb.m) return;
+  if (i >= jb.mpad || j >= jb.mpad) return;
+  if (i >= jb.m || j >= jb.m) {
+    jb.K[(int64_t)i * jb.ldk + j] = (i == j) ? 1.0 : 0.0;
+    return;
+  }
   double d2 = 0.0;
   for (int q = 0; q < jb.d; ++q) {
     const double a = jb.z[(int64_t)i * jb.ldz + q] - jb.z[(int64_t)j * jb.ldz + q];

@@ -18,6 +18,7 @@ struct KuuJobHost {
   double* K;
   int64_t ldk;
   int m;
+  int mpad;
 };
 struct CholJobHost {
   double* A;
@@ -176,5 +177,38 @@ void launch_exact_logpdf_finish(hipStream_t st, const double* L, int64_t ld, int
                                 const int* status, double* out);
 void launch_exact_post(hipStream_t st, const double* W, int64_t ldw, int n, int64_t n_star,
                        const double* w, double kss, double* mean, double* var);
+
+// k_chol.hip (blocked dense tail)
+struct CholJob2Host {
+  double* A;
+  double* T;
+  double* Td;
+  int* status;
+};
+struct TgtJobHost {
+  const double* T;
+  const double* G;
+  double* X;
+  double* Lam;
+};
+struct Finish2JobHost {
+  const double* Tu;
+  const double* Llam;
+  const double* Tdl;
+  const double* r;
+  const double* logs;
+  int64_t nch;
+  const double* a2part;
+  int64_t npart;
+  int64_t n;
+  const int* status;
+  double* out;
+  double* me;
+};
+constexpr int kDenseNB = 64;
+void launch_chol_blocked(hipStream_t st, const CholJob2Host* jobs_dev, int njobs, int64_t ld,
+                         int nb, bool want_t);
+void launch_tgt(hipStream_t st, const TgtJobHost* jobs_dev, int njobs, int64_t ld, int nb);
+void launch_finish2(hipStream_t st, const Finish2JobHost* jobs_dev, int njobs, int64_t ld, int nb);
 
 }  // namespace gpar
