@@ -231,7 +231,7 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
         fixup(s + 1, (ks - 2) * 8 + 4, 4);
       }
     }
-    racc = fma(more ? 1.0 : 0.0, rstep, racc);   // the last step's fix-up ran on a stale slot
+    racc = more ? racc + rstep : racc;   // the last step's fix-up ran on a stale slot (select: NaN-safe)
     __syncthreads();
   }
 
