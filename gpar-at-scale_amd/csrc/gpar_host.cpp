@@ -21,7 +21,11 @@
 
 struct gpar_ctx {
   int device = 0;
-  hipStream_t stream = nullptr;
+  hipStream_t stream = nullptr;   // the stream every launch goes to (see OnStream)
+  hipStream_t main = nullptr;     // the context's stream
+  hipStream_t side = nullptr;     // second stream: alternate outputs of a batch run here
+  hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  int lanes = 2;                  // gpar_ctx_set_lanes: streams a batch's outputs alternate over
   std::string err;
   struct Buf {
     void* p = nullptr;
@@ -121,6 +125,14 @@ static void d2h(gpar_ctx* c, T* dst, const T* src, size_t count) {
   if (count) HIPCHECK(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyDeviceToHost, c->stream));
 }
 static void sync(gpar_ctx* c) { HIPCHECK(hipStreamSynchronize(c->stream)); }
+
+// Route the launches of a scope to another stream (all helpers launch on c->stream).
+struct OnStream {
+  gpar_ctx* c;
+  hipStream_t saved;
+  OnStream(gpar_ctx* c_, hipStream_t s) : c(c_), saved(c_->stream) { c->stream = s; }
+  ~OnStream() { c->stream = saved; }
+};
 
 constexpr int kChunk = 256;   // time-chunk length of the Kalman sweeps (power of two, multiple of 16)
 
@@ -255,7 +267,8 @@ static void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const double* rec, 
     launch_whiten_kfu(c->stream, p.tk, p.ok, rec, v, ldv, (int)p.d, p.z, p.ldz, p.m, p.mp, n,
                       kChunk, nch, 1.0 / th.l_o, s_o, beta, ldb, send, p.mc);
   } else {
-    double* zc = ws<double>(c, "zcenter", (size_t)((p.mp + 255) / 256) * 64);
+    double* zc = ws<double>(c, c->stream == c->side ? "zcenter_1" : "zcenter",
+                            (size_t)((p.mp + 255) / 256) * 64);
     launch_whiten_kfu_mfma(c->stream, p.tk, p.ok, rec, v, ldv, (int)p.d, p.z, p.ldz, zc, p.m, p.mp,
                            n, kChunk, nch, 1.0 / th.l_o, s_o, beta, ldb, send, p.mc);
   }
@@ -307,20 +320,42 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
 
   // beta carries 16 zero rows past n: the Gram kernel's LDS-DMA reads whole 16-row K-steps
   // (zeroed right before each Gram launch: the whitening may write its last chunk's tail rows)
-  double* beta = ws<double>(c, "beta", (size_t)(n + 16) * mpmax);
-  double* alpha = ws<double>(c, "alpha", (size_t)n);
-  double* send = ws<double>(c, "send", (size_t)nch * (mpmax + 1) * 4);
-  double* cin = ws<double>(c, "cin", (size_t)nch * (mpmax + 1) * 4);
+  // Outputs alternate between the context stream and a side stream, each with its own
+  // beta / alpha / carry workspace, so one output's (VALU-bound) whitening overlaps another's
+  // (MFMA-bound) Gram.  Gains are shared: the side stream waits for them (fork event).
+  const int nlanes = (np > 1 && !fix_beta && c->lanes > 1) ? 2 : 1;
+  double* beta_l[2];
+  double* alpha_l[2];
+  double* send_l[2];
+  double* cin_l[2];
+  for (int l = 0; l < nlanes; ++l) {
+    const std::string sfx = l ? "_1" : "";
+    beta_l[l] = ws<double>(c, "beta" + sfx, (size_t)(n + 16) * mpmax);
+    alpha_l[l] = ws<double>(c, "alpha" + sfx, (size_t)n);
+    send_l[l] = ws<double>(c, "send" + sfx, (size_t)nch * (mpmax + 1) * 4);
+    cin_l[l] = ws<double>(c, "cin" + sfx, (size_t)nch * (mpmax + 1) * 4);
+  }
+  if (nlanes > 1) {
+    HIPCHECK(hipEventRecord(c->ev_fork, c->stream));
+    HIPCHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+  }
   for (int i = 0; i < np; ++i) {
     const DevProblem& p = P[i];
     ARGCHECK(p.n == n, "all problems of one call must share n");
+    const int lane = i % nlanes;
+    OnStream on_(c, lane ? c->side : c->main);
+    const std::string sfx = lane ? "_1" : "";
+    double* beta = beta_l[lane];
+    double* alpha = alpha_l[lane];
+    double* send = send_l[lane];
+    double* cin = cin_l[lane];
     GainsOut g;
     if (shared) {
       g = gains[i];
     } else {
       std::vector<ChainParamsHost> cps(1);
       cps[0] = {1.0 / th[i].l_t, th[i].l_t, th[i].sv_t * th[i].sv_t, th[i].sigma * th[i].sigma};
-      g = run_gains(c, p.sdim, p.t, n, cps, nullptr, false, "fit1");
+      g = run_gains(c, p.sdim, p.t, n, cps, nullptr, false, "fit1" + sfx);
       HIPCHECK(hipMemcpyAsync(o.logs + (size_t)i * nch, g.logs, nch * sizeof(double),
                               hipMemcpyDeviceToDevice, c->stream));
     }
@@ -333,14 +368,14 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     launch_whiten_vec(c->stream, p.sdim, g.rec, 0, p.y, 0, n, kChunk, nch, 1, alpha, 0, send, 0,
                       p.mc, p.mp);
     check_launch("whiten_vec");
-    run_carry(c, p.sdim, g.phi, 0, send, cin, 0, nch, p.mc, p.mc, 1, "fitc");
+    run_carry(c, p.sdim, g.phi, 0, send, cin, 0, nch, p.mc, p.mc, 1, "fitc" + sfx);
     check_launch("carry");
     launch_vec_fix(c->stream, p.sdim, alpha, 0, g.g, 0, cin, 0, p.mc, p.mp, n, kChunk, 1,
                    o.a2part + (size_t)i * npart);
     check_launch("vec_fix");
     GramPlan plan = gram_plan(n, p.mp);
-    double* part = ws<double>(c, "gram_part", (size_t)plan.part_doubles);
-    double* rpart = ws<double>(c, "gram_rpart", (size_t)plan.rpart_doubles);
+    double* part = ws<double>(c, "gram_part" + sfx, (size_t)plan.part_doubles);
+    double* rpart = ws<double>(c, "gram_rpart" + sfx, (size_t)plan.rpart_doubles);
     HIPCHECK(hipMemsetAsync(beta + (size_t)n * p.mp, 0, (size_t)16 * p.mp * sizeof(double), c->stream));
     {
       Timed tm_(c, "gram");
@@ -352,6 +387,10 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
       launch_beta_fix(c->stream, p.sdim, beta, p.mp, n, g.g, cin, p.mc, kChunk);
       check_launch("beta_fix");
     }
+  }
+  if (nlanes > 1) {   // join: the dense tail on the context stream needs every G
+    HIPCHECK(hipEventRecord(c->ev_join, c->side));
+    HIPCHECK(hipStreamWaitEvent(c->main, c->ev_join, 0));
   }
   return o;
 }
@@ -751,10 +790,14 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
   if (hipSetDevice(device) != hipSuccess) return GPAR_ERR_HIP;
   auto* c = new gpar_ctx();
   c->device = device;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (hipStreamCreateWithFlags(&c->main, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return GPAR_ERR_HIP;
   }
+  c->stream = c->main;
   *out = c;
   return GPAR_OK;
 }
@@ -762,10 +805,14 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
 int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
   if (!ctx) return GPAR_ERR_STATE;
   (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
+  (void)hipStreamSynchronize(ctx->main);
+  (void)hipStreamSynchronize(ctx->side);
   for (auto& kv : ctx->bufs)
     if (kv.second.p) (void)hipFree(kv.second.p);
-  (void)hipStreamDestroy(ctx->stream);
+  (void)hipEventDestroy(ctx->ev_fork);
+  (void)hipEventDestroy(ctx->ev_join);
+  (void)hipStreamDestroy(ctx->side);
+  (void)hipStreamDestroy(ctx->main);
   delete ctx;
   return GPAR_OK;
 }
@@ -802,6 +849,16 @@ int32_t gpar_ctx_kernel_stats(gpar_ctx* ctx, const char* name, int64_t* launches
   *launches = it == ctx->stats.end() ? 0 : it->second.launches;
   *total_ms = it == ctx->stats.end() ? 0.0 : it->second.ms;
   API_END(ctx)
+}
+
+int32_t gpar_ctx_set_lanes(gpar_ctx* ctx, int32_t lanes) {
+  if (!ctx) return GPAR_ERR_STATE;
+  if (lanes != 1 && lanes != 2) {
+    ctx->err = "gpar_ctx_set_lanes: lanes must be 1 or 2";
+    return GPAR_ERR_ARG;
+  }
+  ctx->lanes = lanes;
+  return GPAR_OK;
 }
 
 int32_t gpar_ctx_reset_stats(gpar_ctx* ctx) {

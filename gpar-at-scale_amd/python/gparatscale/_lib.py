@@ -25,7 +25,7 @@ EXPORTED = (
     "gpar_fit", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
     "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_reset_stats",
-    "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
+    "gpar_ctx_set_lanes", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
 )
 
 
@@ -91,6 +91,7 @@ def load(path: str | None = None):
             "gpar_ctx_set_profiling": (i32, [vp, i32]),
             "gpar_ctx_kernel_stats": (i32, [vp, C.c_char_p, C.POINTER(i64), C.POINTER(C.c_double)]),
             "gpar_ctx_reset_stats": (i32, [vp]),
+            "gpar_ctx_set_lanes": (i32, [vp, i32]),
             "gpar_dtc_objective": (i32, [vp, C.POINTER(GparProblem), i32, dp, dp]),
             "gpar_dtc_objective_A": (i32, [vp, C.POINTER(GparProblem), dp, dp, dp]),
             "gpar_fit": (i32, [vp, C.POINTER(GparProblem), i32, dp, C.POINTER(GparFitOptions),
@@ -177,6 +178,10 @@ class Context:
 
     def reset_stats(self):
         self.check(load().gpar_ctx_reset_stats(self.h))
+
+    def set_lanes(self, lanes):
+        """1: serial batched evaluation; 2 (default): outputs alternate over two HIP streams."""
+        self.check(load().gpar_ctx_set_lanes(self.h, int(lanes)))
 
 
 _ctx: dict[int, Context] = {}
