@@ -51,6 +51,24 @@ __device__ __forceinline__ double exp_neg(double x) {
   return ldexp(p, (int)nf);
 }
 
+// sqrt for x >= 0 (squared distances): v_rsq_f64 seed + the Goldschmidt / Newton refinement
+// hipcc uses for sqrt(double), without its denormal rescaling and inf/nan class fix-ups (x is
+// clamped to >= 1e-200, whose root 1e-100 is 0 for every kernel here).  ~1 ulp; 11 VALU ops
+// instead of 18.
+__device__ __forceinline__ double sqrt_pos(double x) {
+  const double xs = fmax(x, 1e-200);
+  const double y = __builtin_amdgcn_rsq(xs);
+  double g = xs * y;
+  double h = 0.5 * y;
+  const double r = fma(-h, g, 0.5);
+  g = fma(g, r, g);
+  h = fma(h, r, h);
+  double d = fma(-g, g, xs);
+  g = fma(d, h, g);
+  d = fma(-g, g, xs);
+  return fma(d, h, g);
+}
+
 // Unit-variance, unit-length kernel of the distance r >= 0.
 template <int KIND>
 __device__ __forceinline__ double kappa(double r) {
@@ -73,7 +91,23 @@ __device__ __forceinline__ double kappa_sq(double d2, double inv_l) {
   if constexpr (KIND == KEQ) {
     return exp_neg(0.5 * d2 * inv_l * inv_l);
   } else {
-    return kappa<KIND>(sqrt(d2) * inv_l);
+    return kappa<KIND>(sqrt_pos(d2) * inv_l);
+  }
+}
+
+// s * kappa from a squared distance, the variance folded into the Matern polynomial.
+template <int KIND>
+__device__ __forceinline__ double skappa_sq(double d2, double inv_l, double s) {
+  if constexpr (KIND == KEQ) {
+    return s * exp_neg(0.5 * d2 * inv_l * inv_l);
+  } else if constexpr (KIND == KM12) {
+    return s * exp_neg(sqrt_pos(d2) * inv_l);
+  } else if constexpr (KIND == KM32) {
+    const double x = kSqrt3 * inv_l * sqrt_pos(d2);
+    return fma(s, x, s) * exp_neg(x);
+  } else {
+    const double x = kSqrt5 * inv_l * sqrt_pos(d2);
+    return fma(x, fma(x, s * (1.0 / 3.0), s), s) * exp_neg(x);
   }
 }
 

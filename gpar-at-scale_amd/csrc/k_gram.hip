@@ -21,6 +21,9 @@ constexpr int kPW = 64;               // panel width (columns of beta / of G)
 constexpr int kBK = 16;               // time rows per K-step
 constexpr int kPanelD = kBK * kPW;    // doubles per staged panel
 constexpr int kRing = kBK * 4;        // g_k (3, zero-padded) + alpha_k per row
+#ifndef GRAM_ABL
+#define GRAM_ABL 0   // timing ablations only: 1 no fix-up math, 2 no LDS-DMA, 3 no MFMA, 4 no fix-up pass
+#endif
 
 // Work decomposition.  G's lower triangle is cut into 64 x 64 sub-tiles (p_i >= p_j over
 // npan = Mp / 64 panels).  A workgroup = 4 waves = up to 4 sub-tiles whose operands come from
@@ -129,9 +132,12 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[a][c] = d4{0.0, 0.0, 0.0, 0.0};
-  double racc = 0.0;
-  double rstep = 0.0;   // r contribution of the rows fixed up in the current K-step
-  double cnx[D];
+  // r = beta^T alpha per column tile c (C layout: lanes lq = lane >> 4 hold 4 rows each);
+  // reduced over lq at the end
+  double racc4[4] = {0.0, 0.0, 0.0, 0.0};
+  double rstep4[4];     // contribution of the rows fixed up in the current K-step
+  double cb[4];         // MFMA B operand of the fix-up: carry component lq of column c*16 + lc
+  const int lq = lane >> 4, lc = lane & 15;
 
   // ---- staging of K-step `s` into LDS slot s & 1 (this wave: its panel + its ring copy)
   // beta: 8 x global_load_lds_dwordx4, each 2 rows x 64 doubles (lane l: row 2i + l/32,
@@ -145,12 +151,19 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
     const int64_t k0 = kb + (int64_t)s * kBK;
     const int64_t ch = k0 >> lsh;
 #pragma unroll
-    for (int i = 0; i < D; ++i) cnx[i] = cin[(ch * mc + (int64_t)spanel * kPW + lane) * kSStride + i];
+    for (int c = 0; c < 4; ++c) {
+      const double v = cin[(ch * mc + (int64_t)spanel * kPW + c * 16 + lc) * kSStride + lq];
+      cb[c] = (lq < D) ? v : 0.0;
+    }
     double* img = smem + ((s & 1) * 4 + wave) * kPanelD;
 #pragma unroll
     for (int i = 0; i < kBK / 2; ++i) {
       const char* rowp = bbase + (k0 + 2 * i) * ldb * 8;
+#if GRAM_ABL != 2
       __builtin_amdgcn_global_load_lds(rowp + boff, img + 2 * i * kPW, 16, 0, 0);
+#else
+      (void)rowp;
+#endif
     }
     if (lane < 32) {
       // rows >= n read zeros (beta's pad rows), so those rows come out exactly 0: no masks
@@ -163,32 +176,41 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
       __builtin_amdgcn_global_load_lds(as, ringa + ((s & 1) * 4 + wave) * kBK, 4, 0, 0);
     }
   };
-  // fix-up of rows [r0, r0 + nr) of step s in place: beta += g_k . c_chunk, r += alpha_k beta_k,
-  // swizzled store (odd rows swap their 16-column halves).
-  auto fixup = [&](int s, int r0, int nr) __attribute__((always_inline)) {
+  // Fix-up of step s in place, one 32-column tile pair tp at a time: with the 16 rows of the
+  // K-step in one chunk, beta_true = beta_loc + Gamma C is a rank-D product, done on the MFMA
+  // pipe (f64 VALU does not co-execute with f64 MFMA): A = g rows (16 x 4, comp 3 zeroed),
+  // B = carry C (4 x 16 per column tile), accumulator = the raw tile in C layout.  Then
+  // r += alpha_k beta_k and the swizzled store (odd rows swap 16-column halves, inside the pair).
+  auto fixup = [&](int s, int tp) __attribute__((always_inline)) {
     double* img = smem + ((s & 1) * 4 + wave) * kPanelD;
     const double* gr = ringg + ((s & 1) * 4 + wave) * kRing;
     const double* ar = ringa + ((s & 1) * 4 + wave) * kBK;
     // hipcc does not order this wave's LDS-DMA writes before its own ds_reads: wait for them
     // explicitly (the memory clobber keeps the reads below the wait).
-    if (r0 == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    double v[8];
+    if (tp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    d4 t[2];
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (j < nr) v[j] = img[(r0 + j) * kPW + lane];
+    for (int h = 0; h < 2; ++h)
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      if (j >= nr) continue;
-      const int r = r0 + j;
-      double x = v[j];
+      for (int r = 0; r < 4; ++r) t[h][r] = img[(lq + 4 * r) * kPW + (2 * tp + h) * 16 + lc];
+    const double ga = (lq < D) ? gr[lc * 4 + lq] : 0.0;
 #pragma unroll
-      for (int i = 0; i < D; ++i) x = fma(gr[r * 4 + i], cnx[i], x);
-      rstep = fma(ar[r], x, rstep);
-      v[j] = x;
+    for (int h = 0; h < 2; ++h) {
+#if GRAM_ABL != 1
+      t[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ga, cb[2 * tp + h], t[h], 0, 0, 0);
+#endif
+      double rs = 0.0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) rs = fma(ar[lq + 4 * r], t[h][r], rs);
+      rstep4[2 * tp + h] = rs;
     }
 #pragma unroll
-    for (int j = 0; j < 8; ++j)
-      if (j < nr) img[(r0 + j) * kPW + (lane ^ (((r0 + j) & 1) << 4))] = v[j];
+    for (int h = 0; h < 2; ++h)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = lq + 4 * r;
+        img[row * kPW + ((((2 * tp + h) * 16) + lc) ^ ((row & 1) << 4))] = t[h][r];
+      }
   };
 
   const int frow = lane >> 4, fcol = lane & 15;
@@ -202,15 +224,15 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
 
   if (nsteps > 0) {
     issue(0);
-    fixup(0, 0, 8);
-    fixup(0, 8, 8);
-    racc = rstep;
+    fixup(0, 0);
+    fixup(0, 1);
+#pragma unroll
+    for (int c = 0; c < 4; ++c) racc4[c] = rstep4[c];
   }
   __syncthreads();
   for (int s = 0; s < nsteps; ++s) {
     const bool more = s + 1 < nsteps;
     if (more) issue(s + 1);
-    rstep = 0.0;
     const double* base = smem + (s & 1) * 4 * kPanelD;
 #pragma unroll
     for (int ks = 0; ks < kBK / 4; ++ks) {
@@ -219,19 +241,26 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
       for (int a = 0; a < 4; ++a) fa[a] = base[offa[a] + ks * 4 * kPW];
 #pragma unroll
       for (int c = 0; c < 4; ++c) fb[c] = base[offb[c] + ks * 4 * kPW];
+#if GRAM_ABL == 3
+      acc[0][0][0] += fa[0] * fb[0] + fa[1] * fb[1] + fa[2] * fb[2] + fa[3] * fb[3];
+#else
+      __builtin_amdgcn_s_setprio(1);   // favour the MFMA-issuing wave of the SIMD pair
 #pragma unroll
       for (int a = 0; a < 4; ++a)
 #pragma unroll
         for (int c = 0; c < 4; ++c)
           acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[c], acc[a][c], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+#endif
       // the next step's rows are fixed up behind the last two MFMA groups (after the last
       // step this rewrites a slot nobody reads again)
-      if (ks >= 2) {
-        fixup(s + 1, (ks - 2) * 8, 4);
-        fixup(s + 1, (ks - 2) * 8 + 4, 4);
-      }
+#if GRAM_ABL != 4
+      if (ks >= 2) fixup(s + 1, ks - 2);
+#endif
     }
-    racc = more ? racc + rstep : racc;   // the last step's fix-up ran on a stale slot (select: NaN-safe)
+    // the last step's fix-up ran on a stale slot: select (NaN-safe), not multiply
+#pragma unroll
+    for (int c = 0; c < 4; ++c) racc4[c] = more ? racc4[c] + rstep4[c] : racc4[c];
     __syncthreads();
   }
 
@@ -244,7 +273,13 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
 #pragma unroll
         for (int r = 0; r < 4; ++r) pt[(a * 16 + frow + 4 * r) * kPW + c * 16 + fcol] = acc[a][c][r];
   }
-  if (owns_r) rpart[(int64_t)split * npan * kPW + (int64_t)spanel * kPW + lane] = racc;
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    double v = racc4[c];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (owns_r && lq == 0) rpart[(int64_t)split * npan * kPW + (int64_t)spanel * kPW + c * 16 + lc] = v;
+  }
 }
 
 // Sum split partials in split order (deterministic) into the full symmetric G (ldg); the

@@ -383,7 +383,7 @@ __global__ __launch_bounds__(256) void whiten_kfu(
           d2b = fma(a1, a1, d2b);
         }
       }
-      const double x = valid ? s_o * kappa_sq<OK>(d2a + d2b, inv_lo) : 0.0;
+      const double x = valid ? skappa_sq<OK>(d2a + d2b, inv_lo, s_o) : 0.0;
       const double* r = rec + k * RS;
       double mm[D];
 #pragma unroll
@@ -522,7 +522,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
       for (int ct = 0; ct < 4; ++ct) {
         double d2 = vn + zn[ct] - 2.0 * acc[ct][r];
         d2 = d2 > 0.0 ? d2 : 0.0;
-        xt[wave][fq + 4 * r][ct * 16 + fr] = s_o * kappa_sq<OK>(d2, inv_lo);
+        xt[wave][fq + 4 * r][ct * 16 + fr] = skappa_sq<OK>(d2, inv_lo, s_o);
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
