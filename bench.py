@@ -161,9 +161,11 @@ def main():
     iso = None
     if problems:
         ctx.set_lanes(1)
+        th1 = np.array([[1.0, 1.0, 1.0, 1.0, 0.2]])
+        G.dtc_objective_batch(problems[:1], th1, device=local)        # warm
         ctx.reset_stats()
-        G.dtc_objective_batch(problems[:2], np.tile([1.0, 1.0, 1.0, 1.0, 0.2], (min(2, len(problems)), 1)),
-                              device=local)
+        for _ in range(4):
+            G.dtc_objective_batch(problems[:1], th1, device=local)
         iso = ctx.kernel_stats("gram")
         ctx.set_lanes(2)
 
