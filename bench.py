@@ -56,6 +56,10 @@ def main():
     ap.add_argument("--evals", type=int, default=None)
     ap.add_argument("--predict", default="analytic", choices=["analytic", "mc"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--lanes", type=int, default=1, choices=[1, 2],
+                    help="HIP streams a batched objective alternates outputs over (gpar_ctx_set_lanes); "
+                         "2 overlaps one output's whitening with another's Gram (+2%% throughput, but "
+                         "per-launch kernel durations then include the sharing)")
     args = ap.parse_args()
 
     import torch
@@ -118,6 +122,7 @@ def main():
         f"M={M} P={P} outputs={mine}")
 
     ctx = G.context(local)
+    ctx.set_lanes(args.lanes)
 
     def step():
         res = {}
@@ -155,20 +160,6 @@ def main():
         el = float(e[0])
     gram_n, gram_ms = ctx.kernel_stats("gram")
     wh_n, wh_ms = ctx.kernel_stats("whiten")
-    # Isolated Gram launches (untimed, after the timed region): inside the timed region the
-    # two-stream batch overlaps one output's whitening with another's Gram, so per-launch
-    # durations there include sharing the GPU; this pass shows the kernel alone.
-    iso = None
-    if problems:
-        ctx.set_lanes(1)
-        th1 = np.array([[1.0, 1.0, 1.0, 1.0, 0.2]])
-        G.dtc_objective_batch(problems[:1], th1, device=local)        # warm
-        ctx.reset_stats()
-        for _ in range(4):
-            G.dtc_objective_batch(problems[:1], th1, device=local)
-        iso = ctx.kernel_stats("gram")
-        ctx.set_lanes(2)
-
     out = None
     if rank == 0:
         value = n_eff * P / (el / 1e3)
@@ -201,16 +192,10 @@ def main():
                          "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic, "kernel": "gram_kernel (beta^T beta, fp64 MFMA)",
                          "launches": gram_n, "avg_ms": avg, "flops_per_launch": flops,
-                         "note": "avg over the timed region, where the Gram of one output shares the GPU "
-                                 "with the whitening of another (two streams)"},
+                         "lanes": args.lanes},
             "kernels": {"gram_ms_per_step": gram_ms / args.steps, "whiten_ms_per_step": wh_ms / args.steps,
                         "whiten_launches": wh_n},
         }
-        if iso and iso[0]:
-            iso_avg = iso[1] / iso[0]
-            iso_tf = flops / (iso_avg * 1e-3) / 1e12
-            out["roofline"]["isolated"] = {"launches": iso[0], "avg_ms": iso_avg, "achieved": iso_tf,
-                                           "frac": iso_tf / FP64_MFMA_PEAK_TFLOPS}
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(n_eff, ns_eff, M, P, EV, cfg["out_kernel"])
         print(json.dumps(out), flush=True)

@@ -25,7 +25,7 @@ struct gpar_ctx {
   hipStream_t main = nullptr;     // the context's stream
   hipStream_t side = nullptr;     // second stream: alternate outputs of a batch run here
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
-  int lanes = 2;                  // gpar_ctx_set_lanes: streams a batch's outputs alternate over
+  int lanes = 1;                  // gpar_ctx_set_lanes: streams a batch's outputs alternate over
   std::string err;
   struct Buf {
     void* p = nullptr;

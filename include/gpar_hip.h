@@ -108,8 +108,9 @@ int32_t gpar_ctx_set_profiling(gpar_ctx* ctx, int32_t on);
 int32_t gpar_ctx_kernel_stats(gpar_ctx* ctx, const char* name, int64_t* launches, double* total_ms);
 int32_t gpar_ctx_reset_stats(gpar_ctx* ctx);
 /* Concurrency of batched calls (gpar_dtc_objective / gpar_fit with nprob > 1): lanes = 2
- * (default) alternates the outputs' whitening + Gram between two HIP streams with separate
- * workspaces so one output's whitening overlaps another's Gram; 1 serialises them. */
+ * alternates the outputs' whitening + Gram between two HIP streams with separate workspaces so
+ * one output's whitening overlaps another's Gram (~2 % faster at N = 1e6, M = 512, two beta
+ * buffers); 1 (default) serialises them on the context stream. */
 int32_t gpar_ctx_set_lanes(gpar_ctx* ctx, int32_t lanes);
 
 /* ---------------------------------------------------------------- DTC objective
