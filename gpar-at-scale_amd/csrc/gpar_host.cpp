@@ -296,6 +296,13 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   o.r = ws<double>(c, "r", (size_t)np * mpmax);
   o.a2part = ws<double>(c, "a2part", (size_t)np * npart);
   o.logs = ws<double>(c, "logs_all", (size_t)np * nch);
+  // problems narrower than the batch's widest: their G / r padding must read as zero in the
+  // dense tail (the Gram writes only the mp x mp corner)
+  for (int i = 0; i < np; ++i)
+    if (P[i].mp != mpmax) {
+      HIPCHECK(hipMemsetAsync(o.G + (size_t)i * mpmax * mpmax, 0, (size_t)mpmax * mpmax * sizeof(double), c->stream));
+      HIPCHECK(hipMemsetAsync(o.r + (size_t)i * mpmax, 0, (size_t)mpmax * sizeof(double), c->stream));
+    }
 
   // group problems sharing (t, n, time kernel) into one batched gains launch
   bool shared = true;
@@ -425,11 +432,6 @@ static DenseOut run_dense(gpar_ctx* c, const std::vector<DevProblem>& P,
   o.Tdl = ws<double>(c, "Tdl", (size_t)np * nb * kDenseNB * kDenseNB);
   o.status = ws<int>(c, "status", (size_t)np * 2);
   HIPCHECK(hipMemsetAsync(o.status, 0, np * 2 * sizeof(int), c->stream));
-  bool mixed = false;
-  for (auto& p : P) mixed |= (p.mp != ld);
-  if (mixed)   // problems narrower than ld: zero their G padding
-    for (int i = 0; i < np; ++i)
-      if (P[i].mp != ld) HIPCHECK(hipMemsetAsync(go.G + (size_t)i * sq, 0, sq * sizeof(double), c->stream));
   std::vector<KuuJobHost> kj(np);
   std::vector<CholJob2Host> cu(np), cl(np);
   std::vector<TgtJobHost> tj(np);

@@ -1,0 +1,101 @@
+"""GPU edge cases against the oracle: chunk / K-step / panel boundaries, tiny and odd sizes,
+repeated time stamps, mixed-size batches, single-point and out-of-range predictions, many
+temporal chains (config 3's shape), argument errors.  fp64 tolerances as in test_gpu_dtc."""
+import numpy as np
+import pytest
+
+from oracle import gpar_oracle as O
+
+pytestmark = pytest.mark.gpu
+G = pytest.importorskip("gparatscale")
+
+
+def _case(n, D, M, seed, gaps=0, noise=0.3):
+    t, Y = O.synthetic_gpar(n, D + 1, seed=seed, noise=noise, gaps=gaps, gap_len=max(1, n // 20))
+    V = Y[:, :D].T.copy()
+    y = Y[:, D].copy()
+    Z = O.pick_pseudo_inputs(V, min(M, n), seed + 7) if M <= n else \
+        np.random.default_rng(seed).normal(size=(D, M)) + V.mean(axis=1, keepdims=True)
+    return t, V, Z, y
+
+
+SIZES = [  # n, D, M: chunk (256) and K-step (16) boundaries, panel (64/128) boundaries, D buckets
+    (1, 1, 1), (5, 2, 3), (17, 1, 16), (255, 3, 64), (256, 3, 65), (257, 4, 127), (513, 2, 128),
+    (300, 17, 129), (400, 63, 40), (1000, 1, 200),
+]
+
+
+@pytest.mark.parametrize("n,D,M", SIZES, ids=[f"n{a}_D{b}_M{c}" for a, b, c in SIZES])
+def test_dtc_sizes(n, D, M):
+    t, V, Z, y = _case(n, D, M, seed=n + D + M)
+    theta = (1.2, 0.9, 1.0 + 0.1 * D ** 0.5, 1.1, 0.3)
+    ref, _ = O.compute_gpar_dtc_objective(V, Z, t, y, theta)
+    got = G.compute_gpar_dtc_objective(V, Z, t, y, theta)
+    assert abs(got - ref) <= 1e-10 * max(1.0, abs(ref)), (got, ref)
+
+
+def test_repeated_time_stamps():
+    t, V, Z, y = _case(400, 3, 30, 5)
+    t = np.repeat(t[::2], 2)[: len(t)]          # every time twice: steps of length 0
+    theta = (0.9, 1.1, 1.3, 0.8, 0.4)
+    ref, _ = O.compute_gpar_dtc_objective(V, Z, t, y, theta)
+    got = G.compute_gpar_dtc_objective(V, Z, t, y, theta)
+    assert abs(got - ref) <= 1e-10 * abs(ref)
+
+
+def test_unsorted_times_rejected():
+    t, V, Z, y = _case(100, 2, 10, 6)
+    t = t.copy()
+    t[[10, 20]] = t[[20, 10]]
+    with pytest.raises(G.DomainError):
+        G.compute_gpar_dtc_objective(V, Z, t, y, (1.0, 1.0, 1.0, 1.0, 0.3))
+
+
+def test_bad_theta_rejected():
+    t, V, Z, y = _case(100, 2, 10, 6)
+    with pytest.raises(G.DomainError):
+        G.compute_gpar_dtc_objective(V, Z, t, y, (1.0, -1.0, 1.0, 1.0, 0.3))
+
+
+def test_mixed_batch_sizes():
+    """One batched call over outputs with different M and D (G padded to the widest)."""
+    t, Y = O.synthetic_gpar(700, 5, seed=9, noise=0.3)
+    probs, keep, thetas, refs = [], [], [], []
+    for p, M in zip(range(2, 6), (20, 150, 64, 300)):
+        V = Y[:, : p - 1].T.copy()
+        Z = O.pick_pseudo_inputs(V, M, p)
+        th = (1.0, 0.9, 1.0 + 0.2 * p, 1.1, 0.25)
+        pr, k = G.make_problem(V, Z, t, Y[:, p - 1])
+        probs.append(pr); keep.append(k); thetas.append(th)
+        refs.append(O.compute_gpar_dtc_objective(V, Z, t, Y[:, p - 1], th)[0])
+    got = G.dtc_objective_batch(probs, thetas)
+    np.testing.assert_allclose(got, refs, rtol=1e-10)
+
+
+def test_predict_single_and_out_of_range_points():
+    t, V, Z, y = _case(600, 2, 25, 11)
+    theta = (1.0, 1.0, 1.5, 1.0, 0.3)
+    ts = np.array([t[0] - 1.0, t[-1] + 2.0, t[300]])
+    Vs = V[:, [0, -1, 300]] + 0.05
+    for k in (1, 3):
+        mean, std = G.predict_scaled(V, Z, t, y, theta, ts[:k], Vs[:, :k])
+        rm, rs = O.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts[:k], Vs[:, :k], theta)
+        np.testing.assert_allclose(mean, rm, rtol=1e-7, atol=1e-9)
+        np.testing.assert_allclose(std, rs, rtol=1e-7, atol=1e-9)
+
+
+def test_many_temporal_chains_matern32():
+    """Config 3's shape at small N: 16 Matern-3/2 chains sharing t (temporal_gp_inference.jl)."""
+    t, Y = O.synthetic_gpar(3000, 16, seed=12, noise=0.4, gaps=2, gap_len=100)
+    th = np.column_stack([np.linspace(0.3, 3.0, 16), np.linspace(0.5, 2.0, 16), np.full(16, 0.3)])
+    got = G.lgssm_logpdf_batch(t, Y.T.copy(), th, "matern32")
+    ref = [O.lgssm_logpdf(O.create_lgssm(t, *th[i], kind="matern32"), Y[:, i]) for i in range(16)]
+    np.testing.assert_allclose(got, ref, rtol=1e-10)
+
+
+def test_lgssm_single_step():
+    t = np.array([0.5])
+    y = np.array([0.7])
+    got = G.lgssm_logpdf_batch(t, y[None, :], [[1.0, 1.2, 0.3]], "matern52")[0]
+    ref = O.lgssm_logpdf(O.create_lgssm(t, 1.0, 1.2, 0.3), y)
+    assert abs(got - ref) <= 1e-12 * abs(ref)
