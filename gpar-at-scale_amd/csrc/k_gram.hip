@@ -94,7 +94,7 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
     const double* __restrict__ beta, int64_t ldb, int64_t n, const double* __restrict__ g,
     const double* __restrict__ cin, int64_t mc, int L, const double* __restrict__ alpha,
     int npan, int ngroups, int nsplit, int64_t rows_per_split, double* __restrict__ part,
-    double* __restrict__ rpart) {
+    double* __restrict__ rpart, int xcd) {
   // LDS: img [2 slot][4 panel][kBK rows][64]  (raw beta lands here by LDS-DMA, is fixed up in
   //      place and XOR-swizzled into the MFMA operand layout)
   //      ring [2 slot][4 wave][kBK][4] g_k rows | ar [2 slot][4 wave][kBK] alpha_k  (wave-private)
@@ -104,11 +104,17 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
 
   // XCD-aware decode: blocks b and b+8 share an XCD; each XCD group takes whole splits, so
   // the groups of one split (which read the same beta rows) share that XCD's L2.
+  // (xcd == 0, more than 64 groups: a split no longer fits one XCD's 64 slots; linear decode)
   const int b = blockIdx.x;
-  const int xg = b & 7;
-  const int q = b >> 3;
-  const int split = (q / ngroups) * 8 + xg;
-  const int gid = q % ngroups;
+  int split, gid;
+  if (xcd) {
+    const int q = b >> 3;
+    split = (q / ngroups) * 8 + (b & 7);
+    gid = q % ngroups;
+  } else {
+    split = b / ngroups;
+    gid = b % ngroups;
+  }
   if (split >= nsplit) return;
 
   const int tid = threadIdx.x;
@@ -340,13 +346,25 @@ GramPlan gram_plan(int64_t n, int64_t mp) {
   const int nb = p.npan / 2;
   const int noff = nb * (nb - 1) / 2;
   p.ngroups = noff + (3 * nb + 3) / 4;
-  int spx = 64 / p.ngroups;                // splits per XCD: one wave of blocks fills 8 x 64 slots
-  if (spx < 1) spx = 1;
-  int ns = 8 * spx;
   int64_t maxs = (n + 255) / 256;          // keep >= 256 rows per split
-  if (maxs < 8) maxs = 8;
-  if (ns > maxs) ns = (int)((maxs / 8) * 8);
-  if (ns < 8) ns = 8;
+  int ns;
+  // XCD-aware decode (whole splits per XCD, so a split's groups share one L2) while it still
+  // fills the 8 x 64 co-resident slots; otherwise a linear decode over ~512 blocks.
+  const int spx0 = 64 / p.ngroups;
+  const double occ_xcd = spx0 > 0 ? 8.0 * p.ngroups * spx0 / 512.0 : 0.0;
+  const double occ_lin = (double)p.ngroups * (512 / p.ngroups > 0 ? 512 / p.ngroups : 1) / 512.0;
+  if (spx0 > 0 && (occ_xcd >= 0.9 || occ_xcd >= occ_lin - 0.02)) {
+    p.xcd = 1;
+    ns = 8 * (64 / p.ngroups);
+    if (maxs < 8) maxs = 8;
+    if (ns > maxs) ns = (int)((maxs / 8) * 8);
+    if (ns < 8) ns = 8;
+  } else {                                 // wide G (M > 768): fill the 512 slots linearly
+    p.xcd = 0;
+    ns = 512 / p.ngroups;
+    if (ns < 1) ns = 1;
+    if (ns > maxs) ns = (int)(maxs < 1 ? 1 : maxs);
+  }
   p.nsplit = ns;
   int64_t rps = (n + ns - 1) / ns;
   rps = ((rps + kBK - 1) / kBK) * kBK;
@@ -360,11 +378,11 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
                  int64_t ldb, int64_t n, const double* g, const double* cin, int64_t mc, int L,
                  const double* alpha, double* part, double* rpart, double* G, int64_t ldg,
                  double* r) {
-  const int nblk = plan.ngroups * ((plan.nsplit + 7) / 8) * 8;
+  const int nblk = plan.xcd ? plan.ngroups * ((plan.nsplit + 7) / 8) * 8 : plan.ngroups * plan.nsplit;
   switch (sdim) {
-    case 1: gram_kernel<1><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart); break;
-    case 2: gram_kernel<2><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart); break;
-    default: gram_kernel<3><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart); break;
+    case 1: gram_kernel<1><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart, plan.xcd); break;
+    case 2: gram_kernel<2><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart, plan.xcd); break;
+    default: gram_kernel<3><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart, plan.xcd); break;
   }
   dim3 rgrid((kPW * kPW + 255) / 256, plan.ngroups * 4 + 1);
   gram_reduce<<<rgrid, 256, 0, st>>>(part, rpart, plan.npan, plan.ngroups, plan.nsplit, G, ldg, r);

@@ -66,6 +66,7 @@ struct TrsvJobHost {
 
 struct GramPlan {
   int npan = 0, ngroups = 0, nsplit = 0;   // 64-column panels, 4-sub-tile groups, time splits
+  int xcd = 1;                              // XCD-aware block decode (ngroups <= 64)
   int64_t rows_per_split = 0;
   int64_t part_doubles = 0, rpart_doubles = 0;
 };
