@@ -406,6 +406,7 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
 struct DenseOut {
   double *Lu, *Llam;   // chol(Kuu [+ s2 I]) and chol(Lambda), row-major lower, ld x ld per problem
   double *Tu;          // L_u^-1 (full lower)
+  double *Tl;          // L_lam^-1 (full lower; q(u) mode only, else null)
   double *Tdl;         // inverses of L_lam's 64 x 64 diagonal blocks
   int* status;         // 2 flags per problem
   int64_t ld;
@@ -430,6 +431,7 @@ static DenseOut run_dense(gpar_ctx* c, const std::vector<DevProblem>& P,
   double* X = ws<double>(c, "TG", (size_t)np * sq);
   double* Tdu = ws<double>(c, "Tdu", (size_t)np * nb * kDenseNB * kDenseNB);
   o.Tdl = ws<double>(c, "Tdl", (size_t)np * nb * kDenseNB * kDenseNB);
+  o.Tl = nullptr;
   o.status = ws<int>(c, "status", (size_t)np * 2);
   HIPCHECK(hipMemsetAsync(o.status, 0, np * 2 * sizeof(int), c->stream));
   std::vector<KuuJobHost> kj(np);
@@ -441,7 +443,8 @@ static DenseOut run_dense(gpar_ctx* c, const std::vector<DevProblem>& P,
     kj[i] = {p.z, p.ldz, (int)p.d, p.ok, 1.0 / th[i].l_o, th[i].sv_o * th[i].sv_o,
              (qu_mode ? p.qu_noise : p.kuu_noise) ? s2 : 0.0, o.Lu + i * sq, ld, (int)p.m, (int)ld};
     cu[i] = {o.Lu + i * sq, o.Tu + i * sq, Tdu + (size_t)i * nb * kDenseNB * kDenseNB, o.status + 2 * i};
-    cl[i] = {o.Llam + i * sq, nullptr, o.Tdl + (size_t)i * nb * kDenseNB * kDenseNB, o.status + 2 * i + 1};
+    cl[i] = {o.Llam + i * sq, o.Tl ? o.Tl + i * sq : nullptr,
+             o.Tdl + (size_t)i * nb * kDenseNB * kDenseNB, o.status + 2 * i + 1};
     tj[i] = {o.Tu + i * sq, go.G + i * sq, X + i * sq, o.Llam + i * sq};
   }
   auto* dkj = ws<KuuJobHost>(c, "kuujobs", np);
@@ -509,7 +512,9 @@ static void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::v
 
 struct QuOut {
   double *me, *cov, *Ucol;
+  const double *Tu, *Tl;   // L_u^-1, L_D^-1 (full lower, ld)
   int64_t ld;
+  int nb;
 };
 
 // compute_q_u (gpar_scaled_inference.jl:141-196): Cuu without noise, D = L_u^-1 G L_u^-T + I,
@@ -527,10 +532,16 @@ static QuOut run_q_u(gpar_ctx* c, const DevProblem& p, const Theta& th) {
   h2d(c, dfj, &fj, 1);
   launch_finish2(c->stream, dfj, 1, dn.ld, dn.nb);
   check_launch("finish(q_u)");
-  // X = L_D^{-1} I ; cov = X^T X
+  // X = L_D^{-1} I by substitution; cov = X^T X.  q(u) factors the noise-free Cuu
+  // (gpar_scaled_inference.jl:157; cond up to ~1e10), where products of explicit inverses lose
+  // accuracy that triangular substitution keeps -- the objective's T_u = chol(Kuu + s2 I)^-1
+  // is regularised by the noise and stays on the blocked-inverse path.
   double* I = ws<double>(c, "qu_eye", (size_t)dn.ld * dn.ld);
   double* X = ws<double>(c, "qu_X", (size_t)dn.ld * dn.ld);
   q.cov = ws<double>(c, "qu_cov", (size_t)dn.ld * dn.ld);
+  q.Tu = dn.Tu;
+  q.Tl = nullptr;
+  q.nb = dn.nb;
   launch_eye(c->stream, I, dn.ld, (int)p.m);
   TrsmJobHost tj{dn.Llam, dn.ld, I, dn.ld, X, dn.ld, (int)p.m, p.m, 0, 0};
   auto* dtj = ws<TrsmJobHost>(c, "trsmjobsQ", 1);
@@ -614,13 +625,12 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
   const double* Lu = ws<double>(c, "Kuu", 1);
   const double* LD = ws<double>(c, "Lam", 1);
   const int64_t ld = q.ld;
-  // w = L_u^{-T} m_e
-  double* w = ws<double>(c, "pr_w", m);
+  // w = L_u^{-T} m_e and V = L_D^{-1} L_u^{-1} by substitution (noise-free Cuu: see run_q_u)
+  double* w = ws<double>(c, "pr_w", ld);
   TrsvJobHost tv{Lu, ld, (int)m, q.me, w, 1};
   auto* dtv = ws<TrsvJobHost>(c, "pr_trsv", 1);
   h2d(c, dtv, &tv, 1);
   launch_trsv(c->stream, dtv, 1);
-  // V = L_D^{-1} L_u^{-1}
   double* I = ws<double>(c, "qu_eye", (size_t)ld * ld);
   double* X1 = ws<double>(c, "pr_X1", (size_t)ld * ld);
   double* Vm = ws<double>(c, "pr_V", (size_t)ld * ld);

@@ -381,6 +381,16 @@ __global__ __launch_bounds__(256) void finish2_kernel(const Finish2Job* __restri
   }
 }
 
+// y_j = sum_{i >= j} T_ij x_i (T lower, row-major ld): one thread per column, coalesced rows.
+__global__ __launch_bounds__(256) void gemv_tn_lower(const double* __restrict__ T, int64_t ld, int mp,
+                                                     const double* __restrict__ x, double* __restrict__ y) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= mp) return;
+  double s = 0.0;
+  for (int i = j; i < mp; ++i) s = fma(T[(int64_t)i * ld + j], x[i], s);
+  y[j] = s;
+}
+
 }  // namespace gpar
 
 // ============================================================================ launch wrappers
@@ -408,6 +418,15 @@ void launch_tgt(hipStream_t st, const TgtJobHost* jobs_dev, int njobs, int64_t l
   const auto* jobs = reinterpret_cast<const TgtJob*>(jobs_dev);
   tgt_kernel<<<dim3(nb * nb, njobs), 256, 0, st>>>(jobs, ld, nb, 0);
   tgt_kernel<<<dim3(nb * (nb + 1) / 2, njobs), 256, 0, st>>>(jobs, ld, nb, 1);
+}
+
+void launch_tg(hipStream_t st, const TgtJobHost* jobs_dev, int njobs, int64_t ld, int nb) {
+  tgt_kernel<<<dim3(nb * nb, njobs), 256, 0, st>>>(reinterpret_cast<const TgtJob*>(jobs_dev), ld, nb, 0);
+}
+
+void launch_gemv_tn_lower(hipStream_t st, const double* T, int64_t ld, int mp, const double* x,
+                          double* y) {
+  gemv_tn_lower<<<(mp + 255) / 256, 256, 0, st>>>(T, ld, mp, x, y);
 }
 
 void launch_finish2(hipStream_t st, const Finish2JobHost* jobs_dev, int njobs, int64_t ld, int nb) {

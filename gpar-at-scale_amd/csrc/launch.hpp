@@ -211,5 +211,9 @@ void launch_chol_blocked(hipStream_t st, const CholJob2Host* jobs_dev, int njobs
                          int nb, bool want_t);
 void launch_tgt(hipStream_t st, const TgtJobHost* jobs_dev, int njobs, int64_t ld, int nb);
 void launch_finish2(hipStream_t st, const Finish2JobHost* jobs_dev, int njobs, int64_t ld, int nb);
+// X = T G only (tgt mode 0): V = L_D^-1 L_u^-1 from the two inverses
+void launch_tg(hipStream_t st, const TgtJobHost* jobs_dev, int njobs, int64_t ld, int nb);
+void launch_gemv_tn_lower(hipStream_t st, const double* T, int64_t ld, int mp, const double* x,
+                          double* y);
 
 }  // namespace gpar

@@ -99,3 +99,18 @@ def test_lgssm_single_step():
     got = G.lgssm_logpdf_batch(t, y[None, :], [[1.0, 1.2, 0.3]], "matern52")[0]
     ref = O.lgssm_logpdf(O.create_lgssm(t, 1.0, 1.2, 0.3), y)
     assert abs(got - ref) <= 1e-12 * abs(ref)
+
+
+@pytest.mark.parametrize("sigma", [0.05, 0.01, 0.002])
+def test_dtc_small_noise_ill_conditioned_kuu(sigma):
+    """Small noise: cond(Kuu + s2 I) reaches ~3e7 (EQ, M = 200, sigma = 0.002).  The build forms
+    Lambda = L_u^-1 (beta^T beta) L_u^-T; the reference forms A = L_u^-1 beta^T, then A A^T
+    (dtc.jl:119-120).  The two associations differ by ~cond * eps in exact-data fp64 (numpy with
+    triangular solves throughout: 8.6e-8 relative at sigma = 0.002), so the bound scales with
+    the conditioning: rel <= max(1e-10, 1e-14 * cond)."""
+    t, V, Z, y = _case(800, 3, 200, 21)
+    theta = (1.0, 1.0, 1.5, 1.0, sigma)
+    ref, parts = O.compute_gpar_dtc_objective(V, Z, t, y, theta, "eq", "matern52", return_parts=True)
+    got = G.compute_gpar_dtc_objective(V, Z, t, y, theta, "eq", "matern52")
+    tol = max(1e-10, 1e-14 * np.linalg.cond(parts["Kuu"]))
+    assert abs(got - ref) <= tol * abs(ref), (got, ref, abs(got - ref) / abs(ref), tol)
