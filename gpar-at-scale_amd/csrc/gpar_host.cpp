@@ -135,6 +135,7 @@ struct OnStream {
 };
 
 constexpr int kChunk = 256;   // time-chunk length of the Kalman sweeps (power of two, multiple of 16)
+static_assert(kChunk == 256, "vec_fix runs one 256-thread block per chunk");
 
 static int sde_dim(int kind) {
   if (kind == GPAR_MATERN12) return 1;
@@ -261,16 +262,16 @@ static GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
 // kernels, direct-difference kernel for Matern-1/2 (kappa not smooth in d^2 at 0).
 static void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const double* rec, const double* v,
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
-                           int64_t ldb, double* send) {
+                           int64_t ldb, double* send, const double* g, double* hsum) {
   const double s_o = th.sv_o * th.sv_o;
   if (p.ok == GPAR_MATERN12) {
     launch_whiten_kfu(c->stream, p.tk, p.ok, rec, v, ldv, (int)p.d, p.z, p.ldz, p.m, p.mp, n,
-                      kChunk, nch, 1.0 / th.l_o, s_o, beta, ldb, send, p.mc);
+                      kChunk, nch, 1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum);
   } else {
     double* zc = ws<double>(c, c->stream == c->side ? "zcenter_1" : "zcenter",
                             (size_t)((p.mp + 255) / 256) * 64);
     launch_whiten_kfu_mfma(c->stream, p.tk, p.ok, rec, v, ldv, (int)p.d, p.z, p.ldz, zc, p.m, p.mp,
-                           n, kChunk, nch, 1.0 / th.l_o, s_o, beta, ldb, send, p.mc);
+                           n, kChunk, nch, 1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum);
   }
 }
 
@@ -281,7 +282,13 @@ struct GramOut {
 };
 
 // For every problem: G = beta^T beta, r = beta^T alpha, sum alpha^2 partials, sum log S
-// partials, at hyperparameters th.  `beta_keep` (single problem) keeps the corrected beta.
+// partials, at hyperparameters th.
+// fix_beta = false (the objective): the Gram streams the chunk-local beta and adds the chunk
+//   correction sum_j E_j C_j^T + C_j E_j^T (k_gram.hip) -- no extra pass over beta.
+// fix_beta = true (q(u), the (dtc, A) entry point): beta is fixed up in place first and the
+//   Gram is a plain beta^T beta.  One extra pass over beta, but G carries the rounding of the
+//   true beta only: q(u) factors the noise-free Cuu (cond >= 1e7), which amplifies the ~10x
+//   larger rounding of the correction form (emulated: 7e-15 vs 7e-16 of max |G|).
 static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
                               const std::vector<Theta>& th, bool fix_beta = false) {
   const int np = (int)P.size();
@@ -335,12 +342,16 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   double* alpha_l[2];
   double* send_l[2];
   double* cin_l[2];
+  double* hsum_l[2];
+  double* qv_l[2];
   for (int l = 0; l < nlanes; ++l) {
     const std::string sfx = l ? "_1" : "";
     beta_l[l] = ws<double>(c, "beta" + sfx, (size_t)(n + 16) * mpmax);
     alpha_l[l] = ws<double>(c, "alpha" + sfx, (size_t)n);
     send_l[l] = ws<double>(c, "send" + sfx, (size_t)nch * (mpmax + 1) * 4);
     cin_l[l] = ws<double>(c, "cin" + sfx, (size_t)nch * (mpmax + 1) * 4);
+    hsum_l[l] = ws<double>(c, "hsum" + sfx, (size_t)nch * (mpmax + 1) * 4);
+    qv_l[l] = ws<double>(c, "qv" + sfx, (size_t)nch * 4);
   }
   if (nlanes > 1) {
     HIPCHECK(hipEventRecord(c->ev_fork, c->stream));
@@ -356,6 +367,8 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     double* alpha = alpha_l[lane];
     double* send = send_l[lane];
     double* cin = cin_l[lane];
+    double* hsum = hsum_l[lane];
+    double* qv = qv_l[lane];
     GainsOut g;
     if (shared) {
       g = gains[i];
@@ -369,7 +382,7 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     const double s_o = th[i].sv_o * th[i].sv_o;
     {
       Timed tm_(c, "whiten");
-      whiten_kfu_any(c, p, g.rec, p.v, p.ldv, n, nch, th[i], beta, p.mp, send);
+      whiten_kfu_any(c, p, g.rec, p.v, p.ldv, n, nch, th[i], beta, p.mp, send, g.g, hsum);
     }
     check_launch("whiten_kfu");
     launch_whiten_vec(c->stream, p.sdim, g.rec, 0, p.y, 0, n, kChunk, nch, 1, alpha, 0, send, 0,
@@ -377,23 +390,25 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     check_launch("whiten_vec");
     run_carry(c, p.sdim, g.phi, 0, send, cin, 0, nch, p.mc, p.mc, 1, "fitc" + sfx);
     check_launch("carry");
+    // alpha fix-up, plus the Gram's chunk correction E_j = H_j + W_j C_j / 2 and q_j
     launch_vec_fix(c->stream, p.sdim, alpha, 0, g.g, 0, cin, 0, p.mc, p.mp, n, kChunk, 1,
-                   o.a2part + (size_t)i * npart);
+                   o.a2part + (size_t)i * npart, fix_beta ? nullptr : hsum, p.mp, qv);
     check_launch("vec_fix");
+    if (fix_beta) {
+      launch_beta_fix(c->stream, p.sdim, beta, p.mp, n, g.g, cin, p.mc, kChunk);
+      check_launch("beta_fix");
+    }
     GramPlan plan = gram_plan(n, p.mp);
     double* part = ws<double>(c, "gram_part" + sfx, (size_t)plan.part_doubles);
     double* rpart = ws<double>(c, "gram_rpart" + sfx, (size_t)plan.rpart_doubles);
     HIPCHECK(hipMemsetAsync(beta + (size_t)n * p.mp, 0, (size_t)16 * p.mp * sizeof(double), c->stream));
     {
       Timed tm_(c, "gram");
-      launch_gram(c->stream, p.sdim, plan, beta, p.mp, n, g.g, cin, p.mc, kChunk, alpha, part,
-                  rpart, o.G + (size_t)i * mpmax * mpmax, mpmax, o.r + (size_t)i * mpmax);
+      launch_gram(c->stream, p.sdim, plan, beta, p.mp, n, fix_beta ? nullptr : hsum, cin, qv,
+                  p.mc, kChunk, alpha, part, rpart, o.G + (size_t)i * mpmax * mpmax, mpmax,
+                  o.r + (size_t)i * mpmax);
     }
     check_launch("gram");
-    if (fix_beta) {
-      launch_beta_fix(c->stream, p.sdim, beta, p.mp, n, g.g, cin, p.mc, kChunk);
-      check_launch("beta_fix");
-    }
   }
   if (nlanes > 1) {   // join: the dense tail on the context stream needs every G
     HIPCHECK(hipEventRecord(c->ev_join, c->side));
@@ -522,7 +537,7 @@ struct QuOut {
 static QuOut run_q_u(gpar_ctx* c, const DevProblem& p, const Theta& th) {
   std::vector<DevProblem> P{p};
   std::vector<Theta> T{th};
-  GramOut go = run_gram_stage(c, P, T);
+  GramOut go = run_gram_stage(c, P, T, /*fix_beta=*/true);
   DenseOut dn = run_dense(c, P, T, go, /*qu_mode=*/true);
   QuOut q;
   q.ld = dn.ld;
@@ -664,7 +679,7 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
   double* bend = ws<double>(c, "pr_bend", (size_t)nch * mc * 4);
   double* chat = ws<double>(c, "pr_chat", (size_t)nch * mc * 4);
   double* h = ws<double>(c, "pr_h", (size_t)nt * 4);
-  whiten_kfu_any(c, P, g.rec, vm, d, nt, nch, th, X, ldx, send);
+  whiten_kfu_any(c, P, g.rec, vm, d, nt, nch, th, X, ldx, send, g.g, nullptr);
   launch_whiten_vec(c->stream, P.sdim, g.rec, 0, ym, 0, nt, kChunk, nch, 1, X + mp, 0, send, 0,
                     mc, mp, ldx);
   check_launch("predict: whiten");

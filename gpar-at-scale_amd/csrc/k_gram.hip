@@ -1,16 +1,21 @@
 // k_gram.hip -- the dominant contraction of the DTC objective on fp64 MFMA.
 //
-// G = beta^T beta (M x M) and r = beta^T alpha over N time steps, where
-// beta[k, c] = beta_loc[k, c] + g_k . cin[chunk(k)][c] applies the chunk fix-up of the
-// time-chunked Kalman whitening on the fly (k_lgssm.hip), so the corrected beta is never
-// written to HBM.  In the reference this is the M x M x N trsm + gemm of dtc.jl:119-120
+// G = beta^T beta (M x M) and r = beta^T alpha over N time steps.  The whitening writes the
+// chunk-local beta_loc (k_lgssm.hip); the true beta is beta_loc + g_k C_j^T in chunk j, with C_j
+// (M x d) the carried-in filter states.  Expanding the product per chunk,
+//   G = sum_k beta_loc,k^T beta_loc,k + sum_j (E_j C_j^T + C_j E_j^T),
+//   E_j = H_j + C_j W_j / 2,  H_j = sum_{k in j} beta_loc,k^T g_k,  W_j = sum_{k in j} g_k^T g_k,
+//   r = sum_k beta_loc,k^T alpha_k + sum_j C_j q_j,  q_j = sum_{k in j} g_k alpha_k,
+// so the streamed loop is a plain Gram of beta_loc and the fix-up collapses to a rank-2d term per
+// chunk (K = 2 d N / 256, ~2 % of the loop), computed in each split's tail from E_j (whitening +
+// vec_fix) and C_j (carry).  In the reference this is the M x M x N trsm + gemm of dtc.jl:119-120
 // (A = L_u^{-1} beta^T; Lambda = A A^T + I), which the build reassociates as
 // Lambda = L_u^{-1} (beta^T beta) L_u^{-T} + I.
 //
 // Tiling: split-K over the time axis; one 256-thread workgroup = 4 waves, each owning one
 // 64 x 64 lower-triangle sub-tile of G = 4 x 4 MFMA tiles of v_mfma_f64_16x16x4_f64
 // (C/D: col = lane & 15, row = (lane >> 4) + 4 * reg).  K-step = 16 time rows staged
-// global -> VGPR (fix-up) -> LDS, double buffered; each wave stages one 64-column panel.
+// global -> LDS by LDS-DMA (no VGPRs), double buffered; each wave stages one 64-column panel.
 #include "device_common.hpp"
 
 namespace gpar {
@@ -20,9 +25,8 @@ typedef double d4 __attribute__((ext_vector_type(4)));
 constexpr int kPW = 64;               // panel width (columns of beta / of G)
 constexpr int kBK = 16;               // time rows per K-step
 constexpr int kPanelD = kBK * kPW;    // doubles per staged panel
-constexpr int kRing = kBK * 4;        // g_k (3, zero-padded) + alpha_k per row
 #ifndef GRAM_ABL
-#define GRAM_ABL 0   // timing ablations only: 1 no fix-up math, 2 no LDS-DMA, 3 no MFMA, 4 no fix-up pass
+#define GRAM_ABL 0   // timing ablations only: 2 no LDS-DMA, 3 no MFMA, 5 no chunk-correction tail
 #endif
 
 // Work decomposition.  G's lower triangle is cut into 64 x 64 sub-tiles (p_i >= p_j over
@@ -91,16 +95,15 @@ __device__ __forceinline__ WaveInfo decode_wave(int gid, int npan, int w) {
 
 template <int D>
 __global__ __launch_bounds__(256, 2) void gram_kernel(
-    const double* __restrict__ beta, int64_t ldb, int64_t n, const double* __restrict__ g,
-    const double* __restrict__ cin, int64_t mc, int L, const double* __restrict__ alpha,
-    int npan, int ngroups, int nsplit, int64_t rows_per_split, double* __restrict__ part,
-    double* __restrict__ rpart, int xcd) {
-  // LDS: img [2 slot][4 panel][kBK rows][64]  (raw beta lands here by LDS-DMA, is fixed up in
-  //      place and XOR-swizzled into the MFMA operand layout)
-  //      ring [2 slot][4 wave][kBK][4] g_k rows | ar [2 slot][4 wave][kBK] alpha_k  (wave-private)
-  __shared__ __attribute__((aligned(16))) double smem[8 * kPanelD + 2 * 4 * kRing + 2 * 4 * kBK];
-  double* ringg = smem + 8 * kPanelD;
-  double* ringa = ringg + 2 * 4 * kRing;
+    const double* __restrict__ beta, int64_t ldb, int64_t n, const double* __restrict__ ecor,
+    const double* __restrict__ cin, const double* __restrict__ qv, int64_t mc, int L,
+    const double* __restrict__ alpha, int npan, int ngroups, int nsplit, int64_t rows_per_split,
+    double* __restrict__ part, double* __restrict__ rpart, int xcd) {
+  // LDS: img [2 slot][4 panel][kBK rows][64], XOR-swizzled (odd rows swap their 16-column
+  //      halves: conflict-free MFMA operand reads) by the LDS-DMA source addresses;
+  //      ar [2 slot][4 wave][kBK] alpha_k (wave-private)
+  __shared__ __attribute__((aligned(16))) double smem[8 * kPanelD + 2 * 4 * kBK];
+  double* ringa = smem + 8 * kPanelD;
 
   // XCD-aware decode: blocks b and b+8 share an XCD; each XCD group takes whole splits, so
   // the groups of one split (which read the same beta rows) share that XCD's L2.
@@ -126,7 +129,6 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
   const int spanel = gi.stage < 0 ? gi.pa : gi.stage;
   const bool owns_r = gi.rown != 0;
   const bool mf = wave < gi.nsub;
-  const int lsh = __builtin_ctz(L);   // L (the Kalman chunk) is a power of two
 
   const int64_t kb = (int64_t)split * rows_per_split;
   int64_t ke = kb + rows_per_split;
@@ -138,29 +140,23 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
   for (int a = 0; a < 4; ++a)
 #pragma unroll
     for (int c = 0; c < 4; ++c) acc[a][c] = d4{0.0, 0.0, 0.0, 0.0};
-  // r = beta^T alpha per column tile c (C layout: lanes lq = lane >> 4 hold 4 rows each);
-  // reduced over lq at the end
+  // r = beta^T alpha for the staged panel's column tiles c (C layout: lanes lq = lane >> 4 hold
+  // rows lq + 4 i); reduced over lq at the end
   double racc4[4] = {0.0, 0.0, 0.0, 0.0};
-  double rstep4[4];     // contribution of the rows fixed up in the current K-step
-  double cb[4];         // MFMA B operand of the fix-up: carry component lq of column c*16 + lc
   const int lq = lane >> 4, lc = lane & 15;
 
-  // ---- staging of K-step `s` into LDS slot s & 1 (this wave: its panel + its ring copy)
-  // beta: 8 x global_load_lds_dwordx4, each 2 rows x 64 doubles (lane l: row 2i + l/32,
-  // columns 2(l%32), +1).  The beta workspace carries kBK zero rows past n, so no row is
-  // clamped: scalar row base + a constant per-lane byte offset.
+  // ---- staging of K-step `s` into LDS slot s & 1 (this wave: its panel + its alpha copy)
+  // beta: 8 x global_load_lds_dwordx4, each 2 rows x 64 doubles; lane l lands at LDS row
+  // 2i + l/32, columns 2(l%32), +1 and fetches the source columns XORed with 16 on the odd row,
+  // which writes the swizzled image directly.  The beta workspace carries kBK zero rows past n,
+  // so no row is clamped: scalar row base + a constant per-lane byte offset.
   const int hl = lane >> 5, cl2 = (lane & 31) * 2;
-  const uint32_t boff = (uint32_t)(((int64_t)hl * ldb + (int64_t)spanel * kPW + cl2) * 8);
+  const uint32_t boff =
+      (uint32_t)(((int64_t)hl * ldb + (int64_t)spanel * kPW + (cl2 ^ (hl << 4))) * 8);
   const char* bbase = reinterpret_cast<const char*>(beta);
   const double* zrow = beta + n * ldb;   // first of the kBK zero pad rows
   auto issue = [&](int s) __attribute__((always_inline)) {
     const int64_t k0 = kb + (int64_t)s * kBK;
-    const int64_t ch = k0 >> lsh;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) {
-      const double v = cin[(ch * mc + (int64_t)spanel * kPW + c * 16 + lc) * kSStride + lq];
-      cb[c] = (lq < D) ? v : 0.0;
-    }
     double* img = smem + ((s & 1) * 4 + wave) * kPanelD;
 #pragma unroll
     for (int i = 0; i < kBK / 2; ++i) {
@@ -172,51 +168,12 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
 #endif
     }
     if (lane < 32) {
-      // rows >= n read zeros (beta's pad rows), so those rows come out exactly 0: no masks
+      // rows >= n read zeros (beta's pad rows)
       const int64_t kr = k0 + (lane >> 1);
-      const bool in = kr < n;
-      const double* gs = in ? g + kr * kGStride + (lane & 1) * 2 : zrow;
-      const unsigned* as = in ? reinterpret_cast<const unsigned*>(alpha + kr) + (lane & 1)
-                              : reinterpret_cast<const unsigned*>(zrow);
-      __builtin_amdgcn_global_load_lds(gs, ringg + ((s & 1) * 4 + wave) * kRing, 16, 0, 0);
+      const unsigned* as = kr < n ? reinterpret_cast<const unsigned*>(alpha + kr) + (lane & 1)
+                                  : reinterpret_cast<const unsigned*>(zrow);
       __builtin_amdgcn_global_load_lds(as, ringa + ((s & 1) * 4 + wave) * kBK, 4, 0, 0);
     }
-  };
-  // Fix-up of step s in place, one 32-column tile pair tp at a time: with the 16 rows of the
-  // K-step in one chunk, beta_true = beta_loc + Gamma C is a rank-D product, done on the MFMA
-  // pipe (f64 VALU does not co-execute with f64 MFMA): A = g rows (16 x 4, comp 3 zeroed),
-  // B = carry C (4 x 16 per column tile), accumulator = the raw tile in C layout.  Then
-  // r += alpha_k beta_k and the swizzled store (odd rows swap 16-column halves, inside the pair).
-  auto fixup = [&](int s, int tp) __attribute__((always_inline)) {
-    double* img = smem + ((s & 1) * 4 + wave) * kPanelD;
-    const double* gr = ringg + ((s & 1) * 4 + wave) * kRing;
-    const double* ar = ringa + ((s & 1) * 4 + wave) * kBK;
-    // hipcc does not order this wave's LDS-DMA writes before its own ds_reads: wait for them
-    // explicitly (the memory clobber keeps the reads below the wait).
-    if (tp == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    d4 t[2];
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) t[h][r] = img[(lq + 4 * r) * kPW + (2 * tp + h) * 16 + lc];
-    const double ga = (lq < D) ? gr[lc * 4 + lq] : 0.0;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-#if GRAM_ABL != 1
-      t[h] = __builtin_amdgcn_mfma_f64_16x16x4f64(ga, cb[2 * tp + h], t[h], 0, 0, 0);
-#endif
-      double rs = 0.0;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) rs = fma(ar[lq + 4 * r], t[h][r], rs);
-      rstep4[2 * tp + h] = rs;
-    }
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = lq + 4 * r;
-        img[row * kPW + ((((2 * tp + h) * 16) + lc) ^ ((row & 1) << 4))] = t[h][r];
-      }
   };
 
   const int frow = lane >> 4, fcol = lane & 15;
@@ -227,18 +184,16 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
     offa[a] = gi.sa * kPanelD + frow * kPW + ((a ^ par) << 4) + fcol;
     offb[a] = gi.sb * kPanelD + frow * kPW + ((a ^ par) << 4) + fcol;
   }
+  // r operand: this wave's own staged panel, rows lq + 4 i, column c * 16 + lc (swizzled)
+  const int roff = wave * kPanelD + lq * kPW + lc;
 
-  if (nsteps > 0) {
-    issue(0);
-    fixup(0, 0);
-    fixup(0, 1);
-#pragma unroll
-    for (int c = 0; c < 4; ++c) racc4[c] = rstep4[c];
-  }
+  if (nsteps > 0) issue(0);
+  // hipcc does not order LDS-DMA writes before later ds_reads: wait explicitly (the memory
+  // clobber keeps the reads below the wait), then the barrier publishes every wave's panel.
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   for (int s = 0; s < nsteps; ++s) {
-    const bool more = s + 1 < nsteps;
-    if (more) issue(s + 1);
+    if (s + 1 < nsteps) issue(s + 1);
     const double* base = smem + (s & 1) * 4 * kPanelD;
 #pragma unroll
     for (int ks = 0; ks < kBK / 4; ++ks) {
@@ -258,17 +213,71 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
           acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[c], acc[a][c], 0, 0, 0);
       __builtin_amdgcn_s_setprio(0);
 #endif
-      // the next step's rows are fixed up behind the last two MFMA groups (after the last
-      // step this rewrites a slot nobody reads again)
-#if GRAM_ABL != 4
-      if (ks >= 2) fixup(s + 1, ks - 2);
-#endif
     }
-    // the last step's fix-up ran on a stale slot: select (NaN-safe), not multiply
+    {
+      const double* ar = ringa + ((s & 1) * 4 + wave) * kBK;
+      const double* im = base + roff;
 #pragma unroll
-    for (int c = 0; c < 4; ++c) racc4[c] = more ? racc4[c] + rstep4[c] : racc4[c];
+      for (int i = 0; i < 4; ++i) {
+        const double av = ar[lq + 4 * i];
+        const int rsw = (i * 4 + lq) & 1;   // row parity = lq parity
+#pragma unroll
+        for (int c = 0; c < 4; ++c)
+          racc4[c] = fma(av, im[4 * i * kPW + ((c ^ rsw) << 4)], racc4[c]);
+      }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+
+#if GRAM_ABL != 5
+  // ---- chunk-correction tail (ecor null: beta was fixed up beforehand, nothing to add): chunks [j0, j1) of this split.  MFMA operands straight from
+  // global memory: E_j / C_j are stored [col][4] per chunk, which is exactly the 16 x 4 (A) and
+  // 4 x 16 (B) fragment layout (lane: column lane & 15, component lane >> 4); component 3 and
+  // components >= d are zero in E, and the C fragments are masked.
+  if (ecor) {
+    const int64_t nch = (n + L - 1) / L;
+    const int64_t j0 = (int64_t)split * nch / nsplit, j1 = (int64_t)(split + 1) * nch / nsplit;
+    const bool cv = lq < D;
+    const int64_t oa = ((int64_t)gi.pa * kPW + lc) * kSStride + lq;
+    const int64_t ob = ((int64_t)gi.pb * kPW + lc) * kSStride + lq;
+    const int64_t os = ((int64_t)spanel * kPW + lc) * kSStride + lq;
+    const int64_t cstride = mc * kSStride;
+    double ea[4], ca[4], eb[4], cb[4], cs[4], qq;
+    auto load = [&](int64_t j) __attribute__((always_inline)) {
+      const double* ej = ecor + j * cstride;
+      const double* cj = cin + j * cstride;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        ea[t] = ej[oa + t * 16 * kSStride];
+        eb[t] = ej[ob + t * 16 * kSStride];
+        ca[t] = cj[oa + t * 16 * kSStride];
+        cb[t] = cj[ob + t * 16 * kSStride];
+        cs[t] = cj[os + t * 16 * kSStride];
+      }
+      qq = qv[j * 4 + lq];
+    };
+    for (int64_t j = j0; j < j1; ++j) {
+      load(j);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        ca[t] = cv ? ca[t] : 0.0;
+        cb[t] = cv ? cb[t] : 0.0;
+        cs[t] = cv ? cs[t] : 0.0;
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ea[a], cb[c], acc[a][c], 0, 0, 0);
+          acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[a], eb[c], acc[a][c], 0, 0, 0);
+        }
+      // r: column c * 16 + lc of the staged panel gets C_j[col, lq] q_j[lq] (summed over lq below)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) racc4[c] = fma(cs[c], cv ? qq : 0.0, racc4[c]);
+    }
+  }
+#endif
 
   if (mf) {
     double* pt = part + (((int64_t)split * ngroups + gid) * 4 + wave) * (kPW * kPW);
@@ -375,14 +384,14 @@ GramPlan gram_plan(int64_t n, int64_t mp) {
 }
 
 void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* beta,
-                 int64_t ldb, int64_t n, const double* g, const double* cin, int64_t mc, int L,
-                 const double* alpha, double* part, double* rpart, double* G, int64_t ldg,
-                 double* r) {
+                 int64_t ldb, int64_t n, const double* ecor, const double* cin, const double* qv,
+                 int64_t mc, int L, const double* alpha, double* part, double* rpart, double* G,
+                 int64_t ldg, double* r) {
   const int nblk = plan.xcd ? plan.ngroups * ((plan.nsplit + 7) / 8) * 8 : plan.ngroups * plan.nsplit;
   switch (sdim) {
-    case 1: gram_kernel<1><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart, plan.xcd); break;
-    case 2: gram_kernel<2><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart, plan.xcd); break;
-    default: gram_kernel<3><<<nblk, 256, 0, st>>>(beta, ldb, n, g, cin, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart, plan.xcd); break;
+    case 1: gram_kernel<1><<<nblk, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart, plan.xcd); break;
+    case 2: gram_kernel<2><<<nblk, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart, plan.xcd); break;
+    default: gram_kernel<3><<<nblk, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart, plan.xcd); break;
   }
   dim3 rgrid((kPW * kPW + 255) / 256, plan.ngroups * 4 + 1);
   gram_reduce<<<rgrid, 256, 0, st>>>(part, rpart, plan.npan, plan.ngroups, plan.nsplit, G, ldg, r);

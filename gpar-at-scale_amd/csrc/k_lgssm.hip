@@ -339,7 +339,10 @@ __global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t
 // beta_loc[k, c] = chunk-local whitened Kfu[k, c] with Kfu computed on the fly:
 // Kfu[k, c] = s_o kappa(||v_k - z_c|| / l_o)   (Stheno pairwise, dtc.jl:104).
 // grid: (nch, ceil(mp / 256)); block 256, one column per thread.
-// send[(j * mc + c) * 4 + i] = local end state of chunk j.
+// send[(j * mc + c) * 4 + i] = local end state of chunk j;
+// hsum[(j * mc + c) * 4 + i] = sum_{k in chunk j} beta_loc[k, c] g_k[i]  (H_j, the chunk's
+// moment against the fix-up rows: the Gram applies the carry fix-up through it, k_gram.hip;
+// null: not wanted).
 constexpr int kVTile = 32;
 
 template <int TK, int OK, int DP>
@@ -347,10 +350,11 @@ __global__ __launch_bounds__(256) void whiten_kfu(
     const double* __restrict__ rec, const double* __restrict__ v, int64_t ldv, int d,
     const double* __restrict__ z, int64_t ldz, int64_t m, int64_t mp, int64_t n, int L,
     double inv_lo, double s_o, double* __restrict__ beta, int64_t ldb, double* __restrict__ send,
-    int64_t mc) {
+    int64_t mc, const double* __restrict__ g, double* __restrict__ hsum) {
   constexpr int D = Sde<TK>::d;
   constexpr int RS = Rec<D>::size;
   __shared__ __attribute__((aligned(16))) double vs[kVTile][DP];
+  __shared__ double gs[kVTile * kGStride];
   const int64_t j = blockIdx.x;
   const int64_t c = (int64_t)blockIdx.y * 256 + threadIdx.x;
   const bool valid = c < m;
@@ -358,9 +362,9 @@ __global__ __launch_bounds__(256) void whiten_kfu(
   double zr[DP];
 #pragma unroll
   for (int i = 0; i < DP; ++i) zr[i] = (valid && i < d) ? z[c * ldz + i] : 0.0;
-  double mst[D];
+  double mst[D], hs[D];
 #pragma unroll
-  for (int i = 0; i < D; ++i) mst[i] = 0.0;
+  for (int i = 0; i < D; ++i) mst[i] = hs[i] = 0.0;
   const int64_t k0 = j * L;
   const int64_t k1 = (k0 + L < n) ? k0 + L : n;
   for (int64_t kt = k0; kt < k1; kt += kVTile) {
@@ -370,6 +374,8 @@ __global__ __launch_bounds__(256) void whiten_kfu(
       const int kk = e / DP, i = e % DP;
       vs[kk][i] = (kk < nt && i < d) ? v[(kt + kk) * ldv + i] : 0.0;
     }
+    if (threadIdx.x < kVTile * kGStride)
+      gs[threadIdx.x] = (threadIdx.x < nt * kGStride) ? g[kt * kGStride + threadIdx.x] : 0.0;
     __syncthreads();
     for (int kk = 0; kk < nt; ++kk) {
       const int64_t k = kt + kk;
@@ -397,12 +403,17 @@ __global__ __launch_bounds__(256) void whiten_kfu(
       const double al = ev * r[D * D + D];
 #pragma unroll
       for (int i = 0; i < D; ++i) mst[i] = fma(r[D * D + i], ev, mm[i]);
+#pragma unroll
+      for (int i = 0; i < D; ++i) hs[i] = fma(al, gs[kk * kGStride + i], hs[i]);
       if (active) beta[k * ldb + c] = al;
     }
   }
   if (active) {
 #pragma unroll
-    for (int i = 0; i < D; ++i) send[(j * mc + c) * kSStride + i] = mst[i];
+    for (int i = 0; i < D; ++i) {
+      send[(j * mc + c) * kSStride + i] = mst[i];
+      if (hsum) hsum[(j * mc + c) * kSStride + i] = hs[i];
+    }
   }
 }
 
@@ -423,7 +434,8 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     const double* __restrict__ rec, const double* __restrict__ v, int64_t ldv, int d,
     const double* __restrict__ z, int64_t ldz, const double* __restrict__ zc, int64_t m,
     int64_t mp, int64_t n, int L, double inv_lo, double s_o, double* __restrict__ beta,
-    int64_t ldb, double* __restrict__ send, int64_t mc) {
+    int64_t ldb, double* __restrict__ send, int64_t mc, const double* __restrict__ g,
+    double* __restrict__ hsum) {
   typedef double d4 __attribute__((ext_vector_type(4)));
   constexpr int SD = Sde<TK>::d;
   constexpr int RS = Rec<SD>::size;
@@ -432,6 +444,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
   __shared__ __attribute__((aligned(16))) double vs[kMT * VS];
   __shared__ __attribute__((aligned(16))) double xt[4][kMT][65];
   __shared__ __attribute__((aligned(16))) double rl[kMT * RS];   // the sub-tile's gains records
+  __shared__ __attribute__((aligned(16))) double gl[kMT * kGStride];   // and fix-up rows g_k
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t j = blockIdx.x;
   const int64_t cw0 = (int64_t)blockIdx.y * 256 + wave * 64;   // wave's first column
@@ -460,16 +473,16 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     zn[ct] = part;   // full |z - c|^2 of column ct*16 + fr (dims padded with zeros)
   }
   const int nks = (d + 3) / 4;
-  double mst[SD];
+  double mst[SD], hs[SD];
 #pragma unroll
-  for (int i = 0; i < SD; ++i) mst[i] = 0.0;
+  for (int i = 0; i < SD; ++i) mst[i] = hs[i] = 0.0;
   const int64_t k0 = j * L;
   const int64_t k1 = (k0 + L < n) ? k0 + L : n;
   const bool colv = col < m, cola = col < mp;
   // next sub-tile's V rows and gains records are prefetched into registers (one MFMA /
   // kernel-evaluation phase ahead) and written to LDS between the two barriers.
   constexpr int VPT = (kMT * DP + 255) / 256;   // V elements per thread
-  double pv[VPT], pr;
+  double pv[VPT], pr, pg;
   auto prefetch = [&](int64_t kt_) {
     const int nt_ = (kt_ + kMT <= k1) ? kMT : (int)(k1 - kt_);
 #pragma unroll
@@ -481,6 +494,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
       pv[q] = ok_ ? v[kr * ldv + (ok_ ? i : 0)] - cg[i < DP ? i : 0] : 0.0;
     }
     pr = (tid < nt_ * RS) ? rec[kt_ * RS + tid] : 0.0;
+    pg = (tid < nt_ * kGStride) ? g[kt_ * kGStride + tid] : 0.0;
   };
   auto commit = [&]() {
 #pragma unroll
@@ -489,6 +503,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
       if (e < kMT * DP) vs[(e / DP) * VS + e % DP] = pv[q];
     }
     if (tid < kMT * RS) rl[tid] = pr;
+    if (tid < kMT * kGStride) gl[tid] = pg;
   };
   if (k0 < k1) prefetch(k0);
   for (int64_t kt = k0; kt < k1; kt += kMT) {
@@ -543,12 +558,17 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
       const double al = ev * rr[SD * SD + SD];
 #pragma unroll
       for (int i = 0; i < SD; ++i) mst[i] = fma(rr[SD * SD + i], ev, mm[i]);
+#pragma unroll
+      for (int i = 0; i < SD; ++i) hs[i] = fma(al, gl[kk * kGStride + i], hs[i]);
       if (cola) beta[k * ldb + col] = al;
     }
   }
   if (cola) {
 #pragma unroll
-    for (int i = 0; i < SD; ++i) send[(j * mc + col) * kSStride + i] = mst[i];
+    for (int i = 0; i < SD; ++i) {
+      send[(j * mc + col) * kSStride + i] = mst[i];
+      if (hsum) hsum[(j * mc + col) * kSStride + i] = hs[i];
+    }
   }
 }
 
@@ -1039,31 +1059,90 @@ __global__ __launch_bounds__(256) void cov_out(const double* __restrict__ vloc,
 
 // ---------------------------------------------------------------------------- fix-up of a vector
 // alpha[k] += g_k . cin[chunk(k)][col]; per-block partial sums of alpha^2 into part[b][blk].
+// One 256-thread block per chunk (L == 256).  With `hsum` (single chain, the DTC objective) the
+// block also prepares the Gram's chunk correction (k_gram.hip):
+//   W_j = sum_k g_k g_k^T,  q_j = sum_k g_k alpha_k  (alpha fixed)       -> qout[j * 4 + i]
+//   E_j[c] = H_j[c] + W_j C_j[c] / 2   for the ncols beta columns, in place of H_j (hsum).
 template <int D>
 __global__ __launch_bounds__(256) void vec_fix(double* __restrict__ alpha, int64_t lda,
                                                const double* __restrict__ g, int64_t gstride,
                                                const double* __restrict__ cin, int64_t sstride,
                                                int64_t mc, int64_t col, int64_t n, int L,
-                                               double* __restrict__ part) {
-  __shared__ double red[4];
+                                               double* __restrict__ part, double* __restrict__ hsum,
+                                               int64_t ncols, double* __restrict__ qout) {
+  constexpr int NW = D * (D + 1) / 2;   // packed upper triangle of W
+  constexpr int NV = 1 + NW + D;        // alpha^2 | W | q
+  __shared__ double red[4][NV];
+  __shared__ double wq[NW + D];
   const int b = blockIdx.y;
-  const int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
-  double a2 = 0.0;
+  const int64_t j = blockIdx.x;
+  const int64_t k = j * L + threadIdx.x;
+  double vals[NV];
+#pragma unroll
+  for (int e = 0; e < NV; ++e) vals[e] = 0.0;
   if (k < n) {
-    const int64_t j = k >> __builtin_ctz(L);  // L is a power of two (kChunk)
     const double* gp = g + (int64_t)b * gstride + k * kGStride;
     const double* cp = cin + (int64_t)b * sstride + (j * mc + col) * kSStride;
     double a = alpha[(int64_t)b * lda + k];
+    double gk[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) a = fma(gp[i], cp[i], a);
+    for (int i = 0; i < D; ++i) {
+      gk[i] = gp[i];
+      a = fma(gk[i], cp[i], a);
+    }
     alpha[(int64_t)b * lda + k] = a;
-    a2 = a * a;
+    vals[0] = a * a;
+    int e = 1;
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = i; q < D; ++q) vals[e++] = gk[i] * gk[q];
+#pragma unroll
+    for (int i = 0; i < D; ++i) vals[1 + NW + i] = gk[i] * a;
   }
-  a2 = wave_sum(a2);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = a2;
+  const int nv = hsum ? NV : 1;
+  for (int e = 0; e < nv; ++e) {
+    const double v = wave_sum(vals[e]);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][e] = v;
+  }
   __syncthreads();
   if (threadIdx.x == 0)
-    part[(int64_t)b * gridDim.x + blockIdx.x] = ((red[0] + red[1]) + red[2]) + red[3];
+    part[(int64_t)b * gridDim.x + blockIdx.x] = ((red[0][0] + red[1][0]) + red[2][0]) + red[3][0];
+  if (!hsum) return;
+  if (threadIdx.x < NW + D) {
+    const int e = 1 + threadIdx.x;
+    wq[threadIdx.x] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) qout[j * 4 + threadIdx.x] = threadIdx.x < D ? wq[NW + threadIdx.x] : 0.0;
+  double W[D][D];
+  {
+    int e = 0;
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = i; q < D; ++q) {
+        W[i][q] = wq[e];
+        W[q][i] = wq[e];
+        ++e;
+      }
+  }
+  for (int64_t c = threadIdx.x; c < ncols; c += 256) {
+    const double* cp = cin + (j * mc + c) * kSStride;
+    double* hp = hsum + (j * mc + c) * kSStride;
+    double cv[D], ev[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) cv[i] = cp[i];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < D; ++q) acc = fma(W[i][q], cv[q], acc);
+      ev[i] = fma(0.5, acc, hp[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < kSStride; ++i) hp[i] = i < D ? ev[i] : 0.0;
+  }
 }
 
 // ---------------------------------------------------------------------------- chain log-likelihood
@@ -1121,13 +1200,13 @@ static void launch_whiten_kfu_k(hipStream_t st, int dp, dim3 grid, const double*
                                 const double* v, int64_t ldv, int d, const double* z,
                                 int64_t ldz, int64_t m, int64_t mp, int64_t n, int L,
                                 double inv_lo, double s_o, double* beta, int64_t ldb,
-                                double* send, int64_t mc) {
+                                double* send, int64_t mc, const double* g, double* hsum) {
   switch (dp) {
-    case 4: whiten_kfu<TK, OK, 4><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    case 8: whiten_kfu<TK, OK, 8><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    case 16: whiten_kfu<TK, OK, 16><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    case 32: whiten_kfu<TK, OK, 32><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    default: whiten_kfu<TK, OK, 64><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case 4: whiten_kfu<TK, OK, 4><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case 8: whiten_kfu<TK, OK, 8><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case 16: whiten_kfu<TK, OK, 16><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case 32: whiten_kfu<TK, OK, 32><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    default: whiten_kfu<TK, OK, 64><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
   }
 }
 
@@ -1136,12 +1215,12 @@ static void launch_whiten_kfu_t(hipStream_t st, int ok, int dp, dim3 grid, const
                                 const double* v, int64_t ldv, int d, const double* z,
                                 int64_t ldz, int64_t m, int64_t mp, int64_t n, int L,
                                 double inv_lo, double s_o, double* beta, int64_t ldb,
-                                double* send, int64_t mc) {
+                                double* send, int64_t mc, const double* g, double* hsum) {
   switch (ok) {
-    case KM12: launch_whiten_kfu_k<TK, KM12>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    case KM32: launch_whiten_kfu_k<TK, KM32>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    case KM52: launch_whiten_kfu_k<TK, KM52>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    default: launch_whiten_kfu_k<TK, KEQ>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case KM12: launch_whiten_kfu_k<TK, KM12>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case KM32: launch_whiten_kfu_k<TK, KM32>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case KM52: launch_whiten_kfu_k<TK, KM52>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    default: launch_whiten_kfu_k<TK, KEQ>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
   }
 }
 
@@ -1159,12 +1238,12 @@ static void launch_whiten_mfma_k(hipStream_t st, int dp, dim3 grid, const double
                                  const double* v, int64_t ldv, int d, const double* z,
                                  int64_t ldz, const double* zc, int64_t m, int64_t mp, int64_t n,
                                  int L, double inv_lo, double s_o, double* beta, int64_t ldb,
-                                 double* send, int64_t mc) {
+                                 double* send, int64_t mc, const double* g, double* hsum) {
   switch (dp) {
-    case 16: whiten_kfu_mfma<TK, OK, 16><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    case 32: whiten_kfu_mfma<TK, OK, 32><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    case 48: whiten_kfu_mfma<TK, OK, 48><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    default: whiten_kfu_mfma<TK, OK, 64><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case 16: whiten_kfu_mfma<TK, OK, 16><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case 32: whiten_kfu_mfma<TK, OK, 32><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case 48: whiten_kfu_mfma<TK, OK, 48><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    default: whiten_kfu_mfma<TK, OK, 64><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
   }
 }
 
@@ -1173,11 +1252,12 @@ static void launch_whiten_mfma_t(hipStream_t st, int dp, dim3 grid, const double
                                  const double* v, int64_t ldv, int d, const double* z,
                                  int64_t ldz, const double* zc, int64_t m, int64_t mp, int64_t n,
                                  int L, int ok, double inv_lo, double s_o, double* beta,
-                                 int64_t ldb, double* send, int64_t mc) {
+                                 int64_t ldb, double* send, int64_t mc, const double* g,
+                                 double* hsum) {
   switch (ok) {
-    case KM32: launch_whiten_mfma_k<TK, KM32>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    case KEQ: launch_whiten_mfma_k<TK, KEQ>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    default: launch_whiten_mfma_k<TK, KM52>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case KM32: launch_whiten_mfma_k<TK, KM32>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case KEQ: launch_whiten_mfma_k<TK, KEQ>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    default: launch_whiten_mfma_k<TK, KM52>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
   }
 }
 
@@ -1193,27 +1273,28 @@ void launch_whiten_kfu_mfma(hipStream_t st, int time_kind, int out_kind, const d
                             const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
                             double* zc, int64_t m, int64_t mp, int64_t n, int L, int64_t nch,
                             double inv_lo, double s_o, double* beta, int64_t ldb, double* send,
-                            int64_t mc) {
+                            int64_t mc, const double* g, double* hsum) {
   const int dp = mfma_dp_bucket(d);
   zcenter_kernel<<<(unsigned)((mp + 255) / 256), 64, 0, st>>>(z, ldz, d, m, dp, zc);
   dim3 grid((unsigned)nch, (unsigned)((mp + 255) / 256));
   switch (time_kind) {
-    case KM12: launch_whiten_mfma_t<KM12>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc); break;
-    case KM32: launch_whiten_mfma_t<KM32>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc); break;
-    default: launch_whiten_mfma_t<KM52>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc); break;
+    case KM12: launch_whiten_mfma_t<KM12>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case KM32: launch_whiten_mfma_t<KM32>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    default: launch_whiten_mfma_t<KM52>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
   }
 }
 
 void launch_whiten_kfu(hipStream_t st, int time_kind, int out_kind, const double* rec,
                        const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
                        int64_t m, int64_t mp, int64_t n, int L, int64_t nch, double inv_lo,
-                       double s_o, double* beta, int64_t ldb, double* send, int64_t mc) {
+                       double s_o, double* beta, int64_t ldb, double* send, int64_t mc,
+                       const double* g, double* hsum) {
   dim3 grid((unsigned)nch, (unsigned)((mp + 255) / 256));
   const int dp = dp_bucket(d);
   switch (time_kind) {
-    case KM12: launch_whiten_kfu_t<KM12>(st, out_kind, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    case KM32: launch_whiten_kfu_t<KM32>(st, out_kind, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
-    default: launch_whiten_kfu_t<KM52>(st, out_kind, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc); break;
+    case KM12: launch_whiten_kfu_t<KM12>(st, out_kind, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case KM32: launch_whiten_kfu_t<KM32>(st, out_kind, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    default: launch_whiten_kfu_t<KM52>(st, out_kind, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
   }
 }
 
@@ -1296,9 +1377,10 @@ int64_t vec_fix_blocks(int64_t n) { return (n + 255) / 256; }
 
 void launch_vec_fix(hipStream_t st, int sdim, double* alpha, int64_t lda, const double* g,
                     int64_t gstride, const double* cin, int64_t sstride, int64_t mc,
-                    int64_t col, int64_t n, int L, int nchains, double* part) {
+                    int64_t col, int64_t n, int L, int nchains, double* part, double* hsum,
+                    int64_t ncols, double* qout) {
   dim3 grid((unsigned)vec_fix_blocks(n), (unsigned)nchains);
-  GPAR_DISPATCH_D(sdim, vec_fix<DD><<<grid, 256, 0, st>>>(alpha, lda, g, gstride, cin, sstride, mc, col, n, L, part));
+  GPAR_DISPATCH_D(sdim, vec_fix<DD><<<grid, 256, 0, st>>>(alpha, lda, g, gstride, cin, sstride, mc, col, n, L, part, hsum, ncols, qout));
 }
 
 void launch_chain_lml(hipStream_t st, const double* logs, int64_t nch, const double* a2part,

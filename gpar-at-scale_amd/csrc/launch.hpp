@@ -85,14 +85,15 @@ int dp_bucket(int d);
 void launch_whiten_kfu(hipStream_t st, int time_kind, int out_kind, const double* rec,
                        const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
                        int64_t m, int64_t mp, int64_t n, int L, int64_t nch, double inv_lo,
-                       double s_o, double* beta, int64_t ldb, double* send, int64_t mc);
+                       double s_o, double* beta, int64_t ldb, double* send, int64_t mc,
+                       const double* g, double* hsum);
 // MFMA Gram-form Kfu (smooth out kernels: Matern-3/2, Matern-5/2, EQ); zc: (mp/64) x 64 workspace
 int mfma_dp_bucket(int d);
 void launch_whiten_kfu_mfma(hipStream_t st, int time_kind, int out_kind, const double* rec,
                             const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
                             double* zc, int64_t m, int64_t mp, int64_t n, int L, int64_t nch,
                             double inv_lo, double s_o, double* beta, int64_t ldb, double* send,
-                            int64_t mc);
+                            int64_t mc, const double* g, double* hsum);
 void launch_whiten_vec(hipStream_t st, int sdim, const double* rec, int64_t recstride,
                        const double* y, int64_t ldy, int64_t n, int L, int64_t nch, int nchains,
                        double* alpha, int64_t lda, double* send, int64_t sendstride, int64_t mc,
@@ -123,16 +124,18 @@ void launch_cov_smooth(hipStream_t st, int sdim, const double* t, const double* 
 int64_t vec_fix_blocks(int64_t n);
 void launch_vec_fix(hipStream_t st, int sdim, double* alpha, int64_t lda, const double* g,
                     int64_t gstride, const double* cin, int64_t sstride, int64_t mc,
-                    int64_t col, int64_t n, int L, int nchains, double* part);
+                    int64_t col, int64_t n, int L, int nchains, double* part,
+                    double* hsum = nullptr, int64_t ncols = 0, double* qout = nullptr);
 void launch_chain_lml(hipStream_t st, const double* logs, int64_t nch, const double* a2part,
                       int64_t npart, int64_t n, int nchains, double* lml);
 
 // k_gram.hip
 GramPlan gram_plan(int64_t n, int64_t mp);
+// ecor: E_j (nch x mc x 4, vec_fix), cin: C_j (carry), qv: q_j (nch x 4, vec_fix)
 void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* beta,
-                 int64_t ldb, int64_t n, const double* g, const double* cin, int64_t mc, int L,
-                 const double* alpha, double* part, double* rpart, double* G, int64_t ldg,
-                 double* r);
+                 int64_t ldb, int64_t n, const double* ecor, const double* cin, const double* qv,
+                 int64_t mc, int L, const double* alpha, double* part, double* rpart, double* G,
+                 int64_t ldg, double* r);
 void launch_beta_fix(hipStream_t st, int sdim, double* beta, int64_t ldb, int64_t n,
                      const double* g, const double* cin, int64_t mc, int L);
 
