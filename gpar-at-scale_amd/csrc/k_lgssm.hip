@@ -573,26 +573,49 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
 }
 
 // Centres of the pseudo-input column groups (256 columns each): zc[g][i] = mean_c z[c][i].
-__global__ void zcenter_kernel(const double* __restrict__ z, int64_t ldz, int d, int64_t m,
-                               int dp, double* __restrict__ zc) {
+// Block of 256 threads = dp dims x (256 / dp) column lanes, 8 independent loads in flight per
+// thread, partial sums combined through LDS in a fixed order.
+__global__ __launch_bounds__(256) void zcenter_kernel(const double* __restrict__ z, int64_t ldz,
+                                                      int d, int64_t m, int dp,
+                                                      double* __restrict__ zc) {
+  __shared__ double red[256];
   const int64_t g = blockIdx.x;
-  const int i = threadIdx.x;
-  if (i >= dp) return;
-  double s = 0.0;
-  int cnt = 0;
-  for (int64_t c = g * 256; c < g * 256 + 256 && c < m; ++c) {
-    if (i < d) s += z[c * ldz + i];
-    ++cnt;
+  const int i = threadIdx.x % dp, q = threadIdx.x / dp, nq = 256 / dp;
+  const int64_t c0 = g * 256, c1 = (c0 + 256 < m) ? c0 + 256 : m;
+  double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  if (i < d && q < nq) {   // dp = 48: threads 240..255 idle
+    for (int64_t c = c0 + q; c < c1; c += 8 * nq) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t cc = c + (int64_t)u * nq;
+        if (cc < c1) s[u] += z[cc * ldz + i];
+      }
+    }
   }
-  zc[g * dp + i] = (cnt > 0 && i < d) ? s / cnt : 0.0;
+  red[threadIdx.x] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (threadIdx.x < dp) {
+    double t = 0.0;
+    for (int u = 0; u < nq; ++u) t += red[u * dp + threadIdx.x];
+    const int64_t cnt = c1 - c0;
+    zc[g * dp + threadIdx.x] = (cnt > 0 && threadIdx.x < d) ? t / (double)cnt : 0.0;
+  }
 }
 
 // ---------------------------------------------------------------------------- whitening of a vector per chain
-// One 64-thread block per (chunk, chain): the chunk's gains records and data are staged into
-// LDS with coalesced loads, lane 0 runs the recursion out of LDS, and the block writes the
-// whitened chunk back coalesced.  x_c[k] = y[c * ldy + k]; alpha_loc[c * lda + k]; local end
-// state -> send[c * sendstride + (j * mc + col) * 4].
-constexpr int kVecL = 256;   // == host chunk length
+// One 64-lane wave per (chunk, chain).  The chunk's filter from a zero state is the affine
+// recurrence m_k = Abar_k m_{k-1} + K_k x_k (Abar_k = (I - K_k e1^T) A_k), so it is scanned
+// in parallel: lane l filters steps 4l..4l+3 from zero (alpha', local end state e_l, transfer
+// T_l, and gamma_k = -rs_k (A_k T_{k-1})[0, :]), a Hillis-Steele scan over the 64 lanes composes
+// (T, e) into each segment's incoming state s_l, and alpha_k = alpha'_k + gamma_k . s_l.
+// x_c[k] = y[c * ldy + k]; alpha_loc[c * lda + k * astride]; chunk end state (from zero at the
+// chunk start; the carry across chunks is vec_fix's) -> send[c * sendstride + (j * mc + col) * 4].
+constexpr int kVecL = 256;   // == host chunk length (64 lanes x 4 steps)
+constexpr int kVecSeg = kVecL / 64;
+
+__device__ __forceinline__ double shfl_up_d(double v, int off, int lane) {
+  return __shfl(v, lane >= off ? lane - off : lane, 64);
+}
 
 template <int D>
 __global__ __launch_bounds__(64) void whiten_vec(const double* __restrict__ rec, int64_t recstride,
@@ -602,44 +625,106 @@ __global__ __launch_bounds__(64) void whiten_vec(const double* __restrict__ rec,
                                                  double* __restrict__ send, int64_t sendstride,
                                                  int64_t mc, int64_t col, int64_t astride) {
   constexpr int RS = Rec<D>::size;
-  __shared__ __attribute__((aligned(16))) double rl[kVecL * RS];
-  __shared__ double yl[kVecL];
   const int64_t j = blockIdx.x;
   const int c = blockIdx.y;
   const int lane = threadIdx.x;
   const double* rp = rec + (int64_t)c * recstride;
   const double* yp = y + (int64_t)c * ldy;
-  const int64_t k0 = j * L;
-  const int nk = (int)(((k0 + L < n) ? k0 + L : n) - k0);
-  for (int e = lane; e < nk * RS; e += 64) rl[e] = rp[k0 * RS + e];
-  for (int e = lane; e < nk; e += 64) yl[e] = yp[k0 + e];
-  __syncthreads();
-  if (lane == 0) {
-    double mst[D];
+  const int64_t k0 = j * L + (int64_t)lane * kVecSeg;
+  const int64_t kend = (j * L + L < n) ? j * L + L : n;
+  // ---- local pass over this lane's segment
+  double m[D], T[D][D], gam[kVecSeg][D], al[kVecSeg];
 #pragma unroll
-    for (int i = 0; i < D; ++i) mst[i] = 0.0;
-    for (int kk = 0; kk < nk; ++kk) {
-      const double* r = rl + kk * RS;
-      double mm[D];
+  for (int i = 0; i < D; ++i) m[i] = 0.0;
+  mat_eye(T);
+#pragma unroll
+  for (int u = 0; u < kVecSeg; ++u) {
+    const int64_t k = k0 + u;
+    const bool live = k < kend;
+    const double* r = rp + (live ? k : 0) * RS;
+    double A[D][D], K[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+#pragma unroll
+      for (int q = 0; q < D; ++q) A[i][q] = live ? r[i * D + q] : (i == q ? 1.0 : 0.0);
+      K[i] = live ? r[D * D + i] : 0.0;
+    }
+    const double rs = live ? r[D * D + D] : 0.0;
+    const double x = live ? yp[k] : 0.0;
+    double mm[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < D; ++q) acc = fma(A[i][q], m[q], acc);
+      mm[i] = acc;
+    }
+    const double ev = x - mm[0];
+    al[u] = ev * rs;
+#pragma unroll
+    for (int i = 0; i < D; ++i) m[i] = fma(K[i], ev, mm[i]);
+    // gamma = -rs (A T)[0, :];  T <- (I - K e1^T) A T
+    double AT[D][D];
+    mat_mul(A, T, AT);
+#pragma unroll
+    for (int q = 0; q < D; ++q) gam[u][q] = -rs * AT[0][q];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) T[i][q] = fma(-K[i], AT[0][q], AT[i][q]);
+  }
+  // ---- inclusive scan of the segment maps s -> T s + e over the lanes
+  double e[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) e[i] = m[i];
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    double Tp[D][D], ep[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      ep[i] = shfl_up_d(e[i], off, lane);
+#pragma unroll
+      for (int q = 0; q < D; ++q) Tp[i][q] = shfl_up_d(T[i][q], off, lane);
+    }
+    if (lane >= off) {
+      double Tn[D][D], en[D];
 #pragma unroll
       for (int i = 0; i < D; ++i) {
-        double acc = 0.0;
+        double acc = e[i];
 #pragma unroll
-        for (int q = 0; q < D; ++q) acc = fma(r[i * D + q], mst[q], acc);
-        mm[i] = acc;
+        for (int q = 0; q < D; ++q) acc = fma(T[i][q], ep[q], acc);
+        en[i] = acc;
       }
-      const double ev = yl[kk] - mm[0];
-      yl[kk] = ev * r[D * D + D];
+      mat_mul(T, Tp, Tn);
 #pragma unroll
-      for (int i = 0; i < D; ++i) mst[i] = fma(r[D * D + i], ev, mm[i]);
+      for (int i = 0; i < D; ++i) {
+        e[i] = en[i];
+#pragma unroll
+        for (int q = 0; q < D; ++q) T[i][q] = Tn[i][q];
+      }
     }
+  }
+  // incoming state of segment l = inclusive result of lane l - 1
+  double sin_[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    const double v = shfl_up_d(e[i], 1, lane);
+    sin_[i] = lane > 0 ? v : 0.0;
+  }
+  double* ap = alpha + (int64_t)c * lda;
+#pragma unroll
+  for (int u = 0; u < kVecSeg; ++u) {
+    const int64_t k = k0 + u;
+    double a = al[u];
+#pragma unroll
+    for (int q = 0; q < D; ++q) a = fma(gam[u][q], sin_[q], a);
+    if (k < kend) ap[k * astride] = a;
+  }
+  if (lane == 63) {
     double* sp = send + (int64_t)c * sendstride;
 #pragma unroll
-    for (int i = 0; i < D; ++i) sp[(j * mc + col) * kSStride + i] = mst[i];
+    for (int i = 0; i < D; ++i) sp[(j * mc + col) * kSStride + i] = e[i];
   }
-  __syncthreads();
-  double* ap = alpha + (int64_t)c * lda;
-  for (int e = lane; e < nk; e += 64) ap[(k0 + e) * astride] = yl[e];
 }
 
 // ---------------------------------------------------------------------------- carry over chunks
@@ -1275,7 +1360,7 @@ void launch_whiten_kfu_mfma(hipStream_t st, int time_kind, int out_kind, const d
                             double inv_lo, double s_o, double* beta, int64_t ldb, double* send,
                             int64_t mc, const double* g, double* hsum) {
   const int dp = mfma_dp_bucket(d);
-  zcenter_kernel<<<(unsigned)((mp + 255) / 256), 64, 0, st>>>(z, ldz, d, m, dp, zc);
+  zcenter_kernel<<<(unsigned)((mp + 255) / 256), 256, 0, st>>>(z, ldz, d, m, dp, zc);
   dim3 grid((unsigned)nch, (unsigned)((mp + 255) / 256));
   switch (time_kind) {
     case KM12: launch_whiten_mfma_t<KM12>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
