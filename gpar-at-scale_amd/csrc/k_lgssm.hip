@@ -428,6 +428,9 @@ __global__ __launch_bounds__(256) void whiten_kfu(
 // Matern-5/2, EQ: a d^2 error of eps |v - c| |z - c| is harmless); Matern-1/2 keeps the direct
 // form (its kappa is not smooth in d^2 at 0).
 constexpr int kMT = 16;   // steps per sub-tile
+#ifndef WHITEN_ABL
+#define WHITEN_ABL 0   // timing ablations only: 1 no kernel evaluation, 2 no MFMA, 3 no recursion, 4 no beta store
+#endif
 
 template <int TK, int OK, int DP>
 __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
@@ -480,37 +483,64 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
   const int64_t k1 = (k0 + L < n) ? k0 + L : n;
   const bool colv = col < m, cola = col < mp;
   // next sub-tile's V rows and gains records are prefetched into registers (one MFMA /
-  // kernel-evaluation phase ahead) and written to LDS between the two barriers.
+  // kernel-evaluation phase ahead) and written to LDS between the two barriers.  The loads are
+  // unconditional (clamped in-bounds addresses) and the masks are applied at commit, so no wait
+  // is forced at the load: vmcnt also counts this wave's beta stores, and a wait right after
+  // the prefetch would stall on the previous sub-tile's 16 stores.
   constexpr int VPT = (kMT * DP + 255) / 256;   // V elements per thread
-  double pv[VPT], pr, pg;
-  auto prefetch = [&](int64_t kt_) {
-    const int nt_ = (kt_ + kMT <= k1) ? kMT : (int)(k1 - kt_);
+  double pv[VPT], pcg[VPT], pr, pg;
+  int pkk[VPT], pii[VPT];
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    const int e = tid + q * 256;
+    pkk[q] = e < kMT * DP ? e / DP : kMT;   // row kMT: never committed
+    pii[q] = e % DP;
+    pcg[q] = pii[q] < d ? cg[pii[q]] : 0.0;
+  }
+  const int dl = d - 1;
+  auto prefetch = [&](int64_t kt_) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < VPT; ++q) {
-      const int e = tid + q * 256;
-      const int kk = e / DP, i = e % DP;
-      const bool ok_ = e < kMT * DP && kk < nt_ && i < d;
-      const int64_t kr = ok_ ? kt_ + kk : kt_;
-      pv[q] = ok_ ? v[kr * ldv + (ok_ ? i : 0)] - cg[i < DP ? i : 0] : 0.0;
+      int64_t kr = kt_ + (pkk[q] < kMT ? pkk[q] : 0);
+      kr = kr < n ? kr : n - 1;
+      pv[q] = v[kr * ldv + (pii[q] < d ? pii[q] : dl)];
     }
-    pr = (tid < nt_ * RS) ? rec[kt_ * RS + tid] : 0.0;
-    pg = (tid < nt_ * kGStride) ? g[kt_ * kGStride + tid] : 0.0;
+    int64_t ir = kt_ * RS + tid;
+    pr = rec[ir < n * RS ? ir : n * RS - 1];
+    int64_t ig = kt_ * kGStride + tid;
+    pg = g[ig < n * kGStride ? ig : n * kGStride - 1];
   };
-  auto commit = [&]() {
+  auto commit = [&](int nt_) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < VPT; ++q) {
       const int e = tid + q * 256;
-      if (e < kMT * DP) vs[(e / DP) * VS + e % DP] = pv[q];
+      if (e < kMT * DP)
+        vs[pkk[q] * VS + pii[q]] = (pkk[q] < nt_ && pii[q] < d) ? pv[q] - pcg[q] : 0.0;
     }
-    if (tid < kMT * RS) rl[tid] = pr;
-    if (tid < kMT * kGStride) gl[tid] = pg;
+    if (tid < kMT * RS) rl[tid] = tid < nt_ * RS ? pr : 0.0;
+    if (tid < kMT * kGStride) gl[tid] = tid < nt_ * kGStride ? pg : 0.0;
+  };
+  // beta of a sub-tile is left in the wave's xt rows by the recursion and flushed to HBM at the
+  // start of the next iteration, after commit's wait: the stores then drain behind a whole
+  // sub-tile of compute before the next wait on this wave's vmcnt.
+  int ntp = 0;
+  int64_t ktp = k0;
+  auto flush = [&]() __attribute__((always_inline)) {
+    if (cola) {
+#pragma unroll
+      for (int kk = 0; kk < kMT; ++kk)
+        if (kk < ntp) beta[(ktp + kk) * ldb + col] = xt[wave][kk][lane];
+    }
   };
   if (k0 < k1) prefetch(k0);
   for (int64_t kt = k0; kt < k1; kt += kMT) {
     const int nt = (kt + kMT <= k1) ? kMT : (int)(k1 - kt);
     __syncthreads();
-    commit();
+    commit(nt);
     __syncthreads();
+#if WHITEN_ABL != 4
+    flush();
+#endif
     if (kt + kMT < k1) prefetch(kt + kMT);
     // cross products (v - c).(z - c) and the step norms |v - c|^2
     d4 acc[4];
@@ -522,9 +552,13 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
       if (ks < nks) {
         const double a = vs[fr * VS + 4 * ks + fq];
         vnp = fma(a, a, vnp);
+#if WHITEN_ABL != 2
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct)
           acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bf[ct][ks], acc[ct], 0, 0, 0);
+#else
+        acc[0][0] += a * bf[0][ks];
+#endif
       }
     }
     vnp += __shfl_xor(vnp, 16, 64);
@@ -537,14 +571,21 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
       for (int ct = 0; ct < 4; ++ct) {
         double d2 = vn + zn[ct] - 2.0 * acc[ct][r];
         d2 = d2 > 0.0 ? d2 : 0.0;
+#if WHITEN_ABL != 1
         xt[wave][fq + 4 * r][ct * 16 + fr] = skappa_sq<OK>(d2, inv_lo, s_o);
+#else
+        xt[wave][fq + 4 * r][ct * 16 + fr] = d2;
+#endif
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
     for (int kk = 0; kk < nt; ++kk) {
-      const int64_t k = kt + kk;
       const double x = colv ? xt[wave][kk][lane] : 0.0;
+#if WHITEN_ABL == 3
+      xt[wave][kk][lane] = x;
+      continue;
+#endif
       const double* rr = rl + kk * RS;
       double mm[SD];
 #pragma unroll
@@ -560,9 +601,14 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
       for (int i = 0; i < SD; ++i) mst[i] = fma(rr[SD * SD + i], ev, mm[i]);
 #pragma unroll
       for (int i = 0; i < SD; ++i) hs[i] = fma(al, gl[kk * kGStride + i], hs[i]);
-      if (cola) beta[k * ldb + col] = al;
+      xt[wave][kk][lane] = al;
     }
+    ntp = nt;
+    ktp = kt;
   }
+#if WHITEN_ABL != 4
+  flush();
+#endif
   if (cola) {
 #pragma unroll
     for (int i = 0; i < SD; ++i) {
