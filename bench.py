@@ -167,7 +167,7 @@ def main():
         avg = gram_ms / max(gram_n, 1)
         achieved = flops / (avg * 1e-3) / 1e12 if gram_n else None
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "gram_pmc_r01.json")
+        pmc = os.path.join(ROOT, "profiles", "gram_pmc_r01b.json")
         if os.path.exists(pmc):
             with open(pmc) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")

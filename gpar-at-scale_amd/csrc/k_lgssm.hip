@@ -525,11 +525,21 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
   // sub-tile of compute before the next wait on this wave's vmcnt.
   int ntp = 0;
   int64_t ktp = k0;
+  // Lane l stores rows 2i + l/32, column pair 2(l%32), +1 of the wave's 64 columns: 8 x 16 B
+  // stores per sub-tile instead of 16 x 8 B (store issue, not bandwidth, bounds this tail).
+  const int fh = lane >> 5, fc2 = (lane & 31) * 2;
   auto flush = [&]() __attribute__((always_inline)) {
-    if (cola) {
+    if (cw0 < mp) {   // mp is a multiple of 128: whole waves are in or out
 #pragma unroll
-      for (int kk = 0; kk < kMT; ++kk)
-        if (kk < ntp) beta[(ktp + kk) * ldb + col] = xt[wave][kk][lane];
+      for (int i = 0; i < kMT / 2; ++i) {
+        const int kk = 2 * i + fh;
+        if (kk < ntp) {
+          double2 v2;
+          v2.x = xt[wave][kk][fc2];
+          v2.y = xt[wave][kk][fc2 + 1];
+          *reinterpret_cast<double2*>(beta + (ktp + kk) * ldb + cw0 + fc2) = v2;
+        }
+      }
     }
   };
   if (k0 < k1) prefetch(k0);

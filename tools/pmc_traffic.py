@@ -9,6 +9,7 @@ import json
 import sys
 
 N, M, D = 1_000_000, 512, 32
+NCH = (N + 255) // 256
 
 
 def per_dispatch(path, needle):
@@ -31,8 +32,9 @@ def main(fetch_dir, write_dir):
                  "The Gram stages beta by global_load_lds_dwordx4 (16 B/lane, the calibrated width).",
         "gram_kernel": {"launches": n1, "fetch_kib_raw": gf, "write_kib_raw": gw,
                         "hbm_read_bytes": gf * 2048, "hbm_write_bytes": gw * 1024,
-                        "algorithmic_bytes": N * M * 8 + N * 40,
-                        "algorithmic_note": "beta (N x M f64) read once + g (4 doubles) and alpha per row"},
+                        "algorithmic_bytes": N * M * 8 + N * 8 + NCH * M * 4 * 8 * 2,
+                        "algorithmic_note": "beta (N x M f64) and alpha read once + the chunk correction's "
+                                            "E_j, C_j (nch x M x 4 f64 each)"},
         "whiten_kfu_mfma_D32": {"fetch_kib_raw": wf, "write_kib_raw": ww, "hbm_read_bytes": wf * 2048,
                                 "hbm_write_bytes": ww * 1024,
                                 "algorithmic_bytes": N * D * 8 + N * 16 * 8 + N * M * 8},
