@@ -75,11 +75,24 @@ __device__ __forceinline__ void store_c(double* G, int64_t ld, const d4 (&acc)[4
 }
 
 // ---------------------------------------------------------------- diagonal block
-// The 64 x 64 diagonal block is factored in LDS by 256 threads: thread (row i = t & 63,
-// column class c = t >> 6) updates the columns j = c (mod 4) of row i; every thread computes
-// the pivot itself, so a column step costs three barriers and no serial section.  Then the
-// inverse T_kk = L_kk^-1: column j by 4 lanes of one wave (k-split dot products).
+// The 64 x 64 diagonal block is factored by 256 threads: thread (row i = t & 63, class
+// c = t >> 6) keeps the entries j = c + 4u (u < 16) of row i in registers.  Unscaled
+// elimination: after step k, S_ij (j > k) holds A_ij - sum_{p<=k} A_ip A_jp / piv_p, and the
+// entry that has just become final (column k + 1) is published to LDS, so every step is one
+// barrier + 16 independent broadcast reads of column k.  Then the inverse T_kk = L_kk^-1,
+// right-looking with the partial sums of row r in registers: row k of T is published, then
+// every row r > k adds L_rk T_k. (one barrier per row).
 constexpr int kSD = kNB + 1;
+
+// 1 / p for p > 0: v_rcp_f64 seed + two Newton steps (~1 ulp)
+__device__ __forceinline__ double rcp_pos(double p) {
+  double r = __builtin_amdgcn_rcp(p);
+  double e = fma(-p, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-p, r, 1.0);
+  return fma(r, e, r);
+}
+
 __global__ __launch_bounds__(256) void potrf_diag(const CholJob2* __restrict__ jobs, int64_t ld,
                                                   int kb, int want_t) {
   const CholJob2 jb = jobs[blockIdx.x];
@@ -88,22 +101,41 @@ __global__ __launch_bounds__(256) void potrf_diag(const CholJob2* __restrict__ j
   __shared__ double Ti[kNB * kSD];
   __shared__ double dinv[kNB], dkk[kNB];
   double* Ablk = jb.A + (int64_t)kb * kNB * ld + (int64_t)kb * kNB;
-  for (int e = tid; e < kNB * kNB; e += 256) S[(e >> 6) * kSD + (e & 63)] = Ablk[(int64_t)(e >> 6) * ld + (e & 63)];
-  __syncthreads();
-  // Unscaled elimination: after step k, S_ij (j > k) holds A_ij - sum_{p<=k} A_ip A_jp / piv_p
-  // (Schur complement) while column k keeps A_ik; one reciprocal and one barrier per step.
   const int i = tid & 63, cls = tid >> 6;
+  double rv[16];
+#pragma unroll
+  for (int u = 0; u < 16; ++u) rv[u] = Ablk[(int64_t)i * ld + cls + 4 * u];
+  if (cls == 0) S[i * kSD] = rv[0];   // column 0 is final from the start
+  __syncthreads();
   bool bad = false;
-  for (int k = 0; k < kNB; ++k) {
+#ifndef POTRF_ABL
+#define POTRF_ABL 0   // timing ablations only: 1 no elimination loop, 2 no inverse loop
+#endif
+  for (int k = 0; k < (POTRF_ABL == 1 ? 0 : kNB - 1); ++k) {
     double piv = S[k * kSD + k];
     if (!(piv > 0.0)) { bad = true; piv = 1.0; }
-    if (i > k) {
-      const double c = S[i * kSD + k] / piv;
-      for (int j = k + 1 + ((cls - (k + 1)) & 3); j <= i; j += 4)
-        S[i * kSD + j] = fma(-c, S[j * kSD + k], S[i * kSD + j]);
+    const double c = (i > k) ? S[i * kSD + k] * rcp_pos(piv) : 0.0;
+    // loads unconditional (in bounds) and the predicate a select: a load inside the branch
+    // would be waited on one at a time
+    double sk[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) sk[u] = S[(cls + 4 * u) * kSD + k];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) {
+      const int j = cls + 4 * u;
+      const double nv = fma(-c, sk[u], rv[u]);
+      rv[u] = (j > k && j <= i) ? nv : rv[u];
+    }
+    {
+      const int u1 = (k + 1) >> 2;   // publish column k + 1 (owner class (k + 1) & 3)
+      double v1 = rv[0];
+#pragma unroll
+      for (int u = 1; u < 16; ++u) v1 = (u == u1) ? rv[u] : v1;
+      if (cls == ((k + 1) & 3) && i >= k + 1) S[i * kSD + k + 1] = v1;
     }
     __syncthreads();
   }
+  if (!(S[(kNB - 1) * kSD + kNB - 1] > 0.0)) bad = true;
   // scale: L_kk = sqrt(piv_k), L_ik = A_ik / L_kk
   if (tid < kNB) {
     const double pv = S[tid * kSD + tid];
@@ -118,20 +150,17 @@ __global__ __launch_bounds__(256) void potrf_diag(const CholJob2* __restrict__ j
     if (c < r) v = S[r * kSD + c] * dinv[c];
     else if (c == r) v = dkk[r];
     Ablk[(int64_t)r * ld + c] = v;
+    if (c <= r) S[r * kSD + c] = v;
   }
   __syncthreads();
-  for (int e = tid; e < kNB * kNB; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    if (c < r) S[r * kSD + c] *= dinv[c];
-    else if (c == r) S[r * kSD + c] = dkk[r];
-  }
-  __syncthreads();
+  // T = L^-1 column by column: column j by the 4 lanes 4j..4j+3 of one wave (k-split dot
+  // products); only wave-level ordering is needed (a column never leaves its wave).
   {
     const int j = tid >> 2, q = tid & 3;
     if (q == 0) Ti[j * kSD + j] = dinv[j];
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    for (int r = 1; r < kNB; ++r) {
+    for (int r = 1; r < (POTRF_ABL == 2 ? 0 : kNB); ++r) {
       double acc = 0.0;
       if (r > j)
         for (int k = j + q; k < r; k += 4) acc = fma(S[r * kSD + k], Ti[k * kSD + j], acc);
