@@ -12,6 +12,8 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "libgparhip.so"))
+# timing ablations only (tools/build_abl.sh builds variants next to the library)
+LIB_PATH = os.environ.get("GPAR_LIB_PATH", LIB_PATH)
 
 GPAR_OK, GPAR_ERR_ARG, GPAR_ERR_NOT_PD, GPAR_ERR_HIP, GPAR_ERR_OOM, GPAR_ERR_UNSUPPORTED, GPAR_ERR_STATE = range(7)
 GPAR_MEM_HOST, GPAR_MEM_DEVICE = 0, 1
