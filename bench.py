@@ -204,39 +204,50 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(N, NS, M, P, EV, out_kernel, n_sample=20_000, d_sample=32):
-    """Time the numpy oracle (oracle/gpar_oracle.py, the CPU restatement of the reference;
-    "port") on a bounded sample -- one DTC objective evaluation and one analytic prediction at
-    n_sample points, D = d_sample -- and scale linearly in N (every piece is O(N)) to the job:
+def cpu_baseline(N, NS, M, P, EV, out_kernel, samples=(50_000, 100_000), d_sample=32):
+    """Time the C/OpenMP CPU restatement of the reference path (oracle/cpu_ref.{c,py}, SURVEY §8d
+    "cpu_ref": kernel assembly, Kalman gains and per-column decorrelate sweeps, RTS smoother in C;
+    cholesky / trsm / gemm in OpenBLAS, as the reference leaves them to Julia's OpenBLAS; "port")
+    on a bounded sample: one DTC objective evaluation and one analytic prediction (N* = n/4) at
+    two sizes n, D = d_sample.  Every piece is O(n), so the job time is extrapolated linearly
+    from the larger sample (the smaller one reports how linear it is):
     (P-1) outputs x EV evaluations + (P-1) predictions (+ the temporal output, negligible)."""
     sys.path.insert(0, ROOT)
     from oracle import gpar_oracle as O
+    from oracle import cpu_ref as CR
     try:
         from threadpoolctl import threadpool_info
-        cores = max([x.get("num_threads", 1) for x in threadpool_info()] + [1])
+        blas = max([x.get("num_threads", 1) for x in threadpool_info() if x.get("user_api") == "blas"] + [1])
     except Exception:
-        cores = os.cpu_count() or 1
-    t, Y = O.synthetic_gpar(n_sample, d_sample + 1, seed=1, noise=0.8)
-    V = Y[:, :d_sample].T
-    y = Y[:, d_sample]
-    Z = O.pick_pseudo_inputs(V, M, 3)
+        blas = 1
+    cores = max(CR.threads(), blas)
     theta = (2.0, 2.0, 2.0, 2.0, float(np.exp(-2.0) + 1e-3))
-    t0 = time.perf_counter()
-    O.compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel, "matern52")
-    t_eval = time.perf_counter() - t0
-    ns = n_sample // 4
-    ts = np.sort(np.random.default_rng(2).uniform(t[0], t[-1], ns))
-    Vs = np.vstack([np.interp(ts, t, V[q]) for q in range(d_sample)])
-    t0 = time.perf_counter()
-    O.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, out_kernel, "matern52", "analytic")
-    t_pred = time.perf_counter() - t0
-    scale = N / n_sample
-    pred_scale = (N + NS) / (n_sample + ns)
-    t_job = (P - 1) * (EV * t_eval * scale + t_pred * pred_scale)
+    per = []
+    for n_sample in samples:
+        t, Y = O.synthetic_gpar(n_sample, d_sample + 1, seed=1, noise=0.8)
+        V = Y[:, :d_sample].T
+        y = Y[:, d_sample]
+        Z = O.pick_pseudo_inputs(V, M, 3)
+        t0 = time.perf_counter()
+        CR.compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel, "matern52")
+        t_eval = time.perf_counter() - t0
+        ns = n_sample // 4
+        ts = np.sort(np.random.default_rng(2).uniform(t[0], t[-1], ns))
+        Vs = np.vstack([np.interp(ts, t, V[q]) for q in range(d_sample)])
+        t0 = time.perf_counter()
+        CR.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, out_kernel, "matern52",
+                                             qu_kuu_noise=True)
+        t_pred = time.perf_counter() - t0
+        per.append((n_sample, ns, t_eval, t_pred))
+    n_sample, ns, t_eval, t_pred = per[-1]
+    t_job = (P - 1) * (EV * t_eval * N / n_sample + t_pred * (N + NS) / (n_sample + ns))
+    lin = (per[-1][2] / per[-1][0]) / (per[0][2] / per[0][0])
     return {"value": N * P / t_job, "unit": "pts*outputs/s", "cores": int(cores), "kind": "port",
-            "sample": f"numpy oracle: 1 DTC objective eval (N={n_sample}, M={M}, D={d_sample}) = {t_eval:.2f}s "
-                      f"+ 1 analytic predict (N={n_sample}, N*={ns}) = {t_pred:.2f}s, scaled linearly in N "
-                      f"to {P - 1} outputs x {EV} evals + {P - 1} predicts: est {t_job:.0f}s per job"}
+            "sample": f"C/OpenMP + OpenBLAS restatement (oracle/cpu_ref): 1 DTC objective eval (N={n_sample}, "
+                      f"M={M}, D={d_sample}) = {t_eval:.2f}s + 1 analytic predict (N={n_sample}, N*={ns}) = "
+                      f"{t_pred:.2f}s; per-point eval cost at N={per[0][0]} vs N={n_sample} differs by x{lin:.2f}; "
+                      f"scaled linearly in N to {P - 1} outputs x {EV} evals + {P - 1} predicts: "
+                      f"est {t_job:.0f}s per job"}
 
 
 if __name__ == "__main__":
