@@ -36,6 +36,9 @@ CONFIGS = {
     # configs[1]: DTC sparse GPAR N=1e5, M=256, P=8, RBF (EQ) output kernel
     "dtc": dict(N=100_000, M=256, P=8, evals=50, out_kernel="eq"),
     "small": dict(N=20_000, M=128, P=4, evals=20, out_kernel="matern52"),
+    # configs[2]: state-space (Matern-3/2) temporal-only chains, N=1e6, P=16 (a9, batched over
+    # chains: one NM over all chains, then RTS smoothing at N* = N test times)
+    "ssm": dict(N=1_000_000, M=0, P=16, evals=50, out_kernel="matern32", temporal=True),
 }
 # MI355X dense fp64 matrix peak: 1024 SIMDs x 2048 flop per v_mfma_f64_16x16x4_f64 / 64 cycles
 # (SQ_VALU_MFMA_BUSY_CYCLES / SQ_INSTS_MFMA = 64, profiles/) x 2.4 GHz = 78.6 TF/s (AMD spec value)
@@ -102,8 +105,10 @@ def main():
         t_d.copy_(torch.from_numpy(t_h)); Y_d.copy_(torch.from_numpy(Y_h))
         ts_d.copy_(torch.from_numpy(ts_h)); Fs_d.copy_(torch.from_numpy(Fs_h))
     S.broadcast_inputs((t_d, Y_d, ts_d, Fs_d))   # RCCL broadcast of the shared inputs over xGMI
-    mine = S.assign_outputs(P, world)[rank]
-    gpar_out = [p for p in mine if p >= 2]
+    temporal = cfg.get("temporal", False)
+    mine = S.assign_outputs(P, world)[rank] if not temporal else \
+        [p for p in range(1, P + 1) if (p - 1) % world == rank]
+    gpar_out = [p for p in mine if p >= 2] if not temporal else []
     Yh = Y_d.cpu().numpy() if gpar_out else None
     # q(u) with Kuu + sigma^2 I (qu_kuu_noise): the reference's jitter-free Cuu
     # (gpar_scaled_inference.jl:157) is numerically singular for M=512 pseudo-inputs drawn from
@@ -116,6 +121,8 @@ def main():
         problems.append(pr)
         keep.append(k)
     y1 = Y_d[:, 0].contiguous() if 1 in mine else None
+    if temporal:   # every owned output is a temporal-only chain (rows of one contiguous block)
+        y1 = Y_d[:, [p - 1 for p in mine]].T.contiguous() if mine else None
     x0 = np.tile(np.array([0.0, 0.0, 0.0, 0.0, -2.0]), (len(problems), 1))
     torch.cuda.synchronize()
     log(f"[rank {rank}] inputs ready in {time.perf_counter() - t0:.1f}s: N={n_eff} N*={ns_eff} "
@@ -131,9 +138,14 @@ def main():
             for i, p in enumerate(gpar_out):
                 res[p] = fr.theta[i]
         if y1 is not None:
-            th1, m1, v1 = G.get_sde_predictions_device(t_d, y1, ts_d, "matern52", (0.0, 0.0, -2.0),
+            tk = cfg["out_kernel"] if temporal else "matern52"
+            th1, m1, v1 = G.get_sde_predictions_device(t_d, y1, ts_d, tk, (0.0, 0.0, -2.0),
                                                        max_evals=EV, device=local)
-            res[1] = np.array(list(th1) + [0.0, 0.0])
+            if temporal:
+                for i, p in enumerate(mine):
+                    res[p] = np.array(list(np.atleast_2d(th1)[i]) + [0.0, 0.0])
+            else:
+                res[1] = np.array(list(th1) + [0.0, 0.0])
         for i, p in enumerate(gpar_out):
             G.predict_scaled(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], res[p], ts_d, Fs_d[:, : p - 1],
                              cfg["out_kernel"], "matern52", mode=args.predict, samples=100,
@@ -167,14 +179,16 @@ def main():
         avg = gram_ms / max(gram_n, 1)
         achieved = flops / (avg * 1e-3) / 1e12 if gram_n else None
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "gram_pmc_r01b.json")
-        if os.path.exists(pmc):
+        pmc = os.path.join(ROOT, "profiles", "gram_pmc_r01b.json")   # measured at the north config
+        if args.config == "north" and os.path.exists(pmc):
             with open(pmc) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
         out = {
-            "metric": "GPAR fit+predict wall-clock (ms) and pts*outputs/sec, N=1e6 M=512 P=64",
+            # BASELINE.json's metric string (north), the same wording at the other configs' sizes
+            "metric": "GPAR fit+predict wall-clock (ms) and pts\u00b7outputs/sec, "
+                      f"N={D.fmt_count(N)} M={M} P={P}",
             "value": value,
-            "unit": "pts*outputs/s",
+            "unit": "pts\u00b7outputs/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
@@ -196,7 +210,12 @@ def main():
             "kernels": {"gram_ms_per_step": gram_ms / args.steps, "whiten_ms_per_step": wh_ms / args.steps,
                         "whiten_launches": wh_n},
         }
-        if world == 1 and not args.no_cpu_baseline:
+        if temporal:
+            out["metric"] = "temporal-only LGSSM fit+smooth (Matern-3/2 chains), pts*chains/s"
+            out["roofline"] = None
+            out["config"]["workload"] = f"temporal-only chains fit+smooth ({args.config})"
+            out["config"]["time_kernel"] = cfg["out_kernel"]
+        if world == 1 and not args.no_cpu_baseline and not temporal:
             out["cpu_baseline"] = cpu_baseline(n_eff, ns_eff, M, P, EV, cfg["out_kernel"])
         print(json.dumps(out), flush=True)
     if world > 1:
@@ -242,7 +261,7 @@ def cpu_baseline(N, NS, M, P, EV, out_kernel, samples=(50_000, 100_000), d_sampl
     n_sample, ns, t_eval, t_pred = per[-1]
     t_job = (P - 1) * (EV * t_eval * N / n_sample + t_pred * (N + NS) / (n_sample + ns))
     lin = (per[-1][2] / per[-1][0]) / (per[0][2] / per[0][0])
-    return {"value": N * P / t_job, "unit": "pts*outputs/s", "cores": int(cores), "kind": "port",
+    return {"value": N * P / t_job, "unit": "pts\u00b7outputs/s", "cores": int(cores), "kind": "port",
             "sample": f"C/OpenMP + OpenBLAS restatement (oracle/cpu_ref): 1 DTC objective eval (N={n_sample}, "
                       f"M={M}, D={d_sample}) = {t_eval:.2f}s + 1 analytic predict (N={n_sample}, N*={ns}) = "
                       f"{t_pred:.2f}s; per-point eval cost at N={per[0][0]} vs N={n_sample} differs by x{lin:.2f}; "

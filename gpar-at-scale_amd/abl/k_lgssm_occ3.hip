@@ -1,0 +1,1532 @@
+// k_lgssm.hip -- state-space (Kalman) sweeps of the time GP on gfx950.
+//
+// Replaces the sequential TemporalGPs `decorrelate`/`logpdf` calls of the reference
+// (dtc.jl:106-117, gpar_scaled_inference.jl:170-183, temporal_gp_inference.jl:295) with a
+// time-chunked formulation whose every sequential dependency is short:
+//
+//  gains (data-independent, per chain = per output or temporal chain):
+//    phase 1  per chunk: fold the chunk's covariance elements (A, C, J) of the parallel
+//             Kalman filter (Sarkka & Garcia-Fernandez 2021, covariance part only);
+//    phase 2  per chain: exclusive scan of the chunk aggregates -> filtered covariance at
+//             every chunk start;
+//    phase 3  per chunk: ordinary Riccati recursion from that covariance, emitting the
+//             per-step record {A_k, K_k, 1/sqrt(S_k)}, the fix-up vectors
+//             g_k = -rs_k (A_k Phi_{k-1})[0,:], the chunk transition Phi_j and sum log S_k.
+//  columns (data): the filter is affine in the data with data-independent coefficients,
+//    m_k = (I - K_k h) A_k m_{k-1} + K_k x_k, so each chunk is filtered from a zero state
+//    (whiten_*), the true chunk-start states follow from a short carry recursion over chunks
+//    (carry_kernel), and alpha_k(true) = alpha_k(local) + g_k . c_chunk (applied by the
+//    consumer: vec_fix_kernel here, the Gram loader in k_gram.hip).
+#include "device_common.hpp"
+
+namespace gpar {
+
+struct ChainParams {
+  double inv_l;   // 1 / time lengthscale
+  double l;       // time lengthscale
+  double s;       // time-kernel variance (time_var^2)
+  double r;       // observation noise variance (sigma^2), used when no noise vector
+};
+
+template <int D>
+struct Elem {
+  double A[D][D];
+  double C[D][D];
+  double J[D][D];
+};
+
+template <int D>
+__device__ __forceinline__ void elem_identity(Elem<D>& e) {
+  mat_eye(e.A);
+  mat_zero(e.C);
+  mat_zero(e.J);
+}
+
+// e = e1 (earlier) (x) e2 (later)
+template <int D>
+__device__ __forceinline__ void elem_combine(const Elem<D>& e1, const Elem<D>& e2, Elem<D>& out) {
+  double Mi[D][D], M[D][D], T[D][D], X[D][D], V[D][D], U[D][D];
+  mat_mul(e1.C, e2.J, Mi);
+#pragma unroll
+  for (int i = 0; i < D; ++i) Mi[i][i] += 1.0;
+  mat_inv(Mi, M);
+  mat_mul(e2.A, M, T);                 // T = A2 M
+  Elem<D> r;
+  mat_mul(T, e1.A, r.A);               // A = A2 M A1
+  mat_mul(T, e1.C, X);                 // X = A2 M C1
+  mat_mul_bt(X, e2.A, r.C);            // C = A2 M C1 A2^T + C2
+  mat_mul(M, e1.A, V);                 // V = M A1
+  mat_mul(e2.J, e1.A, U);              // U = J2 A1
+  mat_mul_at(V, U, r.J);               // J = A1^T M^T J2 A1 + J1
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      r.C[i][j] += e2.C[i][j];
+      r.J[i][j] += e1.J[i][j];
+    }
+  // keep the covariance parts exactly symmetric
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < i; ++j) {
+      const double c = 0.5 * (r.C[i][j] + r.C[j][i]);
+      r.C[i][j] = c; r.C[j][i] = c;
+      const double q = 0.5 * (r.J[i][j] + r.J[j][i]);
+      r.J[i][j] = q; r.J[j][i] = q;
+    }
+  out = r;
+}
+
+// Observation noise of step k: the shared per-step vector when given (prediction grids: 1e10 at
+// test points, gpar_scaled_inference.jl:100-107), where a negative entry means "this chain's
+// own sigma^2" (train points of chains with different sigma, temporal_gp_inference.jl:310-313).
+__device__ __forceinline__ double step_noise(const double* __restrict__ noise, int64_t k,
+                                            const ChainParams& cp) {
+  if (!noise) return cp.r;
+  const double v = noise[k];
+  return v < 0.0 ? cp.r : v;
+}
+
+// Transition + process noise for step k of chain p (stationary start: tau_0 = 1).
+template <int D>
+__device__ __forceinline__ void step_model(const double* __restrict__ t, int64_t k,
+                                           const ChainParams& cp, double (&A)[D][D],
+                                           double (&Q)[D][D]) {
+  const double tau = (k == 0) ? 1.0 : (t[k] - t[k - 1]) / cp.l;
+  sde_transition<D>(tau, A);
+  double Pinf[D][D], X[D][D];
+  sde_pinf<D>(cp.s, Pinf);
+  mat_mul(A, Pinf, X);
+  mat_mul_bt(X, A, Q);
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) Q[i][j] = Pinf[i][j] - Q[i][j];
+}
+
+// Covariance element of step k (Sarkka & Garcia-Fernandez, Lemma 7 without the data parts).
+template <int D>
+__device__ __forceinline__ void step_elem(const double* __restrict__ t, int64_t k,
+                                          const ChainParams& cp, double R, Elem<D>& e) {
+  double A[D][D], Q[D][D];
+  step_model<D>(t, k, cp, A, Q);
+  if (k == 0) {
+    double P0[D][D], X[D][D], Pm[D][D];
+    sde_pinf<D>(cp.s, P0);
+    mat_mul(A, P0, X);
+    mat_mul_bt(X, A, Pm);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int j = 0; j < D; ++j) Pm[i][j] += Q[i][j];
+    const double S = Pm[0][0] + R;
+    mat_zero(e.A);
+    mat_zero(e.J);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int j = 0; j < D; ++j) e.C[i][j] = Pm[i][j] - (Pm[i][0] / S) * Pm[0][j];
+  } else {
+    const double S = Q[0][0] + R;
+    const double iS = 1.0 / S;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      const double kk = Q[i][0] * iS;
+#pragma unroll
+      for (int j = 0; j < D; ++j) {
+        e.A[i][j] = A[i][j] - kk * A[0][j];
+        e.C[i][j] = Q[i][j] - kk * Q[0][j];
+        e.J[i][j] = A[0][i] * A[0][j] * iS;
+      }
+    }
+  }
+}
+
+template <int D>
+__device__ __forceinline__ void elem_store(double* __restrict__ p, const Elem<D>& e) {
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      p[i * D + j] = e.A[i][j];
+      p[D * D + i * D + j] = e.C[i][j];
+      p[2 * D * D + i * D + j] = e.J[i][j];
+    }
+}
+
+template <int D>
+__device__ __forceinline__ void elem_load(const double* __restrict__ p, Elem<D>& e) {
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      e.A[i][j] = p[i * D + j];
+      e.C[i][j] = p[D * D + i * D + j];
+      e.J[i][j] = p[2 * D * D + i * D + j];
+    }
+}
+
+// ---------------------------------------------------------------------------- phase 1
+template <int D>
+__global__ __launch_bounds__(256) void gains_phase1(const double* __restrict__ t, int64_t n,
+                                                    int L, int64_t nch,
+                                                    const ChainParams* __restrict__ cps,
+                                                    const double* __restrict__ noise,
+                                                    double* __restrict__ agg) {
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (j >= nch) return;
+  const ChainParams cp = cps[p];
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  Elem<D> acc, e;
+  step_elem<D>(t, k0, cp, step_noise(noise, k0, cp), acc);
+  for (int64_t k = k0 + 1; k < k1; ++k) {
+    step_elem<D>(t, k, cp, step_noise(noise, k, cp), e);
+    elem_combine<D>(acc, e, acc);
+  }
+  elem_store<D>(agg + ((int64_t)p * nch + j) * (3 * D * D), acc);
+}
+
+// ---------------------------------------------------------------------------- phase 2
+// One workgroup per chain: exclusive scan over chunk aggregates; writes the filtered
+// covariance at the end of chunk j-1 into pstart[j] (j >= 1).
+template <int D>
+__global__ __launch_bounds__(256) void gains_phase2(int64_t nch, const double* __restrict__ agg,
+                                                    double* __restrict__ pstart) {
+  constexpr int E = 3 * D * D;
+  __shared__ double buf[2][256 * E];
+  const int p = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t per = (nch + 255) / 256;
+  const int64_t j0 = tid * per;
+  const int64_t j1 = (j0 + per < nch) ? j0 + per : nch;
+  const double* a = agg + (int64_t)p * nch * E;
+  Elem<D> loc, e;
+  elem_identity(loc);
+  for (int64_t j = j0; j < j1; ++j) {
+    elem_load<D>(a + j * E, e);
+    elem_combine<D>(loc, e, loc);
+  }
+  elem_store<D>(&buf[0][tid * E], loc);
+  __syncthreads();
+  int cur = 0;
+  for (int off = 1; off < 256; off <<= 1) {
+    Elem<D> mine;
+    elem_load<D>(&buf[cur][tid * E], mine);
+    if (tid >= off) {
+      Elem<D> prev;
+      elem_load<D>(&buf[cur][(tid - off) * E], prev);
+      elem_combine<D>(prev, mine, mine);
+    }
+    elem_store<D>(&buf[cur ^ 1][tid * E], mine);
+    __syncthreads();
+    cur ^= 1;
+  }
+  Elem<D> pre;
+  if (tid == 0) {
+    elem_identity(pre);
+  } else {
+    elem_load<D>(&buf[cur][(tid - 1) * E], pre);
+  }
+  double* ps = pstart + (int64_t)p * nch * (D * D);
+  for (int64_t j = j0; j < j1; ++j) {
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) ps[j * D * D + i * D + q] = pre.C[i][q];
+    elem_load<D>(a + j * E, e);
+    elem_combine<D>(pre, e, pre);
+  }
+}
+
+// ---------------------------------------------------------------------------- phase 3
+// Riccati recursion inside each chunk from the scanned start covariance.
+//   rec[k]   = {A_k (row-major), K_k, rs_k = 1/sqrt(S_k)}
+//   g[k]     = -rs_k * (A_k Phi_{j,k-1})[0, :]
+//   phi[j]   = prod_{k in chunk} (I - K_k e1^T) A_k   (D x D)
+//   logs[j]  = sum_{k in chunk} log S_k
+// With `smooth` output (prediction): pf[k] = filtered covariance (D x D), used by the RTS pass.
+template <int D>
+__global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t, int64_t n,
+                                                    int L, int64_t nch,
+                                                    const ChainParams* __restrict__ cps,
+                                                    const double* __restrict__ noise,
+                                                    const double* __restrict__ pstart,
+                                                    double* __restrict__ rec,
+                                                    double* __restrict__ g,
+                                                    double* __restrict__ phi,
+                                                    double* __restrict__ logs,
+                                                    double* __restrict__ pf) {
+  constexpr int RS = Rec<D>::size;
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (j >= nch) return;
+  const ChainParams cp = cps[p];
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  double P[D][D];
+  if (j == 0) {
+    sde_pinf<D>(cp.s, P);
+  } else {
+    const double* ps = pstart + ((int64_t)p * nch + j) * (D * D);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) P[i][q] = ps[i * D + q];
+  }
+  double Phi[D][D];
+  mat_eye(Phi);
+  double lsum = 0.0;
+  double* rp = rec + (int64_t)p * n * RS;
+  double* gp = g + (int64_t)p * n * kGStride;
+  double* pfp = pf ? pf + (int64_t)p * n * (D * D) : nullptr;
+  for (int64_t k = k0; k < k1; ++k) {
+    double A[D][D], Q[D][D], X[D][D], Pm[D][D];
+    step_model<D>(t, k, cp, A, Q);
+    mat_mul(A, P, X);
+    mat_mul_bt(X, A, Pm);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) Pm[i][q] += Q[i][q];
+    const double R = step_noise(noise, k, cp);
+    const double S = Pm[0][0] + R;
+    const double rs = 1.0 / sqrt(S);
+    double Kg[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) Kg[i] = Pm[i][0] / S;
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) P[i][q] = Pm[i][q] - Kg[i] * Pm[0][q];
+    double* r = rp + k * RS;
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) r[i * D + q] = A[i][q];
+#pragma unroll
+    for (int i = 0; i < D; ++i) r[D * D + i] = Kg[i];
+    r[D * D + D] = rs;
+    // g_k = -rs (A Phi)[0, :]
+    double AP[D][D];
+    mat_mul(A, Phi, AP);
+#pragma unroll
+    for (int q = 0; q < D; ++q) gp[k * kGStride + q] = -rs * AP[0][q];
+    // Phi <- (I - K e1^T) A Phi
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) Phi[i][q] = AP[i][q] - Kg[i] * AP[0][q];
+    lsum += log(S);
+    if (pfp) {
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) pfp[k * D * D + i * D + q] = P[i][q];
+    }
+  }
+  double* ph = phi + ((int64_t)p * nch + j) * (D * D);
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) ph[i * D + q] = Phi[i][q];
+  logs[(int64_t)p * nch + j] = lsum;
+}
+
+// ---------------------------------------------------------------------------- whitening of Kfu columns
+// beta_loc[k, c] = chunk-local whitened Kfu[k, c] with Kfu computed on the fly:
+// Kfu[k, c] = s_o kappa(||v_k - z_c|| / l_o)   (Stheno pairwise, dtc.jl:104).
+// grid: (nch, ceil(mp / 256)); block 256, one column per thread.
+// send[(j * mc + c) * 4 + i] = local end state of chunk j;
+// hsum[(j * mc + c) * 4 + i] = sum_{k in chunk j} beta_loc[k, c] g_k[i]  (H_j, the chunk's
+// moment against the fix-up rows: the Gram applies the carry fix-up through it, k_gram.hip;
+// null: not wanted).
+constexpr int kVTile = 32;
+
+template <int TK, int OK, int DP>
+__global__ __launch_bounds__(256) void whiten_kfu(
+    const double* __restrict__ rec, const double* __restrict__ v, int64_t ldv, int d,
+    const double* __restrict__ z, int64_t ldz, int64_t m, int64_t mp, int64_t n, int L,
+    double inv_lo, double s_o, double* __restrict__ beta, int64_t ldb, double* __restrict__ send,
+    int64_t mc, const double* __restrict__ g, double* __restrict__ hsum) {
+  constexpr int D = Sde<TK>::d;
+  constexpr int RS = Rec<D>::size;
+  __shared__ __attribute__((aligned(16))) double vs[kVTile][DP];
+  __shared__ double gs[kVTile * kGStride];
+  const int64_t j = blockIdx.x;
+  const int64_t c = (int64_t)blockIdx.y * 256 + threadIdx.x;
+  const bool valid = c < m;
+  const bool active = c < mp;
+  double zr[DP];
+#pragma unroll
+  for (int i = 0; i < DP; ++i) zr[i] = (valid && i < d) ? z[c * ldz + i] : 0.0;
+  double mst[D], hs[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) mst[i] = hs[i] = 0.0;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  for (int64_t kt = k0; kt < k1; kt += kVTile) {
+    const int nt = (kt + kVTile <= k1) ? kVTile : (int)(k1 - kt);
+    __syncthreads();
+    for (int e = threadIdx.x; e < kVTile * DP; e += 256) {
+      const int kk = e / DP, i = e % DP;
+      vs[kk][i] = (kk < nt && i < d) ? v[(kt + kk) * ldv + i] : 0.0;
+    }
+    if (threadIdx.x < kVTile * kGStride)
+      gs[threadIdx.x] = (threadIdx.x < nt * kGStride) ? g[kt * kGStride + threadIdx.x] : 0.0;
+    __syncthreads();
+    for (int kk = 0; kk < nt; ++kk) {
+      const int64_t k = kt + kk;
+      double d2a = 0.0, d2b = 0.0;
+#pragma unroll
+      for (int i = 0; i < DP; i += 2) {
+        const double a0 = vs[kk][i] - zr[i];
+        d2a = fma(a0, a0, d2a);
+        if (i + 1 < DP) {
+          const double a1 = vs[kk][i + 1] - zr[i + 1];
+          d2b = fma(a1, a1, d2b);
+        }
+      }
+      const double x = valid ? skappa_sq<OK>(d2a + d2b, inv_lo, s_o) : 0.0;
+      const double* r = rec + k * RS;
+      double mm[D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        double acc = 0.0;
+#pragma unroll
+        for (int q = 0; q < D; ++q) acc = fma(r[i * D + q], mst[q], acc);
+        mm[i] = acc;
+      }
+      const double ev = x - mm[0];
+      const double al = ev * r[D * D + D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) mst[i] = fma(r[D * D + i], ev, mm[i]);
+#pragma unroll
+      for (int i = 0; i < D; ++i) hs[i] = fma(al, gs[kk * kGStride + i], hs[i]);
+      if (active) beta[k * ldb + c] = al;
+    }
+  }
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      send[(j * mc + c) * kSStride + i] = mst[i];
+      if (hsum) hsum[(j * mc + c) * kSStride + i] = hs[i];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- whitening of Kfu columns, MFMA form
+// Same output as whiten_kfu, with Kfu built by v_mfma_f64_16x16x4_f64 in the Gram form
+// |v - z|^2 = |v - c|^2 + |z - c|^2 - 2 (v - c).(z - c)  (Distances.jl's pairwise form as used by
+// Stheno), centred to limit
+// cancellation (c = mean of the block's 256 pseudo-inputs).  Per 16-step sub-tile and wave (64 columns): DP/4 x 4 MFMAs give the 16 x 64
+// cross products in the C layout (lane: column ct*16 + (l&15), steps (l>>4) + 4r), the kernel
+// values are evaluated there (16 per lane, independent -> ILP), transposed through LDS, and the
+// lane of column c then runs the 16 filter steps.  Used for the smooth kernels (Matern-3/2,
+// Matern-5/2, EQ: a d^2 error of eps |v - c| |z - c| is harmless); Matern-1/2 keeps the direct
+// form (its kappa is not smooth in d^2 at 0).
+constexpr int kMT = 16;   // steps per sub-tile
+#ifndef WHITEN_ABL
+#define WHITEN_ABL 0   // timing ablations only: 1 no kernel evaluation, 2 no MFMA, 3 no recursion, 4 no beta store
+#endif
+
+template <int TK, int OK, int DP>
+__global__ __launch_bounds__(256, (DP <= 32 ? 3 : 2)) void whiten_kfu_mfma(
+    const double* __restrict__ rec, const double* __restrict__ v, int64_t ldv, int d,
+    const double* __restrict__ z, int64_t ldz, const double* __restrict__ zc, int64_t m,
+    int64_t mp, int64_t n, int L, double inv_lo, double s_o, double* __restrict__ beta,
+    int64_t ldb, double* __restrict__ send, int64_t mc, const double* __restrict__ g,
+    double* __restrict__ hsum) {
+  typedef double d4 __attribute__((ext_vector_type(4)));
+  constexpr int SD = Sde<TK>::d;
+  constexpr int RS = Rec<SD>::size;
+  constexpr int VS = DP + 2;      // V tile row stride: conflict-free A-fragment reads
+  constexpr int NKS = DP / 4;
+  __shared__ __attribute__((aligned(16))) double vs[kMT * VS];
+  __shared__ __attribute__((aligned(16))) double xt[4][kMT][65];
+  __shared__ __attribute__((aligned(16))) double rl[kMT * RS];   // the sub-tile's gains records
+  __shared__ __attribute__((aligned(16))) double gl[kMT * kGStride];   // and fix-up rows g_k
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t j = blockIdx.x;
+  const int64_t cw0 = (int64_t)blockIdx.y * 256 + wave * 64;   // wave's first column
+  const int64_t col = cw0 + lane;                               // recursion column of this lane
+  const int fr = lane & 15, fq = lane >> 4;
+  // centre of this block's 256 pseudo-inputs (subtracted from V while staging, from Z here)
+  const double* cg = zc + (int64_t)blockIdx.y * DP;
+  // B fragments (z - c) and |z - c|^2 of the C-layout columns ct*16 + fr
+  double bf[4][NKS];
+  double zn[4];
+#pragma unroll
+  for (int ct = 0; ct < 4; ++ct) {
+    const int64_t zcol = cw0 + ct * 16 + fr;
+    const bool zv = zcol < m;
+    const int64_t zcc = zv ? zcol : 0;
+    double part = 0.0;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      const int dim = 4 * ks + fq;
+      const double zz = (zv && dim < d) ? z[zcc * ldz + dim] - cg[dim] : 0.0;
+      bf[ct][ks] = zz;
+      part = fma(zz, zz, part);
+    }
+    part += __shfl_xor(part, 16, 64);
+    part += __shfl_xor(part, 32, 64);
+    zn[ct] = part;   // full |z - c|^2 of column ct*16 + fr (dims padded with zeros)
+  }
+  const int nks = (d + 3) / 4;
+  double mst[SD], hs[SD];
+#pragma unroll
+  for (int i = 0; i < SD; ++i) mst[i] = hs[i] = 0.0;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  const bool colv = col < m, cola = col < mp;
+  // next sub-tile's V rows and gains records are prefetched into registers (one MFMA /
+  // kernel-evaluation phase ahead) and written to LDS between the two barriers.  The loads are
+  // unconditional (clamped in-bounds addresses) and the masks are applied at commit, so no wait
+  // is forced at the load: vmcnt also counts this wave's beta stores, and a wait right after
+  // the prefetch would stall on the previous sub-tile's 16 stores.
+  constexpr int VPT = (kMT * DP + 255) / 256;   // V elements per thread
+  double pv[VPT], pcg[VPT], pr, pg;
+  int pkk[VPT], pii[VPT];
+#pragma unroll
+  for (int q = 0; q < VPT; ++q) {
+    const int e = tid + q * 256;
+    pkk[q] = e < kMT * DP ? e / DP : kMT;   // row kMT: never committed
+    pii[q] = e % DP;
+    pcg[q] = pii[q] < d ? cg[pii[q]] : 0.0;
+  }
+  const int dl = d - 1;
+  auto prefetch = [&](int64_t kt_) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      int64_t kr = kt_ + (pkk[q] < kMT ? pkk[q] : 0);
+      kr = kr < n ? kr : n - 1;
+      pv[q] = v[kr * ldv + (pii[q] < d ? pii[q] : dl)];
+    }
+    int64_t ir = kt_ * RS + tid;
+    pr = rec[ir < n * RS ? ir : n * RS - 1];
+    int64_t ig = kt_ * kGStride + tid;
+    pg = g[ig < n * kGStride ? ig : n * kGStride - 1];
+  };
+  auto commit = [&](int nt_) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < VPT; ++q) {
+      const int e = tid + q * 256;
+      if (e < kMT * DP)
+        vs[pkk[q] * VS + pii[q]] = (pkk[q] < nt_ && pii[q] < d) ? pv[q] - pcg[q] : 0.0;
+    }
+    if (tid < kMT * RS) rl[tid] = tid < nt_ * RS ? pr : 0.0;
+    if (tid < kMT * kGStride) gl[tid] = tid < nt_ * kGStride ? pg : 0.0;
+  };
+  // beta of a sub-tile is left in the wave's xt rows by the recursion and flushed to HBM at the
+  // start of the next iteration, after commit's wait: the stores then drain behind a whole
+  // sub-tile of compute before the next wait on this wave's vmcnt.
+  int ntp = 0;
+  int64_t ktp = k0;
+  // Lane l stores rows 2i + l/32, column pair 2(l%32), +1 of the wave's 64 columns: 8 x 16 B
+  // stores per sub-tile instead of 16 x 8 B (store issue, not bandwidth, bounds this tail).
+  const int fh = lane >> 5, fc2 = (lane & 31) * 2;
+  auto flush = [&]() __attribute__((always_inline)) {
+    if (cw0 < mp) {   // mp is a multiple of 128: whole waves are in or out
+#pragma unroll
+      for (int i = 0; i < kMT / 2; ++i) {
+        const int kk = 2 * i + fh;
+        if (kk < ntp) {
+          double2 v2;
+          v2.x = xt[wave][kk][fc2];
+          v2.y = xt[wave][kk][fc2 + 1];
+          *reinterpret_cast<double2*>(beta + (ktp + kk) * ldb + cw0 + fc2) = v2;
+        }
+      }
+    }
+  };
+  if (k0 < k1) prefetch(k0);
+  for (int64_t kt = k0; kt < k1; kt += kMT) {
+    const int nt = (kt + kMT <= k1) ? kMT : (int)(k1 - kt);
+    __syncthreads();
+    commit(nt);
+    __syncthreads();
+#if WHITEN_ABL != 4
+    flush();
+#endif
+    if (kt + kMT < k1) prefetch(kt + kMT);
+    // cross products (v - c).(z - c) and the step norms |v - c|^2
+    d4 acc[4];
+#pragma unroll
+    for (int ct = 0; ct < 4; ++ct) acc[ct] = d4{0.0, 0.0, 0.0, 0.0};
+    double vnp = 0.0;
+#pragma unroll
+    for (int ks = 0; ks < NKS; ++ks) {
+      if (ks < nks) {
+        const double a = vs[fr * VS + 4 * ks + fq];
+        vnp = fma(a, a, vnp);
+#if WHITEN_ABL != 2
+#pragma unroll
+        for (int ct = 0; ct < 4; ++ct)
+          acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bf[ct][ks], acc[ct], 0, 0, 0);
+#else
+        acc[0][0] += a * bf[0][ks];
+#endif
+      }
+    }
+    vnp += __shfl_xor(vnp, 16, 64);
+    vnp += __shfl_xor(vnp, 32, 64);   // lanes fr, fr+16, fr+32, fr+48 hold |v_fr - c|^2
+    // kernel values in the C layout: step fq + 4 r, column ct*16 + fr
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const double vn = __shfl(vnp, fq + 4 * r, 64);
+#pragma unroll
+      for (int ct = 0; ct < 4; ++ct) {
+        double d2 = vn + zn[ct] - 2.0 * acc[ct][r];
+        d2 = d2 > 0.0 ? d2 : 0.0;
+#if WHITEN_ABL != 1
+        xt[wave][fq + 4 * r][ct * 16 + fr] = skappa_sq<OK>(d2, inv_lo, s_o);
+#else
+        xt[wave][fq + 4 * r][ct * 16 + fr] = d2;
+#endif
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
+    __builtin_amdgcn_wave_barrier();
+    for (int kk = 0; kk < nt; ++kk) {
+      const double x = colv ? xt[wave][kk][lane] : 0.0;
+#if WHITEN_ABL == 3
+      xt[wave][kk][lane] = x;
+      continue;
+#endif
+      const double* rr = rl + kk * RS;
+      double mm[SD];
+#pragma unroll
+      for (int i = 0; i < SD; ++i) {
+        double a2 = 0.0;
+#pragma unroll
+        for (int q = 0; q < SD; ++q) a2 = fma(rr[i * SD + q], mst[q], a2);
+        mm[i] = a2;
+      }
+      const double ev = x - mm[0];
+      const double al = ev * rr[SD * SD + SD];
+#pragma unroll
+      for (int i = 0; i < SD; ++i) mst[i] = fma(rr[SD * SD + i], ev, mm[i]);
+#pragma unroll
+      for (int i = 0; i < SD; ++i) hs[i] = fma(al, gl[kk * kGStride + i], hs[i]);
+      xt[wave][kk][lane] = al;
+    }
+    ntp = nt;
+    ktp = kt;
+  }
+#if WHITEN_ABL != 4
+  flush();
+#endif
+  if (cola) {
+#pragma unroll
+    for (int i = 0; i < SD; ++i) {
+      send[(j * mc + col) * kSStride + i] = mst[i];
+      if (hsum) hsum[(j * mc + col) * kSStride + i] = hs[i];
+    }
+  }
+}
+
+// Centres of the pseudo-input column groups (256 columns each): zc[g][i] = mean_c z[c][i].
+// Block of 256 threads = dp dims x (256 / dp) column lanes, 8 independent loads in flight per
+// thread, partial sums combined through LDS in a fixed order.
+__global__ __launch_bounds__(256) void zcenter_kernel(const double* __restrict__ z, int64_t ldz,
+                                                      int d, int64_t m, int dp,
+                                                      double* __restrict__ zc) {
+  __shared__ double red[256];
+  const int64_t g = blockIdx.x;
+  const int i = threadIdx.x % dp, q = threadIdx.x / dp, nq = 256 / dp;
+  const int64_t c0 = g * 256, c1 = (c0 + 256 < m) ? c0 + 256 : m;
+  double s[8] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+  if (i < d && q < nq) {   // dp = 48: threads 240..255 idle
+    for (int64_t c = c0 + q; c < c1; c += 8 * nq) {
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int64_t cc = c + (int64_t)u * nq;
+        if (cc < c1) s[u] += z[cc * ldz + i];
+      }
+    }
+  }
+  red[threadIdx.x] = ((s[0] + s[1]) + (s[2] + s[3])) + ((s[4] + s[5]) + (s[6] + s[7]));
+  __syncthreads();
+  if (threadIdx.x < dp) {
+    double t = 0.0;
+    for (int u = 0; u < nq; ++u) t += red[u * dp + threadIdx.x];
+    const int64_t cnt = c1 - c0;
+    zc[g * dp + threadIdx.x] = (cnt > 0 && threadIdx.x < d) ? t / (double)cnt : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------- whitening of a vector per chain
+// One 64-lane wave per (chunk, chain).  The chunk's filter from a zero state is the affine
+// recurrence m_k = Abar_k m_{k-1} + K_k x_k (Abar_k = (I - K_k e1^T) A_k), so it is scanned
+// in parallel: lane l filters steps 4l..4l+3 from zero (alpha', local end state e_l, transfer
+// T_l, and gamma_k = -rs_k (A_k T_{k-1})[0, :]), a Hillis-Steele scan over the 64 lanes composes
+// (T, e) into each segment's incoming state s_l, and alpha_k = alpha'_k + gamma_k . s_l.
+// x_c[k] = y[c * ldy + k]; alpha_loc[c * lda + k * astride]; chunk end state (from zero at the
+// chunk start; the carry across chunks is vec_fix's) -> send[c * sendstride + (j * mc + col) * 4].
+constexpr int kVecL = 256;   // == host chunk length (64 lanes x 4 steps)
+constexpr int kVecSeg = kVecL / 64;
+
+__device__ __forceinline__ double shfl_up_d(double v, int off, int lane) {
+  return __shfl(v, lane >= off ? lane - off : lane, 64);
+}
+
+template <int D>
+__global__ __launch_bounds__(64) void whiten_vec(const double* __restrict__ rec, int64_t recstride,
+                                                 const double* __restrict__ y, int64_t ldy,
+                                                 int64_t n, int L, int64_t nch,
+                                                 double* __restrict__ alpha, int64_t lda,
+                                                 double* __restrict__ send, int64_t sendstride,
+                                                 int64_t mc, int64_t col, int64_t astride) {
+  constexpr int RS = Rec<D>::size;
+  const int64_t j = blockIdx.x;
+  const int c = blockIdx.y;
+  const int lane = threadIdx.x;
+  const double* rp = rec + (int64_t)c * recstride;
+  const double* yp = y + (int64_t)c * ldy;
+  const int64_t k0 = j * L + (int64_t)lane * kVecSeg;
+  const int64_t kend = (j * L + L < n) ? j * L + L : n;
+  // ---- local pass over this lane's segment
+  double m[D], T[D][D], gam[kVecSeg][D], al[kVecSeg];
+#pragma unroll
+  for (int i = 0; i < D; ++i) m[i] = 0.0;
+  mat_eye(T);
+#pragma unroll
+  for (int u = 0; u < kVecSeg; ++u) {
+    const int64_t k = k0 + u;
+    const bool live = k < kend;
+    const double* r = rp + (live ? k : 0) * RS;
+    double A[D][D], K[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+#pragma unroll
+      for (int q = 0; q < D; ++q) A[i][q] = live ? r[i * D + q] : (i == q ? 1.0 : 0.0);
+      K[i] = live ? r[D * D + i] : 0.0;
+    }
+    const double rs = live ? r[D * D + D] : 0.0;
+    const double x = live ? yp[k] : 0.0;
+    double mm[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < D; ++q) acc = fma(A[i][q], m[q], acc);
+      mm[i] = acc;
+    }
+    const double ev = x - mm[0];
+    al[u] = ev * rs;
+#pragma unroll
+    for (int i = 0; i < D; ++i) m[i] = fma(K[i], ev, mm[i]);
+    // gamma = -rs (A T)[0, :];  T <- (I - K e1^T) A T
+    double AT[D][D];
+    mat_mul(A, T, AT);
+#pragma unroll
+    for (int q = 0; q < D; ++q) gam[u][q] = -rs * AT[0][q];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) T[i][q] = fma(-K[i], AT[0][q], AT[i][q]);
+  }
+  // ---- inclusive scan of the segment maps s -> T s + e over the lanes
+  double e[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) e[i] = m[i];
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    double Tp[D][D], ep[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      ep[i] = shfl_up_d(e[i], off, lane);
+#pragma unroll
+      for (int q = 0; q < D; ++q) Tp[i][q] = shfl_up_d(T[i][q], off, lane);
+    }
+    if (lane >= off) {
+      double Tn[D][D], en[D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        double acc = e[i];
+#pragma unroll
+        for (int q = 0; q < D; ++q) acc = fma(T[i][q], ep[q], acc);
+        en[i] = acc;
+      }
+      mat_mul(T, Tp, Tn);
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        e[i] = en[i];
+#pragma unroll
+        for (int q = 0; q < D; ++q) T[i][q] = Tn[i][q];
+      }
+    }
+  }
+  // incoming state of segment l = inclusive result of lane l - 1
+  double sin_[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    const double v = shfl_up_d(e[i], 1, lane);
+    sin_[i] = lane > 0 ? v : 0.0;
+  }
+  double* ap = alpha + (int64_t)c * lda;
+#pragma unroll
+  for (int u = 0; u < kVecSeg; ++u) {
+    const int64_t k = k0 + u;
+    double a = al[u];
+#pragma unroll
+    for (int q = 0; q < D; ++q) a = fma(gam[u][q], sin_[q], a);
+    if (k < kend) ap[k * astride] = a;
+  }
+  if (lane == 63) {
+    double* sp = send + (int64_t)c * sendstride;
+#pragma unroll
+    for (int i = 0; i < D; ++i) sp[(j * mc + col) * kSStride + i] = e[i];
+  }
+}
+
+// ---------------------------------------------------------------------------- carry over chunks
+// cin[j][c] = true filter state at the start of chunk j: cin[0] = 0,
+// cin[j+1] = Phi_j cin[j] + send[j].  Two-level: groups of GS chunks.
+//   a) per (group, column): group end state from zero            -> gend
+//   b) per group: Psi_g = prod Phi_j over the group               -> psi
+//   c) per column: sequential over groups                          -> gin
+//   d) per (group, column): re-propagate inside the group          -> cin
+// Chains (blockIdx.z) are independent; per-chain strides: phistride, sstride (send/cin),
+// gstride_ (gend/gin), psistride.
+// REV: the adjoint's backward carry (chunks visited last to first, Phi transposed):
+// out[J-1] = 0, out[j] = Phi_{j+1}^T out[j+1] + b_{j+1}.
+template <int D, bool REV>
+__device__ __forceinline__ void carry_step(const double* __restrict__ ph, int64_t r,
+                                           const double* __restrict__ sv, double (&st)[D]) {
+  double nx[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    double acc = sv[i];
+#pragma unroll
+    for (int q = 0; q < D; ++q)
+      acc = fma(REV ? ph[r * D * D + q * D + i] : ph[r * D * D + i * D + q], st[q], acc);
+    nx[i] = acc;
+  }
+#pragma unroll
+  for (int i = 0; i < D; ++i) st[i] = nx[i];
+}
+
+template <int D, bool REV>
+__global__ __launch_bounds__(256) void carry_group_local(const double* __restrict__ phi, int64_t phistride,
+                                                         const double* __restrict__ send, int64_t sstride,
+                                                         int64_t nch, int64_t mc, int64_t ncols, int GS,
+                                                         double* __restrict__ gend, int64_t gstride_) {
+  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t gidx = blockIdx.y;
+  const int b = blockIdx.z;
+  if (c >= ncols) return;
+  const double* ph = phi + (int64_t)b * phistride;
+  const double* sp = send + (int64_t)b * sstride;
+  const int64_t j0 = gidx * GS;
+  const int64_t j1 = (j0 + GS < nch) ? j0 + GS : nch;
+  double st[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) st[i] = 0.0;
+#pragma unroll 4
+  for (int64_t j = j0; j < j1; ++j) {
+    const int64_t r = REV ? nch - 1 - j : j;
+    carry_step<D, REV>(ph, r, sp + (r * mc + c) * kSStride, st);
+  }
+  double* ge = gend + (int64_t)b * gstride_ + (gidx * mc + c) * kSStride;
+#pragma unroll
+  for (int i = 0; i < D; ++i) ge[i] = st[i];
+}
+
+template <int D, bool REV>
+__global__ __launch_bounds__(256) void carry_group_phi(const double* __restrict__ phi, int64_t phistride,
+                                                       int64_t nch, int GS, int64_t ngroups,
+                                                       double* __restrict__ psi, int64_t psistride) {
+  const int64_t gidx = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (gidx >= ngroups) return;
+  const double* ph = phi + (int64_t)b * phistride;
+  const int64_t j0 = gidx * GS;
+  const int64_t j1 = (j0 + GS < nch) ? j0 + GS : nch;
+  double P[D][D], X[D][D], F[D][D];
+  mat_eye(P);
+  for (int64_t j = j0; j < j1; ++j) {
+    const int64_t r = REV ? nch - 1 - j : j;
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q)
+        F[i][q] = REV ? ph[r * D * D + q * D + i] : ph[r * D * D + i * D + q];
+    mat_mul(F, P, X);
+    mat_copy(X, P);
+  }
+  double* ps = psi + (int64_t)b * psistride + gidx * D * D;
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) ps[i * D + q] = P[i][q];
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void carry_group_scan(const double* __restrict__ psi, int64_t psistride,
+                                                        const double* __restrict__ gend,
+                                                        double* __restrict__ gin, int64_t gstride_,
+                                                        int64_t ngroups, int64_t mc, int64_t ncols) {
+  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (c >= ncols) return;
+  const double* ps = psi + (int64_t)b * psistride;
+  const double* ge = gend + (int64_t)b * gstride_;
+  double* gi = gin + (int64_t)b * gstride_;
+  double st[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) st[i] = 0.0;
+  for (int64_t g = 0; g < ngroups; ++g) {
+    const int64_t o = (g * mc + c) * kSStride;
+#pragma unroll
+    for (int i = 0; i < D; ++i) gi[o + i] = st[i];
+    double nx[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc = ge[o + i];
+#pragma unroll
+      for (int q = 0; q < D; ++q) acc = fma(ps[g * D * D + i * D + q], st[q], acc);
+      nx[i] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) st[i] = nx[i];
+  }
+}
+
+template <int D, bool REV>
+__global__ __launch_bounds__(256) void carry_group_apply(const double* __restrict__ phi, int64_t phistride,
+                                                         const double* __restrict__ send,
+                                                         double* __restrict__ cin, int64_t sstride,
+                                                         const double* __restrict__ gin, int64_t gstride_,
+                                                         int64_t nch, int64_t mc, int64_t ncols, int GS) {
+  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t gidx = blockIdx.y;
+  const int b = blockIdx.z;
+  if (c >= ncols) return;
+  const double* ph = phi + (int64_t)b * phistride;
+  const double* sp = send + (int64_t)b * sstride;
+  double* cp = cin + (int64_t)b * sstride;
+  const double* gi = gin + (int64_t)b * gstride_ + (gidx * mc + c) * kSStride;
+  const int64_t j0 = gidx * GS;
+  const int64_t j1 = (j0 + GS < nch) ? j0 + GS : nch;
+  double st[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) st[i] = gi[i];
+#pragma unroll 4
+  for (int64_t j = j0; j < j1; ++j) {
+    const int64_t r = REV ? nch - 1 - j : j;
+    const int64_t o = (r * mc + c) * kSStride;
+#pragma unroll
+    for (int i = 0; i < D; ++i) cp[o + i] = st[i];
+    carry_step<D, REV>(ph, r, sp + o, st);
+  }
+}
+
+// ---------------------------------------------------------------------------- adjoint (Sigma^{-1} = W^T W)
+// The whitening alpha = W x is lower triangular; its adjoint u = W^T w runs backwards with the
+// same gains records:  u_k = rs_k w_k + K_k . lambda_k,  lambda_{k-1} = A_k^T (lambda_k - u_k e1),
+// lambda_{N-1} = 0.  Chunked like the forward pass: from lambda = 0 at each chunk end, then
+// u_k(true) = u_k(local) + h_k . chat_j with h_k = Gamma_{j,k}^T K_k,
+// Gamma_{j,k1-1} = I, Gamma_{j,k-1} = Abar_k^T Gamma_{j,k}, and the backward carry chat over
+// chunks with Phi_j^T (carry kernels, REV = true).
+template <int D>
+__global__ __launch_bounds__(256) void gains_adjoint(const double* __restrict__ rec, int64_t n,
+                                                     int L, int64_t nch, double* __restrict__ h) {
+  constexpr int RS = Rec<D>::size;
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int p = blockIdx.y;
+  if (j >= nch) return;
+  const double* rp = rec + (int64_t)p * n * RS;
+  double* hp = h + (int64_t)p * n * kGStride;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  double Gm[D][D];
+  mat_eye(Gm);
+  for (int64_t k = k1 - 1; k >= k0; --k) {
+    const double* r = rp + k * RS;
+    double A[D][D], K[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      K[i] = r[D * D + i];
+#pragma unroll
+      for (int q = 0; q < D; ++q) A[i][q] = r[i * D + q];
+    }
+    // h_k = Gamma^T K
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) acc = fma(Gm[i][q], K[i], acc);
+      hp[k * kGStride + q] = acc;
+    }
+    // Gamma <- Abar^T Gamma,  Abar = A - K A[0,:]
+    double Ab[D][D], X[D][D];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) Ab[i][q] = A[i][q] - K[i] * A[0][q];
+    mat_mul_at(Ab, Gm, X);
+    mat_copy(X, Gm);
+  }
+}
+
+// Backward local pass over a column-major-in-rows matrix X (row k, column c at X[k*ldx + c]):
+// reads w = X[k][c] + g_k . cin[j][c] (forward fix-up applied on the fly), writes u_loc in place,
+// and the chunk's backward end state (lambda before its first step) to bend[(j*mc + c)*4].
+// grid: (nch, ceil(ncols / 64)); block 64 (one column per lane).
+template <int D>
+__global__ __launch_bounds__(64) void adjoint_local(double* __restrict__ X, int64_t ldx,
+                                                    int64_t ncols, const double* __restrict__ rec,
+                                                    const double* __restrict__ g,
+                                                    const double* __restrict__ cin, int64_t mc,
+                                                    int64_t n, int L, double* __restrict__ bend,
+                                                    int64_t xstride, int64_t sstride) {
+  constexpr int RS = Rec<D>::size;
+  const int64_t j = blockIdx.x;
+  {
+    const int b = blockIdx.z;   // chain: gains (rec, g) are per chain, X / cin / bend strided
+    X += (int64_t)b * xstride;
+    rec += (int64_t)b * n * RS;
+    g += (int64_t)b * n * kGStride;
+    cin += (int64_t)b * sstride;
+    bend += (int64_t)b * sstride;
+  }
+  const int64_t c = (int64_t)blockIdx.y * 64 + threadIdx.x;
+  const bool act = c < ncols;
+  const int64_t cc = act ? c : 0;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  double cf[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) cf[i] = cin[(j * mc + cc) * kSStride + i];
+  double lam[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) lam[i] = 0.0;
+#pragma unroll 4
+  for (int64_t k = k1 - 1; k >= k0; --k) {
+    const double* r = rec + k * RS;
+    const double* gk = g + k * kGStride;
+    double w = X[k * ldx + cc];
+#pragma unroll
+    for (int i = 0; i < D; ++i) w = fma(gk[i], cf[i], w);
+    double u = w * r[D * D + D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) u = fma(r[D * D + i], lam[i], u);
+    lam[0] -= u;
+    double nl[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) acc = fma(r[i * D + q], lam[i], acc);
+      nl[q] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) lam[i] = nl[i];
+    if (act) X[k * ldx + c] = u;
+  }
+  if (act) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) bend[(j * mc + c) * kSStride + i] = lam[i];
+  }
+}
+
+// ---------------------------------------------------------------------------- smoothed mean of f
+// f_k = y_k - R_k (Sigma^{-1} y)_k   (S y = y - R Sigma^{-1} y), with
+// (Sigma^{-1} y)_k = u_loc_k + h_k . chat_{chunk(k)};  u_loc: adjoint output (contiguous per chain).
+template <int D>
+__global__ __launch_bounds__(256) void smooth_mean(const double* __restrict__ u,
+                                                   const double* __restrict__ h,
+                                                   const double* __restrict__ chat, int64_t sstride,
+                                                   const double* __restrict__ y, int64_t ldy,
+                                                   const double* __restrict__ noise,
+                                                   const ChainParams* __restrict__ cps, int64_t n,
+                                                   int L, double* __restrict__ mean, int64_t ldm) {
+  const int64_t k = blockIdx.x * (int64_t)256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (k >= n) return;
+  const int64_t j = k >> __builtin_ctz(L);  // L is a power of two (kChunk)
+  const double* hk = h + ((int64_t)b * n + k) * kGStride;
+  const double* ch = chat + (int64_t)b * sstride + j * kSStride;
+  double uu = u[(int64_t)b * n + k];
+#pragma unroll
+  for (int i = 0; i < D; ++i) uu = fma(hk[i], ch[i], uu);
+  const double R = step_noise(noise, k, cps[b]);
+  mean[(int64_t)b * ldm + k] = y[(int64_t)b * ldy + k] - R * uu;
+}
+
+// ---------------------------------------------------------------------------- smoothed covariance
+// RTS: P^s_k = G_k P^s_{k+1} G_k^T + C_k,  G_k = P_k A_{k+1}^T (P^-_{k+1})^{-1},
+// C_k = P_k - G_k P^-_{k+1} G_k^T  (G_{N-1} = 0, C_{N-1} = P_{N-1}).  Chunked: local from 0 at
+// each chunk end, P^s_k = local + Gamma_k Phat_j Gamma_k^T with Gamma_k = G_k ... G_{k1-1};
+// the per-chunk aggregate (local P^s at the chunk start, Gamma_{k0}) feeds a backward carry.
+// Only var_k = P^s_k[0,0] (the latent f, H = e1) is emitted.
+template <int D>
+__global__ __launch_bounds__(256) void cov_local(const double* __restrict__ t,
+                                                 const double* __restrict__ rec,
+                                                 const double* __restrict__ pf,
+                                                 const ChainParams* __restrict__ cps, int64_t n,
+                                                 int L, int64_t nch, double* __restrict__ vloc,
+                                                 double* __restrict__ gam,
+                                                 double* __restrict__ agg) {
+  constexpr int RS = Rec<D>::size;
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (j >= nch) return;
+  const ChainParams cp = cps[b];
+  const double* rp = rec + (int64_t)b * n * RS;
+  const double* pp = pf + (int64_t)b * n * D * D;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  double Ps[D][D], Gm[D][D];
+  mat_zero(Ps);
+  mat_eye(Gm);
+  for (int64_t k = k1 - 1; k >= k0; --k) {
+    double P[D][D];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) P[i][q] = pp[k * D * D + i * D + q];
+    double G[D][D], C[D][D];
+    if (k == n - 1) {
+      mat_zero(G);
+      mat_copy(P, C);
+    } else {
+      double A1[D][D], Q1[D][D], X[D][D], Pm[D][D], Pmi[D][D];
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) A1[i][q] = rp[(k + 1) * RS + i * D + q];
+      // Q_{k+1} = s Pinf - A Pinf A^T (same construction as step_model)
+      double Pinf[D][D];
+      sde_pinf<D>(cp.s, Pinf);
+      mat_mul(A1, Pinf, X);
+      mat_mul_bt(X, A1, Q1);
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) Q1[i][q] = Pinf[i][q] - Q1[i][q];
+      mat_mul(A1, P, X);
+      mat_mul_bt(X, A1, Pm);
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) Pm[i][q] += Q1[i][q];
+      mat_inv(Pm, Pmi);
+      mat_mul_bt(P, A1, X);        // P A^T
+      mat_mul(X, Pmi, G);          // G = P A^T Pm^{-1}
+      double GP[D][D], GPG[D][D];
+      mat_mul(G, Pm, GP);
+      mat_mul_bt(GP, G, GPG);
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) C[i][q] = P[i][q] - GPG[i][q];
+    }
+    double T[D][D], U[D][D];
+    mat_mul(G, Ps, T);
+    mat_mul_bt(T, G, U);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) Ps[i][q] = U[i][q] + C[i][q];
+    mat_mul(G, Gm, T);
+    mat_copy(T, Gm);
+    vloc[(int64_t)b * n + k] = Ps[0][0];
+#pragma unroll
+    for (int q = 0; q < D; ++q) gam[((int64_t)b * n + k) * kGStride + q] = Gm[0][q];
+  }
+  double* ag = agg + ((int64_t)b * nch + j) * (2 * D * D);
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      ag[i * D + q] = Ps[i][q];
+      ag[D * D + i * D + q] = Gm[i][q];
+    }
+}
+
+// Backward carry over chunks (one thread per chain): Phat_{J-1} = 0,
+// Phat_{j-1} = Ps_loc(j) + Gamma_j Phat_j Gamma_j^T.
+template <int D>
+__global__ void cov_carry(const double* __restrict__ agg, int64_t nch, int nchains,
+                          double* __restrict__ phat) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= nchains) return;
+  double Ph[D][D];
+  mat_zero(Ph);
+  for (int64_t j = nch - 1; j >= 0; --j) {
+    double* o = phat + ((int64_t)b * nch + j) * (D * D);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) o[i * D + q] = Ph[i][q];
+    const double* ag = agg + ((int64_t)b * nch + j) * (2 * D * D);
+    double Gm[D][D], T[D][D], U[D][D];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) Gm[i][q] = ag[D * D + i * D + q];
+    mat_mul(Gm, Ph, T);
+    mat_mul_bt(T, Gm, U);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) Ph[i][q] = ag[i * D + q] + U[i][q];
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void cov_out(const double* __restrict__ vloc,
+                                               const double* __restrict__ gam,
+                                               const double* __restrict__ phat, int64_t n, int L,
+                                               int64_t nch, double* __restrict__ var, int64_t ldv) {
+  const int64_t k = blockIdx.x * (int64_t)256 + threadIdx.x;
+  const int b = blockIdx.y;
+  if (k >= n) return;
+  const int64_t j = k >> __builtin_ctz(L);  // L is a power of two (kChunk)
+  const double* gk = gam + ((int64_t)b * n + k) * kGStride;
+  const double* P = phat + ((int64_t)b * nch + j) * (D * D);
+  double v = vloc[(int64_t)b * n + k];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) v = fma(gk[i] * P[i * D + q], gk[q], v);
+  var[(int64_t)b * ldv + k] = v;
+}
+
+// ---------------------------------------------------------------------------- fix-up of a vector
+// alpha[k] += g_k . cin[chunk(k)][col]; per-block partial sums of alpha^2 into part[b][blk].
+// One 256-thread block per chunk (L == 256).  With `hsum` (single chain, the DTC objective) the
+// block also prepares the Gram's chunk correction (k_gram.hip):
+//   W_j = sum_k g_k g_k^T,  q_j = sum_k g_k alpha_k  (alpha fixed)       -> qout[j * 4 + i]
+//   E_j[c] = H_j[c] + W_j C_j[c] / 2   for the ncols beta columns, in place of H_j (hsum).
+template <int D>
+__global__ __launch_bounds__(256) void vec_fix(double* __restrict__ alpha, int64_t lda,
+                                               const double* __restrict__ g, int64_t gstride,
+                                               const double* __restrict__ cin, int64_t sstride,
+                                               int64_t mc, int64_t col, int64_t n, int L,
+                                               double* __restrict__ part, double* __restrict__ hsum,
+                                               int64_t ncols, double* __restrict__ qout) {
+  constexpr int NW = D * (D + 1) / 2;   // packed upper triangle of W
+  constexpr int NV = 1 + NW + D;        // alpha^2 | W | q
+  __shared__ double red[4][NV];
+  __shared__ double wq[NW + D];
+  const int b = blockIdx.y;
+  const int64_t j = blockIdx.x;
+  const int64_t k = j * L + threadIdx.x;
+  double vals[NV];
+#pragma unroll
+  for (int e = 0; e < NV; ++e) vals[e] = 0.0;
+  if (k < n) {
+    const double* gp = g + (int64_t)b * gstride + k * kGStride;
+    const double* cp = cin + (int64_t)b * sstride + (j * mc + col) * kSStride;
+    double a = alpha[(int64_t)b * lda + k];
+    double gk[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      gk[i] = gp[i];
+      a = fma(gk[i], cp[i], a);
+    }
+    alpha[(int64_t)b * lda + k] = a;
+    vals[0] = a * a;
+    int e = 1;
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = i; q < D; ++q) vals[e++] = gk[i] * gk[q];
+#pragma unroll
+    for (int i = 0; i < D; ++i) vals[1 + NW + i] = gk[i] * a;
+  }
+  const int nv = hsum ? NV : 1;
+  for (int e = 0; e < nv; ++e) {
+    const double v = wave_sum(vals[e]);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][e] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0)
+    part[(int64_t)b * gridDim.x + blockIdx.x] = ((red[0][0] + red[1][0]) + red[2][0]) + red[3][0];
+  if (!hsum) return;
+  if (threadIdx.x < NW + D) {
+    const int e = 1 + threadIdx.x;
+    wq[threadIdx.x] = ((red[0][e] + red[1][e]) + red[2][e]) + red[3][e];
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) qout[j * 4 + threadIdx.x] = threadIdx.x < D ? wq[NW + threadIdx.x] : 0.0;
+  double W[D][D];
+  {
+    int e = 0;
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = i; q < D; ++q) {
+        W[i][q] = wq[e];
+        W[q][i] = wq[e];
+        ++e;
+      }
+  }
+  for (int64_t c = threadIdx.x; c < ncols; c += 256) {
+    const double* cp = cin + (j * mc + c) * kSStride;
+    double* hp = hsum + (j * mc + c) * kSStride;
+    double cv[D], ev[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) cv[i] = cp[i];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      double acc = 0.0;
+#pragma unroll
+      for (int q = 0; q < D; ++q) acc = fma(W[i][q], cv[q], acc);
+      ev[i] = fma(0.5, acc, hp[i]);
+    }
+#pragma unroll
+    for (int i = 0; i < kSStride; ++i) hp[i] = i < D ? ev[i] : 0.0;
+  }
+}
+
+// ---------------------------------------------------------------------------- chain log-likelihood
+// lml[b] = -0.5 (n log 2pi + sum logS + sum alpha^2), partials summed in a fixed order.
+__global__ void chain_lml(const double* __restrict__ logs, int64_t nch,
+                          const double* __restrict__ a2part, int64_t npart, int64_t n,
+                          double* __restrict__ lml) {
+  const int b = blockIdx.x;
+  __shared__ double red[2][256];
+  double s1 = 0.0, s2 = 0.0;
+  for (int64_t j = threadIdx.x; j < nch; j += 256) s1 += logs[(int64_t)b * nch + j];
+  for (int64_t j = threadIdx.x; j < npart; j += 256) s2 += a2part[(int64_t)b * npart + j];
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = s2;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + off];
+      red[1][threadIdx.x] += red[1][threadIdx.x + off];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) lml[b] = -0.5 * ((double)n * kLog2Pi + red[0][0] + red[1][0]);
+}
+
+}  // namespace gpar
+
+// ============================================================================ launch wrappers
+#include "launch.hpp"
+
+namespace gpar {
+
+#define GPAR_DISPATCH_D(D, ...)                                   \
+  switch (D) {                                                    \
+    case 1: { constexpr int DD = 1; __VA_ARGS__; } break;         \
+    case 2: { constexpr int DD = 2; __VA_ARGS__; } break;         \
+    default: { constexpr int DD = 3; __VA_ARGS__; } break;        \
+  }
+
+void launch_gains(hipStream_t st, int sdim, const double* t, int64_t n, int L, int64_t nch,
+                  int nchains, const ChainParamsHost* cps_dev, const double* noise,
+                  double* agg, double* pstart, double* rec, double* g, double* phi,
+                  double* logs, double* pf) {
+  const ChainParams* cps = reinterpret_cast<const ChainParams*>(cps_dev);
+  dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, {
+    gains_phase1<DD><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, agg);
+    gains_phase2<DD><<<nchains, 256, 0, st>>>(nch, agg, pstart);
+    gains_phase3<DD><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, pstart, rec, g, phi, logs, pf);
+  });
+}
+
+template <int TK, int OK>
+static void launch_whiten_kfu_k(hipStream_t st, int dp, dim3 grid, const double* rec,
+                                const double* v, int64_t ldv, int d, const double* z,
+                                int64_t ldz, int64_t m, int64_t mp, int64_t n, int L,
+                                double inv_lo, double s_o, double* beta, int64_t ldb,
+                                double* send, int64_t mc, const double* g, double* hsum) {
+  switch (dp) {
+    case 4: whiten_kfu<TK, OK, 4><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case 8: whiten_kfu<TK, OK, 8><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case 16: whiten_kfu<TK, OK, 16><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case 32: whiten_kfu<TK, OK, 32><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    default: whiten_kfu<TK, OK, 64><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+  }
+}
+
+template <int TK>
+static void launch_whiten_kfu_t(hipStream_t st, int ok, int dp, dim3 grid, const double* rec,
+                                const double* v, int64_t ldv, int d, const double* z,
+                                int64_t ldz, int64_t m, int64_t mp, int64_t n, int L,
+                                double inv_lo, double s_o, double* beta, int64_t ldb,
+                                double* send, int64_t mc, const double* g, double* hsum) {
+  switch (ok) {
+    case KM12: launch_whiten_kfu_k<TK, KM12>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case KM32: launch_whiten_kfu_k<TK, KM32>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case KM52: launch_whiten_kfu_k<TK, KM52>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    default: launch_whiten_kfu_k<TK, KEQ>(st, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+  }
+}
+
+int dp_bucket(int d) {
+  if (d <= 4) return 4;
+  if (d <= 8) return 8;
+  if (d <= 16) return 16;
+  if (d <= 32) return 32;
+  if (d <= 64) return 64;
+  return -1;
+}
+
+template <int TK, int OK>
+static void launch_whiten_mfma_k(hipStream_t st, int dp, dim3 grid, const double* rec,
+                                 const double* v, int64_t ldv, int d, const double* z,
+                                 int64_t ldz, const double* zc, int64_t m, int64_t mp, int64_t n,
+                                 int L, double inv_lo, double s_o, double* beta, int64_t ldb,
+                                 double* send, int64_t mc, const double* g, double* hsum) {
+  switch (dp) {
+    case 16: whiten_kfu_mfma<TK, OK, 16><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case 32: whiten_kfu_mfma<TK, OK, 32><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case 48: whiten_kfu_mfma<TK, OK, 48><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    default: whiten_kfu_mfma<TK, OK, 64><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+  }
+}
+
+template <int TK>
+static void launch_whiten_mfma_t(hipStream_t st, int dp, dim3 grid, const double* rec,
+                                 const double* v, int64_t ldv, int d, const double* z,
+                                 int64_t ldz, const double* zc, int64_t m, int64_t mp, int64_t n,
+                                 int L, int ok, double inv_lo, double s_o, double* beta,
+                                 int64_t ldb, double* send, int64_t mc, const double* g,
+                                 double* hsum) {
+  switch (ok) {
+    case KM32: launch_whiten_mfma_k<TK, KM32>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case KEQ: launch_whiten_mfma_k<TK, KEQ>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    default: launch_whiten_mfma_k<TK, KM52>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+  }
+}
+
+int mfma_dp_bucket(int d) {
+  if (d <= 16) return 16;
+  if (d <= 32) return 32;
+  if (d <= 48) return 48;
+  if (d <= 64) return 64;
+  return -1;
+}
+
+void launch_whiten_kfu_mfma(hipStream_t st, int time_kind, int out_kind, const double* rec,
+                            const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
+                            double* zc, int64_t m, int64_t mp, int64_t n, int L, int64_t nch,
+                            double inv_lo, double s_o, double* beta, int64_t ldb, double* send,
+                            int64_t mc, const double* g, double* hsum) {
+  const int dp = mfma_dp_bucket(d);
+  zcenter_kernel<<<(unsigned)((mp + 255) / 256), 256, 0, st>>>(z, ldz, d, m, dp, zc);
+  dim3 grid((unsigned)nch, (unsigned)((mp + 255) / 256));
+  switch (time_kind) {
+    case KM12: launch_whiten_mfma_t<KM12>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case KM32: launch_whiten_mfma_t<KM32>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    default: launch_whiten_mfma_t<KM52>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+  }
+}
+
+void launch_whiten_kfu(hipStream_t st, int time_kind, int out_kind, const double* rec,
+                       const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
+                       int64_t m, int64_t mp, int64_t n, int L, int64_t nch, double inv_lo,
+                       double s_o, double* beta, int64_t ldb, double* send, int64_t mc,
+                       const double* g, double* hsum) {
+  dim3 grid((unsigned)nch, (unsigned)((mp + 255) / 256));
+  const int dp = dp_bucket(d);
+  switch (time_kind) {
+    case KM12: launch_whiten_kfu_t<KM12>(st, out_kind, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case KM32: launch_whiten_kfu_t<KM32>(st, out_kind, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    default: launch_whiten_kfu_t<KM52>(st, out_kind, dp, grid, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+  }
+}
+
+void launch_whiten_vec(hipStream_t st, int sdim, const double* rec, int64_t recstride,
+                       const double* y, int64_t ldy, int64_t n, int L, int64_t nch, int nchains,
+                       double* alpha, int64_t lda, double* send, int64_t sendstride, int64_t mc,
+                       int64_t col, int64_t astride) {
+  dim3 grid((unsigned)nch, (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, whiten_vec<DD><<<grid, 64, 0, st>>>(rec, recstride, y, ldy, n, L, nch, alpha, lda, send, sendstride, mc, col, astride));
+}
+
+int carry_group_size(int64_t nch) {
+  int gs = 1;
+  while ((int64_t)gs * gs < nch) ++gs;
+  return gs;
+}
+
+void launch_carry(hipStream_t st, int sdim, const double* phi, int64_t phistride,
+                  const double* send, double* cin, int64_t sstride, int64_t nch, int64_t mc,
+                  int64_t ncols, int nchains, double* gend, double* gin, double* psi, bool rev) {
+  const int GS = carry_group_size(nch);
+  const int64_t ng = (nch + GS - 1) / GS;
+  const int64_t gstride_ = ng * mc * kSStride;
+  const int64_t psistride = ng * sdim * sdim;
+  dim3 g3((unsigned)((ncols + 255) / 256), (unsigned)ng, (unsigned)nchains);
+  dim3 gp((unsigned)((ng + 255) / 256), (unsigned)nchains);
+  dim3 gc((unsigned)((ncols + 255) / 256), (unsigned)nchains);
+#define GPAR_CARRY_LAUNCH(RV)                                                                       \
+  GPAR_DISPATCH_D(sdim, {                                                                          \
+    carry_group_local<DD, RV><<<g3, 256, 0, st>>>(phi, phistride, send, sstride, nch, mc, ncols, GS, gend, gstride_); \
+    carry_group_phi<DD, RV><<<gp, 256, 0, st>>>(phi, phistride, nch, GS, ng, psi, psistride);      \
+    carry_group_scan<DD><<<gc, 256, 0, st>>>(psi, psistride, gend, gin, gstride_, ng, mc, ncols);   \
+    carry_group_apply<DD, RV><<<g3, 256, 0, st>>>(phi, phistride, send, cin, sstride, gin, gstride_, nch, mc, ncols, GS); \
+  })
+  if (rev) {
+    GPAR_CARRY_LAUNCH(true);
+  } else {
+    GPAR_CARRY_LAUNCH(false);
+  }
+#undef GPAR_CARRY_LAUNCH
+}
+
+void launch_gains_adjoint(hipStream_t st, int sdim, const double* rec, int64_t n, int L,
+                          int64_t nch, int nchains, double* h) {
+  dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, gains_adjoint<DD><<<grid, 256, 0, st>>>(rec, n, L, nch, h));
+}
+
+void launch_adjoint_local(hipStream_t st, int sdim, double* X, int64_t ldx, int64_t ncols,
+                          const double* rec, const double* g, const double* cin, int64_t mc,
+                          int64_t n, int L, int64_t nch, double* bend, int nchains,
+                          int64_t xstride, int64_t sstride) {
+  dim3 grid((unsigned)nch, (unsigned)((ncols + 63) / 64), (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, adjoint_local<DD><<<grid, 64, 0, st>>>(X, ldx, ncols, rec, g, cin, mc, n, L, bend, xstride, sstride));
+}
+
+void launch_smooth_mean(hipStream_t st, int sdim, const double* u, const double* h,
+                        const double* chat, int64_t sstride, const double* y, int64_t ldy,
+                        const double* noise, const ChainParamsHost* cps, int64_t n, int L,
+                        int nchains, double* mean, int64_t ldm) {
+  dim3 grid((unsigned)((n + 255) / 256), (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, smooth_mean<DD><<<grid, 256, 0, st>>>(u, h, chat, sstride, y, ldy, noise, reinterpret_cast<const ChainParams*>(cps), n, L, mean, ldm));
+}
+
+void launch_cov_smooth(hipStream_t st, int sdim, const double* t, const double* rec,
+                       const double* pf, const ChainParamsHost* cps, int64_t n, int L,
+                       int64_t nch, int nchains, double* vloc, double* gam, double* agg,
+                       double* phat, double* var, int64_t ldv) {
+  dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
+  dim3 gout((unsigned)((n + 255) / 256), (unsigned)nchains);
+  const ChainParams* c = reinterpret_cast<const ChainParams*>(cps);
+  GPAR_DISPATCH_D(sdim, {
+    cov_local<DD><<<grid, 256, 0, st>>>(t, rec, pf, c, n, L, nch, vloc, gam, agg);
+    cov_carry<DD><<<(nchains + 63) / 64, 64, 0, st>>>(agg, nch, nchains, phat);
+    cov_out<DD><<<gout, 256, 0, st>>>(vloc, gam, phat, n, L, nch, var, ldv);
+  });
+}
+
+int64_t vec_fix_blocks(int64_t n) { return (n + 255) / 256; }
+
+void launch_vec_fix(hipStream_t st, int sdim, double* alpha, int64_t lda, const double* g,
+                    int64_t gstride, const double* cin, int64_t sstride, int64_t mc,
+                    int64_t col, int64_t n, int L, int nchains, double* part, double* hsum,
+                    int64_t ncols, double* qout) {
+  dim3 grid((unsigned)vec_fix_blocks(n), (unsigned)nchains);
+  GPAR_DISPATCH_D(sdim, vec_fix<DD><<<grid, 256, 0, st>>>(alpha, lda, g, gstride, cin, sstride, mc, col, n, L, part, hsum, ncols, qout));
+}
+
+void launch_chain_lml(hipStream_t st, const double* logs, int64_t nch, const double* a2part,
+                      int64_t npart, int64_t n, int nchains, double* lml) {
+  chain_lml<<<nchains, 256, 0, st>>>(logs, nch, a2part, npart, n, lml);
+}
+
+}  // namespace gpar

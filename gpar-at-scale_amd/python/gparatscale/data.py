@@ -45,6 +45,12 @@ def f_big(p, x, ys):
     return np.cos(ys[p - 2]) ** 2 + np.sin(np.pi * x / (20.0 + p)) + 0.1 * ys[p - 3]
 
 
+def fmt_count(n: int) -> str:
+    """1000000 -> '1e6' (bench metric strings)."""
+    e = len(str(int(n))) - 1
+    return f"{n // 10 ** e}e{e}" if n % 10 ** e == 0 else str(n)
+
+
 def nuke(x, nr_intervals, per_interval):
     """toy_data.jl:42-57."""
     if nr_intervals == 0:

@@ -1,0 +1,140 @@
+"""GPU parity at BASELINE.json's full sizes (SURVEY §8d configs 2-5 and the north star).
+
+The numpy oracle is too slow at these sizes, so the checker here is its C/OpenMP restatement
+(oracle/cpu_ref.{c,py}, itself pinned to the numpy oracle by tests/test_cpu_ref.py), which runs an
+N = 1e6 objective in seconds.  Where even that is out of reach (config 5: N = 1e7, M = 1024) the
+checks are size-independent properties of the objective:
+  * invariance under a permutation of the pseudo-inputs (the Gram, the blocked Cholesky and the
+    chunk carries all see a different column order, the lml must not change beyond rounding);
+  * determinism / idempotence: the same problem twice in one batch gives bit-identical values.
+Tolerances (fp64): objective rel <= 1e-9 at N <= 1e6 against the C port (the GPU sums in a
+different order over 1e6 terms and builds distances in the Gram form), temporal lml rel <= 1e-10,
+smoothed means rtol 1e-8, permutation invariance rel <= 1e-11.
+"""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+G = pytest.importorskip("gparatscale")
+from gparatscale import data as D  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture(scope="module")
+def CR():
+    if not os.path.exists(os.path.join(ROOT, "oracle", "libgpar_cpu.so")):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True, capture_output=True)
+    from oracle import cpu_ref
+    cpu_ref.load()
+    return cpu_ref
+
+
+def _output(ds, p, M, seed=None):
+    V = ds["Y"][:, : p - 1].T.copy()
+    y = ds["Y"][:, p - 1].copy()
+    Z = D.pseudo_inputs(ds["Y"][:, : p - 1], M, seed=p if seed is None else seed).T.copy()
+    return V, Z, y
+
+
+def _rel(a, b):
+    return abs(a - b) / abs(b)
+
+
+def test_north_objective_full_size(CR):
+    """North star: N = 1e6, M = 512, one output with D = 32 (Matern-5/2 x Matern-5/2)."""
+    ds = D.gpar_dataset(1_000_000, 33, seed=0, observation_noise=0.8)
+    V, Z, y = _output(ds, 33, 512)
+    theta = (1.0, 1.0, 1.0, 1.0, 0.2)
+    got = G.compute_gpar_dtc_objective(V, Z, ds["t"], y, theta)
+    ref, _ = CR.compute_gpar_dtc_objective(V, Z, ds["t"], y, theta)
+    assert _rel(got, ref) <= 1e-9, (got, ref)
+
+
+def test_config2_dtc_eq_full_size(CR):
+    """SURVEY config 2: N = 1e5, M = 256, P = 8, EQ output kernel (last output, D = 7)."""
+    ds = D.gpar_dataset(100_000, 8, seed=2, observation_noise=0.8)
+    V, Z, y = _output(ds, 8, 256)
+    theta = (0.7, 1.3, 2.0, 0.9, 0.3)
+    got = G.compute_gpar_dtc_objective(V, Z, ds["t"], y, theta, "eq", "matern52")
+    ref, _ = CR.compute_gpar_dtc_objective(V, Z, ds["t"], y, theta, "eq", "matern52")
+    assert _rel(got, ref) <= 1e-9, (got, ref)
+
+
+def test_config3_temporal_chains_full_size(CR):
+    """SURVEY config 3: 16 Matern-3/2 temporal-only chains (a9), N = 1e6, batched: logpdf of
+    every chain and the smoothed means of two of them against the C port."""
+    n, P = 1_000_000, 16
+    ds = D.gpar_dataset(n, P, seed=3, observation_noise=0.8)
+    t = ds["t"]
+    Y = np.ascontiguousarray(ds["Y"].T)
+    rng = np.random.default_rng(5)
+    theta = np.column_stack([rng.uniform(0.5, 3.0, P), rng.uniform(0.5, 2.0, P), rng.uniform(0.2, 0.9, P)])
+    got = G.lgssm_logpdf_batch(t, Y, theta, "matern32")
+    for c in range(P):
+        l, pv, sg = theta[c]
+        rec, logs, _, _ = CR.gains("matern32", t, l, pv * pv, sg * sg)
+        a = CR.decorrelate("matern32", rec, Y[c])
+        ref = -0.5 * (logs + a @ a + n * np.log(2.0 * np.pi))
+        assert _rel(got[c], ref) <= 1e-10, (c, got[c], ref)
+    sel = [0, 11]
+    mean, _ = G.lgssm_smooth_batch(t, Y[sel], theta[sel], "matern32")
+    for i, c in enumerate(sel):
+        l, pv, sg = theta[c]
+        rec, _, pf, pp = CR.gains("matern32", t, l, pv * pv, sg * sg, covs=True)
+        ref = CR.smooth_first("matern32", rec, pf, pp, Y[c])
+        np.testing.assert_allclose(mean[i], ref, rtol=1e-8, atol=1e-8 * np.abs(ref).max())
+
+
+def test_config4_eeg_shape_batch_full_size(CR):
+    """SURVEY config 4 (EEG shape): N = 1e5, M = 512, P = 64 -- a batch of outputs with D = 1,
+    32 and 63 (the widest input) in one batched objective call, each against the C port."""
+    ds = D.gpar_dataset(100_000, 64, seed=4, observation_noise=0.8)
+    outs = [2, 33, 64]
+    probs, keep, refs, thetas = [], [], [], []
+    for i, p in enumerate(outs):
+        V, Z, y = _output(ds, p, 512)
+        th = (1.0 + 0.2 * i, 1.0, 1.5 - 0.2 * i, 1.1, 0.25)
+        pr, k = G.make_problem(V, Z, ds["t"], y)
+        probs.append(pr)
+        keep.append(k)
+        thetas.append(th)
+        refs.append(CR.compute_gpar_dtc_objective(V, Z, ds["t"], y, th)[0])
+    got = G.dtc_objective_batch(probs, np.array(thetas))
+    for g, r in zip(got, refs):
+        assert _rel(g, r) <= 1e-9, (g, r)
+
+
+def test_config4_prediction_vs_cpu_port(CR):
+    """Analytic prediction (a7) at N = 1e5, N* = 2.5e4, M = 512, D = 32 against the C port."""
+    ds = D.gpar_dataset(100_000, 33, seed=6, observation_noise=0.8, n_star=25_000)
+    V, Z, y = _output(ds, 33, 512)
+    Vs = ds["F_star"][:, :32].T.copy()
+    theta = (1.0, 1.0, 1.0, 1.0, 0.2)
+    mean, std = G.predict_scaled(V, Z, ds["t"], y, theta, ds["t_star"], Vs, qu_kuu_noise=True)
+    rm, rs = CR.get_gpar_scaled_predictions_fixed(V, Z, ds["t"], y, ds["t_star"], Vs, theta,
+                                                  qu_kuu_noise=True)
+    np.testing.assert_allclose(mean, rm, rtol=1e-7, atol=1e-8 * np.abs(rm).max())
+    np.testing.assert_allclose(std, rs, rtol=1e-7, atol=1e-8 * np.abs(rs).max())
+
+
+def test_config5_stress_properties():
+    """SURVEY config 5 (stress): N = 1e7, M = 1024, one output with D = 8.  One evaluation is
+    ~0.3 s on the GPU but hours for any CPU checker, so: pseudo-input permutation invariance and
+    batch idempotence (the same problem twice in one batch, bit-identical)."""
+    n, M = 10_000_000, 1024
+    ds = D.gpar_dataset(n, 9, seed=5, observation_noise=0.8)
+    V, Z, y = _output(ds, 9, M)
+    perm = np.random.default_rng(7).permutation(M)
+    Zp = np.ascontiguousarray(Z[:, perm])
+    theta = (1.0, 1.0, 1.0, 1.0, 0.2)
+    p1, k1 = G.make_problem(V, Z, ds["t"], y)
+    p2, k2 = G.make_problem(V, Zp, ds["t"], y)
+    got = G.dtc_objective_batch([p1, p1, p2], np.array([theta] * 3))
+    assert np.isfinite(got).all()
+    assert got[0] == got[1]
+    assert _rel(got[2], got[0]) <= 1e-11, got
