@@ -164,6 +164,7 @@ struct DevProblem {
   int64_t n, m, d, mp, mc, nch;
   const double *t, *v, *z, *y;
   const double* t_user;  // caller's pointer (grouping key)
+  const double* zc;      // centres of the pseudo-input column groups (MFMA whitening), per problem
   int64_t ldv, ldz;
   int ok, tk, sdim, kuu_noise, qu_noise;
 };
@@ -195,9 +196,13 @@ static DevProblem prepare_problem(gpar_ctx* c, const gpar_problem& p, int idx) {
   d.kuu_noise = p.kuu_noise;
   d.qu_noise = p.qu_kuu_noise;
   d.t_user = p.t;
+  // Z is theta-independent: its group centres are computed once per prepared problem
+  double* zc = ws<double>(c, "prob" + std::to_string(idx) + "_zc", (size_t)((d.mp + 255) / 256) * 64);
+  d.zc = zc;
   if (p.mem == GPAR_MEM_DEVICE) {
     d.t = p.t; d.v = p.v; d.z = p.z; d.y = p.y;
     d.ldv = p.ldv; d.ldz = p.ldz;
+    if (d.ok != GPAR_MATERN12) launch_zcenter(c->stream, d.z, d.ldz, (int)d.d, d.m, d.mp, zc);
     return d;
   }
   check_sorted_host(p.t, p.n);
@@ -214,6 +219,7 @@ static DevProblem prepare_problem(gpar_ctx* c, const gpar_problem& p, int idx) {
                             p.d * sizeof(double), p.m, hipMemcpyHostToDevice, c->stream));
   d.t = t; d.v = v; d.z = z; d.y = y;
   d.ldv = p.d; d.ldz = p.d;
+  if (d.ok != GPAR_MATERN12) launch_zcenter(c->stream, d.z, d.ldz, (int)d.d, d.m, d.mp, zc);
   return d;
 }
 
@@ -268,9 +274,7 @@ static void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const double* rec, 
     launch_whiten_kfu(c->stream, p.tk, p.ok, rec, v, ldv, (int)p.d, p.z, p.ldz, p.m, p.mp, n,
                       kChunk, nch, 1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum);
   } else {
-    double* zc = ws<double>(c, c->stream == c->side ? "zcenter_1" : "zcenter",
-                            (size_t)((p.mp + 255) / 256) * 64);
-    launch_whiten_kfu_mfma(c->stream, p.tk, p.ok, rec, v, ldv, (int)p.d, p.z, p.ldz, zc, p.m, p.mp,
+    launch_whiten_kfu_mfma(c->stream, p.tk, p.ok, rec, v, ldv, (int)p.d, p.z, p.ldz, p.zc, p.m, p.mp,
                            n, kChunk, nch, 1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum);
   }
 }
@@ -537,7 +541,9 @@ struct QuOut {
 static QuOut run_q_u(gpar_ctx* c, const DevProblem& p, const Theta& th) {
   std::vector<DevProblem> P{p};
   std::vector<Theta> T{th};
-  GramOut go = run_gram_stage(c, P, T, /*fix_beta=*/true);
+  // The extra beta fix-up pass is for the noise-free Cuu only; with qu_kuu_noise the factor is
+  // the objective's regularised Kuu + s2 I and the objective's correction-form Gram is enough.
+  GramOut go = run_gram_stage(c, P, T, /*fix_beta=*/!p.qu_noise);
   DenseOut dn = run_dense(c, P, T, go, /*qu_mode=*/true);
   QuOut q;
   q.ld = dn.ld;
@@ -701,7 +707,7 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
   if (mode == GPAR_PREDICT_ANALYTIC) {
     double* rowsq = ws<double>(c, "pr_rowsq", (size_t)ncb * n_star);
     launch_gemm_nt(c->stream, Q, mp, Vm, ld, n_star, m, m, 0, nullptr, 0, rowsq, 0, nullptr,
-                   nullptr, nullptr);
+                   nullptr, nullptr, /*tri=*/1);
     launch_rowsq_finish(c->stream, rowsq, n_star, ncb, dstd);
   } else {
     double* Z = ws<double>(c, "pr_Z", (size_t)n_star * mp);
@@ -709,7 +715,7 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
     double* xi = ws<double>(c, "pr_xi", (size_t)samples * mp);
     double* mmc = ws<double>(c, "pr_mmc", n_star);
     launch_gemm_nt(c->stream, Q, mp, Vm, ld, n_star, m, m, 0, Z, mp, rowsq, 0, nullptr, nullptr,
-                   nullptr);
+                   nullptr, /*tri=*/1);
     launch_normal(c->stream, xi, mp, samples, m, samples, seed);
     launch_gemm_nt(c->stream, Z, mp, xi, mp, n_star, samples, m, 1, nullptr, 0, nullptr, samples,
                    dmean, mmc, dstd);

@@ -1410,13 +1410,17 @@ int mfma_dp_bucket(int d) {
   return -1;
 }
 
+void launch_zcenter(hipStream_t st, const double* z, int64_t ldz, int d, int64_t m, int64_t mp,
+                    double* zc) {
+  zcenter_kernel<<<(unsigned)((mp + 255) / 256), 256, 0, st>>>(z, ldz, d, m, mfma_dp_bucket(d), zc);
+}
+
 void launch_whiten_kfu_mfma(hipStream_t st, int time_kind, int out_kind, const double* rec,
                             const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
-                            double* zc, int64_t m, int64_t mp, int64_t n, int L, int64_t nch,
+                            const double* zc, int64_t m, int64_t mp, int64_t n, int L, int64_t nch,
                             double inv_lo, double s_o, double* beta, int64_t ldb, double* send,
                             int64_t mc, const double* g, double* hsum) {
   const int dp = mfma_dp_bucket(d);
-  zcenter_kernel<<<(unsigned)((mp + 255) / 256), 256, 0, st>>>(z, ldz, d, m, dp, zc);
   dim3 grid((unsigned)nch, (unsigned)((mp + 255) / 256));
   switch (time_kind) {
     case KM12: launch_whiten_mfma_t<KM12>(st, dp, grid, rec, v, ldv, d, z, ldz, zc, m, mp, n, L, out_kind, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;

@@ -87,11 +87,14 @@ void launch_whiten_kfu(hipStream_t st, int time_kind, int out_kind, const double
                        int64_t m, int64_t mp, int64_t n, int L, int64_t nch, double inv_lo,
                        double s_o, double* beta, int64_t ldb, double* send, int64_t mc,
                        const double* g, double* hsum);
-// MFMA Gram-form Kfu (smooth out kernels: Matern-3/2, Matern-5/2, EQ); zc: (mp/64) x 64 workspace
+// MFMA Gram-form Kfu (smooth out kernels: Matern-3/2, Matern-5/2, EQ); zc: (mp/256) x 64
+// pseudo-input centres from launch_zcenter (theta-independent: once per problem)
 int mfma_dp_bucket(int d);
+void launch_zcenter(hipStream_t st, const double* z, int64_t ldz, int d, int64_t m, int64_t mp,
+                    double* zc);
 void launch_whiten_kfu_mfma(hipStream_t st, int time_kind, int out_kind, const double* rec,
                             const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
-                            double* zc, int64_t m, int64_t mp, int64_t n, int L, int64_t nch,
+                            const double* zc, int64_t m, int64_t mp, int64_t n, int L, int64_t nch,
                             double inv_lo, double s_o, double* beta, int64_t ldb, double* send,
                             int64_t mc, const double* g, double* hsum);
 void launch_whiten_vec(hipStream_t st, int sdim, const double* rec, int64_t recstride,
@@ -163,7 +166,7 @@ void launch_predict_rows(hipStream_t st, int sdim, const double* X, int64_t ldx,
 void launch_gemm_nt(hipStream_t st, const double* A, int64_t lda, const double* B, int64_t ldb,
                     int64_t rows, int64_t cols, int64_t K, int mode, double* C, int64_t ldc,
                     double* rowsq, int64_t valid_cols, const double* base, double* out0,
-                    double* out1);
+                    double* out1, int tri = 0);
 void launch_rowsq_finish(hipStream_t st, const double* rowsq, int64_t rows, int nblk,
                          double* std_out);
 void launch_normal(hipStream_t st, double* xi, int64_t ld, int64_t S, int64_t M, int64_t Sp,
