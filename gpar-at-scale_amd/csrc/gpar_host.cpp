@@ -136,6 +136,7 @@ struct OnStream {
 
 constexpr int kChunk = 256;   // time-chunk length of the Kalman sweeps (power of two, multiple of 16)
 static_assert(kChunk == 256, "vec_fix runs one 256-thread block per chunk");
+constexpr int kSStride = 4;   // chunk state vectors padded to 4 doubles (device_common.hpp)
 
 static int sde_dim(int kind) {
   if (kind == GPAR_MATERN12) return 1;
@@ -234,9 +235,13 @@ struct GainsOut {
 };
 
 // Data-independent per-step filter quantities for `nchains` chains sharing t (n steps).
+// With ys (one device data vector per chain): the chains' alpha_loc / chunk end states are
+// filtered inside the gains pass (alpha_loc: nchains x n, asend: nchains x nch x 4).
 static GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                           const std::vector<ChainParamsHost>& cps, const double* noise,
-                          bool want_pf, const std::string& tag) {
+                          bool want_pf, const std::string& tag,
+                          const std::vector<const double*>* ys = nullptr,
+                          double* alpha_loc = nullptr, double* asend = nullptr) {
   const int nchains = (int)cps.size();
   const int64_t nch = (n + kChunk - 1) / kChunk;
   const int rs = rec_size(sdim);
@@ -254,10 +259,15 @@ static GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
   o.phi = ws<double>(c, tag + "_phi", (size_t)nchains * nch * d2);
   o.logs = ws<double>(c, tag + "_logs", (size_t)nchains * nch);
   o.pf = want_pf ? ws<double>(c, tag + "_pf", (size_t)nchains * n * d2) : nullptr;
+  const double** dys = nullptr;
+  if (ys) {
+    dys = ws<const double*>(c, tag + "_ys", nchains);
+    h2d(c, dys, ys->data(), nchains);
+  }
   {
     Timed tm_(c, "gains");
     launch_gains(c->stream, sdim, t, n, kChunk, nch, nchains, dcps, noise, agg, pst, o.rec, o.g,
-                 o.phi, o.logs, o.pf);
+                 o.phi, o.logs, o.pf, dys, alpha_loc, asend);
   }
   check_launch("gains");
   return o;
@@ -320,11 +330,21 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   for (auto& p : P)
     if (p.t_user != P[0].t_user || p.n != n || p.sdim != P[0].sdim) shared = false;
   std::vector<GainsOut> gains(np);
+  // shared gains: every output's alpha_loc (y filtered from zero per chunk) comes out of the
+  // gains pass itself; only its chunk end states are copied into the carry's alpha column
+  double* alpha_all = nullptr;
+  double* asend_all = nullptr;
   if (shared) {
     std::vector<ChainParamsHost> cps(np);
-    for (int i = 0; i < np; ++i)
+    std::vector<const double*> ys(np);
+    for (int i = 0; i < np; ++i) {
       cps[i] = {1.0 / th[i].l_t, th[i].l_t, th[i].sv_t * th[i].sv_t, th[i].sigma * th[i].sigma};
-    GainsOut g = run_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fit");
+      ys[i] = P[i].y;
+    }
+    alpha_all = ws<double>(c, "alpha_all", (size_t)np * n);
+    asend_all = ws<double>(c, "asend_all", (size_t)np * nch * kSStride);
+    GainsOut g = run_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fit", &ys, alpha_all,
+                           asend_all);
     for (int i = 0; i < np; ++i) {
       gains[i] = g;
       gains[i].rec = g.rec + (size_t)i * g.recstride;
@@ -368,7 +388,7 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     OnStream on_(c, lane ? c->side : c->main);
     const std::string sfx = lane ? "_1" : "";
     double* beta = beta_l[lane];
-    double* alpha = alpha_l[lane];
+    double* alpha = shared ? alpha_all + (size_t)i * n : alpha_l[lane];
     double* send = send_l[lane];
     double* cin = cin_l[lane];
     double* hsum = hsum_l[lane];
@@ -389,8 +409,14 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
       whiten_kfu_any(c, p, g.rec, p.v, p.ldv, n, nch, th[i], beta, p.mp, send, g.g, hsum);
     }
     check_launch("whiten_kfu");
-    launch_whiten_vec(c->stream, p.sdim, g.rec, 0, p.y, 0, n, kChunk, nch, 1, alpha, 0, send, 0,
-                      p.mc, p.mp);
+    if (shared) {   // alpha's chunk end states -> column mp of the carry input
+      HIPCHECK(hipMemcpy2DAsync(send + (size_t)p.mp * kSStride, (size_t)p.mc * kSStride * sizeof(double),
+                                asend_all + (size_t)i * nch * kSStride, kSStride * sizeof(double),
+                                kSStride * sizeof(double), nch, hipMemcpyDeviceToDevice, c->stream));
+    } else {
+      launch_whiten_vec(c->stream, p.sdim, g.rec, 0, p.y, 0, n, kChunk, nch, 1, alpha, 0, send, 0,
+                        p.mc, p.mp);
+    }
     check_launch("whiten_vec");
     run_carry(c, p.sdim, g.phi, 0, send, cin, 0, nch, p.mc, p.mc, 1, "fitc" + sfx);
     check_launch("carry");

@@ -88,12 +88,10 @@ __device__ __forceinline__ double step_noise(const double* __restrict__ noise, i
   return v < 0.0 ? cp.r : v;
 }
 
-// Transition + process noise for step k of chain p (stationary start: tau_0 = 1).
+// Transition + process noise of a step of scaled length tau (stationary start: tau_0 = 1).
 template <int D>
-__device__ __forceinline__ void step_model(const double* __restrict__ t, int64_t k,
-                                           const ChainParams& cp, double (&A)[D][D],
-                                           double (&Q)[D][D]) {
-  const double tau = (k == 0) ? 1.0 : (t[k] - t[k - 1]) / cp.l;
+__device__ __forceinline__ void step_model_tau(double tau, const ChainParams& cp,
+                                               double (&A)[D][D], double (&Q)[D][D]) {
   sde_transition<D>(tau, A);
   double Pinf[D][D], X[D][D];
   sde_pinf<D>(cp.s, Pinf);
@@ -105,13 +103,52 @@ __device__ __forceinline__ void step_model(const double* __restrict__ t, int64_t
     for (int j = 0; j < D; ++j) Q[i][j] = Pinf[i][j] - Q[i][j];
 }
 
-// Covariance element of step k (Sarkka & Garcia-Fernandez, Lemma 7 without the data parts).
+// Transition + process noise for step k of chain p.
 template <int D>
-__device__ __forceinline__ void step_elem(const double* __restrict__ t, int64_t k,
-                                          const ChainParams& cp, double R, Elem<D>& e) {
+__device__ __forceinline__ void step_model(const double* __restrict__ t, int64_t k,
+                                           const ChainParams& cp, double (&A)[D][D],
+                                           double (&Q)[D][D]) {
+  step_model_tau<D>((k == 0) ? 1.0 : (t[k] - t[k - 1]) / cp.l, cp, A, Q);
+}
+
+// Per-thread sequential sweeps over a chunk (gains phases 1 and 3) read their step inputs
+// (t_k, the noise entry, the data value) kStepPF steps ahead through a register pipeline: a load
+// consumed in the same step is waited on at once, and on gfx9 vmcnt also counts every store the
+// thread issued before it, so each step would stall for a full memory round trip.  The loop
+// stays rolled (an unrolled block of steps doubles the VGPRs of these 3x3 recursions).
+constexpr int kStepPF = 3;
+struct StepPipe {
+  double t[kStepPF], r[kStepPF], y[kStepPF];
+  const double *tp, *np, *yp;
+  int64_t k1;
+  __device__ __forceinline__ void load(int slot, int64_t k) {
+    const int64_t kk = k < k1 ? k : k1 - 1;
+    t[slot] = tp[kk];
+    r[slot] = np ? np[kk] : 0.0;
+    y[slot] = yp ? yp[kk] : 0.0;
+  }
+  __device__ __forceinline__ void init(const double* t_, const double* n_, const double* y_,
+                                       int64_t k0, int64_t k1_) {
+    tp = t_; np = n_; yp = y_; k1 = k1_;
+#pragma unroll
+    for (int s = 0; s < kStepPF; ++s) load(s, k0 + s);
+  }
+  // values of step k (slot 0), then shift and fetch step k + kStepPF
+  __device__ __forceinline__ void next(int64_t k, double& tk, double& rk, double& yk) {
+    tk = t[0]; rk = r[0]; yk = y[0];
+#pragma unroll
+    for (int s = 0; s + 1 < kStepPF; ++s) { t[s] = t[s + 1]; r[s] = r[s + 1]; y[s] = y[s + 1]; }
+    load(kStepPF - 1, k + kStepPF);
+  }
+};
+
+// Covariance element of a step (Sarkka & Garcia-Fernandez, Lemma 7 without the data parts).
+template <int D>
+__device__ __forceinline__ void step_elem_tau(double tau, bool first, const ChainParams& cp,
+                                              double R, Elem<D>& e) {
   double A[D][D], Q[D][D];
-  step_model<D>(t, k, cp, A, Q);
-  if (k == 0) {
+  step_model_tau<D>(tau, cp, A, Q);
+  if (first) {
     double P0[D][D], X[D][D], Pm[D][D];
     sde_pinf<D>(cp.s, P0);
     mat_mul(A, P0, X);
@@ -181,9 +218,17 @@ __global__ __launch_bounds__(256) void gains_phase1(const double* __restrict__ t
   const int64_t k0 = j * L;
   const int64_t k1 = (k0 + L < n) ? k0 + L : n;
   Elem<D> acc, e;
-  step_elem<D>(t, k0, cp, step_noise(noise, k0, cp), acc);
-  for (int64_t k = k0 + 1; k < k1; ++k) {
-    step_elem<D>(t, k, cp, step_noise(noise, k, cp), e);
+  elem_identity(acc);   // identity (x) e == e exactly: one code path for every step
+  double tprev = k0 > 0 ? t[k0 - 1] : 0.0;
+  StepPipe sp;
+  sp.init(t, noise, nullptr, k0, k1);
+  for (int64_t k = k0; k < k1; ++k) {
+    double tk, rk, yk;
+    sp.next(k, tk, rk, yk);
+    const double tau = (k == 0) ? 1.0 : (tk - tprev) / cp.l;
+    tprev = tk;
+    const double R = noise ? (rk < 0.0 ? cp.r : rk) : cp.r;
+    step_elem_tau<D>(tau, k == 0, cp, R, e);
     elem_combine<D>(acc, e, acc);
   }
   elem_store<D>(agg + ((int64_t)p * nch + j) * (3 * D * D), acc);
@@ -248,6 +293,9 @@ __global__ __launch_bounds__(256) void gains_phase2(int64_t nch, const double* _
 //   phi[j]   = prod_{k in chunk} (I - K_k e1^T) A_k   (D x D)
 //   logs[j]  = sum_{k in chunk} log S_k
 // With `smooth` output (prediction): pf[k] = filtered covariance (D x D), used by the RTS pass.
+// With `ys` (the DTC objective): the chain's own data vector ys[p] is filtered from a zero state
+// in the same pass, with the record still in registers (what whiten_vec would do in a second pass
+// over rec): alpha_loc[p * n + k] and the chunk end state asend[(p * nch + j) * 4 + i].
 template <int D>
 __global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t, int64_t n,
                                                     int L, int64_t nch,
@@ -258,7 +306,10 @@ __global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t
                                                     double* __restrict__ g,
                                                     double* __restrict__ phi,
                                                     double* __restrict__ logs,
-                                                    double* __restrict__ pf) {
+                                                    double* __restrict__ pf,
+                                                    const double* const* __restrict__ ys,
+                                                    double* __restrict__ alpha_loc,
+                                                    double* __restrict__ asend) {
   constexpr int RS = Rec<D>::size;
   const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int p = blockIdx.y;
@@ -279,19 +330,30 @@ __global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t
   double Phi[D][D];
   mat_eye(Phi);
   double lsum = 0.0;
+  const double* yp = ys ? ys[p] : nullptr;
+  double* ap = ys ? alpha_loc + (int64_t)p * n : nullptr;
+  double ma[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) ma[i] = 0.0;
   double* rp = rec + (int64_t)p * n * RS;
   double* gp = g + (int64_t)p * n * kGStride;
   double* pfp = pf ? pf + (int64_t)p * n * (D * D) : nullptr;
+  double tprev = k0 > 0 ? t[k0 - 1] : 0.0;
+  StepPipe spp;
+  spp.init(t, noise, yp, k0, k1);
   for (int64_t k = k0; k < k1; ++k) {
+    double tk, rk, yk;
+    spp.next(k, tk, rk, yk);
     double A[D][D], Q[D][D], X[D][D], Pm[D][D];
-    step_model<D>(t, k, cp, A, Q);
+    step_model_tau<D>((k == 0) ? 1.0 : (tk - tprev) / cp.l, cp, A, Q);
+    tprev = tk;
     mat_mul(A, P, X);
     mat_mul_bt(X, A, Pm);
 #pragma unroll
     for (int i = 0; i < D; ++i)
 #pragma unroll
       for (int q = 0; q < D; ++q) Pm[i][q] += Q[i][q];
-    const double R = step_noise(noise, k, cp);
+    const double R = noise ? (rk < 0.0 ? cp.r : rk) : cp.r;
     const double S = Pm[0][0] + R;
     const double rs = 1.0 / sqrt(S);
     double Kg[D];
@@ -320,6 +382,20 @@ __global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t
 #pragma unroll
       for (int q = 0; q < D; ++q) Phi[i][q] = AP[i][q] - Kg[i] * AP[0][q];
     lsum += log(S);
+    if (yp) {   // alpha filter from zero (same arithmetic as whiten_kfu's column recursion)
+      double mm[D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+        double a2 = 0.0;
+#pragma unroll
+        for (int q = 0; q < D; ++q) a2 = fma(A[i][q], ma[q], a2);
+        mm[i] = a2;
+      }
+      const double ev = yk - mm[0];
+      ap[k] = ev * rs;
+#pragma unroll
+      for (int i = 0; i < D; ++i) ma[i] = fma(Kg[i], ev, mm[i]);
+    }
     if (pfp) {
 #pragma unroll
       for (int i = 0; i < D; ++i)
@@ -333,6 +409,11 @@ __global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t
 #pragma unroll
     for (int q = 0; q < D; ++q) ph[i * D + q] = Phi[i][q];
   logs[(int64_t)p * nch + j] = lsum;
+  if (yp) {
+    double* sp = asend + ((int64_t)p * nch + j) * kSStride;
+#pragma unroll
+    for (int i = 0; i < kSStride; ++i) sp[i] = i < D ? ma[i] : 0.0;
+  }
 }
 
 // ---------------------------------------------------------------------------- whitening of Kfu columns
@@ -826,7 +907,7 @@ __global__ __launch_bounds__(256) void carry_group_local(const double* __restric
   double st[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) st[i] = 0.0;
-#pragma unroll 4
+#pragma unroll 16
   for (int64_t j = j0; j < j1; ++j) {
     const int64_t r = REV ? nch - 1 - j : j;
     carry_step<D, REV>(ph, r, sp + (r * mc + c) * kSStride, st);
@@ -879,6 +960,7 @@ __global__ __launch_bounds__(256) void carry_group_scan(const double* __restrict
   double st[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) st[i] = 0.0;
+#pragma unroll 8
   for (int64_t g = 0; g < ngroups; ++g) {
     const int64_t o = (g * mc + c) * kSStride;
 #pragma unroll
@@ -915,7 +997,7 @@ __global__ __launch_bounds__(256) void carry_group_apply(const double* __restric
   double st[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) st[i] = gi[i];
-#pragma unroll 4
+#pragma unroll 16
   for (int64_t j = j0; j < j1; ++j) {
     const int64_t r = REV ? nch - 1 - j : j;
     const int64_t o = (r * mc + c) * kSStride;
@@ -1326,13 +1408,15 @@ namespace gpar {
 void launch_gains(hipStream_t st, int sdim, const double* t, int64_t n, int L, int64_t nch,
                   int nchains, const ChainParamsHost* cps_dev, const double* noise,
                   double* agg, double* pstart, double* rec, double* g, double* phi,
-                  double* logs, double* pf) {
+                  double* logs, double* pf, const double* const* ys, double* alpha_loc,
+                  double* asend) {
   const ChainParams* cps = reinterpret_cast<const ChainParams*>(cps_dev);
   dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
   GPAR_DISPATCH_D(sdim, {
     gains_phase1<DD><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, agg);
     gains_phase2<DD><<<nchains, 256, 0, st>>>(nch, agg, pstart);
-    gains_phase3<DD><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, pstart, rec, g, phi, logs, pf);
+    gains_phase3<DD><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, pstart, rec, g, phi, logs, pf,
+                                           ys, alpha_loc, asend);
   });
 }
 

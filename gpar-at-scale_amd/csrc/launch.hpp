@@ -80,7 +80,8 @@ inline int rec_size(int sdim) { return sdim == 3 ? 16 : (sdim == 2 ? 8 : 4); }
 void launch_gains(hipStream_t st, int sdim, const double* t, int64_t n, int L, int64_t nch,
                   int nchains, const ChainParamsHost* cps_dev, const double* noise,
                   double* agg, double* pstart, double* rec, double* g, double* phi,
-                  double* logs, double* pf);
+                  double* logs, double* pf, const double* const* ys = nullptr,
+                  double* alpha_loc = nullptr, double* asend = nullptr);
 int dp_bucket(int d);
 void launch_whiten_kfu(hipStream_t st, int time_kind, int out_kind, const double* rec,
                        const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
