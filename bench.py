@@ -59,6 +59,9 @@ def main():
     ap.add_argument("--evals", type=int, default=None)
     ap.add_argument("--predict", default="analytic", choices=["analytic", "mc"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--separate-predict", action="store_true",
+                    help="gpar_fit then one gpar_predict per output (q(u) recomputes the Gram at the "
+                         "fitted theta) instead of gpar_fit_predict (reuses the fit's Gram there)")
     ap.add_argument("--lanes", type=int, default=1, choices=[1, 2],
                     help="HIP streams a batched objective alternates outputs over (gpar_ctx_set_lanes); "
                          "2 overlaps one output's whitening with another's Gram (+2%% throughput, but "
@@ -117,7 +120,8 @@ def main():
     for p in gpar_out:
         ycols[p] = Y_d[:, p - 1].contiguous()
         Zs[p] = torch.from_numpy(D.pseudo_inputs(Yh[:, : p - 1], M, seed=p)).to(dev)
-        pr, k = G.make_problem(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], cfg["out_kernel"], "matern52")
+        pr, k = G.make_problem(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], cfg["out_kernel"], "matern52",
+                               qu_kuu_noise=True)
         problems.append(pr)
         keep.append(k)
     y1 = Y_d[:, 0].contiguous() if 1 in mine else None
@@ -133,7 +137,14 @@ def main():
 
     def step():
         res = {}
-        if problems:
+        if problems and not args.separate_predict:
+            # get_gpar_scaled_predictions for every owned output: batched fit, then predictions
+            fr, _, _ = G.fit_predict_batch(problems, x0, ts_d, [Fs_d[:, : p - 1] for p in gpar_out],
+                                           max_evals=EV, g_tol=-1.0, mode=args.predict, samples=100,
+                                           seed=gpar_out[0], device=local)
+            for i, p in enumerate(gpar_out):
+                res[p] = fr.theta[i]
+        elif problems:
             fr = G.fit_batch(problems, x0, max_evals=EV, g_tol=-1.0, device=local)
             for i, p in enumerate(gpar_out):
                 res[p] = fr.theta[i]
@@ -146,7 +157,7 @@ def main():
                     res[p] = np.array(list(np.atleast_2d(th1)[i]) + [0.0, 0.0])
             else:
                 res[1] = np.array(list(th1) + [0.0, 0.0])
-        for i, p in enumerate(gpar_out):
+        for i, p in enumerate(gpar_out if args.separate_predict else []):
             G.predict_scaled(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], res[p], ts_d, Fs_d[:, : p - 1],
                              cfg["out_kernel"], "matern52", mode=args.predict, samples=100,
                              seed=p, device=local, qu_kuu_noise=True)

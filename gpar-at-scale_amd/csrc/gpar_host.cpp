@@ -534,9 +534,10 @@ static std::vector<Theta> thetas_from(const double* theta, int np) {
 
 // DTC objective for all problems; status_out[i] = 1 if a Cholesky failed for problem i.
 static void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<Theta>& th,
-                     double* out, std::vector<int>& status_out) {
+                     double* out, std::vector<int>& status_out, GramOut* gram_out = nullptr) {
   const int np = (int)P.size();
   GramOut go = run_gram_stage(c, P, th);
+  if (gram_out) *gram_out = go;
   DenseOut dn = run_dense(c, P, th, go, false);
   const int64_t nch = P[0].nch;
   std::vector<Finish2JobHost> fj(np);
@@ -564,12 +565,33 @@ struct QuOut {
 
 // compute_q_u (gpar_scaled_inference.jl:141-196): Cuu without noise, D = L_u^-1 G L_u^-T + I,
 // m_e = D^-1 L_u^-1 r, cov = inv(D) = L_D^-T L_D^-1, U_u = chol(Cuu).U.
-static QuOut run_q_u(gpar_ctx* c, const DevProblem& p, const Theta& th) {
+// The Gram (beta^T beta, beta^T alpha; ld = mp) of one output at one theta, kept by the fit
+// (fit_impl) for its best evaluation so that q(u) at the fitted theta need not recompute it.
+struct GramCache {
+  const double* G = nullptr;
+  const double* r = nullptr;
+};
+
+static QuOut run_q_u(gpar_ctx* c, const DevProblem& p, const Theta& th,
+                     const GramCache* gc = nullptr) {
   std::vector<DevProblem> P{p};
   std::vector<Theta> T{th};
   // The extra beta fix-up pass is for the noise-free Cuu only; with qu_kuu_noise the factor is
-  // the objective's regularised Kuu + s2 I and the objective's correction-form Gram is enough.
-  GramOut go = run_gram_stage(c, P, T, /*fix_beta=*/!p.qu_noise);
+  // the objective's regularised Kuu + s2 I and the objective's correction-form Gram is enough --
+  // the very Gram the fit computed at this theta, when the caller hands it over (gc).
+  GramOut go;
+  if (gc && gc->G && p.qu_noise) {
+    go.ldg = p.mp;
+    go.npart = 1;
+    go.G = const_cast<double*>(gc->G);
+    go.r = const_cast<double*>(gc->r);
+    go.a2part = ws<double>(c, "qu_zero_a2", 1);          // dtc terms: unused in q(u) mode
+    go.logs = ws<double>(c, "qu_zero_logs", (size_t)p.nch);
+    HIPCHECK(hipMemsetAsync(go.a2part, 0, sizeof(double), c->stream));
+    HIPCHECK(hipMemsetAsync(go.logs, 0, (size_t)p.nch * sizeof(double), c->stream));
+  } else {
+    go = run_gram_stage(c, P, T, /*fix_beta=*/!p.qu_noise);
+  }
   DenseOut dn = run_dense(c, P, T, go, /*qu_mode=*/true);
   QuOut q;
   q.ld = dn.ld;
@@ -640,7 +662,7 @@ static void chains_logpdf(gpar_ctx* c, int nchains, int64_t n, const double* t, 
 static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
                          int64_t n_star, const double* t_star_in, const double* v_star_in,
                          int64_t ldvs, int mode, int samples, uint64_t seed, double* mean_out,
-                         double* std_out) {
+                         double* std_out, const GramCache* gc = nullptr) {
   const int64_t n = P.n, m = P.m, d = P.d, mp = P.mp, mc = P.mc;
   // ---- test inputs on device, ascending (host inputs are stably sorted here, outputs
   //      un-permuted at the end; device inputs must already be ascending)
@@ -668,7 +690,7 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
     ldv_s = d;
   }
   // ---- q(u): m_e, L_u = chol(Cuu), L_D = chol(D)
-  QuOut q = run_q_u(c, P, th);
+  QuOut q = run_q_u(c, P, th, gc);
   const double* Lu = ws<double>(c, "Kuu", 1);
   const double* LD = ws<double>(c, "Lam", 1);
   const int64_t ld = q.ld;
@@ -942,20 +964,33 @@ int32_t gpar_dtc_objective(gpar_ctx* ctx, const gpar_problem* probs, int32_t npr
   API_END(ctx)
 }
 
-int32_t gpar_fit(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
-                 const double* log_theta0, const gpar_fit_options* opts, double* theta_out,
-                 double* nlml_out, int32_t* evals_out) {
-  API_BEGIN(ctx)
-  ARGCHECK(probs && nprob >= 1 && log_theta0 && theta_out, "null argument");
-  gpar_fit_options o{0, 1000, 1e-8, 0.0};
-  if (opts) o = *opts;
-  std::vector<DevProblem> P;
-  for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
+// Batched Nelder-Mead over the outputs: one objective round serves every pending point.
+// keep (optional): per output, the Gram of its lowest-value evaluation (ld = mp) in context
+// workspace, and whether that evaluation is the returned minimiser (bitwise).
+struct FitKeep {
+  std::vector<GramCache> gram;
+  std::vector<char> valid;
+};
+
+static void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P, const double* log_theta0,
+                     const gpar_fit_options& o, double* theta_out, double* nlml_out,
+                     int32_t* evals_out, FitKeep* keep) {
+  const int nprob = (int)P.size();
   std::vector<NelderMead> nm;
   nm.reserve(nprob);
   for (int i = 0; i < nprob; ++i)
     nm.emplace_back(std::vector<double>(log_theta0 + 5 * i, log_theta0 + 5 * i + 5), o.max_evals,
                     o.max_iterations, o.g_tol, o.time_limit);
+  std::vector<double> best_f(nprob, INFINITY);
+  std::vector<std::vector<double>> best_x(nprob);
+  std::vector<double*> kG(nprob, nullptr), kr(nprob, nullptr);
+  if (keep) {
+    for (int i = 0; i < nprob; ++i) {
+      const size_t mp = (size_t)P[i].mp;
+      kG[i] = ws<double>(ctx, "fitkeep_G" + std::to_string(i), mp * mp);
+      kr[i] = ws<double>(ctx, "fitkeep_r" + std::to_string(i), mp);
+    }
+  }
   std::vector<double> vals;
   while (true) {
     std::vector<int> act;
@@ -971,11 +1006,23 @@ int32_t gpar_fit(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
     }
     vals.assign(act.size(), 0.0);
     std::vector<int> st;
-    eval_dtc(ctx, sub, th, vals.data(), st);
+    GramOut go;
+    eval_dtc(ctx, sub, th, vals.data(), st, keep ? &go : nullptr);
     for (size_t a = 0; a < act.size(); ++a) {
       double f = -vals[a];
       if (st[a] || !std::isfinite(f)) f = INFINITY;  // PosDefException -> reject the point
-      nm[act[a]].tell(f);
+      const int i = act[a];
+      if (keep && f < best_f[i]) {   // this round's G / r of output i, before the next round
+        best_f[i] = f;
+        best_x[i] = nm[i].ask();
+        const size_t mp = (size_t)P[i].mp;
+        HIPCHECK(hipMemcpy2DAsync(kG[i], mp * sizeof(double), go.G + a * go.ldg * go.ldg,
+                                  go.ldg * sizeof(double), mp * sizeof(double), mp,
+                                  hipMemcpyDeviceToDevice, ctx->stream));
+        HIPCHECK(hipMemcpyAsync(kr[i], go.r + a * go.ldg, mp * sizeof(double),
+                                hipMemcpyDeviceToDevice, ctx->stream));
+      }
+      nm[i].tell(f);
     }
   }
   for (int i = 0; i < nprob; ++i) {
@@ -983,6 +1030,60 @@ int32_t gpar_fit(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
     for (int j = 0; j < 5; ++j) theta_out[5 * i + j] = unpack(x[j]);
     if (nlml_out) nlml_out[i] = nm[i].f_min();
     if (evals_out) evals_out[i] = nm[i].evals();
+  }
+  if (keep) {
+    keep->gram.assign(nprob, GramCache{});
+    keep->valid.assign(nprob, 0);
+    for (int i = 0; i < nprob; ++i) {
+      keep->valid[i] = !best_x[i].empty() && best_x[i] == nm[i].x_min();
+      if (keep->valid[i]) keep->gram[i] = GramCache{kG[i], kr[i]};
+    }
+  }
+}
+
+int32_t gpar_fit(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                 const double* log_theta0, const gpar_fit_options* opts, double* theta_out,
+                 double* nlml_out, int32_t* evals_out) {
+  API_BEGIN(ctx)
+  ARGCHECK(probs && nprob >= 1 && log_theta0 && theta_out, "null argument");
+  gpar_fit_options o{0, 1000, 1e-8, 0.0};
+  if (opts) o = *opts;
+  std::vector<DevProblem> P;
+  for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
+  fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, nullptr);
+  API_END(ctx)
+}
+
+int32_t gpar_fit_predict(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                         const double* log_theta0, const gpar_fit_options* opts, int64_t n_star,
+                         const double* t_star, const double* const* v_star, const int64_t* ldvs,
+                         int32_t mode, int32_t samples, uint64_t seed, double* theta_out,
+                         double* nlml_out, int32_t* evals_out, double* const* mean_out,
+                         double* const* std_out) {
+  API_BEGIN(ctx)
+  ARGCHECK(probs && nprob >= 1 && log_theta0 && theta_out && t_star && v_star && ldvs &&
+               mean_out && std_out, "null argument");
+  ARGCHECK(n_star >= 1, "n_star must be >= 1");
+  ARGCHECK(mode == GPAR_PREDICT_ANALYTIC || mode == GPAR_PREDICT_MC, "bad mode");
+  if (mode == GPAR_PREDICT_MC)
+    ARGCHECK(samples >= 2 && samples <= 128, "MC mode supports 2..128 samples");
+  for (int i = 0; i < nprob; ++i) {
+    ARGCHECK(v_star[i] && mean_out[i] && std_out[i], "null per-output pointer");
+    ARGCHECK(ldvs[i] >= probs[i].d, "ldvs must be >= d");
+    ARGCHECK(probs[i].mem == probs[0].mem, "all outputs must share one memory space");
+  }
+  gpar_fit_options o{0, 1000, 1e-8, 0.0};
+  if (opts) o = *opts;
+  std::vector<DevProblem> P;
+  for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
+  FitKeep keep;
+  fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, &keep);
+  for (int i = 0; i < nprob; ++i) {
+    const double* q = theta_out + 5 * i;
+    const Theta th{q[0], q[1], q[2], q[3], q[4]};
+    predict_impl(ctx, P[i], th, probs[i].mem, n_star, t_star, v_star[i], ldvs[i], mode, samples,
+                 seed + (uint64_t)i, mean_out[i], std_out[i],
+                 keep.valid[i] ? &keep.gram[i] : nullptr);
   }
   API_END(ctx)
 }

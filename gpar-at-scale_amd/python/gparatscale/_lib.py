@@ -24,7 +24,7 @@ KERNEL_ID = {"matern12": 0, "matern32": 1, "matern52": 2, "eq": 3}
 EXPORTED = (
     "gpar_abi_version", "gpar_ctx_create", "gpar_ctx_destroy", "gpar_last_error",
     "gpar_ctx_workspace_bytes", "gpar_ctx_trim", "gpar_dtc_objective", "gpar_dtc_objective_A",
-    "gpar_fit", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
+    "gpar_fit", "gpar_fit_predict", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
     "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_reset_stats",
     "gpar_ctx_set_lanes", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
@@ -98,6 +98,8 @@ def load(path: str | None = None):
             "gpar_dtc_objective_A": (i32, [vp, C.POINTER(GparProblem), dp, dp, dp]),
             "gpar_fit": (i32, [vp, C.POINTER(GparProblem), i32, dp, C.POINTER(GparFitOptions),
                                dp, dp, dp]),
+            "gpar_fit_predict": (i32, [vp, C.POINTER(GparProblem), i32, dp, C.POINTER(GparFitOptions),
+                                       i64, vp, vp, vp, i32, i32, C.c_uint64, dp, dp, dp, vp, vp]),
             "gpar_q_u": (i32, [vp, C.POINTER(GparProblem), dp, dp, dp, dp]),
             "gpar_predict": (i32, [vp, C.POINTER(GparProblem), dp, i64, dp, dp, i64, i32, i32,
                                    C.c_uint64, dp, dp]),

@@ -209,6 +209,61 @@ def fit_batch(problems, log_theta0, max_evals=0, max_iterations=1000, g_tol=1e-8
     return FitResult(theta, nlml, evals)
 
 
+def fit_predict_batch(problems, log_theta0, t_star, V_stars, max_evals=0, max_iterations=1000,
+                      g_tol=1e-8, time_limit=0.0, mode="analytic", samples=100, seed=0, device=0,
+                      keep=None):
+    """get_gpar_scaled_predictions (gpar_scaled_inference.jl:20-136) for a batch of outputs
+    (gpar_fit_predict): the batched fit, then each output's prediction at its fitted theta,
+    reusing the fit's Gram at that theta for q(u) when the problem has qu_kuu_noise.
+
+    Device problems (make_problem on torch tensors): t_star a device vector, V_stars[i] output
+    i's test inputs (N* x D_i tensor, rows = points); returns (FitResult, means, stds) with
+    means/stds lists of device tensors.  Host problems: numpy t_star and D_i x N* ColVecs."""
+    ctx = context(device)
+    lib = _lib.load()
+    P = len(problems)
+    keep = keep if keep is not None else _Keep()
+    arr = (GparProblem * P)(*problems)
+    x0 = np.ascontiguousarray(np.asarray(log_theta0, dtype=np.float64).reshape(P, 5))
+    opts = GparFitOptions(int(max_evals), int(max_iterations), float(g_tol), float(time_limit))
+    theta = np.zeros((P, 5))
+    nlml = np.zeros(P)
+    evals = np.zeros(P, dtype=np.int32)
+    dev = problems[0].mem == _lib.GPAR_MEM_DEVICE
+    vptr, ldvs, means, stds = [], [], [], []
+    if dev:
+        import torch
+        tsp = _dev_vec(t_star, keep)
+        for Vs in V_stars:
+            p_, ld_, ns, _ = _dev_points(Vs, keep)
+            vptr.append(p_)
+            ldvs.append(ld_)
+            means.append(torch.empty(ns, dtype=torch.float64, device=t_star.device))
+            stds.append(torch.empty(ns, dtype=torch.float64, device=t_star.device))
+        mp_ = [m.data_ptr() for m in means]
+        sp_ = [x.data_ptr() for x in stds]
+    else:
+        tsp = _host_vec(t_star, keep)
+        for Vs in V_stars:
+            p_, ld_, ns, _ = _host_points(Vs, keep)
+            vptr.append(p_)
+            ldvs.append(ld_)
+            means.append(np.zeros(ns))
+            stds.append(np.zeros(ns))
+        mp_ = [m.ctypes.data for m in means]
+        sp_ = [x.ctypes.data for x in stds]
+    ns = len(t_star)
+    VP = (C.c_void_p * P)(*vptr)
+    LD = (C.c_int64 * P)(*ldvs)
+    MP = (C.c_void_p * P)(*mp_)
+    SP = (C.c_void_p * P)(*sp_)
+    md = _lib.GPAR_PREDICT_MC if mode == "mc" else _lib.GPAR_PREDICT_ANALYTIC
+    ctx.check(lib.gpar_fit_predict(ctx.h, arr, P, _ptr(x0), C.byref(opts), ns, tsp, VP, LD, md,
+                                   int(samples), int(seed), _ptr(theta), _ptr(nlml), _ptr(evals),
+                                   MP, SP))
+    return FitResult(theta, nlml, evals), means, stds
+
+
 def get_optim_scaled_gpar_params(input_locations, pseudo_input_locations, time_loc, outputs,
                                  out_kernel="matern52", time_kernel="matern52",
                                  i_log_time_l=None, i_log_time_var=None, i_log_out_l=None,

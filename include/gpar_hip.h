@@ -156,6 +156,23 @@ int32_t gpar_predict(gpar_ctx* ctx, const gpar_problem* prob, const double* thet
                      int64_t n_star, const double* t_star, const double* v_star, int64_t ldvs,
                      int32_t mode, int32_t samples, uint64_t seed, double* mean, double* std);
 
+/* ---------------------------------------------------------------- fit + predict
+ * Replaces get_gpar_scaled_predictions (src/gp/gpar_scaled_inference.jl:20-136) -- the fit of
+ * get_optim_scaled_gpar_params, then q(u) and the prediction at the fitted theta -- for `nprob`
+ * outputs at once: the batched fit of gpar_fit, then per output exactly gpar_predict at its
+ * fitted theta (theta_out row i).  With probs[i].qu_kuu_noise = 1, q(u)'s Gram at the fitted
+ * theta is the one the fit already computed there (same kernels, same inputs: bit-identical), so
+ * it is reused instead of recomputed; otherwise q(u) recomputes it.  Test inputs: t_star [n_star]
+ * shared, output i's at v_star[i] (point k dim j at v_star[i][k*ldvs[i] + j]); mean_out[i],
+ * std_out[i] [n_star]; all in probs[i].mem (one memory space for all outputs).  MC mode draws
+ * output i with seed + i. */
+int32_t gpar_fit_predict(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                         const double* log_theta0, const gpar_fit_options* opts, int64_t n_star,
+                         const double* t_star, const double* const* v_star, const int64_t* ldvs,
+                         int32_t mode, int32_t samples, uint64_t seed, double* theta_out,
+                         double* nlml_out, int32_t* evals_out, double* const* mean_out,
+                         double* const* std_out);
+
 /* ---------------------------------------------------------------- temporal-only (LGSSM) chains
  * `nchains` independent chains sharing the time grid t [n] (ascending); chain c's
  * observations at y[c*ldy + k].  theta: nchains x 3 natural (l, process_var, noise_sigma)

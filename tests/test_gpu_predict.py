@@ -101,3 +101,37 @@ def test_sde_predictions_match_oracle():
     np.testing.assert_allclose(th, th_ref, rtol=1e-6)
     np.testing.assert_allclose(m, m_ref, rtol=1e-6, atol=1e-8)
     np.testing.assert_allclose(v, v_ref, rtol=1e-6, atol=1e-10)
+
+
+@pytest.mark.parametrize("qu_noise", [True, False])
+def test_fit_predict_equals_fit_then_predict(qu_noise):
+    """gpar_fit_predict (get_gpar_scaled_predictions, gpar_scaled_inference.jl:20-136, batched
+    over outputs) == gpar_fit followed by one gpar_predict per output at the fitted theta --
+    bit for bit: with qu_kuu_noise q(u) reuses the fit's Gram at that theta, which is the same
+    computation it would redo; without, q(u) recomputes it."""
+    import torch
+    dev = torch.device("cuda", 0)
+    t, Y = O.synthetic_gpar(900, 5, seed=23, noise=0.3)
+    rng = np.random.default_rng(4)
+    ts = np.sort(rng.uniform(t[0], t[-1], 200))
+    Fs = np.column_stack([np.interp(ts, t, Y[:, q]) for q in range(5)])
+    t_d, Y_d = torch.from_numpy(t).to(dev), torch.from_numpy(Y).to(dev)
+    ts_d, Fs_d = torch.from_numpy(ts).to(dev), torch.from_numpy(Fs).to(dev)
+    outs = [2, 4, 5]
+    probs, keep, Zs = [], [], {}
+    for p in outs:
+        Zs[p] = torch.from_numpy(O.pick_pseudo_inputs(Y[:, : p - 1].T, 70, p).T.copy()).to(dev)
+        pr, k = G.make_problem(Y_d[:, : p - 1], Zs[p], t_d, Y_d[:, p - 1].contiguous(),
+                               qu_kuu_noise=qu_noise)
+        probs.append(pr)
+        keep.append(k)
+    x0 = np.tile([0.0, 0.0, 0.0, 0.0, -2.0], (len(outs), 1))
+    fr, means, stds = G.fit_predict_batch(probs, x0, ts_d, [Fs_d[:, : p - 1] for p in outs],
+                                          max_evals=30, g_tol=-1.0)
+    fr2 = G.fit_batch(probs, x0, max_evals=30, g_tol=-1.0)
+    np.testing.assert_array_equal(fr.theta, fr2.theta)
+    for i, p in enumerate(outs):
+        m2, s2 = G.predict_scaled(Y_d[:, : p - 1], Zs[p], t_d, Y_d[:, p - 1].contiguous(),
+                                  fr.theta[i], ts_d, Fs_d[:, : p - 1], qu_kuu_noise=qu_noise)
+        np.testing.assert_array_equal(means[i].cpu().numpy(), m2.cpu().numpy())
+        np.testing.assert_array_equal(stds[i].cpu().numpy(), s2.cpu().numpy())
