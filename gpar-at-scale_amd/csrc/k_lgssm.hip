@@ -661,7 +661,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
 #pragma unroll
       for (int ct = 0; ct < 4; ++ct) {
         double d2 = vn + zn[ct] - 2.0 * acc[ct][r];
-        d2 = d2 > 0.0 ? d2 : 0.0;
+        if constexpr (OK == KEQ) d2 = d2 > 0.0 ? d2 : 0.0;   // the Matern forms clamp in sqrt_pos
 #if WHITEN_ABL != 1
         xt[wave][fq + 4 * r][ct * 16 + fr] = skappa_sq<OK>(d2, inv_lo, s_o);
 #else
