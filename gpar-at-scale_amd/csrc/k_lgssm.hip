@@ -891,26 +891,65 @@ __device__ __forceinline__ void carry_step(const double* __restrict__ ph, int64_
   for (int i = 0; i < D; ++i) st[i] = nx[i];
 }
 
+// The group's chunk transitions, staged once per block into LDS (uniform across the block's
+// columns): read from memory inside the sequential loop they were scalar loads, each waited on.
+constexpr int kMaxCarryGS = 128;   // carry_group_size caps the group length here
+template <int D, bool REV>
+__device__ __forceinline__ void stage_phi(const double* __restrict__ ph, int64_t nch, int64_t j0,
+                                          int64_t j1, double* __restrict__ lph) {
+  const int cnt = (int)(j1 - j0) * D * D;
+  for (int e = threadIdx.x; e < cnt; e += blockDim.x) {
+    const int64_t jj = j0 + e / (D * D);
+    const int64_t r = REV ? nch - 1 - jj : jj;
+    lph[e] = ph[r * D * D + e % (D * D)];
+  }
+  __syncthreads();
+}
+
 template <int D, bool REV>
 __global__ __launch_bounds__(256) void carry_group_local(const double* __restrict__ phi, int64_t phistride,
                                                          const double* __restrict__ send, int64_t sstride,
                                                          int64_t nch, int64_t mc, int64_t ncols, int GS,
-                                                         double* __restrict__ gend, int64_t gstride_) {
-  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+                                                         double* __restrict__ gend, int64_t gstride_,
+                                                         double* __restrict__ psi, int64_t psistride) {
+  __shared__ double lph[kMaxCarryGS * D * D];
   const int64_t gidx = blockIdx.y;
   const int b = blockIdx.z;
-  if (c >= ncols) return;
   const double* ph = phi + (int64_t)b * phistride;
   const double* sp = send + (int64_t)b * sstride;
   const int64_t j0 = gidx * GS;
   const int64_t j1 = (j0 + GS < nch) ? j0 + GS : nch;
+  stage_phi<D, REV>(ph, nch, j0, j1, lph);
+  if (blockIdx.x == gridDim.x - 1) {   // the extra column block: the group's Psi = prod Phi_j
+    if (threadIdx.x == 0) {
+      double P[D][D], X[D][D], F[D][D];
+      mat_eye(P);
+      for (int64_t j = j0; j < j1; ++j) {
+        const double* f = lph + (j - j0) * D * D;
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+          for (int q = 0; q < D; ++q) F[i][q] = REV ? f[q * D + i] : f[i * D + q];
+        mat_mul(F, P, X);
+        mat_copy(X, P);
+      }
+      double* pp = psi + (int64_t)b * psistride + gidx * D * D;
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) pp[i * D + q] = P[i][q];
+    }
+    return;
+  }
+  const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  if (c >= ncols) return;
   double st[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) st[i] = 0.0;
 #pragma unroll 16
   for (int64_t j = j0; j < j1; ++j) {
     const int64_t r = REV ? nch - 1 - j : j;
-    carry_step<D, REV>(ph, r, sp + (r * mc + c) * kSStride, st);
+    carry_step<D, REV>(lph + (j - j0) * D * D, 0, sp + (r * mc + c) * kSStride, st);
   }
   double* ge = gend + (int64_t)b * gstride_ + (gidx * mc + c) * kSStride;
 #pragma unroll
@@ -984,16 +1023,18 @@ __global__ __launch_bounds__(256) void carry_group_apply(const double* __restric
                                                          double* __restrict__ cin, int64_t sstride,
                                                          const double* __restrict__ gin, int64_t gstride_,
                                                          int64_t nch, int64_t mc, int64_t ncols, int GS) {
+  __shared__ double lph[kMaxCarryGS * D * D];
   const int64_t c = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
   const int64_t gidx = blockIdx.y;
   const int b = blockIdx.z;
-  if (c >= ncols) return;
   const double* ph = phi + (int64_t)b * phistride;
   const double* sp = send + (int64_t)b * sstride;
   double* cp = cin + (int64_t)b * sstride;
-  const double* gi = gin + (int64_t)b * gstride_ + (gidx * mc + c) * kSStride;
   const int64_t j0 = gidx * GS;
   const int64_t j1 = (j0 + GS < nch) ? j0 + GS : nch;
+  stage_phi<D, REV>(ph, nch, j0, j1, lph);
+  if (c >= ncols) return;
+  const double* gi = gin + (int64_t)b * gstride_ + (gidx * mc + c) * kSStride;
   double st[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) st[i] = gi[i];
@@ -1003,7 +1044,7 @@ __global__ __launch_bounds__(256) void carry_group_apply(const double* __restric
     const int64_t o = (r * mc + c) * kSStride;
 #pragma unroll
     for (int i = 0; i < D; ++i) cp[o + i] = st[i];
-    carry_step<D, REV>(ph, r, sp + o, st);
+    carry_step<D, REV>(lph + (j - j0) * D * D, 0, sp + o, st);
   }
 }
 
@@ -1537,7 +1578,7 @@ void launch_whiten_vec(hipStream_t st, int sdim, const double* rec, int64_t recs
 
 int carry_group_size(int64_t nch) {
   int gs = 1;
-  while ((int64_t)gs * gs < nch) ++gs;
+  while ((int64_t)gs * gs < nch && gs < kMaxCarryGS) ++gs;
   return gs;
 }
 
@@ -1549,12 +1590,11 @@ void launch_carry(hipStream_t st, int sdim, const double* phi, int64_t phistride
   const int64_t gstride_ = ng * mc * kSStride;
   const int64_t psistride = ng * sdim * sdim;
   dim3 g3((unsigned)((ncols + 255) / 256), (unsigned)ng, (unsigned)nchains);
-  dim3 gp((unsigned)((ng + 255) / 256), (unsigned)nchains);
+  dim3 g3p((unsigned)((ncols + 255) / 256 + 1), (unsigned)ng, (unsigned)nchains);   // + Psi block
   dim3 gc((unsigned)((ncols + 255) / 256), (unsigned)nchains);
 #define GPAR_CARRY_LAUNCH(RV)                                                                       \
   GPAR_DISPATCH_D(sdim, {                                                                          \
-    carry_group_local<DD, RV><<<g3, 256, 0, st>>>(phi, phistride, send, sstride, nch, mc, ncols, GS, gend, gstride_); \
-    carry_group_phi<DD, RV><<<gp, 256, 0, st>>>(phi, phistride, nch, GS, ng, psi, psistride);      \
+    carry_group_local<DD, RV><<<g3p, 256, 0, st>>>(phi, phistride, send, sstride, nch, mc, ncols, GS, gend, gstride_, psi, psistride); \
     carry_group_scan<DD><<<gc, 256, 0, st>>>(psi, psistride, gend, gin, gstride_, ng, mc, ncols);   \
     carry_group_apply<DD, RV><<<g3, 256, 0, st>>>(phi, phistride, send, cin, sstride, gin, gstride_, nch, mc, ncols, GS); \
   })
