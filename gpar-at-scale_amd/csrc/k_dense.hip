@@ -166,53 +166,67 @@ __global__ __launch_bounds__(256) void chol_kernel(const CholJob* __restrict__ j
 }
 
 // ---------------------------------------------------------------------------- TRSM
-// X = L^{-1} B (or L^{-1} B^T), 64 right-hand-side columns per workgroup, one 16-column
-// tile per wave; blocked forward substitution with the off-diagonal updates on MFMA.
+// X = L^{-1} B (or L^{-1} B^T): one 16-column right-hand-side tile per workgroup of 4 waves.
+// Row blocks of 16 are solved in order.  Block ib's update  B_ib - sum_{kb < ib} L_{ib,kb} X_kb
+// is split over the 4 waves by kb mod 4 (v_mfma_f64_16x16x4, operands from L2), the 4 partial
+// tiles are summed through LDS, and 16 lanes run the 16-row substitution against the diagonal
+// block staged in LDS.  (The earlier form had one wave walk every kb of a tile: a 4x longer
+// dependent chain, with 4x fewer workgroups.)
 __global__ __launch_bounds__(256) void trsm_kernel(const TrsmJob* __restrict__ jobs) {
   const TrsmJob jb = jobs[blockIdx.y];
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t c0 = (int64_t)blockIdx.x * 64 + wave * 16;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int64_t c0 = (int64_t)blockIdx.x * 16;
+  if (c0 >= jb.ncols) return;
   const int m = jb.m;
-  __shared__ double T[4][16][17];
+  __shared__ double part[4][16][17];
+  __shared__ double Ld[16][17];
   const int nblk = (m + 15) / 16;
+  const int fr = lane & 15, fq = lane >> 4;
+  const int64_t colf = c0 + fr;                    // this lane's fragment column
+  const bool colv = colf < jb.ncols;
   for (int ib = 0; ib < nblk; ++ib) {
     const int r0 = ib * 16;
-    d4 acc;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int row = r0 + (lane >> 4) + 4 * r;
-      const int64_t col = c0 + (lane & 15);
-      double v = 0.0;
-      if (row < m && col < jb.ncols)
-        v = jb.transB ? jb.B[col * jb.ldb + row] : jb.B[(int64_t)row * jb.ldb + col];
-      acc[r] = v;
+    {
+      const int i = tid >> 4, j = tid & 15;
+      Ld[i][j] = (r0 + i < m && r0 + j < m && j <= i) ? jb.L[(int64_t)(r0 + i) * jb.ldl + r0 + j] : 0.0;
     }
-    for (int kb = 0; kb < ib; ++kb) {
+    d4 acc = {0.0, 0.0, 0.0, 0.0};
+    if (wave == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = r0 + fq + 4 * r;
+        double v = 0.0;
+        if (row < m && colv)
+          v = jb.transB ? jb.B[colf * jb.ldb + row] : jb.B[(int64_t)row * jb.ldb + colf];
+        acc[r] = v;
+      }
+    }
+    const int ra = r0 + fr;
+    const bool rav = ra < m;
+#pragma unroll 2
+    for (int kb = wave; kb < ib; kb += 4) {
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const int kk = kb * 16 + ks * 4 + (lane >> 4);
-        const int ra = r0 + (lane & 15);
-        const int64_t col = c0 + (lane & 15);
-        const double fa = (ra < m) ? -jb.L[(int64_t)ra * jb.ldl + kk] : 0.0;
-        const double fb = (col < jb.ncols)
-                              ? (jb.transX ? jb.X[col * jb.ldx + kk] : jb.X[(int64_t)kk * jb.ldx + col])
-                              : 0.0;
+        const int kk = kb * 16 + ks * 4 + fq;
+        const double fa = rav ? -jb.L[(int64_t)ra * jb.ldl + kk] : 0.0;
+        const double fb = colv ? (jb.transX ? jb.X[colf * jb.ldx + kk] : jb.X[(int64_t)kk * jb.ldx + colf])
+                               : 0.0;
         acc = __builtin_amdgcn_mfma_f64_16x16x4f64(fa, fb, acc, 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) T[wave][(lane >> 4) + 4 * r][lane & 15] = acc[r];
+    for (int r = 0; r < 4; ++r) part[wave][fq + 4 * r][fr] = acc[r];
     __syncthreads();
-    if (lane < 16) {
+    if (wave == 0 && lane < 16) {
       const int64_t col = c0 + lane;
       double x[16];
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
         if (r0 + i < m) {
-          double s = T[wave][i][lane];
+          double s = ((part[0][i][lane] + part[1][i][lane]) + part[2][i][lane]) + part[3][i][lane];
 #pragma unroll
-          for (int p = 0; p < i; ++p) s -= jb.L[(int64_t)(r0 + i) * jb.ldl + r0 + p] * x[p];
-          x[i] = s / jb.L[(int64_t)(r0 + i) * jb.ldl + r0 + i];
+          for (int q = 0; q < i; ++q) s = fma(-Ld[i][q], x[q], s);
+          x[i] = s / Ld[i][i];
         } else {
           x[i] = 0.0;
         }
@@ -382,7 +396,7 @@ void launch_chol(hipStream_t st, const CholJobHost* jobs_dev, int njobs) {
 }
 
 void launch_trsm(hipStream_t st, const TrsmJobHost* jobs_dev, int njobs, int64_t ncols_max) {
-  dim3 grid((unsigned)((ncols_max + 63) / 64), njobs);
+  dim3 grid((unsigned)((ncols_max + 15) / 16), njobs);
   trsm_kernel<<<grid, 256, 0, st>>>(reinterpret_cast<const TrsmJob*>(jobs_dev));
 }
 
