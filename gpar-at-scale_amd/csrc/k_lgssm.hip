@@ -116,7 +116,7 @@ __device__ __forceinline__ void step_model(const double* __restrict__ t, int64_t
 // consumed in the same step is waited on at once, and on gfx9 vmcnt also counts every store the
 // thread issued before it, so each step would stall for a full memory round trip.  The loop
 // stays rolled (an unrolled block of steps doubles the VGPRs of these 3x3 recursions).
-constexpr int kStepPF = 3;
+constexpr int kStepPF = 2;
 struct StepPipe {
   double t[kStepPF], r[kStepPF], y[kStepPF];
   const double *tp, *np, *yp;
@@ -297,7 +297,7 @@ __global__ __launch_bounds__(256) void gains_phase2(int64_t nch, const double* _
 // in the same pass, with the record still in registers (what whiten_vec would do in a second pass
 // over rec): alpha_loc[p * n + k] and the chunk end state asend[(p * nch + j) * 4 + i].
 template <int D>
-__global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t, int64_t n,
+__global__ __launch_bounds__(256, 2) void gains_phase3(const double* __restrict__ t, int64_t n,
                                                     int L, int64_t nch,
                                                     const ChainParams* __restrict__ cps,
                                                     const double* __restrict__ noise,
@@ -311,14 +311,25 @@ __global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t
                                                     double* __restrict__ alpha_loc,
                                                     double* __restrict__ asend) {
   constexpr int RS = Rec<D>::size;
+  // Output staging: thread = chunk, so a plain per-thread store of step s's record writes 64
+  // lines 32 KB apart per instruction (measured: the stores were 5.6 of the 6.9 ms of a
+  // 63-chain launch).  Each wave parks its 64 records (and the g rows) in LDS and writes them
+  // back 16 bytes per lane, RS/2 lanes per record; the alpha values are parked 16 steps at a
+  // time and written back as whole 128-byte lines the same way.
+  constexpr int RP = RS + 1;
+  constexpr int AS = 16;        // alpha steps per flush
+  __shared__ double rbuf[4][64 * RP];
+  __shared__ double abuf[4][64 * (AS + 1)];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t jw = j - lane;  // the wave's first chunk
   const int p = blockIdx.y;
-  if (j >= nch) return;
+  const bool jv = j < nch;
   const ChainParams cp = cps[p];
-  const int64_t k0 = j * L;
+  const int64_t k0 = (jv ? j : nch - 1) * L;
   const int64_t k1 = (k0 + L < n) ? k0 + L : n;
   double P[D][D];
-  if (j == 0) {
+  if (j == 0 || !jv) {
     sde_pinf<D>(cp.s, P);
   } else {
     const double* ps = pstart + ((int64_t)p * nch + j) * (D * D);
@@ -338,10 +349,15 @@ __global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t
   double* rp = rec + (int64_t)p * n * RS;
   double* gp = g + (int64_t)p * n * kGStride;
   double* pfp = pf ? pf + (int64_t)p * n * (D * D) : nullptr;
+  double* rb = rbuf[wave];
+  double* ab = abuf[wave];
   double tprev = k0 > 0 ? t[k0 - 1] : 0.0;
   StepPipe spp;
   spp.init(t, noise, yp, k0, k1);
-  for (int64_t k = k0; k < k1; ++k) {
+  // every lane runs all L steps (the wave writes cooperatively); past k1 nothing is committed
+  for (int sidx = 0; sidx < L; ++sidx) {
+    const int64_t k = k0 + sidx;
+    const bool live = jv && k < k1;
     double tk, rk, yk;
     spp.next(k, tk, rk, yk);
     double A[D][D], Q[D][D], X[D][D], Pm[D][D];
@@ -359,29 +375,33 @@ __global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t
     double Kg[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) Kg[i] = Pm[i][0] / S;
-#pragma unroll
-    for (int i = 0; i < D; ++i)
-#pragma unroll
-      for (int q = 0; q < D; ++q) P[i][q] = Pm[i][q] - Kg[i] * Pm[0][q];
-    double* r = rp + k * RS;
-#pragma unroll
-    for (int i = 0; i < D; ++i)
-#pragma unroll
-      for (int q = 0; q < D; ++q) r[i * D + q] = A[i][q];
-#pragma unroll
-    for (int i = 0; i < D; ++i) r[D * D + i] = Kg[i];
-    r[D * D + D] = rs;
-    // g_k = -rs (A Phi)[0, :]
     double AP[D][D];
     mat_mul(A, Phi, AP);
-#pragma unroll
-    for (int q = 0; q < D; ++q) gp[k * kGStride + q] = -rs * AP[0][q];
-    // Phi <- (I - K e1^T) A Phi
+    // park the record {A, K, rs, pad} and g_k = -rs (A Phi)[0, :]
 #pragma unroll
     for (int i = 0; i < D; ++i)
 #pragma unroll
-      for (int q = 0; q < D; ++q) Phi[i][q] = AP[i][q] - Kg[i] * AP[0][q];
-    lsum += log(S);
+      for (int q = 0; q < D; ++q) rb[lane * RP + i * D + q] = A[i][q];
+#pragma unroll
+    for (int i = 0; i < D; ++i) rb[lane * RP + D * D + i] = Kg[i];
+    rb[lane * RP + D * D + D] = rs;
+#pragma unroll
+    for (int e = D * D + D + 1; e < RS; ++e) rb[lane * RP + e] = 0.0;
+    double gk[kGStride];
+#pragma unroll
+    for (int q = 0; q < kGStride; ++q) gk[q] = q < D ? -rs * AP[0][q] : 0.0;
+    if (live) {
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) P[i][q] = Pm[i][q] - Kg[i] * Pm[0][q];
+      // Phi <- (I - K e1^T) A Phi
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) Phi[i][q] = AP[i][q] - Kg[i] * AP[0][q];
+      lsum += log(S);
+    }
     if (yp) {   // alpha filter from zero (same arithmetic as whiten_kfu's column recursion)
       double mm[D];
 #pragma unroll
@@ -392,17 +412,81 @@ __global__ __launch_bounds__(256) void gains_phase3(const double* __restrict__ t
         mm[i] = a2;
       }
       const double ev = yk - mm[0];
-      ap[k] = ev * rs;
+      ab[lane * (AS + 1) + (sidx % AS)] = ev * rs;
+      if (live) {
 #pragma unroll
-      for (int i = 0; i < D; ++i) ma[i] = fma(Kg[i], ev, mm[i]);
+        for (int i = 0; i < D; ++i) ma[i] = fma(Kg[i], ev, mm[i]);
+      }
     }
-    if (pfp) {
+    if (pfp && live) {
 #pragma unroll
       for (int i = 0; i < D; ++i)
 #pragma unroll
         for (int q = 0; q < D; ++q) pfp[k * D * D + i * D + q] = P[i][q];
     }
+    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's parked values landed
+    __builtin_amdgcn_wave_barrier();
+    // write back: lane -> (record rr = e / (RS/2), 16-byte piece e % (RS/2))
+#pragma unroll
+    for (int it = 0; it < RS / 2; ++it) {
+      const int e = it * 64 + lane;
+      const int rr = e / (RS / 2), pc = e % (RS / 2);
+      const int64_t jr = jw + rr;
+      const int64_t kr = jr * L + sidx;
+      if (jr < nch && kr < n) {
+        double2 v;
+        v.x = rb[rr * RP + 2 * pc];
+        v.y = rb[rr * RP + 2 * pc + 1];
+        *reinterpret_cast<double2*>(rp + kr * RS + 2 * pc) = v;
+      }
+    }
+    // g rows: two 16-byte pieces per step, straight from registers through a lane exchange
+    {
+#pragma unroll
+      for (int q = 0; q < kGStride; ++q) rb[lane * RP + q] = gk[q];
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int e = it * 64 + lane;
+        const int rr = e >> 1, pc = e & 1;
+        const int64_t jr = jw + rr;
+        const int64_t kr = jr * L + sidx;
+        if (jr < nch && kr < n) {
+          double2 v;
+          v.x = rb[rr * RP + 2 * pc];
+          v.y = rb[rr * RP + 2 * pc + 1];
+          *reinterpret_cast<double2*>(gp + kr * kGStride + 2 * pc) = v;
+        }
+      }
+      __builtin_amdgcn_wave_barrier();   // rb is rewritten by the next step
+    }
+    if (yp && (sidx % AS == AS - 1 || sidx == L - 1)) {
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+      const int s0 = sidx - (sidx % AS);
+#pragma unroll
+      for (int it = 0; it < AS / 2; ++it) {
+        const int e = it * 64 + lane;
+        const int rr = e / (AS / 2), pc = e % (AS / 2);
+        const int64_t jr = jw + rr;
+        const int64_t kr = jr * L + s0 + 2 * pc;
+        const int64_t kend = (jr * L + L < n) ? jr * L + L : n;
+        if (jr < nch && kr < kend) {
+          if (kr + 1 < kend) {
+            double2 v;
+            v.x = ab[rr * (AS + 1) + 2 * pc];
+            v.y = ab[rr * (AS + 1) + 2 * pc + 1];
+            *reinterpret_cast<double2*>(ap + kr) = v;
+          } else {
+            ap[kr] = ab[rr * (AS + 1) + 2 * pc];
+          }
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
   }
+  if (!jv) return;
   double* ph = phi + ((int64_t)p * nch + j) * (D * D);
 #pragma unroll
   for (int i = 0; i < D; ++i)
