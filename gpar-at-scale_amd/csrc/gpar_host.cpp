@@ -740,7 +740,9 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
   run_carry(c, P.sdim, g.phi, 0, send, cin, 0, nch, mc, mc, 1, "predf");
   // ---- adjoint: Sigma^{-1} x = W^T (W x)
   launch_gains_adjoint(c->stream, P.sdim, g.rec, nt, kChunk, nch, 1, h);
-  launch_adjoint_local(c->stream, P.sdim, X, ldx, mc, g.rec, g.g, cin, mc, nt, kChunk, nch, bend);
+  // u is read back only at the test rows (predict_rows), where rm = 1e10
+  launch_adjoint_local_wide(c->stream, P.sdim, X, ldx, mc, g.rec, g.g, cin, mc, nt, kChunk, nch,
+                            bend, rm);
   check_launch("predict: adjoint");
   run_carry(c, P.sdim, g.phi, 0, bend, chat, 0, nch, mc, mc, 1, "predb", /*rev=*/true);
   // ---- per test row: Q = R Sigma^{-1} Cf*u, mean

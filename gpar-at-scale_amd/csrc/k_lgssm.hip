@@ -1241,6 +1241,70 @@ __global__ __launch_bounds__(64) void adjoint_local(double* __restrict__ X, int6
   }
 }
 
+// Wide form for the prediction's many columns: a 256-column workgroup per chunk stages the
+// chunk's gains records and fix-up rows in LDS once (read back as broadcasts; from memory they
+// were scalar loads waited on step by step), and with `wmask` writes u only at the rows the
+// caller reads (test points: wmask[k] >= 1e10, gpar_scaled_inference.jl:100-107).
+template <int D>
+__global__ __launch_bounds__(256) void adjoint_local_wide(double* __restrict__ X, int64_t ldx,
+                                                         int64_t ncols, const double* __restrict__ rec,
+                                                         const double* __restrict__ g,
+                                                         const double* __restrict__ cin, int64_t mc,
+                                                         int64_t n, int L, double* __restrict__ bend,
+                                                         const double* __restrict__ wmask) {
+  constexpr int RS = Rec<D>::size;
+  constexpr int RU = D * D + D + 1;   // record entries used
+  __shared__ double lrec[256 * RU];
+  __shared__ double lg[256 * D];
+  __shared__ unsigned char lw[256];
+  const int64_t j = blockIdx.x;
+  const int tid = threadIdx.x;
+  const int64_t c = (int64_t)blockIdx.y * 256 + tid;
+  const bool act = c < ncols;
+  const int64_t cc = act ? c : 0;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  const int nk = (int)(k1 - k0);
+  for (int e = tid; e < nk * RU; e += 256) lrec[e] = rec[(k0 + e / RU) * RS + e % RU];
+  for (int e = tid; e < nk * D; e += 256) lg[e] = g[(k0 + e / D) * kGStride + e % D];
+  if (tid < nk) lw[tid] = wmask ? (wmask[k0 + tid] >= 1e10) : 1;
+  __syncthreads();
+  double cf[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) cf[i] = cin[(j * mc + cc) * kSStride + i];
+  double lam[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) lam[i] = 0.0;
+#pragma unroll 4
+  for (int s = nk - 1; s >= 0; --s) {
+    const int64_t k = k0 + s;
+    const double* r = lrec + s * RU;
+    const double* gk = lg + s * D;
+    double w = X[k * ldx + cc];
+#pragma unroll
+    for (int i = 0; i < D; ++i) w = fma(gk[i], cf[i], w);
+    double u = w * r[D * D + D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) u = fma(r[D * D + i], lam[i], u);
+    lam[0] -= u;
+    double nl[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) acc = fma(r[i * D + q], lam[i], acc);
+      nl[q] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) lam[i] = nl[i];
+    if (act && lw[s]) X[k * ldx + c] = u;
+  }
+  if (act) {
+#pragma unroll
+    for (int i = 0; i < D; ++i) bend[(j * mc + c) * kSStride + i] = lam[i];
+  }
+}
+
 // ---------------------------------------------------------------------------- smoothed mean of f
 // f_k = y_k - R_k (Sigma^{-1} y)_k   (S y = y - R Sigma^{-1} y), with
 // (Sigma^{-1} y)_k = u_loc_k + h_k . chat_{chunk(k)};  u_loc: adjoint output (contiguous per chain).
@@ -1702,6 +1766,13 @@ void launch_adjoint_local(hipStream_t st, int sdim, double* X, int64_t ldx, int6
                           int64_t xstride, int64_t sstride) {
   dim3 grid((unsigned)nch, (unsigned)((ncols + 63) / 64), (unsigned)nchains);
   GPAR_DISPATCH_D(sdim, adjoint_local<DD><<<grid, 64, 0, st>>>(X, ldx, ncols, rec, g, cin, mc, n, L, bend, xstride, sstride));
+}
+
+void launch_adjoint_local_wide(hipStream_t st, int sdim, double* X, int64_t ldx, int64_t ncols,
+                               const double* rec, const double* g, const double* cin, int64_t mc,
+                               int64_t n, int L, int64_t nch, double* bend, const double* wmask) {
+  dim3 grid((unsigned)nch, (unsigned)((ncols + 255) / 256));
+  GPAR_DISPATCH_D(sdim, adjoint_local_wide<DD><<<grid, 256, 0, st>>>(X, ldx, ncols, rec, g, cin, mc, n, L, bend, wmask));
 }
 
 void launch_smooth_mean(hipStream_t st, int sdim, const double* u, const double* h,

@@ -115,6 +115,11 @@ void launch_adjoint_local(hipStream_t st, int sdim, double* X, int64_t ldx, int6
                           const double* rec, const double* g, const double* cin, int64_t mc,
                           int64_t n, int L, int64_t nch, double* bend, int nchains = 1,
                           int64_t xstride = 0, int64_t sstride = 0);
+// Single chain, many columns (prediction): LDS-staged gains; wmask (optional): write u only at
+// rows with wmask[k] >= 1e10 (the merged grid's test points).
+void launch_adjoint_local_wide(hipStream_t st, int sdim, double* X, int64_t ldx, int64_t ncols,
+                               const double* rec, const double* g, const double* cin, int64_t mc,
+                               int64_t n, int L, int64_t nch, double* bend, const double* wmask);
 // temporal chains: smoothed mean f = y - R Sigma^{-1} y, smoothed variance of f (RTS)
 void launch_smooth_mean(hipStream_t st, int sdim, const double* u, const double* h,
                         const double* chat, int64_t sstride, const double* y, int64_t ldy,
