@@ -1,0 +1,76 @@
+"""Summarise tools/pmc_passes.sh: per-dispatch counters of the Gram and whitening kernels
+(rocprofv3 --pmc, one counter group per pass) -> derived figures, JSON on stdout.
+
+Conventions (MI355X_MICROARCH.md): SQ_WAVE_CYCLES / SQ_WAIT_* / SQ_ACTIVE_INST_* in quad-cycles
+summed over waves; SQ_VALU_MFMA_BUSY_CYCLES in cycles summed over SIMDs; GRBM_GUI_ACTIVE summed
+over the 8 XCDs (effective clock = GRBM_GUI_ACTIVE / 8 / kernel time); FETCH_SIZE (KiB) reports
+half of wide streaming reads on gfx950 (doubled here); WRITE_SIZE (KiB) exact."""
+import csv
+import glob
+import json
+import sys
+from collections import defaultdict
+
+N, M, D = 1_000_000, 512, 32
+SIMDS = 1024
+
+
+def load(d):
+    per = defaultdict(lambda: defaultdict(float))   # (kernel, dispatch) -> counter -> value
+    dur = {}
+    for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = "gram" if "gram_kernel" in r["Kernel_Name"] else "whiten"
+            key = (k, r["Dispatch_Id"])
+            per[key][r["Counter_Name"]] += float(r["Counter_Value"])
+            if "Start_Timestamp" in r and r.get("End_Timestamp"):
+                dur[key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
+    out = defaultdict(lambda: defaultdict(list))
+    for (k, _), cs in per.items():
+        for c, v in cs.items():
+            out[k][c].append(v)
+    durs = defaultdict(list)
+    for (k, _), t in dur.items():
+        durs[k].append(t)
+    return out, durs
+
+
+def avg(x):
+    return sum(x) / len(x) if x else None
+
+
+def main(root):
+    res = {"source": "tools/pmc_passes.sh: rocprofv3 --pmc passes over tools/gram_probe.py "
+                     f"--evals 2 (N={N}, M={M}, D={D}); per-dispatch averages"}
+    sq, dsq = load(root + "/sq1")
+    fe, _ = load(root + "/fetch")
+    wr, _ = load(root + "/write")
+    for k in ("gram", "whiten"):
+        c = {n: avg(v) for n, v in sq[k].items()}
+        t = avg(dsq[k])
+        e = {"counters": c, "kernel_s_under_pmc": t}
+        if t and c.get("GRBM_GUI_ACTIVE"):
+            clk = c["GRBM_GUI_ACTIVE"] / 8 / t
+            e["effective_clock_GHz"] = clk / 1e9
+            if c.get("SQ_VALU_MFMA_BUSY_CYCLES"):
+                e["mfma_busy_fraction"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / (SIMDS * clk * t)
+            if c.get("SQ_INSTS_MFMA"):
+                e["cycles_per_mfma"] = c["SQ_VALU_MFMA_BUSY_CYCLES"] / c["SQ_INSTS_MFMA"]
+        w = c.get("SQ_WAVE_CYCLES")
+        if w:
+            e["wave_time_fraction"] = {"active_inst_any": c.get("SQ_ACTIVE_INST_ANY", 0) / w,
+                                       "wait_inst_any (issue stall)": c.get("SQ_WAIT_INST_ANY", 0) / w,
+                                       "wait_any (waitcnt/barrier)": c.get("SQ_WAIT_ANY", 0) / w}
+        f = avg(fe[k].get("FETCH_SIZE", []))
+        wb = avg(wr[k].get("WRITE_SIZE", []))
+        e["hbm_read_bytes"] = f * 1024 * 2 if f is not None else None
+        e["hbm_write_bytes"] = wb * 1024 if wb is not None else None
+        res[k] = e
+    res["gram"]["algorithmic"] = {"flop": N * M * (M + 1), "bytes": N * M * 8}
+    res["whiten"]["algorithmic"] = {"bytes": N * D * 8 + N * 16 * 8 + N * M * 8,
+                                    "note": "V read, gains records read, beta written"}
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main(sys.argv[1])
