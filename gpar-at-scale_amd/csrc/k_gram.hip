@@ -16,6 +16,8 @@
 // 64 x 64 lower-triangle sub-tile of G = 4 x 4 MFMA tiles of v_mfma_f64_16x16x4_f64
 // (C/D: col = lane & 15, row = (lane >> 4) + 4 * reg).  K-step = 16 time rows staged
 // global -> LDS by LDS-DMA (no VGPRs), double buffered; each wave stages one 64-column panel.
+#include <type_traits>
+
 #include "device_common.hpp"
 
 namespace gpar {
@@ -297,6 +299,363 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
   }
 }
 
+// ============================================================================ v2 decomposition
+// The v1 groups compute every diagonal 64 x 64 sub-tile whole although 6 of its 16 tiles lie
+// above G's diagonal (12 % of the MFMAs at M = 512), and every workgroup's critical path is a
+// full sub-tile, so the waste sets the kernel time.  v2 re-packs the work into two workgroup
+// types of equal per-wave work, each with its own number of time splits:
+//   * OFF(a, b), a > b (unchanged): the 2 x 2 sub-tiles of the off-diagonal 128 x 128 block
+//     (diagonal-block indices a, b; panels 2a, 2a+1 | 2b, 2b+1), 16 tiles of 16 x 16 per wave;
+//   * DG(q): the lower triangles of the diagonal 128-blocks a0 = 2q, a1 = 2q + 1 (panels
+//     2a0, 2a0+1, 2a1, 2a1+1 in slots 0..3), 36 tiles each, split 18 + 18 over two waves:
+//     half 0 owns local tile rows {0, 1, 2, 3, 7}, half 1 rows {4, 5, 6} (local row r in 0..7:
+//     slot base + r / 4, tile r % 4 of that panel).  Nothing above the diagonal is computed
+//     except the upper halves of the 8 diagonal 16 x 16 tiles themselves.
+// gram2_plan picks the split counts so the per-wave work (tiles x rows) of the two types
+// matches and the workgroups fill the 512 co-resident slots.  DG also owns r = beta^T alpha
+// (every panel is staged by exactly one DG workgroup per split).
+constexpr int kD2T = 18;   // tiles per DG wave (accumulators: 72 doubles)
+
+template <int H>
+__device__ __forceinline__ constexpr int d2_row(int ia) { return H == 0 ? (ia < 4 ? ia : 7) : 4 + ia; }
+template <int H>
+__device__ __forceinline__ constexpr int d2_na() { return H == 0 ? 5 : 3; }
+template <int H>
+__device__ __forceinline__ constexpr int d2_nb() { return H == 0 ? 8 : 7; }
+template <int H>
+__device__ __forceinline__ constexpr int d2_tile(int ia, int c) {
+  int t = 0;
+  for (int i = 0; i < ia; ++i) t += d2_row<H>(i) + 1;
+  return t + c;
+}
+
+template <int D>
+__global__ __launch_bounds__(256, 2) void gram2_kernel(
+    const double* __restrict__ beta, int64_t ldb, int64_t n, const double* __restrict__ ecor,
+    const double* __restrict__ cin, const double* __restrict__ qv, int64_t mc, int L,
+    const double* __restrict__ alpha, int npan, int noff, int ndg, int soff, int sdg,
+    int64_t rows_off, int64_t rows_dg, double* __restrict__ part, double* __restrict__ rpart) {
+  __shared__ __attribute__((aligned(16))) double smem[8 * kPanelD + 2 * 4 * kBK];
+  double* ringa = smem + 8 * kPanelD;
+  const int nbk = npan >> 1;   // diagonal 128-blocks
+
+  // linear decode: all OFF workgroups (group fastest), then all DG workgroups
+  const int b = blockIdx.x;
+  bool dg;
+  int split, gid, nsplit;
+  int64_t rows;
+  if (b < noff * soff) {
+    dg = false; gid = b % noff; split = b / noff; nsplit = soff; rows = rows_off;
+  } else {
+    const int bb = b - noff * soff;
+    dg = true; gid = bb % ndg; split = bb / ndg; nsplit = sdg; rows = rows_dg;
+  }
+  if (split >= nsplit) return;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // this wave's staged panel, operand slots, and role
+  int spanel, sa = 0, sb = 0, pa = 0, pb = 0, half = 0, blk = 0;
+  bool mf = true, owns_r = false;
+  if (!dg) {
+    int a = 1;
+    while (a * (a + 1) / 2 <= gid) ++a;
+    const int bo = gid - a * (a - 1) / 2;
+    sa = wave >> 1;
+    sb = 2 + (wave & 1);
+    pa = 2 * a + (wave >> 1);
+    pb = 2 * bo + (wave & 1);
+    spanel = (wave < 2) ? 2 * a + wave : 2 * bo + (wave - 2);
+  } else {
+    const int a0 = 2 * gid, a1 = 2 * gid + 1;
+    blk = (wave < 2) ? a0 : a1;
+    half = wave & 1;
+    mf = blk < nbk;
+    const int pblk = mf ? blk : a0;                       // a missing second block: duplicate
+    spanel = 2 * pblk + (wave & 1);                        // slot w holds panel 2 blk + (w & 1)
+    sa = (wave < 2) ? 0 : 2;                               // slot base of this wave's block
+    owns_r = mf;
+  }
+
+  const int64_t kb = (int64_t)split * rows;
+  int64_t ke = kb + rows;
+  if (ke > n) ke = n;
+  const int nsteps = (int)(ke > kb ? (ke - kb + kBK - 1) / kBK : 0);
+
+  double racc4[4] = {0.0, 0.0, 0.0, 0.0};
+  const int lq = lane >> 4, lc = lane & 15;
+  const int hl = lane >> 5, cl2 = (lane & 31) * 2;
+  const uint32_t boff =
+      (uint32_t)(((int64_t)hl * ldb + (int64_t)spanel * kPW + (cl2 ^ (hl << 4))) * 8);
+  const char* bbase = reinterpret_cast<const char*>(beta);
+  const double* zrow = beta + n * ldb;
+  auto issue = [&](int s) __attribute__((always_inline)) {
+    const int64_t k0 = kb + (int64_t)s * kBK;
+    double* img = smem + ((s & 1) * 4 + wave) * kPanelD;
+#pragma unroll
+    for (int i = 0; i < kBK / 2; ++i) {
+      const char* rowp = bbase + (k0 + 2 * i) * ldb * 8;
+      __builtin_amdgcn_global_load_lds(rowp + boff, img + 2 * i * kPW, 16, 0, 0);
+    }
+    if (lane < 32) {
+      const int64_t kr = k0 + (lane >> 1);
+      const unsigned* as = kr < n ? reinterpret_cast<const unsigned*>(alpha + kr) + (lane & 1)
+                                  : reinterpret_cast<const unsigned*>(zrow);
+      __builtin_amdgcn_global_load_lds(as, ringa + ((s & 1) * 4 + wave) * kBK, 4, 0, 0);
+    }
+  };
+  const int frow = lane >> 4, fcol = lane & 15;
+  const int par = frow & 1;
+  // fragment offset of tile t (0..3) of slot sl at k-substep 0
+  auto foff = [&](int sl, int t) __attribute__((always_inline)) {
+    return sl * kPanelD + frow * kPW + ((t ^ par) << 4) + fcol;
+  };
+  const int roff = wave * kPanelD + lq * kPW + lc;
+  auto r_update = [&](int s, const double* base) __attribute__((always_inline)) {
+    const double* ar = ringa + ((s & 1) * 4 + wave) * kBK;
+    const double* im = base + roff;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const double av = ar[lq + 4 * i];
+      const int rsw = (i * 4 + lq) & 1;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) racc4[c] = fma(av, im[4 * i * kPW + ((c ^ rsw) << 4)], racc4[c]);
+    }
+  };
+
+  if (nsteps > 0) issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int64_t nch = (n + L - 1) / L;
+  const int64_t j0 = (int64_t)split * nch / nsplit, j1 = (int64_t)(split + 1) * nch / nsplit;
+  const bool cv = lq < D;
+  const int64_t cstride = mc * kSStride;
+  double* ptile = part + (((int64_t)b * 4 + wave) * kD2T) * 256;   // this wave's tile slots
+
+  // store tile t of acc: C layout (col = lane & 15, row = (lane >> 4) + 4 r)
+  auto store_tile = [&](int t, const d4& v) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) ptile[t * 256 + (frow + 4 * r) * 16 + fcol] = v[r];
+  };
+
+  if (!dg) {
+    // ---------------- OFF: 4 x 4 tiles, A tiles 0..3 of slot sa, B tiles 0..3 of slot sb
+    d4 acc[4][4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[a][c] = d4{0.0, 0.0, 0.0, 0.0};
+    int offa[4], offb[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) { offa[a] = foff(sa, a); offb[a] = foff(sb, a); }
+    for (int s = 0; s < nsteps; ++s) {
+      if (s + 1 < nsteps) issue(s + 1);
+      const double* base = smem + (s & 1) * 4 * kPanelD;
+#pragma unroll
+      for (int ks = 0; ks < kBK / 4; ++ks) {
+        double fa[4], fb[4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) fa[a] = base[offa[a] + ks * 4 * kPW];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) fb[c] = base[offb[c] + ks * 4 * kPW];
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[c], acc[a][c], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    if (ecor) {
+      const int64_t oa = ((int64_t)pa * kPW + lc) * kSStride + lq;
+      const int64_t ob = ((int64_t)pb * kPW + lc) * kSStride + lq;
+      for (int64_t jj = j0; jj < j1; ++jj) {
+        const double* ej = ecor + jj * cstride;
+        const double* cj = cin + jj * cstride;
+        double ea[4], ca[4], eb[4], cb[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) {
+          ea[t] = ej[oa + t * 16 * kSStride];
+          eb[t] = ej[ob + t * 16 * kSStride];
+          ca[t] = cv ? cj[oa + t * 16 * kSStride] : 0.0;
+          cb[t] = cv ? cj[ob + t * 16 * kSStride] : 0.0;
+        }
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ea[a], cb[c], acc[a][c], 0, 0, 0);
+            acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[a], eb[c], acc[a][c], 0, 0, 0);
+          }
+      }
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) store_tile(a * 4 + c, acc[a][c]);
+    return;
+  }
+
+  // ---------------- DG: 18 tiles of the diagonal block blk (local rows per half)
+  auto dg_body = [&](auto htag) __attribute__((always_inline)) {
+    constexpr int H = decltype(htag)::value;
+    constexpr int NA = d2_na<H>(), NB = d2_nb<H>();
+    d4 acc[kD2T];
+#pragma unroll
+    for (int t = 0; t < kD2T; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    int offa[NA], offb[NB];
+#pragma unroll
+    for (int ia = 0; ia < NA; ++ia) {
+      const int r = d2_row<H>(ia);
+      offa[ia] = foff(sa + (r >> 2), r & 3);
+    }
+#pragma unroll
+    for (int c = 0; c < NB; ++c) offb[c] = foff(sa + (c >> 2), c & 3);
+    for (int s = 0; s < nsteps; ++s) {
+      if (s + 1 < nsteps) issue(s + 1);
+      const double* base = smem + (s & 1) * 4 * kPanelD;
+#pragma unroll
+      for (int ks = 0; ks < kBK / 4; ++ks) {
+        double fa[NA], fb[NB];
+#pragma unroll
+        for (int ia = 0; ia < NA; ++ia) fa[ia] = base[offa[ia] + ks * 4 * kPW];
+#pragma unroll
+        for (int c = 0; c < NB; ++c) fb[c] = base[offb[c] + ks * 4 * kPW];
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int ia = 0; ia < NA; ++ia)
+#pragma unroll
+          for (int c = 0; c <= d2_row<H>(ia); ++c)
+            acc[d2_tile<H>(ia, c)] =
+                __builtin_amdgcn_mfma_f64_16x16x4f64(fa[ia], fb[c], acc[d2_tile<H>(ia, c)], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+      if (owns_r) r_update(s, base);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    if (ecor && mf) {
+      const int64_t pbase = (int64_t)2 * blk * kPW;   // first column of the diagonal block
+      const int64_t os = ((int64_t)spanel * kPW + lc) * kSStride + lq;
+      for (int64_t jj = j0; jj < j1; ++jj) {
+        const double* ej = ecor + jj * cstride;
+        const double* cj = cin + jj * cstride;
+        double ea[NA], ca[NA], eb[NB], cb[NB];
+#pragma unroll
+        for (int ia = 0; ia < NA; ++ia) {
+          const int64_t o = (pbase + d2_row<H>(ia) * 16 + lc) * kSStride + lq;
+          ea[ia] = ej[o];
+          ca[ia] = cv ? cj[o] : 0.0;
+        }
+#pragma unroll
+        for (int c = 0; c < NB; ++c) {
+          const int64_t o = (pbase + c * 16 + lc) * kSStride + lq;
+          eb[c] = ej[o];
+          cb[c] = cv ? cj[o] : 0.0;
+        }
+#pragma unroll
+        for (int ia = 0; ia < NA; ++ia)
+#pragma unroll
+          for (int c = 0; c <= d2_row<H>(ia); ++c) {
+            acc[d2_tile<H>(ia, c)] = __builtin_amdgcn_mfma_f64_16x16x4f64(ea[ia], cb[c], acc[d2_tile<H>(ia, c)], 0, 0, 0);
+            acc[d2_tile<H>(ia, c)] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[ia], eb[c], acc[d2_tile<H>(ia, c)], 0, 0, 0);
+          }
+        if (owns_r) {
+          const double qq = cv ? qv[jj * 4 + lq] : 0.0;
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            const double csv = cv ? cj[os + c * 16 * kSStride] : 0.0;
+            racc4[c] = fma(csv, qq, racc4[c]);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < kD2T; ++t) store_tile(t, acc[t]);
+  };
+  if (half == 0)
+    dg_body(std::integral_constant<int, 0>{});
+  else
+    dg_body(std::integral_constant<int, 1>{});
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    double v = racc4[c];
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    if (owns_r && lq == 0) rpart[(int64_t)split * npan * kPW + (int64_t)spanel * kPW + c * 16 + lc] = v;
+  }
+}
+
+// v2 reduction: one grid row per (workgroup of the first split, wave, tile); sums that tile's
+// partials over the type's splits in split order and writes G (and its mirror).  The last grid
+// row sums r over the DG splits.
+__global__ __launch_bounds__(256) void gram2_reduce(const double* __restrict__ part,
+                                                    const double* __restrict__ rpart, int npan,
+                                                    int noff, int ndg, int soff, int sdg,
+                                                    double* __restrict__ G, int64_t ldg,
+                                                    double* __restrict__ r) {
+  const int e = threadIdx.x;   // element of the 16 x 16 tile (C layout row-major 16 x 16)
+  const int y = blockIdx.x;
+  const int nbk = npan >> 1;
+  const int nrow_off = noff * 4 * 16, nrow_dg = ndg * 4 * kD2T;
+  if (y == nrow_off + nrow_dg) {
+    const int mp = npan * kPW;
+    for (int c = e; c < mp; c += 256) {
+      double s = 0.0;
+      for (int sp = 0; sp < sdg; ++sp) s += rpart[(int64_t)sp * mp + c];
+      r[c] = s;
+    }
+    return;
+  }
+  int64_t grow, gcol;
+  int64_t wb;        // workgroup index (first split) and wave
+  int w, t, nsp, stride;
+  bool diag_tile = false;
+  if (y < nrow_off) {
+    const int gid = y / 64, rem = y % 64;
+    w = rem / 16; t = rem % 16;
+    int a = 1;
+    while (a * (a + 1) / 2 <= gid) ++a;
+    const int bo = gid - a * (a - 1) / 2;
+    const int pa = 2 * a + (w >> 1), pb = 2 * bo + (w & 1);
+    grow = (int64_t)pa * kPW + (t >> 2) * 16;
+    gcol = (int64_t)pb * kPW + (t & 3) * 16;
+    wb = gid; nsp = soff; stride = noff;
+  } else {
+    const int yy = y - nrow_off;
+    const int gid = yy / (4 * kD2T), rem = yy % (4 * kD2T);
+    w = rem / kD2T; t = rem % kD2T;
+    const int blk = (w < 2) ? 2 * gid : 2 * gid + 1;
+    if (blk >= nbk) return;
+    // invert d2_tile: walk the half's rows
+    const int H = w & 1;
+    int ia = 0, tt = t, rr = 0;
+    for (;;) {
+      rr = (H == 0) ? (ia < 4 ? ia : 7) : 4 + ia;
+      if (tt <= rr) break;
+      tt -= rr + 1;
+      ++ia;
+    }
+    grow = (int64_t)2 * blk * kPW + rr * 16;
+    gcol = (int64_t)2 * blk * kPW + tt * 16;
+    diag_tile = rr == tt;
+    wb = (int64_t)noff * soff + gid; nsp = sdg; stride = ndg;
+  }
+  const int er = e / 16, ec = e % 16;
+  if (diag_tile && er < ec) return;
+  double s = 0.0;
+  for (int sp = 0; sp < nsp; ++sp)
+    s += part[(((wb + (int64_t)sp * stride) * 4 + w) * kD2T + t) * 256 + e];
+  const int64_t gr = grow + er, gc = gcol + ec;
+  G[gr * ldg + gc] = s;
+  G[gc * ldg + gr] = s;
+}
+
 // Sum split partials in split order (deterministic) into the full symmetric G (ldg); the
 // last grid row sums r.
 __global__ __launch_bounds__(256) void gram_reduce(const double* __restrict__ part,
@@ -349,8 +708,57 @@ __global__ __launch_bounds__(256) void beta_fix_kernel(double* __restrict__ beta
 
 namespace gpar {
 
+#ifndef GRAM_V1
+#define GRAM_V1 0   // 1: the v1 decomposition (whole diagonal sub-tiles), for A/B only
+#endif
+
+// v2: split counts for the OFF and DG workgroups minimising the per-CU work
+// ceil(workgroups / 256) x max(16 x rows_off, 18 x rows_dg), at most 512 workgroups (2 per CU);
+// at M = 512, N = 1e6: 6 x 62 OFF + 2 x 70 DG = 512 workgroups, 16 x 16144 vs 18 x 14288
+// tile-rows per wave (v1: 16 x 17872).
+static void gram2_plan(int64_t n, int64_t mp, GramPlan& p) {
+  const int nbk = (int)(mp / 128);
+  p.v2 = 1;
+  p.npan = 2 * nbk;
+  p.noff = nbk * (nbk - 1) / 2;
+  p.ndg = (nbk + 1) / 2;
+  // >= 256 rows per split, but at least 8 splits: shorter sequential sums per accumulator (the
+  // noise-free q(u) factors a Cuu with cond ~1e7 and sees the Gram's rounding)
+  const int64_t maxs = (n + 255) / 256 > 8 ? (n + 255) / 256 : 8;
+  auto rows_of = [&](int64_t s) { return (((n + s - 1) / s + kBK - 1) / kBK) * kBK; };
+  double best = 1e300;
+  int bo = 1, bd = 1, bw = 0;
+  for (int so = (p.noff ? 1 : 0); so <= (p.noff ? 512 : 0); ++so) {
+    if (so > maxs) break;
+    const int left = 512 - p.noff * so;
+    if (left < p.ndg) break;
+    for (int sd = 1; sd <= left / p.ndg && sd <= maxs; ++sd) {
+      const int wgs = p.noff * so + p.ndg * sd;
+      const double wo = so ? 16.0 * (double)rows_of(so) : 0.0;
+      const double wd = 18.0 * (double)rows_of(sd);
+      // one workgroup per CU leaves one wave per SIMD, with nothing to hide its barrier and LDS
+      // waits behind: priced 15 % worse than the same work spread two per CU
+      const double cost = (double)((wgs + 255) / 256) * (wo > wd ? wo : wd) * (wgs > 384 ? 1.0 : 1.15);
+      if (cost < best * (1.0 - 1e-9) || (cost <= best * (1.0 + 1e-9) && wgs > bw)) {
+        best = cost; bo = so; bd = sd; bw = wgs;
+      }
+    }
+  }
+  p.soff = p.noff ? bo : 0;
+  p.sdg = bd;
+  p.rows_off = p.noff ? rows_of(p.soff) : 0;
+  p.rows_dg = rows_of(p.sdg);
+  p.nsplit = p.sdg;
+  p.part_doubles = (int64_t)(p.noff * p.soff + p.ndg * p.sdg) * 4 * kD2T * 256;
+  p.rpart_doubles = (int64_t)p.sdg * mp;
+}
+
 GramPlan gram_plan(int64_t n, int64_t mp) {
   GramPlan p;
+  if (!GRAM_V1) {
+    gram2_plan(n, mp, p);
+    return p;
+  }
   p.npan = (int)(mp / kPW);
   const int nb = p.npan / 2;
   const int noff = nb * (nb - 1) / 2;
@@ -387,6 +795,17 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
                  int64_t ldb, int64_t n, const double* ecor, const double* cin, const double* qv,
                  int64_t mc, int L, const double* alpha, double* part, double* rpart, double* G,
                  int64_t ldg, double* r) {
+  if (plan.v2) {
+    const int nwg = plan.noff * plan.soff + plan.ndg * plan.sdg;
+    switch (sdim) {
+      case 1: gram2_kernel<1><<<nwg, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, plan.rows_off, plan.rows_dg, part, rpart); break;
+      case 2: gram2_kernel<2><<<nwg, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, plan.rows_off, plan.rows_dg, part, rpart); break;
+      default: gram2_kernel<3><<<nwg, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, plan.rows_off, plan.rows_dg, part, rpart); break;
+    }
+    const int nrows = plan.noff * 4 * 16 + plan.ndg * 4 * kD2T + 1;
+    gram2_reduce<<<nrows, 256, 0, st>>>(part, rpart, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, G, ldg, r);
+    return;
+  }
   const int nblk = plan.xcd ? plan.ngroups * ((plan.nsplit + 7) / 8) * 8 : plan.ngroups * plan.nsplit;
   switch (sdim) {
     case 1: gram_kernel<1><<<nblk, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart, plan.xcd); break;

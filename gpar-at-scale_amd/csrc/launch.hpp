@@ -69,6 +69,9 @@ struct GramPlan {
   int xcd = 1;                              // XCD-aware block decode (ngroups <= 64)
   int64_t rows_per_split = 0;
   int64_t part_doubles = 0, rpart_doubles = 0;
+  // v2 decomposition (k_gram.hip): OFF / DG workgroup counts, their time splits and rows
+  int v2 = 0, noff = 0, ndg = 0, soff = 0, sdg = 0;
+  int64_t rows_off = 0, rows_dg = 0;
 };
 
 constexpr int kGramTile = 128;
