@@ -190,7 +190,7 @@ def main():
         avg = gram_ms / max(gram_n, 1)
         achieved = flops / (avg * 1e-3) / 1e12 if gram_n else None
         traffic = None
-        pmc = os.path.join(ROOT, "profiles", "gram_pmc_r01b.json")   # measured at the north config
+        pmc = os.path.join(ROOT, "profiles", "pmc_gram2_whiten_r01i.json")   # tools/pmc_passes.sh at the north config
         if args.config == "north" and os.path.exists(pmc):
             with open(pmc) as f:
                 traffic = json.load(f).get("hbm_bytes_per_launch")
@@ -215,7 +215,7 @@ def main():
                        "parallelism": f"outputs sharded over {world} GPU(s)"},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
-                         "traffic": traffic, "kernel": "gram_kernel (beta^T beta, fp64 MFMA)",
+                         "traffic": traffic, "kernel": "gram2_kernel (beta^T beta, fp64 MFMA)",
                          "launches": gram_n, "avg_ms": avg, "flops_per_launch": flops,
                          "lanes": args.lanes},
             "kernels": {"gram_ms_per_step": gram_ms / args.steps, "whiten_ms_per_step": wh_ms / args.steps,

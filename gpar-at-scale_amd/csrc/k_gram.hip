@@ -339,8 +339,14 @@ __global__ __launch_bounds__(256, 2) void gram2_kernel(
   double* ringa = smem + 8 * kPanelD;
   const int nbk = npan >> 1;   // diagonal 128-blocks
 
-  // linear decode: all OFF workgroups (group fastest), then all DG workgroups
-  const int b = blockIdx.x;
+  // Work items in order: all OFF workgroups (group fastest), then all DG workgroups.  Blocks
+  // are dealt to the 8 XCDs round-robin (blockIdx % 8), so item i runs as block
+  // 8 (i % per) + i / per: every XCD gets a run of consecutive items, and the 6 OFF groups of
+  // a split -- 24 panel reads of 8 distinct panels -- share one L2.
+  const int nwg = noff * soff + ndg * sdg;
+  const int per = (nwg + 7) >> 3;
+  const int b = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);
+  if (b >= nwg) return;
   bool dg;
   int split, gid, nsplit;
   int64_t rows;
@@ -474,10 +480,11 @@ __global__ __launch_bounds__(256, 2) void gram2_kernel(
     if (ecor) {
       const int64_t oa = ((int64_t)pa * kPW + lc) * kSStride + lq;
       const int64_t ob = ((int64_t)pb * kPW + lc) * kSStride + lq;
-      for (int64_t jj = j0; jj < j1; ++jj) {
+      // chunk jj + 1's E / C rows are loaded while chunk jj's 32 MFMAs run
+      double ea[4], ca[4], eb[4], cb[4];
+      auto ld = [&](int64_t jj) __attribute__((always_inline)) {
         const double* ej = ecor + jj * cstride;
         const double* cj = cin + jj * cstride;
-        double ea[4], ca[4], eb[4], cb[4];
 #pragma unroll
         for (int t = 0; t < 4; ++t) {
           ea[t] = ej[oa + t * 16 * kSStride];
@@ -485,12 +492,19 @@ __global__ __launch_bounds__(256, 2) void gram2_kernel(
           ca[t] = cv ? cj[oa + t * 16 * kSStride] : 0.0;
           cb[t] = cv ? cj[ob + t * 16 * kSStride] : 0.0;
         }
+      };
+      if (j0 < j1) ld(j0);
+      for (int64_t jj = j0; jj < j1; ++jj) {
+        double xa[4], ya[4], xb[4], yb[4];
+#pragma unroll
+        for (int t = 0; t < 4; ++t) { xa[t] = ea[t]; ya[t] = ca[t]; xb[t] = eb[t]; yb[t] = cb[t]; }
+        if (jj + 1 < j1) ld(jj + 1);
 #pragma unroll
         for (int a = 0; a < 4; ++a)
 #pragma unroll
           for (int c = 0; c < 4; ++c) {
-            acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ea[a], cb[c], acc[a][c], 0, 0, 0);
-            acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[a], eb[c], acc[a][c], 0, 0, 0);
+            acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(xa[a], yb[c], acc[a][c], 0, 0, 0);
+            acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ya[a], xb[c], acc[a][c], 0, 0, 0);
           }
       }
     }
@@ -541,37 +555,37 @@ __global__ __launch_bounds__(256, 2) void gram2_kernel(
     }
     if (ecor && mf) {
       const int64_t pbase = (int64_t)2 * blk * kPW;   // first column of the diagonal block
-      const int64_t os = ((int64_t)spanel * kPW + lc) * kSStride + lq;
-      for (int64_t jj = j0; jj < j1; ++jj) {
+      // E / C rows of the block, indexed by local tile column 0..7 (rows and columns share
+      // them); chunk jj + 1's are loaded while chunk jj's MFMAs run
+      double e8[8], c8[8];   // 8: the r update reads columns 4 H .. 4 H + 3
+      auto ld = [&](int64_t jj) __attribute__((always_inline)) {
         const double* ej = ecor + jj * cstride;
         const double* cj = cin + jj * cstride;
-        double ea[NA], ca[NA], eb[NB], cb[NB];
 #pragma unroll
-        for (int ia = 0; ia < NA; ++ia) {
-          const int64_t o = (pbase + d2_row<H>(ia) * 16 + lc) * kSStride + lq;
-          ea[ia] = ej[o];
-          ca[ia] = cv ? cj[o] : 0.0;
-        }
-#pragma unroll
-        for (int c = 0; c < NB; ++c) {
+        for (int c = 0; c < 8; ++c) {
           const int64_t o = (pbase + c * 16 + lc) * kSStride + lq;
-          eb[c] = ej[o];
-          cb[c] = cv ? cj[o] : 0.0;
+          e8[c] = ej[o];
+          c8[c] = cv ? cj[o] : 0.0;
         }
+      };
+      if (j0 < j1) ld(j0);
+      for (int64_t jj = j0; jj < j1; ++jj) {
+        double xe[8], xc[8];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) { xe[c] = e8[c]; xc[c] = c8[c]; }
+        if (jj + 1 < j1) ld(jj + 1);
 #pragma unroll
         for (int ia = 0; ia < NA; ++ia)
 #pragma unroll
           for (int c = 0; c <= d2_row<H>(ia); ++c) {
-            acc[d2_tile<H>(ia, c)] = __builtin_amdgcn_mfma_f64_16x16x4f64(ea[ia], cb[c], acc[d2_tile<H>(ia, c)], 0, 0, 0);
-            acc[d2_tile<H>(ia, c)] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[ia], eb[c], acc[d2_tile<H>(ia, c)], 0, 0, 0);
+            const int r = d2_row<H>(ia);
+            acc[d2_tile<H>(ia, c)] = __builtin_amdgcn_mfma_f64_16x16x4f64(xe[r], xc[c], acc[d2_tile<H>(ia, c)], 0, 0, 0);
+            acc[d2_tile<H>(ia, c)] = __builtin_amdgcn_mfma_f64_16x16x4f64(xc[r], xe[c], acc[d2_tile<H>(ia, c)], 0, 0, 0);
           }
-        if (owns_r) {
+        if (owns_r) {   // this wave's staged panel is tile columns 4 H .. 4 H + 3 of the block
           const double qq = cv ? qv[jj * 4 + lq] : 0.0;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            const double csv = cv ? cj[os + c * 16 * kSStride] : 0.0;
-            racc4[c] = fma(csv, qq, racc4[c]);
-          }
+          for (int c = 0; c < 4; ++c) racc4[c] = fma(xc[4 * H + c], qq, racc4[c]);
         }
       }
     }
@@ -607,6 +621,7 @@ __global__ __launch_bounds__(256) void gram2_reduce(const double* __restrict__ p
     const int mp = npan * kPW;
     for (int c = e; c < mp; c += 256) {
       double s = 0.0;
+#pragma unroll 8
       for (int sp = 0; sp < sdg; ++sp) s += rpart[(int64_t)sp * mp + c];
       r[c] = s;
     }
@@ -648,9 +663,12 @@ __global__ __launch_bounds__(256) void gram2_reduce(const double* __restrict__ p
   }
   const int er = e / 16, ec = e % 16;
   if (diag_tile && er < ec) return;
+  // split order kept (deterministic); unrolled so the loads are in flight together
+  const double* pp = part + ((wb * 4 + w) * kD2T + t) * 256 + e;
+  const int64_t pstride = (int64_t)stride * 4 * kD2T * 256;
   double s = 0.0;
-  for (int sp = 0; sp < nsp; ++sp)
-    s += part[(((wb + (int64_t)sp * stride) * 4 + w) * kD2T + t) * 256 + e];
+#pragma unroll 8
+  for (int sp = 0; sp < nsp; ++sp) s += pp[sp * pstride];
   const int64_t gr = grow + er, gc = gcol + ec;
   G[gr * ldg + gc] = s;
   G[gc * ldg + gr] = s;
@@ -796,7 +814,7 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
                  int64_t mc, int L, const double* alpha, double* part, double* rpart, double* G,
                  int64_t ldg, double* r) {
   if (plan.v2) {
-    const int nwg = plan.noff * plan.soff + plan.ndg * plan.sdg;
+    const int nwg = ((plan.noff * plan.soff + plan.ndg * plan.sdg + 7) / 8) * 8;   // XCD deal
     switch (sdim) {
       case 1: gram2_kernel<1><<<nwg, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, plan.rows_off, plan.rows_dg, part, rpart); break;
       case 2: gram2_kernel<2><<<nwg, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, plan.rows_off, plan.rows_dg, part, rpart); break;

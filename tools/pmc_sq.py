@@ -20,7 +20,8 @@ def load(d):
     dur = {}
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
-            k = "gram" if "gram_kernel" in r["Kernel_Name"] else "whiten"
+            name = r["Kernel_Name"]
+            k = "gram" if ("gram" in name and "_kernel" in name) else "whiten"
             key = (k, r["Dispatch_Id"])
             per[key][r["Counter_Name"]] += float(r["Counter_Value"])
             if "Start_Timestamp" in r and r.get("End_Timestamp"):
@@ -66,7 +67,11 @@ def main(root):
         e["hbm_read_bytes"] = f * 1024 * 2 if f is not None else None
         e["hbm_write_bytes"] = wb * 1024 if wb is not None else None
         res[k] = e
-    res["gram"]["algorithmic"] = {"flop": N * M * (M + 1), "bytes": N * M * 8}
+    res["gram"]["algorithmic"] = {"flop": N * M * (M + 1), "bytes": N * M * 8,
+                                  "mfma": N * M * (M + 1) // 2048}
+    g = res["gram"]
+    if g.get("hbm_read_bytes") is not None and g.get("hbm_write_bytes") is not None:
+        res["hbm_bytes_per_launch"] = g["hbm_read_bytes"] + g["hbm_write_bytes"]   # bench.py traffic
     res["whiten"]["algorithmic"] = {"bytes": N * D * 8 + N * 16 * 8 + N * M * 8,
                                     "note": "V read, gains records read, beta written"}
     print(json.dumps(res, indent=1))
