@@ -272,7 +272,34 @@ def cpu_baseline(N, NS, M, P, EV, out_kernel, samples=(50_000, 100_000), d_sampl
     n_sample, ns, t_eval, t_pred = per[-1]
     t_job = (P - 1) * (EV * t_eval * N / n_sample + t_pred * (N + NS) / (n_sample + ns))
     lin = (per[-1][2] / per[-1][0]) / (per[0][2] / per[0][0])
+    # SURVEY §8d also asks for one thread, as the reference's sequential column loop runs
+    # (dtc.jl:110-117): the same two pieces at n = 2e4 under threadpoolctl's limit of 1.
+    single = None
+    try:
+        from threadpoolctl import threadpool_limits
+        n1 = 20_000
+        t, Y = O.synthetic_gpar(n1, d_sample + 1, seed=1, noise=0.8)
+        V, y = Y[:, :d_sample].T, Y[:, d_sample]
+        Z = O.pick_pseudo_inputs(V, M, 3)
+        ns1 = n1 // 4
+        ts = np.sort(np.random.default_rng(2).uniform(t[0], t[-1], ns1))
+        Vs = np.vstack([np.interp(ts, t, V[q]) for q in range(d_sample)])
+        with threadpool_limits(limits=1):
+            t0 = time.perf_counter()
+            CR.compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel, "matern52")
+            e1 = time.perf_counter() - t0
+            t0 = time.perf_counter()
+            CR.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, out_kernel, "matern52",
+                                                 qu_kuu_noise=True)
+            p1 = time.perf_counter() - t0
+        tj1 = (P - 1) * (EV * e1 * N / n1 + p1 * (N + NS) / (n1 + ns1))
+        single = {"value": N * P / tj1, "cores": 1,
+                  "sample": f"1 thread: 1 eval (N={n1}) = {e1:.2f}s + 1 predict (N*={ns1}) = {p1:.2f}s, "
+                            f"same linear scaling: est {tj1:.0f}s per job"}
+    except Exception as exc:   # threadpoolctl missing: report the threaded figure only
+        single = {"value": None, "error": repr(exc)}
     return {"value": N * P / t_job, "unit": "pts\u00b7outputs/s", "cores": int(cores), "kind": "port",
+            "single_thread": single,
             "sample": f"C/OpenMP + OpenBLAS restatement (oracle/cpu_ref): 1 DTC objective eval (N={n_sample}, "
                       f"M={M}, D={d_sample}) = {t_eval:.2f}s + 1 analytic predict (N={n_sample}, N*={ns}) = "
                       f"{t_pred:.2f}s; per-point eval cost at N={per[0][0]} vs N={n_sample} differs by x{lin:.2f}; "
