@@ -694,7 +694,17 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
   // stores per sub-tile instead of 16 x 8 B (store issue, not bandwidth, bounds this tail).
   const int fh = lane >> 5, fc2 = (lane & 31) * 2;
   auto flush = [&]() __attribute__((always_inline)) {
-    if (cw0 < mp) {   // mp is a multiple of 128: whole waves are in or out
+    if (cw0 < mp && ntp == kMT) {   // all LDS reads first, then the 8 stores (no per-row branch)
+      double2 v2[kMT / 2];
+#pragma unroll
+      for (int i = 0; i < kMT / 2; ++i) {
+        v2[i].x = xt[wave][2 * i + fh][fc2];
+        v2[i].y = xt[wave][2 * i + fh][fc2 + 1];
+      }
+#pragma unroll
+      for (int i = 0; i < kMT / 2; ++i)
+        *reinterpret_cast<double2*>(beta + (ktp + 2 * i + fh) * ldb + cw0 + fc2) = v2[i];
+    } else if (cw0 < mp) {   // mp is a multiple of 128: whole waves are in or out
 #pragma unroll
       for (int i = 0; i < kMT / 2; ++i) {
         const int kk = 2 * i + fh;
@@ -721,19 +731,43 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     d4 acc[4];
 #pragma unroll
     for (int ct = 0; ct < 4; ++ct) acc[ct] = d4{0.0, 0.0, 0.0, 0.0};
+    // DP <= 32: all A fragments are read before the first MFMA (dims >= d are staged as zeros,
+    // so the norm runs over every ks and keeps the reads unconditional: one LDS latency per
+    // sub-tile instead of one per ks); the MFMAs skip ks >= nks.  DP >= 48 keeps the per-ks
+    // form: its VGPRs are already at the limit.
     double vnp = 0.0;
+    if constexpr (DP <= 32) {
+      double af[NKS];
 #pragma unroll
-    for (int ks = 0; ks < NKS; ++ks) {
-      if (ks < nks) {
-        const double a = vs[fr * VS + 4 * ks + fq];
-        vnp = fma(a, a, vnp);
+      for (int ks = 0; ks < NKS; ++ks) af[ks] = vs[fr * VS + 4 * ks + fq];
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) vnp = fma(af[ks], af[ks], vnp);
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        if (ks < nks) {
 #if WHITEN_ABL != 2
 #pragma unroll
-        for (int ct = 0; ct < 4; ++ct)
-          acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bf[ct][ks], acc[ct], 0, 0, 0);
+          for (int ct = 0; ct < 4; ++ct)
+            acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[ks], bf[ct][ks], acc[ct], 0, 0, 0);
 #else
-        acc[0][0] += a * bf[0][ks];
+          acc[0][0] += af[ks] * bf[0][ks];
 #endif
+        }
+      }
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < NKS; ++ks) {
+        if (ks < nks) {
+          const double a = vs[fr * VS + 4 * ks + fq];
+          vnp = fma(a, a, vnp);
+#if WHITEN_ABL != 2
+#pragma unroll
+          for (int ct = 0; ct < 4; ++ct)
+            acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bf[ct][ks], acc[ct], 0, 0, 0);
+#else
+          acc[0][0] += a * bf[0][ks];
+#endif
+        }
       }
     }
     vnp += __shfl_xor(vnp, 16, 64);
@@ -755,11 +789,11 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
-    for (int kk = 0; kk < nt; ++kk) {
+    auto step = [&](int kk) __attribute__((always_inline)) {
       const double x = colv ? xt[wave][kk][lane] : 0.0;
 #if WHITEN_ABL == 3
       xt[wave][kk][lane] = x;
-      continue;
+      return;
 #endif
       const double* rr = rl + kk * RS;
       double mm[SD];
@@ -777,6 +811,12 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
 #pragma unroll
       for (int i = 0; i < SD; ++i) hs[i] = fma(al, gl[kk * kGStride + i], hs[i]);
       xt[wave][kk][lane] = al;
+    };
+    if (nt == kMT) {   // unrolled: the next steps' LDS reads are issued under this step's chain
+#pragma unroll 4
+      for (int kk = 0; kk < kMT; ++kk) step(kk);
+    } else {
+      for (int kk = 0; kk < nt; ++kk) step(kk);
     }
     ntp = nt;
     ktp = kt;

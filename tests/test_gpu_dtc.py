@@ -29,6 +29,10 @@ CASES = [
     (257, 9, 17, 5, ("matern12", "matern52"), (3.0, 2.0, 4.0, 0.9, 0.05)),
     # M = 450: 8 diagonal blocks of the blocked 64 x 64 dense tail
     (700, 4, 450, 6, ("matern52", "matern52"), (1.1, 0.8, 0.9, 1.2, 0.3)),
+    # Gram v2 shapes with an odd number of 128-blocks (Mp = 384, 640): off-diagonal groups plus
+    # a diagonal group whose second block is missing
+    (800, 3, 300, 12, ("matern52", "matern52"), (1.2, 0.9, 1.0, 1.1, 0.25)),
+    (600, 3, 600, 13, ("matern32", "matern52"), (0.9, 1.1, 1.4, 0.9, 0.3)),
 ]
 
 
