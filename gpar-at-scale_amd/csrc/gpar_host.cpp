@@ -25,6 +25,11 @@ struct gpar_ctx {
   hipStream_t main = nullptr;     // the context's stream
   hipStream_t side = nullptr;     // second stream: alternate outputs of a batch run here
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
+  // the caller's stream, e.g. the copies that produce its device inputs
+  bool has_input_stream = false;
+  hipStream_t input_stream = nullptr;
+  hipEvent_t ev_input = nullptr;
   int lanes = 1;                  // gpar_ctx_set_lanes: streams a batch's outputs alternate over
   std::string err;
   struct Buf {
@@ -137,6 +142,7 @@ struct OnStream {
 constexpr int kChunk = 256;   // time-chunk length of the Kalman sweeps (power of two, multiple of 16)
 static_assert(kChunk == 256, "vec_fix runs one 256-thread block per chunk");
 constexpr int kSStride = 4;   // chunk state vectors padded to 4 doubles (device_common.hpp)
+constexpr int64_t kFusedMaxD = 64;   // widest input the fused Kfu + whitening kernels take
 
 static int sde_dim(int kind) {
   if (kind == GPAR_MATERN12) return 1;
@@ -175,15 +181,33 @@ static void check_sorted_host(const double* t, int64_t n) {
     ARGCHECK(t[k] >= t[k - 1], "time locations must be ascending (dtc.jl:102 does not sort)");
 }
 
-static DevProblem prepare_problem(gpar_ctx* c, const gpar_problem& p, int idx) {
+// Host-side argument checks of one problem (no device work).
+static void check_problem(const gpar_problem& p) {
   ARGCHECK(p.n >= 1 && p.m >= 1, "n and m must be >= 1");
   ARGCHECK(p.d >= 1, "d must be >= 1 (use the LGSSM entry points for time-only outputs)");
   ARGCHECK(p.ldv >= p.d && p.ldz >= p.d, "ldv/ldz must be >= d");
   ARGCHECK(p.t && p.v && p.z && p.y, "null input pointer");
   ARGCHECK(p.out_kernel >= 0 && p.out_kernel <= 3, "bad out_kernel");
+  ARGCHECK(p.time_kernel >= 0 && p.time_kernel <= 3, "bad time_kernel");
   ARGCHECK(p.mem == GPAR_MEM_HOST || p.mem == GPAR_MEM_DEVICE, "bad mem");
-  if (p.d > 64) throw Error(GPAR_ERR_UNSUPPORTED, "input dimension d > 64 not supported yet");
   if (p.m > 2048) throw Error(GPAR_ERR_UNSUPPORTED, "m > 2048 not supported");
+  (void)sde_dim(p.time_kernel);
+  if (p.mem == GPAR_MEM_HOST) check_sorted_host(p.t, p.n);
+}
+
+// Every problem of a batched call is validated before the first launch: a failure part-way
+// through the launch loop would leave kernels reading caller memory the caller then frees.
+static void check_batch(const gpar_problem* probs, int nprob) {
+  ARGCHECK(probs && nprob >= 1, "null argument");
+  for (int i = 0; i < nprob; ++i) {
+    check_problem(probs[i]);
+    ARGCHECK(probs[i].n == probs[0].n, "all problems of one call must share n");
+    ARGCHECK(probs[i].mem == probs[0].mem, "all problems of one call must share one memory space");
+  }
+}
+
+static DevProblem prepare_problem(gpar_ctx* c, const gpar_problem& p, int idx) {
+  check_problem(p);
   DevProblem d{};
   d.n = p.n;
   d.m = p.m;
@@ -198,15 +222,20 @@ static DevProblem prepare_problem(gpar_ctx* c, const gpar_problem& p, int idx) {
   d.qu_noise = p.qu_kuu_noise;
   d.t_user = p.t;
   // Z is theta-independent: its group centres are computed once per prepared problem
-  double* zc = ws<double>(c, "prob" + std::to_string(idx) + "_zc", (size_t)((d.mp + 255) / 256) * 64);
+  double* zc = ws<double>(c, "prob" + std::to_string(idx) + "_zc",
+                          (size_t)((d.mp + 255) / 256) * zc_stride((int)d.d));
   d.zc = zc;
+  auto centres = [&]() {
+    if (d.ok == GPAR_MATERN12) return;
+    if (d.d <= kFusedMaxD) launch_zcenter(c->stream, d.z, d.ldz, (int)d.d, d.m, d.mp, zc);
+    else launch_zcenter_wide(c->stream, d.z, d.ldz, (int)d.d, d.m, d.mp, zc);
+  };
   if (p.mem == GPAR_MEM_DEVICE) {
     d.t = p.t; d.v = p.v; d.z = p.z; d.y = p.y;
     d.ldv = p.ldv; d.ldz = p.ldz;
-    if (d.ok != GPAR_MATERN12) launch_zcenter(c->stream, d.z, d.ldz, (int)d.d, d.m, d.mp, zc);
+    centres();
     return d;
   }
-  check_sorted_host(p.t, p.n);
   const std::string k = "prob" + std::to_string(idx);
   double* t = ws<double>(c, k + "_t", p.n);
   double* v = ws<double>(c, k + "_v", (size_t)p.n * p.d);
@@ -220,7 +249,7 @@ static DevProblem prepare_problem(gpar_ctx* c, const gpar_problem& p, int idx) {
                             p.d * sizeof(double), p.m, hipMemcpyHostToDevice, c->stream));
   d.t = t; d.v = v; d.z = z; d.y = y;
   d.ldv = p.d; d.ldz = p.d;
-  if (d.ok != GPAR_MATERN12) launch_zcenter(c->stream, d.z, d.ldz, (int)d.d, d.m, d.mp, zc);
+  centres();
   return d;
 }
 
@@ -276,11 +305,18 @@ static GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
 
 // Kfu assembly + chunk-local whitening: fp64-MFMA Gram-form kernel for the smooth output
 // kernels, direct-difference kernel for Matern-1/2 (kappa not smooth in d^2 at 0).
+// Inputs wider than kFusedMaxD (the fused kernels keep a column's pseudo-input in registers):
+// the squared distances are a separate MFMA (or direct-difference) pass into beta itself, which
+// the whitening then reads and overwrites in place (k_dist.hip).
 static void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const double* rec, const double* v,
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
                            int64_t ldb, double* send, const double* g, double* hsum) {
   const double s_o = th.sv_o * th.sv_o;
-  if (p.ok == GPAR_MATERN12) {
+  if (p.d > kFusedMaxD) {
+    launch_dist2(c->stream, p.ok, v, ldv, n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, beta, ldb);
+    launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, beta, ldb, p.m, p.mp, n, kChunk, nch,
+                         1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum);
+  } else if (p.ok == GPAR_MATERN12) {
     launch_whiten_kfu(c->stream, p.tk, p.ok, rec, v, ldv, (int)p.d, p.z, p.ldz, p.m, p.mp, n,
                       kChunk, nch, 1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum);
   } else {
@@ -383,7 +419,6 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   }
   for (int i = 0; i < np; ++i) {
     const DevProblem& p = P[i];
-    ARGCHECK(p.n == n, "all problems of one call must share n");
     const int lane = i % nlanes;
     OnStream on_(c, lane ? c->side : c->main);
     const std::string sfx = lane ? "_1" : "";
@@ -842,21 +877,41 @@ static double unpack(double p) { return std::exp(p) + 1e-3; }
 
 using namespace gpar;
 
+// Entry: order the context's streams after the caller's input stream (if one was set).
+static void enter(gpar_ctx* c) {
+  c->err.clear();
+  HIPCHECK(hipSetDevice(c->device));
+  c->stream = c->main;
+  if (c->has_input_stream) {
+    HIPCHECK(hipEventRecord(c->ev_input, c->input_stream));
+    HIPCHECK(hipStreamWaitEvent(c->main, c->ev_input, 0));
+    HIPCHECK(hipStreamWaitEvent(c->side, c->ev_input, 0));
+  }
+}
+
+// Failure exit: nothing queued by the failed call may still be reading caller memory when the
+// error returns (callers free their inputs on an error), so both streams are drained first.
+static int fail(gpar_ctx* c, int code, const char* what) {
+  c->err = what;
+  c->stream = c->main;
+  (void)hipStreamSynchronize(c->main);
+  (void)hipStreamSynchronize(c->side);
+  (void)hipGetLastError();
+  return code;
+}
+
 #define API_BEGIN(ctx)                                          \
   if (!(ctx)) return GPAR_ERR_STATE;                            \
   try {                                                         \
-    (ctx)->err.clear();                                         \
-    HIPCHECK(hipSetDevice((ctx)->device));
+    enter(ctx);
 
 #define API_END(ctx)                                            \
   }                                                             \
   catch (const gpar::Error& e) {                                \
-    (ctx)->err = e.what();                                      \
-    return e.code;                                              \
+    return fail((ctx), e.code, e.what());                       \
   }                                                             \
   catch (const std::exception& e) {                             \
-    (ctx)->err = e.what();                                      \
-    return GPAR_ERR_HIP;                                        \
+    return fail((ctx), GPAR_ERR_HIP, e.what());                 \
   }                                                             \
   return GPAR_OK;
 
@@ -876,7 +931,8 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
   if (hipStreamCreateWithFlags(&c->main, hipStreamNonBlocking) != hipSuccess ||
       hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_input, hipEventDisableTiming) != hipSuccess) {
     delete c;
     return GPAR_ERR_HIP;
   }
@@ -894,6 +950,7 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
     if (kv.second.p) (void)hipFree(kv.second.p);
   (void)hipEventDestroy(ctx->ev_fork);
   (void)hipEventDestroy(ctx->ev_join);
+  (void)hipEventDestroy(ctx->ev_input);
   (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->main);
   delete ctx;
@@ -934,6 +991,13 @@ int32_t gpar_ctx_kernel_stats(gpar_ctx* ctx, const char* name, int64_t* launches
   API_END(ctx)
 }
 
+int32_t gpar_ctx_set_input_stream(gpar_ctx* ctx, void* stream, int32_t enable) {
+  if (!ctx) return GPAR_ERR_STATE;
+  ctx->has_input_stream = enable != 0;
+  ctx->input_stream = reinterpret_cast<hipStream_t>(stream);
+  return GPAR_OK;
+}
+
 int32_t gpar_ctx_set_lanes(gpar_ctx* ctx, int32_t lanes) {
   if (!ctx) return GPAR_ERR_STATE;
   if (lanes != 1 && lanes != 2) {
@@ -955,6 +1019,7 @@ int32_t gpar_dtc_objective(gpar_ctx* ctx, const gpar_problem* probs, int32_t npr
                            const double* theta, double* dtc_out) {
   API_BEGIN(ctx)
   ARGCHECK(probs && nprob >= 1 && theta && dtc_out, "null argument");
+  check_batch(probs, nprob);
   std::vector<DevProblem> P;
   for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
   std::vector<Theta> th = thetas_from(theta, nprob);
@@ -1048,6 +1113,7 @@ int32_t gpar_fit(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
                  double* nlml_out, int32_t* evals_out) {
   API_BEGIN(ctx)
   ARGCHECK(probs && nprob >= 1 && log_theta0 && theta_out, "null argument");
+  check_batch(probs, nprob);
   gpar_fit_options o{0, 1000, 1e-8, 0.0};
   if (opts) o = *opts;
   std::vector<DevProblem> P;
@@ -1072,8 +1138,8 @@ int32_t gpar_fit_predict(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob
   for (int i = 0; i < nprob; ++i) {
     ARGCHECK(v_star[i] && mean_out[i] && std_out[i], "null per-output pointer");
     ARGCHECK(ldvs[i] >= probs[i].d, "ldvs must be >= d");
-    ARGCHECK(probs[i].mem == probs[0].mem, "all outputs must share one memory space");
   }
+  check_batch(probs, nprob);
   gpar_fit_options o{0, 1000, 1e-8, 0.0};
   if (opts) o = *opts;
   std::vector<DevProblem> P;
@@ -1254,7 +1320,7 @@ int32_t gpar_sde_predictions(gpar_ctx* ctx, int32_t nchains, int64_t n, const do
     sync(ctx);
     dt = tt; dy = yy; dts = ts; ldyd = n;
   }
-  // ---- NM fit of (l, process_var, noise_sigma) per chain on -logpdf (temporal_gp_inference.jl:286-300)
+  // ---- NM fit of (l, process_var, noise_sigma) per chain on -logpdf (temporal_gp_inference.jl:69-82)
   std::vector<NelderMead> nm;
   nm.reserve(nchains);
   for (int i = 0; i < nchains; ++i)

@@ -1,7 +1,7 @@
 // k_lgssm.hip -- state-space (Kalman) sweeps of the time GP on gfx950.
 //
 // Replaces the sequential TemporalGPs `decorrelate`/`logpdf` calls of the reference
-// (dtc.jl:106-117, gpar_scaled_inference.jl:170-183, temporal_gp_inference.jl:295) with a
+// (dtc.jl:106-117, gpar_scaled_inference.jl:170-183, temporal_gp_inference.jl:78) with a
 // time-chunked formulation whose every sequential dependency is short:
 //
 //  gains (data-independent, per chain = per output or temporal chain):
@@ -80,7 +80,7 @@ __device__ __forceinline__ void elem_combine(const Elem<D>& e1, const Elem<D>& e
 
 // Observation noise of step k: the shared per-step vector when given (prediction grids: 1e10 at
 // test points, gpar_scaled_inference.jl:100-107), where a negative entry means "this chain's
-// own sigma^2" (train points of chains with different sigma, temporal_gp_inference.jl:310-313).
+// own sigma^2" (train points of chains with different sigma, temporal_gp_inference.jl:93-97).
 __device__ __forceinline__ double step_noise(const double* __restrict__ noise, int64_t k,
                                             const ChainParams& cp) {
   if (!noise) return cp.r;

@@ -101,6 +101,21 @@ void launch_whiten_kfu_mfma(hipStream_t st, int time_kind, int out_kind, const d
                             const double* zc, int64_t m, int64_t mp, int64_t n, int L, int64_t nch,
                             double inv_lo, double s_o, double* beta, int64_t ldb, double* send,
                             int64_t mc, const double* g, double* hsum);
+// k_dist.hip: D > 64 (and any D when the distances are precomputed).  zc_stride(d): doubles per
+// 256-column group in the centres array (launch_zcenter for d <= 64, launch_zcenter_wide above).
+int64_t zc_stride(int d);
+void launch_zcenter_wide(hipStream_t st, const double* z, int64_t ldz, int d, int64_t m,
+                         int64_t mp, double* zc);
+// d2[k][c] (k < n, c < mp; 0 for c >= m) into out (ld ldo): MFMA Gram form, centred per 256-column
+// group (smooth kernels), or direct differences (out_kind = Matern-1/2)
+void launch_dist2(hipStream_t st, int out_kind, const double* v, int64_t ldv, int64_t n,
+                  const double* z, int64_t ldz, int64_t m, int64_t mp, int d, const double* zc,
+                  double* out, int64_t ldo);
+// whiten_kfu from precomputed squared distances (src may equal beta: in place)
+void launch_whiten_kfu_d2(hipStream_t st, int time_kind, int out_kind, const double* rec,
+                          const double* src, int64_t lds, int64_t m, int64_t mp, int64_t n, int L,
+                          int64_t nch, double inv_lo, double s_o, double* beta, int64_t ldb,
+                          double* send, int64_t mc, const double* g, double* hsum);
 void launch_whiten_vec(hipStream_t st, int sdim, const double* rec, int64_t recstride,
                        const double* y, int64_t ldy, int64_t n, int L, int64_t nch, int nchains,
                        double* alpha, int64_t lda, double* send, int64_t sendstride, int64_t mc,

@@ -1,7 +1,7 @@
 // nelder_mead.hpp -- Optim.jl NelderMead() as an ask/tell state machine.
 //
 // Restates the optimiser the reference calls at dtc.jl:58-61 (and
-// temporal_gp_inference.jl:299, optimized.jl:45,164): AffineSimplexer(a = 0.025, b = 0.5),
+// temporal_gp_inference.jl:82, optimized.jl:45,164): AffineSimplexer(a = 0.025, b = 0.5),
 // AdaptiveParameters (alpha = 1, beta = 1 + 2/n, gamma = 0.75 - 1/(2n), delta = 1 - 1/n),
 // convergence on the simplex value spread (g_tol), iteration cap, wall-clock time_limit,
 // and Optim's after_while! (evaluate the centroid, keep the better of it and the best

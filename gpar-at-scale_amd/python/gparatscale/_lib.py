@@ -27,7 +27,7 @@ EXPORTED = (
     "gpar_fit", "gpar_fit_predict", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
     "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_reset_stats",
-    "gpar_ctx_set_lanes", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
+    "gpar_ctx_set_lanes", "gpar_ctx_set_input_stream", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
 )
 
 
@@ -45,7 +45,7 @@ class PosDefException(GparError):
 
 
 class DomainError(GparError, ValueError):
-    """Mirrors Julia's DomainError / ArgumentError on malformed inputs (util.jl:127-133)."""
+    """Mirrors Julia's DomainError / ArgumentError on malformed inputs (util.jl:112-117)."""
 
 
 class Unsupported(GparError):
@@ -94,6 +94,7 @@ def load(path: str | None = None):
             "gpar_ctx_kernel_stats": (i32, [vp, C.c_char_p, C.POINTER(i64), C.POINTER(C.c_double)]),
             "gpar_ctx_reset_stats": (i32, [vp]),
             "gpar_ctx_set_lanes": (i32, [vp, i32]),
+            "gpar_ctx_set_input_stream": (i32, [vp, vp, i32]),
             "gpar_dtc_objective": (i32, [vp, C.POINTER(GparProblem), i32, dp, dp]),
             "gpar_dtc_objective_A": (i32, [vp, C.POINTER(GparProblem), dp, dp, dp]),
             "gpar_fit": (i32, [vp, C.POINTER(GparProblem), i32, dp, C.POINTER(GparFitOptions),
@@ -180,11 +181,16 @@ class Context:
         self.check(load().gpar_ctx_kernel_stats(self.h, name.encode(), C.byref(n), C.byref(ms)))
         return int(n.value), float(ms.value)
 
+    def follow_stream(self, stream_ptr):
+        """Order every later call after the work queued on `stream_ptr` (a hipStream_t handle,
+        e.g. torch.cuda.current_stream().cuda_stream) at the time of the call."""
+        self.check(load().gpar_ctx_set_input_stream(self.h, C.c_void_p(int(stream_ptr)), 1))
+
     def reset_stats(self):
         self.check(load().gpar_ctx_reset_stats(self.h))
 
     def set_lanes(self, lanes):
-        """1: serial batched evaluation; 2 (default): outputs alternate over two HIP streams."""
+        """1 (the default): serial batched evaluation; 2: outputs alternate over two HIP streams."""
         self.check(load().gpar_ctx_set_lanes(self.h, int(lanes)))
 
 

@@ -11,8 +11,8 @@ Reference functions mirrored (TudorParas/GPAR-at-scale):
   create_optim_gp[_post] / create_optim_gpar[_post] logpdf / marginals  src/gp/optimized.jl
 
 Inputs follow the reference's conventions: V / Z are ColVecs-like D x N matrices (or a list of
-D length-N vectors, util.jl:16-31); theta in natural units (unpack_gpar, util.jl:61-71);
-initial values are log-params (i_log_*), missing ones drawn U(0,1) like util.jl:144-150.
+D length-N vectors, util.jl:16-31); theta in natural units (unpack_gpar, util.jl:45-55);
+initial values are log-params (i_log_*), missing ones drawn U(0,1) like util.jl:128-134.
 Host numpy arrays go through GPAR_MEM_HOST; torch CUDA tensors (rows = points) through
 GPAR_MEM_DEVICE without host copies.
 """
@@ -31,24 +31,24 @@ DEFAULT_TIME_LIMIT = 1000.0  # dtc.jl:21
 
 # ----------------------------------------------------------------------------- util.jl
 def unpack_gp(params):
-    """util.jl:52-59."""
+    """util.jl:36-43."""
     return tuple(float(np.exp(p) + 1e-3) for p in list(params)[:3])
 
 
 def unpack_gpar(params):
-    """util.jl:61-71."""
+    """util.jl:45-55."""
     return tuple(float(np.exp(p) + 1e-3) for p in list(params)[:5])
 
 
 def get_time_mask(input_length):
-    """util.jl:118-122."""
+    """util.jl:102-106."""
     m = np.zeros(input_length)
     m[0] = 1.0
     return m
 
 
 def get_output_mask(input_length):
-    """util.jl:127-139; DomainError for input_length <= 1."""
+    """util.jl:111-123; DomainError for input_length <= 1."""
     if input_length <= 1:
         raise _lib.DomainError(_lib.GPAR_ERR_ARG, "Input length must be integer greater than 1")
     m = np.zeros((input_length - 1, input_length))
@@ -58,13 +58,25 @@ def get_output_mask(input_length):
 
 
 def parse_initial_params(vals, rng=None):
-    """util.jl:144-185: missing initial log-params are U(0,1) draws."""
+    """util.jl:141-169: missing initial log-params are U(0,1) draws."""
     rng = rng if rng is not None else np.random.default_rng()
     return np.array([rng.random() if v is None else float(v) for v in vals], dtype=np.float64)
 
 
+def parse_initial_gp_params(i_log_l, i_log_process_var, i_log_noise_sigma, rng=None):
+    """util.jl:141-147."""
+    return parse_initial_params([i_log_l, i_log_process_var, i_log_noise_sigma], rng)
+
+
+def parse_initial_gpar_params(i_log_time_l, i_log_time_var, i_log_out_l, i_log_out_var,
+                              i_log_noise_sigma, rng=None):
+    """util.jl:154-169."""
+    return parse_initial_params([i_log_time_l, i_log_time_var, i_log_out_l, i_log_out_var,
+                                 i_log_noise_sigma], rng)
+
+
 def to_colvecs(inputs):
-    """util.jl:32-47: list of per-dimension vectors -> D x N."""
+    """util.jl:16-31: list of per-dimension vectors -> D x N."""
     if _is_torch(inputs):
         return inputs
     if isinstance(inputs, np.ndarray):
@@ -118,6 +130,17 @@ def _dev_vec(x, keep):
     return x.data_ptr()
 
 
+def _order_after_torch(ctx):
+    """Device inputs are produced on torch's current stream (a .contiguous() copy above may still
+    be in flight): the library's streams wait for it, device side, before the call's kernels."""
+    import torch
+    ctx.follow_stream(torch.cuda.current_stream(ctx.device).cuda_stream)
+
+
+def _arg_error(msg):
+    return _lib.DomainError(_lib.GPAR_ERR_ARG, msg)
+
+
 def make_problem(V, Z, t, y, out_kernel="matern52", time_kernel="matern52", kuu_noise=True,
                  keep=None, qu_kuu_noise=False):
     """Build a gpar_problem.  Host: V, Z as D x N / D x M (ColVecs).  Device: torch tensors
@@ -131,6 +154,9 @@ def make_problem(V, Z, t, y, out_kernel="matern52", time_kernel="matern52", kuu_
         p.t = _dev_vec(t, keep)
         p.y = _dev_vec(y, keep)
         p.mem = _lib.GPAR_MEM_DEVICE
+        # the C side cannot see device buffer lengths: check them here
+        if t.numel() != n or y.numel() != n:
+            raise _arg_error("t, y and V must have the same length")
     else:
         p.v, p.ldv, n, d = _host_points(V, keep)
         p.z, p.ldz, m, dz = _host_points(Z, keep)
@@ -138,7 +164,7 @@ def make_problem(V, Z, t, y, out_kernel="matern52", time_kernel="matern52", kuu_
         p.y = _host_vec(y, keep)
         p.mem = _lib.GPAR_MEM_HOST
         if len(np.asarray(t)) != n or len(np.asarray(y)) != n:
-            raise _lib.DomainError(_lib.GPAR_ERR_ARG, "t, y and V must have the same length")
+            raise _arg_error("t, y and V must have the same length")
     if d != dz:
         raise _lib.DomainError(_lib.GPAR_ERR_ARG, "V and Z must have the same dimension")
     p.n, p.m, p.d = n, m, d
@@ -165,6 +191,8 @@ def compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel="matern52", time_ke
     p, keep = make_problem(V, Z, t, y, out_kernel, time_kernel, kuu_noise)
     th = np.ascontiguousarray(np.asarray(theta, dtype=np.float64).reshape(5))
     out = np.zeros(1)
+    if p.mem == _lib.GPAR_MEM_DEVICE:
+        _order_after_torch(ctx)
     if return_A:
         A = np.zeros((p.n, p.m))  # column-major M x N == row-major N x M
         ctx.check(lib.gpar_dtc_objective_A(ctx.h, C.byref(p), _ptr(th), _ptr(out), _ptr(A)))
@@ -180,6 +208,8 @@ def dtc_objective_batch(problems, thetas, device=0):
     arr = (GparProblem * len(problems))(*problems)
     th = np.ascontiguousarray(np.asarray(thetas, dtype=np.float64).reshape(len(problems), 5))
     out = np.zeros(len(problems))
+    if problems[0].mem == _lib.GPAR_MEM_DEVICE:
+        _order_after_torch(ctx)
     ctx.check(lib.gpar_dtc_objective(ctx.h, arr, len(problems), _ptr(th), _ptr(out)))
     return out
 
@@ -204,6 +234,8 @@ def fit_batch(problems, log_theta0, max_evals=0, max_iterations=1000, g_tol=1e-8
     theta = np.zeros((P, 5))
     nlml = np.zeros(P)
     evals = np.zeros(P, dtype=np.int32)
+    if problems[0].mem == _lib.GPAR_MEM_DEVICE:
+        _order_after_torch(ctx)
     ctx.check(lib.gpar_fit(ctx.h, arr, P, _ptr(x0), C.byref(opts), _ptr(theta), _ptr(nlml),
                            _ptr(evals)))
     return FitResult(theta, nlml, evals)
@@ -231,11 +263,16 @@ def fit_predict_batch(problems, log_theta0, t_star, V_stars, max_evals=0, max_it
     evals = np.zeros(P, dtype=np.int32)
     dev = problems[0].mem == _lib.GPAR_MEM_DEVICE
     vptr, ldvs, means, stds = [], [], [], []
+    if len(V_stars) != P:
+        raise _arg_error("one V_star per problem")
+    n_star = t_star.numel() if dev else len(np.asarray(t_star))
     if dev:
         import torch
         tsp = _dev_vec(t_star, keep)
-        for Vs in V_stars:
-            p_, ld_, ns, _ = _dev_points(Vs, keep)
+        for i, Vs in enumerate(V_stars):
+            p_, ld_, ns, ds = _dev_points(Vs, keep)
+            if ns != n_star or ds != problems[i].d:
+                raise _arg_error(f"V_stars[{i}] must be N* x D = {n_star} x {problems[i].d}")
             vptr.append(p_)
             ldvs.append(ld_)
             means.append(torch.empty(ns, dtype=torch.float64, device=t_star.device))
@@ -244,15 +281,19 @@ def fit_predict_batch(problems, log_theta0, t_star, V_stars, max_evals=0, max_it
         sp_ = [x.data_ptr() for x in stds]
     else:
         tsp = _host_vec(t_star, keep)
-        for Vs in V_stars:
-            p_, ld_, ns, _ = _host_points(Vs, keep)
+        for i, Vs in enumerate(V_stars):
+            p_, ld_, ns, ds = _host_points(Vs, keep)
+            if ns != n_star or ds != problems[i].d:
+                raise _arg_error(f"V_stars[{i}] must be D x N* = {problems[i].d} x {n_star}")
             vptr.append(p_)
             ldvs.append(ld_)
             means.append(np.zeros(ns))
             stds.append(np.zeros(ns))
         mp_ = [m.ctypes.data for m in means]
         sp_ = [x.ctypes.data for x in stds]
-    ns = len(t_star)
+    ns = n_star
+    if dev:
+        _order_after_torch(ctx)
     VP = (C.c_void_p * P)(*vptr)
     LD = (C.c_int64 * P)(*ldvs)
     MP = (C.c_void_p * P)(*mp_)
@@ -282,17 +323,20 @@ def get_optim_scaled_gpar_params(input_locations, pseudo_input_locations, time_l
 
 # ----------------------------------------------------------------------------- q(u)
 def compute_q_u(input_locations, pseudo_input_locations, time_loc, outputs, theta,
-                out_kernel="matern52", time_kernel="matern52", device=0):
-    """gpar_scaled_inference.jl:141-196 -> (m_e, cov_e = inv(D), U_u upper)."""
+                out_kernel="matern52", time_kernel="matern52", device=0, qu_kuu_noise=False):
+    """gpar_scaled_inference.jl:141-196 -> (m_e, cov_e = inv(D), U_u upper).  qu_kuu_noise:
+    Cuu + sigma^2 I instead of the reference's noise-free Cuu (:157), as gpar_problem documents."""
     ctx = context(device)
     lib = _lib.load()
     p, keep = make_problem(input_locations, pseudo_input_locations, time_loc, outputs,
-                           out_kernel, time_kernel)
+                           out_kernel, time_kernel, qu_kuu_noise=qu_kuu_noise)
     th = np.ascontiguousarray(np.asarray(theta, dtype=np.float64).reshape(5))
     m = p.m
     me = np.zeros(m)
     cov = np.zeros((m, m))
     U = np.zeros((m, m))  # column-major -> read as transposed
+    if p.mem == _lib.GPAR_MEM_DEVICE:
+        _order_after_torch(ctx)
     ctx.check(lib.gpar_q_u(ctx.h, C.byref(p), _ptr(th), _ptr(me), _ptr(cov), _ptr(U)))
     return me, cov, U.T.copy()
 
@@ -314,7 +358,7 @@ def create_lgssm(latent_locations, l, process_var, noise_sigma, kernel_structure
 
 
 def logpdf(lgssm: LGSSMSpec, y, device=0):
-    """logpdf(lgssm, y) (temporal_gp_inference.jl:295)."""
+    """logpdf(lgssm, y) (temporal_gp_inference.jl:78)."""
     return float(lgssm_logpdf_batch(lgssm.t, np.asarray(y, dtype=np.float64)[None, :],
                                     [[lgssm.l, lgssm.process_var, lgssm.noise_sigma]],
                                     lgssm.kernel, device)[0])
@@ -354,6 +398,9 @@ def predict_scaled(input_locations, pseudo_input_locations, time_loc, outputs, t
         import torch
         vsp, ldvs, ns, ds = _dev_points(inference_input_locations, keep)
         tsp = _dev_vec(inference_time_loc, keep)
+        if ns != inference_time_loc.numel() or ds != p.d:
+            raise _arg_error("inference inputs must be N* x D with N* = len(inference_time_loc)")
+        _order_after_torch(ctx)
         mean = torch.empty(ns, dtype=torch.float64, device=inference_time_loc.device)
         std = torch.empty(ns, dtype=torch.float64, device=inference_time_loc.device)
         ctx.check(lib.gpar_predict(ctx.h, C.byref(p), _ptr(th), ns, tsp, vsp, ldvs, md,
@@ -361,8 +408,9 @@ def predict_scaled(input_locations, pseudo_input_locations, time_loc, outputs, t
         return mean, std
     vsp, ldvs, ns, ds = _host_points(inference_input_locations, keep)
     tsp = _host_vec(inference_time_loc, keep)
-    if ds != p.d:
-        raise _lib.DomainError(_lib.GPAR_ERR_ARG, "inference inputs must have the training dimension")
+    if ds != p.d or ns != len(np.asarray(inference_time_loc)):
+        raise _arg_error("inference inputs must have the training dimension and one point per "
+                         "inference time")
     mean = np.zeros(ns)
     std = np.zeros(ns)
     ctx.check(lib.gpar_predict(ctx.h, C.byref(p), _ptr(th), ns, tsp, vsp, ldvs, md, int(samples),
@@ -455,8 +503,13 @@ def get_sde_predictions_device(t, Y, t_star, kernel_structure="matern52", log_th
     ns = t_star.shape[0]
     mean = torch.empty((nch, ns), dtype=torch.float64, device=t.device)
     var = torch.empty((nch, ns), dtype=torch.float64, device=t.device)
-    ctx.check(lib.gpar_sde_predictions(ctx.h, nch, n, _dev_vec(t, keep), Y2.data_ptr(), n, ns,
-                                       _dev_vec(t_star, keep), _kernel_id(kernel_structure),
+    if t.numel() != n:
+        raise _arg_error("t and Y must have the same length")
+    ts_ = _dev_vec(t_star, keep)
+    tt_ = _dev_vec(t, keep)
+    _order_after_torch(ctx)
+    ctx.check(lib.gpar_sde_predictions(ctx.h, nch, n, tt_, Y2.data_ptr(), n, ns,
+                                       ts_, _kernel_id(kernel_structure),
                                        _ptr(x0), C.byref(opts), _lib.GPAR_MEM_DEVICE, _ptr(theta),
                                        mean.data_ptr(), var.data_ptr()))
     if nch == 1:

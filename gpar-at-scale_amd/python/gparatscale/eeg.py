@@ -64,7 +64,7 @@ def run_eeg(data: dict, max_evals: int = 0, time_limit: float = 3.0, mode: str =
 
     max_evals > 0 bounds every Nelder-Mead run (reproducible); otherwise the fits stop on
     g_tol / iterations, and the scaled ones at `time_limit` seconds (eeg.jl: 3.0).  Missing
-    initial log-parameters are drawn U(0,1) from `seed` (util.jl:144-150)."""
+    initial log-parameters are drawn U(0,1) from `seed` (util.jl:128-134)."""
     rng = np.random.default_rng(seed)
     tr = data["train"]
     t_all = tr["time"]

@@ -10,7 +10,7 @@
  *   - return value: gpar_status (0 = OK); gpar_last_error(ctx) describes the failure.
  *     GPAR_ERR_NOT_PD mirrors Julia's PosDefException thrown by `cholesky`
  *     (dtc.jl:119-120, gpar_scaled_inference.jl:159,188); GPAR_ERR_ARG mirrors the
- *     DomainError of util.jl:127-133 and malformed inputs.
+ *     DomainError of util.jl:112-117 and malformed inputs.
  *   - fp64 only.  Sizes are int64_t.  Calls are synchronous on return.
  *   - Pointers are borrowed: read-only inputs, never retained past return.  Inputs live
  *     in host memory (mem = GPAR_MEM_HOST) or are already resident in device HBM
@@ -19,7 +19,7 @@
  *   - Inputs V (one point = one column of the reference's ColVecs, util.jl:16-31): point k,
  *     dimension i lives at v[k*ldv + i]; ldv >= d lets V be a view into an N x P
  *     row-major output matrix (GPAR's previous outputs).
- *   - theta in natural units, as returned by unpack_gpar (util.jl:61-71):
+ *   - theta in natural units, as returned by unpack_gpar (util.jl:45-55):
  *     (time_l, time_var, out_l, out_var, noise_sigma); kernel variances are the squares
  *     (dtc.jl:31,37).  log_theta = the reference's i_log_* initial values.
  *   - One gpar_ctx per GPU, one host thread per ctx (not thread-safe).
@@ -109,9 +109,14 @@ int32_t gpar_ctx_kernel_stats(gpar_ctx* ctx, const char* name, int64_t* launches
 int32_t gpar_ctx_reset_stats(gpar_ctx* ctx);
 /* Concurrency of batched calls (gpar_dtc_objective / gpar_fit with nprob > 1): lanes = 2
  * alternates the outputs' whitening + Gram between two HIP streams with separate workspaces so
- * one output's whitening overlaps another's Gram (~2 % faster at N = 1e6, M = 512, two beta
- * buffers); 1 (default) serialises them on the context stream. */
+ * one output's whitening overlaps another's Gram (~1 % faster at N = 1e6, M = 512, two beta
+ * buffers); 1 (the default) serialises them on the context stream. */
 int32_t gpar_ctx_set_lanes(gpar_ctx* ctx, int32_t lanes);
+/* Producer ordering for GPAR_MEM_DEVICE inputs: with enable = 1, every later call on ctx first
+ * makes its streams wait (device side, hipStreamWaitEvent) for all work queued so far on
+ * `stream` (a hipStream_t; 0 = the null stream), e.g. the copies that produced its device inputs
+ * on the caller's stream.  enable = 0 turns it off (the default). */
+int32_t gpar_ctx_set_input_stream(gpar_ctx* ctx, void* stream, int32_t enable);
 
 /* ---------------------------------------------------------------- DTC objective
  * Replaces compute_gpar_dtc_objective (src/gp/dtc.jl:83-128), batched over `nprob`
@@ -176,9 +181,9 @@ int32_t gpar_fit_predict(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob
 /* ---------------------------------------------------------------- temporal-only (LGSSM) chains
  * `nchains` independent chains sharing the time grid t [n] (ascending); chain c's
  * observations at y[c*ldy + k].  theta: nchains x 3 natural (l, process_var, noise_sigma)
- * (unpack_gp, util.jl:52-59), host.
+ * (unpack_gp, util.jl:36-43), host.
  *
- * logpdf(create_lgssm(t, l, pv, sigma, k), y)  (temporal_gp_inference.jl:286-296):
+ * logpdf(create_lgssm(t, l, pv, sigma, k), y)  (temporal_gp_inference.jl:69-82):
  * lml_out [nchains] host. */
 int32_t gpar_lgssm_logpdf(gpar_ctx* ctx, int32_t nchains, int64_t n, const double* t,
                           const double* y, int64_t ldy, int32_t kernel, const double* theta,

@@ -16,7 +16,7 @@ for the hot path, following the reference's own operation order:
 * ``get_gpar_scaled_predictions``     src/gp/gpar_scaled_inference.jl:20-136
 * ``create_lgssm`` / ``get_sde_predictions``  src/gp/temporal_gp_inference.jl:15-114
 * exact GP / GPAR                     src/gp/optimized.jl:19-239
-* ``unpack_gp[ar]``, masks, init      src/util.jl:52-185
+* ``unpack_gp[ar]``, masks, init      src/util.jl:36-169
 * toy data                            src/data/toy_data.jl:9-98
 
 The arithmetic the reference delegates to third-party Julia packages is restated
@@ -63,26 +63,26 @@ KERNEL_ID = {k: i for i, k in enumerate(KERNELS)}
 
 # ----------------------------------------------------------------------------- util.jl
 def unpack_gp(params):
-    """src/util.jl:52-59 -> (l, process_var, noise_sigma) = exp(p) + 1e-3."""
+    """src/util.jl:36-43 -> (l, process_var, noise_sigma) = exp(p) + 1e-3."""
     p = np.asarray(params, dtype=np.float64)
     return tuple(float(np.exp(v) + 1e-3) for v in p[:3])
 
 
 def unpack_gpar(params):
-    """src/util.jl:61-71 -> (time_l, time_var, out_l, out_var, noise_sigma)."""
+    """src/util.jl:45-55 -> (time_l, time_var, out_l, out_var, noise_sigma)."""
     p = np.asarray(params, dtype=np.float64)
     return tuple(float(np.exp(v) + 1e-3) for v in p[:5])
 
 
 def get_time_mask(input_length):
-    """src/util.jl:118-122."""
+    """src/util.jl:102-106."""
     m = np.zeros(input_length)
     m[0] = 1.0
     return m
 
 
 def get_output_mask(input_length):
-    """src/util.jl:127-139 (DomainError for input_length <= 1)."""
+    """src/util.jl:111-123 (DomainError for input_length <= 1)."""
     if input_length <= 1:
         raise ValueError("Input length must be integer greater than 1")
     m = np.zeros((input_length - 1, input_length))
@@ -92,13 +92,13 @@ def get_output_mask(input_length):
 
 
 def parse_initial_params(vals, rng=None):
-    """src/util.jl:144-185: missing initial log-params are drawn U(0,1) (rand())."""
+    """src/util.jl:141-169: missing initial log-params are drawn U(0,1) (rand())."""
     rng = rng if rng is not None else np.random.default_rng()
     return np.array([rng.random() if v is None else float(v) for v in vals])
 
 
 def to_colvecs(inputs):
-    """src/util.jl:32-47: list of 1-D arrays (one per input dim) -> D x N matrix."""
+    """src/util.jl:16-31: list of 1-D arrays (one per input dim) -> D x N matrix."""
     if isinstance(inputs, np.ndarray):
         return np.atleast_2d(np.asarray(inputs, dtype=np.float64))
     return np.vstack([np.asarray(a, dtype=np.float64) for a in inputs])
@@ -277,7 +277,7 @@ def decorrelate(lg, X):
 
 
 def lgssm_logpdf(lg, y):
-    """TemporalGPs ``logpdf(lgssm, y)`` (temporal_gp_inference.jl:295)."""
+    """TemporalGPs ``logpdf(lgssm, y)`` (temporal_gp_inference.jl:78)."""
     return float(decorrelate(lg, y)[0])
 
 
@@ -542,8 +542,12 @@ def get_optim_scaled_gpar_params(V, Z, t, y, out_kernel="matern52", time_kernel=
     return (theta, nm) if return_nm else theta
 
 
-def compute_q_u(V, Z, t, y, theta, out_kernel="matern52", time_kernel="matern52"):
-    """src/gp/gpar_scaled_inference.jl:141-196.  Cuu has NO noise (:157).
+def compute_q_u(V, Z, t, y, theta, out_kernel="matern52", time_kernel="matern52",
+                qu_kuu_noise=False):
+    """src/gp/gpar_scaled_inference.jl:141-196.  Cuu has NO noise (:157) unless qu_kuu_noise:
+    then Cuu + sigma^2 I, the FiniteGP cov(u) the objective uses (dtc.jl:35) -- the build's
+    opt-in for pseudo-input sets whose noise-free Cuu is numerically singular (the branch the
+    north-star bench runs, gpar_problem.qu_kuu_noise).
 
     Returns (m_e, cov_e = inv(D), U_u upper, D)."""
     l_t, sv_t, l_o, sv_o, sigma = (float(v) for v in theta)
@@ -552,6 +556,8 @@ def compute_q_u(V, Z, t, y, theta, out_kernel="matern52", time_kernel="matern52"
     m = Z.shape[1]
     Cfu = pairwise(out_kernel, V, Z, l_o, s_o)
     Cuu = pairwise(out_kernel, Z, Z, l_o, s_o)
+    if qu_kuu_noise:
+        Cuu = Cuu + s2 * np.eye(m)
     U_u = np.linalg.cholesky(Cuu).T
     L_u = U_u.T
     lg = build_lgssm(t, time_kernel, l_t, s_t, s2)
@@ -574,18 +580,20 @@ def merge_grid(t, t_star):
 
 def get_gpar_scaled_predictions_fixed(V, Z, t, y, t_star, V_star, theta, out_kernel="matern52",
                                       time_kernel="matern52", mode="analytic", samples=100,
-                                      rng=None):
+                                      rng=None, qu_kuu_noise=False, xi=None):
     """Prediction half of src/gp/gpar_scaled_inference.jl:20-136 at given theta.
 
     mode="mc": the reference's 100-sample Monte Carlo (:91-130) with Bessel std.
     mode="analytic": its S -> infinity limit: mean = (I-S) mu_x + S y*,
     var = diag((I-S) K* U_u^-1 D^-1 U_u^-T K*^T (I-S)^T) (latent f).
+    qu_kuu_noise: q(u) with Cuu + sigma^2 I (see compute_q_u).  xi (M x S): the standard-normal
+    draws of the MC mode, to replay a sampler's exact draws (else drawn from rng).
     Returns (mean, std) at the test points in input order."""
     l_t, sv_t, l_o, sv_o, sigma = (float(v) for v in theta)
     s_t, s_o, s2 = sv_t * sv_t, sv_o * sv_o, sigma * sigma
     V, Z, V_star = to_colvecs(V), to_colvecs(Z), to_colvecs(V_star)
     n, ns = len(t), len(t_star)
-    m_e, cov, U_u, D = compute_q_u(V, Z, t, y, theta, out_kernel, time_kernel)
+    m_e, cov, U_u, D = compute_q_u(V, Z, t, y, theta, out_kernel, time_kernel, qu_kuu_noise)
     tc, perm = merge_grid(t, t_star)
     Vc = np.hstack([V, V_star])[:, perm]
     yc = np.concatenate([np.asarray(y, float), np.zeros(ns)])[perm]
@@ -593,9 +601,11 @@ def get_gpar_scaled_predictions_fixed(V, Z, t, y, t_star, V_star, theta, out_ker
     Kstar = pairwise(out_kernel, Vc, Z, l_o, s_o)
     lg = build_lgssm(tc[perm], time_kernel, l_t, s_t, Rc)
     if mode == "mc":
-        rng = rng if rng is not None else np.random.default_rng()
+        if xi is None:
+            rng = rng if rng is not None else np.random.default_rng()
+            xi = rng.standard_normal((len(m_e), samples))
         Lc = np.linalg.cholesky(cov)
-        E = m_e[:, None] + Lc @ rng.standard_normal((len(m_e), samples))
+        E = m_e[:, None] + Lc @ np.asarray(xi, dtype=np.float64)
         FX = Kstar @ solve_triangular(U_u, E, lower=False)
         ms, _ = rts_smooth(lg, yc[:, None] - FX)
         F = FX + ms[:, 0, :]
@@ -615,13 +625,15 @@ def get_gpar_scaled_predictions_fixed(V, Z, t, y, t_star, V_star, theta, out_ker
 
 def get_gpar_scaled_predictions(V, Z, t, y, t_star, V_star, out_kernel="matern52",
                                 time_kernel="matern52", log_theta0=None, max_evals=None,
-                                mode="analytic", samples=100, rng=None):
+                                mode="analytic", samples=100, rng=None, g_tol=1e-8,
+                                qu_kuu_noise=False):
     """src/gp/gpar_scaled_inference.jl:20-136 (fit, then predict).  Note the reference
     hard-codes Matern52 for the fit (:48-49)."""
     theta = get_optim_scaled_gpar_params(V, Z, t, y, "matern52", "matern52", log_theta0,
-                                         max_evals, rng=rng)
+                                         max_evals, g_tol=g_tol, rng=rng)
     mean, std = get_gpar_scaled_predictions_fixed(V, Z, t, y, t_star, V_star, theta,
-                                                  out_kernel, time_kernel, mode, samples, rng)
+                                                  out_kernel, time_kernel, mode, samples, rng,
+                                                  qu_kuu_noise=qu_kuu_noise)
     return mean, std, theta
 
 

@@ -57,6 +57,27 @@ def test_prediction_matches_oracle(CR, data):
     np.testing.assert_allclose(cs, rs, rtol=1e-7, atol=1e-9)
 
 
+@pytest.mark.parametrize("ok", ["matern52", "eq"])
+def test_qu_kuu_noise_branch_matches_oracle(CR, data, ok):
+    """The branch the north-star bench runs (gpar_problem.qu_kuu_noise = 1: q(u) with Cuu +
+    sigma^2 I): the C port and the numpy oracle agree on q(u) and on the prediction."""
+    t, V, y, Z = data
+    th = (1.3, 0.9, 0.7, 1.1, 0.2)
+    me_r, cov_r, U_r, _ = O.compute_q_u(V, Z, t, y, th, ok, qu_kuu_noise=True)
+    me_c, cov_c, U_c = CR.compute_q_u(V, Z, t, y, th, ok, kuu_noise=True)
+    np.testing.assert_allclose(U_c, U_r, rtol=1e-12, atol=1e-14)
+    np.testing.assert_allclose(me_c, me_r, rtol=1e-9, atol=1e-11 * np.abs(me_r).max())
+    np.testing.assert_allclose(cov_c, cov_r, rtol=1e-9, atol=1e-11 * np.abs(cov_r).max())
+    # the jitter is not a no-op: the noise-free branch differs
+    me_0, _, _, _ = O.compute_q_u(V, Z, t, y, th, ok)
+    assert np.abs(me_0 - me_r).max() > 1e-6 * np.abs(me_r).max()
+    ts, Vs = t[::7] + 0.013, V[:, ::7] + 0.01
+    rm, rs = O.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, th, ok, qu_kuu_noise=True)
+    cm, cs = CR.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, th, ok, qu_kuu_noise=True)
+    np.testing.assert_allclose(cm, rm, rtol=1e-9, atol=1e-11 * np.abs(rm).max())
+    np.testing.assert_allclose(cs, rs, rtol=1e-9, atol=1e-11 * np.abs(rs).max())
+
+
 def test_rejects_unsorted_times(CR):
     with pytest.raises(ValueError):
         CR.gains("matern52", np.array([0.0, 2.0, 1.0]), 1.0, 1.0, 0.1)

@@ -1,7 +1,7 @@
 """GPU parity of the DTC objective, (dtc, A), q(u) and LGSSM logpdf against the oracle.
 
 The oracle (oracle/gpar_oracle.py) restates dtc.jl:83-128, gpar_scaled_inference.jl:141-196 and
-temporal_gp_inference.jl:286-296; tolerances are fp64: lml rel <= 1e-10."""
+temporal_gp_inference.jl:69-82; tolerances are fp64: lml rel <= 1e-10."""
 import numpy as np
 import pytest
 

@@ -6,7 +6,7 @@ and the dense-linear-algebra identities behind every state-space shortcut are *a
 
 * SDE cross-covariance == the stationary kernel                     (TemporalGPs to_sde)
 * Kalman whitening alpha == L_Sigma^{-1} y, sum log S_k == logdet Sigma (TemporalGPs decorrelate)
-* LGSSM logpdf == dense N(y; 0, K + s2 I)                            (temporal_gp_inference.jl:295)
+* LGSSM logpdf == dense N(y; 0, K + s2 I)                            (temporal_gp_inference.jl:78)
 * LGSSM DTC == dense-Sigma DTC == textbook N(y; 0, Kfu Kuu'^-1 Kuf + Sigma) (dtc_example.jl:10-23)
 * RTS smoother marginals == dense GP posterior                       (TemporalGPs smooth)
 * analytic prediction == its dense (I - S) K* q(u) + S y closed form (gpar_scaled_inference.jl:20-136)
@@ -127,7 +127,7 @@ def test_exact_logpdf_is_mvn():
 
 
 def test_unpack_and_masks():
-    # util.jl:52-71: exp(log-param) + 1e-3; util.jl:118-139: masks select t / the outputs
+    # util.jl:36-55: exp(log-param) + 1e-3; util.jl:102-123: masks select t / the outputs
     p = np.log([1.5, 2.0, 0.3, 0.7, 0.1])
     np.testing.assert_allclose(O.unpack_gpar(p), np.array([1.5, 2.0, 0.3, 0.7, 0.1]) + 1e-3)
     np.testing.assert_allclose(O.unpack_gp(p[:3]), np.array([1.5, 2.0, 0.3]) + 1e-3)
