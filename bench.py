@@ -13,13 +13,21 @@ Multi-GPU: one process per GPU (torch.distributed, RCCL); outputs are sharded by
 shared inputs are broadcast from rank 0 once (untimed); per step the fitted thetas are
 all-gathered.  value = N * P / wall-clock per step (pts*outputs/s, whole job).
 
-Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config north|eeg|dtc|small]
+Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config north|eeg|dtc|small|ssm]
+
+Launch: under torchrun (WORLD_SIZE set) every process is one rank.  Started directly with
+--gpus N > 1, the parent checks that N devices are visible (torch.cuda.device_count(), which does
+not initialise HIP) and starts N rank processes itself (RANK / LOCAL_RANK / WORLD_SIZE /
+MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment) before anything touches the GPU; it
+forwards rank 0's JSON line and exits with the first non-zero rank status.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -66,7 +74,15 @@ def main():
                     help="HIP streams a batched objective alternates outputs over (gpar_ctx_set_lanes); "
                          "2 overlaps one output's whitening with another's Gram (+2%% throughput, but "
                          "per-launch kernel durations then include the sharing)")
+    ap.add_argument("--stub", action="store_true",
+                    help="launcher check without a GPU: ranks join a gloo group, take their output "
+                         "shards and report them; no compute (tests/test_bench_launch.py)")
     args = ap.parse_args()
+
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], stub=args.stub))
+    if args.stub:
+        return stub_rank(args)
 
     import torch
     import torch.distributed as dist
@@ -82,6 +98,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        log(f"[rank {rank}] note: --gpus {args.gpus} but WORLD_SIZE={world}; n_gpus reports WORLD_SIZE")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -109,8 +127,9 @@ def main():
         ts_d.copy_(torch.from_numpy(ts_h)); Fs_d.copy_(torch.from_numpy(Fs_h))
     S.broadcast_inputs((t_d, Y_d, ts_d, Fs_d))   # RCCL broadcast of the shared inputs over xGMI
     temporal = cfg.get("temporal", False)
-    mine = S.assign_outputs(P, world)[rank] if not temporal else \
-        [p for p in range(1, P + 1) if (p - 1) % world == rank]
+    shards = S.assign_outputs(P, world) if not temporal else \
+        [[p for p in range(1, P + 1) if (p - 1) % world == r] for r in range(world)]
+    mine = shards[rank]
     gpar_out = [p for p in mine if p >= 2] if not temporal else []
     Yh = Y_d.cpu().numpy() if gpar_out else None
     # q(u) with Kuu + sigma^2 I (qu_kuu_noise): the reference's jitter-free Cuu
@@ -212,7 +231,8 @@ def main():
             "config": {"workload": f"GPAR-DTC fit+predict ({args.config})", "N": n_eff, "N_star": ns_eff,
                        "M": M, "P": P, "evals_per_output": EV, "predict": args.predict,
                        "out_kernel": cfg["out_kernel"], "time_kernel": "matern52",
-                       "parallelism": f"outputs sharded over {world} GPU(s)"},
+                       "parallelism": f"outputs sharded over {world} GPU(s)",
+                       "outputs_per_rank": shards},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic, "kernel": "gram2_kernel (beta^T beta, fp64 MFMA)",
@@ -221,6 +241,11 @@ def main():
             "kernels": {"gram_ms_per_step": gram_ms / args.steps, "whiten_ms_per_step": wh_ms / args.steps,
                         "whiten_launches": wh_n},
         }
+        if args.lanes > 1 and out["roofline"]:
+            # two streams overlap launches: event spans are not the kernel's own duration
+            out["roofline"].update(achieved=None, frac=None,
+                                   note="lanes=2: per-launch event time includes the overlap with "
+                                        "the other lane, not a kernel duration")
         if temporal:
             out["metric"] = "temporal-only LGSSM fit+smooth (Matern-3/2 chains), pts*chains/s"
             out["roofline"] = None
@@ -234,14 +259,94 @@ def main():
         dist.destroy_process_group()
 
 
-def cpu_baseline(N, NS, M, P, EV, out_kernel, samples=(50_000, 100_000), d_sample=32):
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(n, argv, stub=False):
+    """Start one bench process per GPU (rank r on device r) and forward rank 0's JSON line.
+
+    Called before the parent touches the GPU: torch.cuda.device_count() only counts devices.
+    Returns the exit status: 2 when fewer than n devices are visible, else the first non-zero
+    rank status (0 when every rank succeeded)."""
+    if not stub:
+        import torch
+        have = torch.cuda.device_count()
+        if have < n:
+            log(f"bench: --gpus {n} but only {have} device(s) visible")
+            return 2
+    env0 = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
+                WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
+    procs = []
+    for r in range(n):
+        env = dict(env0, RANK=str(r), LOCAL_RANK=str(r))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      stdout=subprocess.PIPE if r == 0 else sys.stderr,
+                                      text=True))
+    out0, _ = procs[0].communicate()
+    codes = [procs[0].returncode] + [p.wait() for p in procs[1:]]
+    for line in out0.splitlines():
+        print(line, flush=True)
+    bad = [c for c in codes if c != 0]
+    if bad:
+        log(f"bench: rank exit statuses {codes}")
+        return bad[0]
+    return 0
+
+
+def stub_rank(args):
+    """One rank of the --stub launcher check: gloo group, output shards, no GPU and no compute."""
+    import torch.distributed as dist
+    from gparatscale import shard as S
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    P = CONFIGS[args.config]["P"]
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    mine = S.assign_outputs(P, world)[rank]
+    got = [None] * world
+    if world > 1:
+        dist.all_gather_object(got, {"rank": rank, "local_rank": int(os.environ.get("LOCAL_RANK", "0")),
+                                     "outputs": mine})
+        dist.destroy_process_group()
+    else:
+        got = [{"rank": 0, "local_rank": 0, "outputs": mine}]
+    if rank == 0:
+        print(json.dumps({"stub": True, "n_gpus": world, "P": P, "ranks": got}), flush=True)
+
+
+def _cpu_sample(CR, O, n, ns, M, d, out_kernel, theta):
+    """One DTC objective evaluation and one analytic prediction of the C port at n training /
+    ns test points (D = d inputs), seconds each."""
+    t, Y = O.synthetic_gpar(n, d + 1, seed=1, noise=0.8)
+    V = Y[:, :d].T
+    y = Y[:, d]
+    Z = O.pick_pseudo_inputs(V, M, 3)
+    t0 = time.perf_counter()
+    CR.compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel, "matern52")
+    t_eval = time.perf_counter() - t0
+    ts = np.sort(np.random.default_rng(2).uniform(t[0], t[-1], ns))
+    Vs = np.vstack([np.interp(ts, t, V[q]) for q in range(d)])
+    t0 = time.perf_counter()
+    CR.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, out_kernel, "matern52",
+                                         qu_kuu_noise=True)
+    return t_eval, time.perf_counter() - t0
+
+
+def cpu_baseline(N, NS, M, P, EV, out_kernel, d_sample=32, single_ns=(20_000, 40_000, 80_000)):
     """Time the C/OpenMP CPU restatement of the reference path (oracle/cpu_ref.{c,py}, SURVEY §8d
     "cpu_ref": kernel assembly, Kalman gains and per-column decorrelate sweeps, RTS smoother in C;
-    cholesky / trsm / gemm in OpenBLAS, as the reference leaves them to Julia's OpenBLAS; "port")
-    on a bounded sample: one DTC objective evaluation and one analytic prediction (N* = n/4) at
-    two sizes n, D = d_sample.  Every piece is O(n), so the job time is extrapolated linearly
-    from the larger sample (the smaller one reports how linear it is):
-    (P-1) outputs x EV evaluations + (P-1) predictions (+ the temporal output, negligible)."""
+    cholesky / trsm / gemm in OpenBLAS, as the reference leaves them to Julia's OpenBLAS; "port").
+
+    Threaded leg (all OpenMP / OpenBLAS threads): one DTC objective evaluation and one analytic
+    prediction at the job's own sizes (N training points, N* = NS test points, M, D = d_sample),
+    so nothing is extrapolated in N: job = (P - 1) outputs x (EV evaluations + 1 prediction).
+    One-thread leg (the reference's sequential column loop, dtc.jl:110-117): the same two pieces
+    at three smaller sizes under threadpoolctl's limit of 1; cost = a + b*N is fitted on the two
+    larger and checked on the smallest (any check off by more than 5 % is reported in
+    `warnings`), then evaluated at the job's sizes."""
     sys.path.insert(0, ROOT)
     from oracle import gpar_oracle as O
     from oracle import cpu_ref as CR
@@ -252,59 +357,45 @@ def cpu_baseline(N, NS, M, P, EV, out_kernel, samples=(50_000, 100_000), d_sampl
         blas = 1
     cores = max(CR.threads(), blas)
     theta = (2.0, 2.0, 2.0, 2.0, float(np.exp(-2.0) + 1e-3))
-    per = []
-    for n_sample in samples:
-        t, Y = O.synthetic_gpar(n_sample, d_sample + 1, seed=1, noise=0.8)
-        V = Y[:, :d_sample].T
-        y = Y[:, d_sample]
-        Z = O.pick_pseudo_inputs(V, M, 3)
-        t0 = time.perf_counter()
-        CR.compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel, "matern52")
-        t_eval = time.perf_counter() - t0
-        ns = n_sample // 4
-        ts = np.sort(np.random.default_rng(2).uniform(t[0], t[-1], ns))
-        Vs = np.vstack([np.interp(ts, t, V[q]) for q in range(d_sample)])
-        t0 = time.perf_counter()
-        CR.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, out_kernel, "matern52",
-                                             qu_kuu_noise=True)
-        t_pred = time.perf_counter() - t0
-        per.append((n_sample, ns, t_eval, t_pred))
-    n_sample, ns, t_eval, t_pred = per[-1]
-    t_job = (P - 1) * (EV * t_eval * N / n_sample + t_pred * (N + NS) / (n_sample + ns))
-    lin = (per[-1][2] / per[-1][0]) / (per[0][2] / per[0][0])
-    # SURVEY §8d also asks for one thread, as the reference's sequential column loop runs
-    # (dtc.jl:110-117): the same two pieces at n = 2e4 under threadpoolctl's limit of 1.
+    warnings = []
+    t_eval, t_pred = _cpu_sample(CR, O, N, NS, M, d_sample, out_kernel, theta)
+    t_job = (P - 1) * (EV * t_eval + t_pred)
     single = None
     try:
         from threadpoolctl import threadpool_limits
-        n1 = 20_000
-        t, Y = O.synthetic_gpar(n1, d_sample + 1, seed=1, noise=0.8)
-        V, y = Y[:, :d_sample].T, Y[:, d_sample]
-        Z = O.pick_pseudo_inputs(V, M, 3)
-        ns1 = n1 // 4
-        ts = np.sort(np.random.default_rng(2).uniform(t[0], t[-1], ns1))
-        Vs = np.vstack([np.interp(ts, t, V[q]) for q in range(d_sample)])
+        per = []
         with threadpool_limits(limits=1):
-            t0 = time.perf_counter()
-            CR.compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel, "matern52")
-            e1 = time.perf_counter() - t0
-            t0 = time.perf_counter()
-            CR.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, out_kernel, "matern52",
-                                                 qu_kuu_noise=True)
-            p1 = time.perf_counter() - t0
-        tj1 = (P - 1) * (EV * e1 * N / n1 + p1 * (N + NS) / (n1 + ns1))
+            for n1 in single_ns:
+                e1, p1 = _cpu_sample(CR, O, n1, n1 // 4, M, d_sample, out_kernel, theta)
+                per.append((n1, e1, p1))
+        # cost = a + b n (the M^3 dense tail does not scale with n): fit on the two larger
+        # sizes, check on the smallest, extrapolate to the job's N
+        (n0, e0, p0), (na, ea, pa), (n1, e1, p1) = per
+        def affine(x0, y0, x1, y1, x):
+            return y1 + (y1 - y0) / (x1 - x0) * (x - x1)
+        chk_e = affine(na, ea, n1, e1, n0) / e0
+        chk_p = affine(na + na // 4, pa, n1 + n1 // 4, p1, n0 + n0 // 4) / p0
+        for what, r in (("one-thread eval", chk_e), ("one-thread predict", chk_p)):
+            if abs(r - 1.0) > 0.05:
+                warnings.append(f"{what}: affine fit on N={na},{n1} predicts N={n0} at x{r:.3f} "
+                                f"of the measured time (> 5 %)")
+        e_job = affine(na, ea, n1, e1, N)
+        p_job = affine(na + na // 4, pa, n1 + n1 // 4, p1, N + NS)
+        tj1 = (P - 1) * (EV * e_job + p_job)
         single = {"value": N * P / tj1, "cores": 1,
-                  "sample": f"1 thread: 1 eval (N={n1}) = {e1:.2f}s + 1 predict (N*={ns1}) = {p1:.2f}s, "
-                            f"same linear scaling: est {tj1:.0f}s per job"}
+                  "sample": "1 thread: 1 eval + 1 predict (N* = N/4) at " +
+                            ", ".join(f"N={a} ({b:.2f}s + {c:.2f}s)" for a, b, c in per) +
+                            f"; cost = a + b*N fitted on the two larger, checked on the smallest "
+                            f"(eval x{chk_e:.3f}, predict x{chk_p:.3f}); at the job's sizes 1 eval = "
+                            f"{e_job:.1f}s, 1 predict = {p_job:.1f}s: est {tj1:.0f}s per job"}
     except Exception as exc:   # threadpoolctl missing: report the threaded figure only
         single = {"value": None, "error": repr(exc)}
     return {"value": N * P / t_job, "unit": "pts\u00b7outputs/s", "cores": int(cores), "kind": "port",
-            "single_thread": single,
-            "sample": f"C/OpenMP + OpenBLAS restatement (oracle/cpu_ref): 1 DTC objective eval (N={n_sample}, "
-                      f"M={M}, D={d_sample}) = {t_eval:.2f}s + 1 analytic predict (N={n_sample}, N*={ns}) = "
-                      f"{t_pred:.2f}s; per-point eval cost at N={per[0][0]} vs N={n_sample} differs by x{lin:.2f}; "
-                      f"scaled linearly in N to {P - 1} outputs x {EV} evals + {P - 1} predicts: "
-                      f"est {t_job:.0f}s per job"}
+            "single_thread": single, "warnings": warnings,
+            "sample": f"C/OpenMP + OpenBLAS restatement (oracle/cpu_ref), {int(cores)} threads, at the job's "
+                      f"own sizes: 1 DTC objective eval (N={N}, M={M}, D={d_sample}) = {t_eval:.2f}s + "
+                      f"1 analytic predict (N={N}, N*={NS}) = {t_pred:.2f}s; job = {P - 1} outputs x "
+                      f"({EV} evals + 1 predict) = {t_job:.0f}s (no extrapolation in N)"}
 
 
 if __name__ == "__main__":
