@@ -47,6 +47,9 @@ struct gpar_ctx {
   std::unordered_map<std::string, Stat> stats;
 };
 
+// MC predictions: most draws a call takes (xi is samples x Mp doubles of workspace)
+static constexpr int kMaxSamples = 65536;
+
 namespace gpar {
 
 struct Error : std::runtime_error {
@@ -795,16 +798,43 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
                    nullptr, nullptr, /*tri=*/1);
     launch_rowsq_finish(c->stream, rowsq, n_star, ncb, dstd);
   } else {
+    // Draws as Distributions samples q_u = MvNormal(m_e, Symmetric(inv(D)))
+    // (gpar_scaled_inference.jl:103,185): m_e + Lc xi with Lc = chol(inv(D)) lower, so a given
+    // xi (gpar_mc_normals) gives the reference's sample; f_s = mean + (I - S) K* U_u^{-1} Lc xi_s.
+    double* Lc = ws<double>(c, "pr_Lc", (size_t)ld * ld);
+    double* Tdc = ws<double>(c, "pr_Tdc", (size_t)q.nb * kDenseNB * kDenseNB);
+    int* stc = ws<int>(c, "pr_stc", 1);
+    HIPCHECK(hipMemsetAsync(stc, 0, sizeof(int), c->stream));
+    launch_pad_identity_copy(c->stream, q.cov, ld, (int)m, Lc);
+    CholJob2Host cj{Lc, nullptr, Tdc, stc};
+    auto* dcj = ws<CholJob2Host>(c, "pr_cholc", 1);
+    h2d(c, dcj, &cj, 1);
+    launch_chol_blocked(c->stream, dcj, 1, ld, q.nb, /*want_t=*/false);
+    double* W = ws<double>(c, "pr_W", (size_t)ld * ld);
+    launch_mc_factor(c->stream, Lc, X1, ld, (int)m, W);
+    check_launch("predict: MC factor");
     double* Z = ws<double>(c, "pr_Z", (size_t)n_star * mp);
     double* rowsq = ws<double>(c, "pr_rowsq", (size_t)ncb * n_star);
     double* xi = ws<double>(c, "pr_xi", (size_t)samples * mp);
     double* mmc = ws<double>(c, "pr_mmc", n_star);
-    launch_gemm_nt(c->stream, Q, mp, Vm, ld, n_star, m, m, 0, Z, mp, rowsq, 0, nullptr, nullptr,
-                   nullptr, /*tri=*/1);
+    launch_gemm_nt(c->stream, Q, mp, W, ld, n_star, m, m, 0, Z, mp, rowsq, 0, nullptr, nullptr,
+                   nullptr, /*tri=*/0);
     launch_normal(c->stream, xi, mp, samples, m, samples, seed);
-    launch_gemm_nt(c->stream, Z, mp, xi, mp, n_star, samples, m, 1, nullptr, 0, nullptr, samples,
-                   dmean, mmc, dstd);
+    if (samples <= 128) {   // one column tile: statistics in the GEMM epilogue
+      launch_gemm_nt(c->stream, Z, mp, xi, mp, n_star, samples, m, 1, nullptr, 0, nullptr, samples,
+                     dmean, mmc, dstd);
+    } else {
+      const int nsb = (int)((samples + 127) / 128);
+      double* part = ws<double>(c, "pr_mcpart", (size_t)nsb * n_star * 2);
+      launch_gemm_nt(c->stream, Z, mp, xi, mp, n_star, samples, m, 2, nullptr, 0, part, 0, nullptr,
+                     nullptr, nullptr);
+      launch_mc_stats_finish(c->stream, part, n_star, nsb, samples, dmean, mmc, dstd);
+    }
     dmean = mmc;
+    int st = 0;
+    d2h(c, &st, stc, 1);
+    sync(c);
+    if (st) throw Error(GPAR_ERR_NOT_PD, "PosDefException: cholesky(Symmetric(inv(D))) failed (MvNormal, gpar_scaled_inference.jl:185)");
   }
   check_launch("predict: gemm");
   // ---- outputs
@@ -1122,22 +1152,27 @@ int32_t gpar_fit(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
   API_END(ctx)
 }
 
-int32_t gpar_fit_predict(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
-                         const double* log_theta0, const gpar_fit_options* opts, int64_t n_star,
-                         const double* t_star, const double* const* v_star, const int64_t* ldvs,
-                         int32_t mode, int32_t samples, uint64_t seed, double* theta_out,
-                         double* nlml_out, int32_t* evals_out, double* const* mean_out,
-                         double* const* std_out) {
-  API_BEGIN(ctx)
+// get_gpar_scaled_predictions for a batch: batched fit, then each output's prediction at its
+// fitted theta (in output order).  chain (optional): after output i's prediction its mean is also
+// written to column chain_col[i] of chain (point k at chain[k * ld_chain + col]), so later outputs'
+// v_star may point into chain and read earlier outputs' predicted means as inference inputs.
+static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                             const double* log_theta0, const gpar_fit_options* opts, int64_t n_star,
+                             const double* t_star, const double* const* v_star, const int64_t* ldvs,
+                             int32_t mode, int32_t samples, uint64_t seed, double* chain,
+                             int64_t ld_chain, const int32_t* chain_col, double* theta_out,
+                             double* nlml_out, int32_t* evals_out, double* const* mean_out,
+                             double* const* std_out) {
   ARGCHECK(probs && nprob >= 1 && log_theta0 && theta_out && t_star && v_star && ldvs &&
                mean_out && std_out, "null argument");
   ARGCHECK(n_star >= 1, "n_star must be >= 1");
   ARGCHECK(mode == GPAR_PREDICT_ANALYTIC || mode == GPAR_PREDICT_MC, "bad mode");
   if (mode == GPAR_PREDICT_MC)
-    ARGCHECK(samples >= 2 && samples <= 128, "MC mode supports 2..128 samples");
+    ARGCHECK(samples >= 2 && samples <= kMaxSamples, "MC mode takes 2..65536 samples");
   for (int i = 0; i < nprob; ++i) {
     ARGCHECK(v_star[i] && mean_out[i] && std_out[i], "null per-output pointer");
     ARGCHECK(ldvs[i] >= probs[i].d, "ldvs must be >= d");
+    if (chain) ARGCHECK(chain_col[i] < ld_chain, "chain_col must be < ld_chain");
   }
   check_batch(probs, nprob);
   gpar_fit_options o{0, 1000, 1e-8, 0.0};
@@ -1146,13 +1181,50 @@ int32_t gpar_fit_predict(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob
   for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
   FitKeep keep;
   fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, &keep);
+  const int mem = probs[0].mem;
   for (int i = 0; i < nprob; ++i) {
     const double* q = theta_out + 5 * i;
     const Theta th{q[0], q[1], q[2], q[3], q[4]};
-    predict_impl(ctx, P[i], th, probs[i].mem, n_star, t_star, v_star[i], ldvs[i], mode, samples,
+    predict_impl(ctx, P[i], th, mem, n_star, t_star, v_star[i], ldvs[i], mode, samples,
                  seed + (uint64_t)i, mean_out[i], std_out[i],
                  keep.valid[i] ? &keep.gram[i] : nullptr);
+    if (chain && chain_col[i] >= 0) {
+      double* dst = chain + chain_col[i];
+      if (mem == GPAR_MEM_DEVICE) {   // stream-ordered before the next output's merge reads it
+        HIPCHECK(hipMemcpy2DAsync(dst, ld_chain * sizeof(double), mean_out[i], sizeof(double),
+                                  sizeof(double), n_star, hipMemcpyDeviceToDevice, ctx->stream));
+      } else {
+        for (int64_t k = 0; k < n_star; ++k) dst[k * ld_chain] = mean_out[i][k];
+      }
+    }
   }
+  if (chain && mem == GPAR_MEM_DEVICE) sync(ctx);
+}
+
+int32_t gpar_fit_predict(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                         const double* log_theta0, const gpar_fit_options* opts, int64_t n_star,
+                         const double* t_star, const double* const* v_star, const int64_t* ldvs,
+                         int32_t mode, int32_t samples, uint64_t seed, double* theta_out,
+                         double* nlml_out, int32_t* evals_out, double* const* mean_out,
+                         double* const* std_out) {
+  API_BEGIN(ctx)
+  fit_predict_impl(ctx, probs, nprob, log_theta0, opts, n_star, t_star, v_star, ldvs, mode, samples,
+                   seed, nullptr, 0, nullptr, theta_out, nlml_out, evals_out, mean_out, std_out);
+  API_END(ctx)
+}
+
+int32_t gpar_fit_predict_chain(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                               const double* log_theta0, const gpar_fit_options* opts,
+                               int64_t n_star, const double* t_star, const double* const* v_star,
+                               const int64_t* ldvs, int32_t mode, int32_t samples, uint64_t seed,
+                               double* chain, int64_t ld_chain, const int32_t* chain_col,
+                               double* theta_out, double* nlml_out, int32_t* evals_out,
+                               double* const* mean_out, double* const* std_out) {
+  API_BEGIN(ctx)
+  ARGCHECK(chain && chain_col && ld_chain >= 1, "null chain argument");
+  fit_predict_impl(ctx, probs, nprob, log_theta0, opts, n_star, t_star, v_star, ldvs, mode, samples,
+                   seed, chain, ld_chain, chain_col, theta_out, nlml_out, evals_out, mean_out,
+                   std_out);
   API_END(ctx)
 }
 
@@ -1245,10 +1317,23 @@ int32_t gpar_predict(gpar_ctx* ctx, const gpar_problem* prob, const double* thet
   ARGCHECK(ldvs >= prob->d, "ldvs must be >= d");
   ARGCHECK(mode == GPAR_PREDICT_ANALYTIC || mode == GPAR_PREDICT_MC, "bad mode");
   if (mode == GPAR_PREDICT_MC)
-    ARGCHECK(samples >= 2 && samples <= 128, "MC mode supports 2..128 samples");
+    ARGCHECK(samples >= 2 && samples <= kMaxSamples, "MC mode takes 2..65536 samples");
   DevProblem P = prepare_problem(ctx, *prob, 0);
   std::vector<Theta> th = thetas_from(theta, 1);
   predict_impl(ctx, P, th[0], prob->mem, n_star, t_star, v_star, ldvs, mode, samples, seed, mean, std);
+  API_END(ctx)
+}
+
+int32_t gpar_mc_normals(gpar_ctx* ctx, int32_t samples, int64_t m, uint64_t seed, double* xi_out) {
+  API_BEGIN(ctx)
+  ARGCHECK(xi_out, "null argument");
+  ARGCHECK(samples >= 1 && samples <= kMaxSamples, "samples must be in 1..65536");
+  ARGCHECK(m >= 1 && m <= (int64_t)1 << 20, "m out of range");
+  double* xi = ws<double>(ctx, "mc_xi_export", (size_t)samples * m);
+  launch_normal(ctx->stream, xi, m, samples, m, samples, seed);
+  check_launch("normal draws");
+  d2h(ctx, xi_out, xi, (size_t)samples * m);
+  sync(ctx);
   API_END(ctx)
 }
 

@@ -104,7 +104,9 @@ __global__ __launch_bounds__(256) void predict_rows(const double* __restrict__ X
 // padded rows: conflict-free fragment reads, see k_gram.hip).
 // Epilogues: mode 0: C written (ldc) + rowsq[colblock][row] = sum_c C^2 over the tile;
 //            mode 1: MC statistics over the tile's first `valid_cols` columns:
-//                    out0[row] = base[row] + mean_c C, out1[row] = Bessel std_c C.
+//                    out0[row] = base[row] + mean_c C, out1[row] = Bessel std_c C;
+//            mode 2: rowsq[colblock][row][2] = (sum_c C, sum_c C^2) over the tile's columns
+//                    < cols, combined by mc_stats_finish (MC with more than 128 samples).
 // tri: B is lower triangular (B[j][k] = 0 for k > j, exactly), so column tile c0 only needs
 //      k < c0 + 128 (V = L_D^{-1} L_u^{-1}: 37.5% of the MFMAs at M = 512).
 constexpr int kPT = 128, kPBK = 16, kPLds = 144;
@@ -189,7 +191,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
       for (int c = 0; c < 4; ++c) {
         const int64_t col = c0 + wc * 64 + c * 16 + fcol;
         const double v = acc[a][c][r];
-        const bool ok = (mode == 0) ? (col < cols) : (col - c0 < valid_cols);
+        const bool ok = (mode == 1) ? (col - c0 < valid_cols) : (col < cols);
         if (ok) { p += v; p2 = fma(v, v, p2); }
         if (mode == 0) {
           const int64_t row = r0 + wr * 64 + a * 16 + frow + 4 * r;
@@ -228,6 +230,10 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
       const double t2 = red[(0 * 128 + tid) * 2 + 1] + red[(1 * 128 + tid) * 2 + 1];
       if (mode == 0) {
         rowsq[(int64_t)blockIdx.y * rows + row] = t2;
+      } else if (mode == 2) {
+        // MC over more than one 128-column tile: partial sum / sum of squares of this tile
+        rowsq[((int64_t)blockIdx.y * rows + row) * 2 + 0] = t1;
+        rowsq[((int64_t)blockIdx.y * rows + row) * 2 + 1] = t2;
       } else {
         // MC: f_s = base + F_s; Bessel-corrected std over the valid_cols samples
         const double S = (double)valid_cols;
@@ -250,9 +256,52 @@ __global__ void rowsq_finish(const double* __restrict__ rowsq, int64_t rows, int
   std_out[i] = sqrt(s);
 }
 
+// MC statistics from mode-2 partials: out0 = base + mean, out1 = Bessel std over S samples
+__global__ void mc_stats_finish(const double* __restrict__ part, int64_t rows, int nblk, double S,
+                                const double* __restrict__ base, double* __restrict__ out0,
+                                double* __restrict__ out1) {
+  const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
+  if (i >= rows) return;
+  double t1 = 0.0, t2 = 0.0;
+  for (int b = 0; b < nblk; ++b) {
+    t1 += part[((int64_t)b * rows + i) * 2 + 0];
+    t2 += part[((int64_t)b * rows + i) * 2 + 1];
+  }
+  const double mu = t1 / S;
+  const double var = (t2 - S * mu * mu) / (S - 1.0);
+  out0[i] = base[i] + mu;
+  out1[i] = sqrt(var > 0.0 ? var : 0.0);
+}
+
+// MC factor W = Lc^T X (m x m, row-major, ld), Lc = chol(inv(D)) lower (Distributions'
+// MvNormal(m_e, Symmetric(inv(D))) draws m_e + Lc xi, gpar_scaled_inference.jl:103,185) and
+// X = L_u^{-1} lower: W[j][k] = sum_{l >= max(j,k)} Lc[l][j] X[l][k].  Row i of Z = Q W^T is then
+// the draw's loading (I - S) K*_i U_u^{-1} Lc.  Zero outside m x m.
+__global__ __launch_bounds__(256) void mc_factor_kernel(const double* __restrict__ Lc,
+                                                        const double* __restrict__ X, int64_t ld,
+                                                        int m, double* __restrict__ W) {
+  const int j = blockIdx.y * 16 + (threadIdx.x >> 4);
+  const int k = blockIdx.x * 16 + (threadIdx.x & 15);
+  if (j >= ld || k >= ld) return;
+  double s = 0.0;
+  if (j < m && k < m)
+    for (int l = j > k ? j : k; l < m; ++l) s = fma(Lc[(int64_t)l * ld + j], X[(int64_t)l * ld + k], s);
+  W[(int64_t)j * ld + k] = s;
+}
+
+// dst = src on the leading m x m block, identity on the padding (ld x ld)
+__global__ void pad_identity_copy(const double* __restrict__ src, int64_t ld, int m,
+                                  double* __restrict__ dst) {
+  const int i = blockIdx.y * 16 + (threadIdx.x >> 4);
+  const int j = blockIdx.x * 16 + (threadIdx.x & 15);
+  if (i >= ld || j >= ld) return;
+  dst[(int64_t)i * ld + j] = (i < m && j < m) ? src[(int64_t)i * ld + j] : (i == j ? 1.0 : 0.0);
+}
+
 // ---------------------------------------------------------------------------- normal draws
 // xi[s * ld + m] ~ N(0, 1) for s < S, m < M (zero beyond), from a counter-based hash
-// (splitmix64) + Box-Muller: reproducible for a given seed, independent of launch geometry.
+// (splitmix64) of (seed, s, m) + Box-Muller: reproducible for a given seed, independent of the
+// launch geometry and of the padding ld (gpar_mc_normals exports the same draws unpadded).
 __device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
   x += 0x9E3779B97F4A7C15ull;
   x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -266,7 +315,8 @@ __global__ void normal_kernel(double* __restrict__ xi, int64_t ld, int64_t S, in
   const int64_t s = e / ld, m = e % ld;
   double v = 0.0;
   if (s < S && m < M) {
-    const uint64_t a = splitmix64(seed ^ splitmix64((uint64_t)e * 2 + 1));
+    const uint64_t key = ((uint64_t)s << 32) | (uint64_t)m;
+    const uint64_t a = splitmix64(seed ^ splitmix64(key * 2 + 1));
     const uint64_t b = splitmix64(a ^ 0xD1B54A32D192ED03ull);
     const double u1 = ((double)(a >> 11) + 0.5) * (1.0 / 9007199254740992.0);
     const double u2 = ((double)(b >> 11)) * (1.0 / 9007199254740992.0);
@@ -336,6 +386,23 @@ void launch_gemm_nt(hipStream_t st, const double* A, int64_t lda, const double* 
 void launch_rowsq_finish(hipStream_t st, const double* rowsq, int64_t rows, int nblk,
                          double* std_out) {
   rowsq_finish<<<(unsigned)((rows + 255) / 256), 256, 0, st>>>(rowsq, rows, nblk, std_out);
+}
+
+void launch_mc_stats_finish(hipStream_t st, const double* part, int64_t rows, int nblk, int64_t S,
+                           const double* base, double* out0, double* out1) {
+  mc_stats_finish<<<(unsigned)((rows + 255) / 256), 256, 0, st>>>(part, rows, nblk, (double)S, base,
+                                                                  out0, out1);
+}
+
+void launch_mc_factor(hipStream_t st, const double* Lc, const double* X, int64_t ld, int m,
+                      double* W) {
+  dim3 grid((unsigned)((ld + 15) / 16), (unsigned)((ld + 15) / 16));
+  mc_factor_kernel<<<grid, 256, 0, st>>>(Lc, X, ld, m, W);
+}
+
+void launch_pad_identity_copy(hipStream_t st, const double* src, int64_t ld, int m, double* dst) {
+  dim3 grid((unsigned)((ld + 15) / 16), (unsigned)((ld + 15) / 16));
+  pad_identity_copy<<<grid, 256, 0, st>>>(src, ld, m, dst);
 }
 
 void launch_normal(hipStream_t st, double* xi, int64_t ld, int64_t S, int64_t M, int64_t Sp,

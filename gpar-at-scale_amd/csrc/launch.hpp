@@ -193,6 +193,11 @@ void launch_gemm_nt(hipStream_t st, const double* A, int64_t lda, const double* 
                     double* out1, int tri = 0);
 void launch_rowsq_finish(hipStream_t st, const double* rowsq, int64_t rows, int nblk,
                          double* std_out);
+void launch_mc_stats_finish(hipStream_t st, const double* part, int64_t rows, int nblk, int64_t S,
+                           const double* base, double* out0, double* out1);
+void launch_mc_factor(hipStream_t st, const double* Lc, const double* X, int64_t ld, int m,
+                      double* W);
+void launch_pad_identity_copy(hipStream_t st, const double* src, int64_t ld, int m, double* dst);
 void launch_normal(hipStream_t st, double* xi, int64_t ld, int64_t S, int64_t M, int64_t Sp,
                    uint64_t seed);
 void launch_scatter_chains(hipStream_t st, const double* src, int64_t lds, int64_t ns,

@@ -24,7 +24,7 @@ KERNEL_ID = {"matern12": 0, "matern32": 1, "matern52": 2, "eq": 3}
 EXPORTED = (
     "gpar_abi_version", "gpar_ctx_create", "gpar_ctx_destroy", "gpar_last_error",
     "gpar_ctx_workspace_bytes", "gpar_ctx_trim", "gpar_dtc_objective", "gpar_dtc_objective_A",
-    "gpar_fit", "gpar_fit_predict", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
+    "gpar_fit", "gpar_fit_predict", "gpar_fit_predict_chain", "gpar_mc_normals", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
     "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_reset_stats",
     "gpar_ctx_set_lanes", "gpar_ctx_set_input_stream", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
@@ -81,6 +81,7 @@ def load(path: str | None = None):
         if not os.path.exists(p):
             raise OSError(f"libgparhip.so not found at {p}: run `make -C gpar-at-scale_amd` "
                           "(or __graft_entry__.build())")
+        _torch_runtime_first()
         lib = C.CDLL(p)
         vp, i32, i64, dp = C.c_void_p, C.c_int32, C.c_int64, C.c_void_p
         sig = {
@@ -101,6 +102,10 @@ def load(path: str | None = None):
                                dp, dp, dp]),
             "gpar_fit_predict": (i32, [vp, C.POINTER(GparProblem), i32, dp, C.POINTER(GparFitOptions),
                                        i64, vp, vp, vp, i32, i32, C.c_uint64, dp, dp, dp, vp, vp]),
+            "gpar_fit_predict_chain": (i32, [vp, C.POINTER(GparProblem), i32, dp,
+                                             C.POINTER(GparFitOptions), i64, vp, vp, vp, i32, i32,
+                                             C.c_uint64, vp, i64, vp, dp, dp, dp, vp, vp]),
+            "gpar_mc_normals": (i32, [vp, i32, i64, C.c_uint64, dp]),
             "gpar_q_u": (i32, [vp, C.POINTER(GparProblem), dp, dp, dp, dp]),
             "gpar_predict": (i32, [vp, C.POINTER(GparProblem), dp, i64, dp, dp, i64, i32, i32,
                                    C.c_uint64, dp, dp]),
@@ -139,6 +144,19 @@ def raise_for(ctx, code):
     if code == GPAR_ERR_UNSUPPORTED:
         raise Unsupported(code, msg)
     raise GparError(code, msg)
+
+
+def _torch_runtime_first():
+    """PyTorch-ROCm bundles its own HIP runtime (torch/lib/libamdhip64.so, SONAME
+    libamdhip64.so.7); this library links libamdhip64.so.7 too.  Imported first, torch's copy
+    satisfies our dependency and the process holds ONE runtime, so torch streams / device pointers
+    and our kernels share it.  Loaded first, ours comes from /opt/rocm and torch then loads its own
+    by file name: two runtimes in one process, and whichever initialises second finds no GPU
+    (measured on MI355X).  So torch, when installed, is imported before the CDLL."""
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
 
 
 class Context:

@@ -243,18 +243,41 @@ def fit_batch(problems, log_theta0, max_evals=0, max_iterations=1000, g_tol=1e-8
 
 def fit_predict_batch(problems, log_theta0, t_star, V_stars, max_evals=0, max_iterations=1000,
                       g_tol=1e-8, time_limit=0.0, mode="analytic", samples=100, seed=0, device=0,
-                      keep=None):
+                      keep=None, chain=None, chain_cols=None):
     """get_gpar_scaled_predictions (gpar_scaled_inference.jl:20-136) for a batch of outputs
     (gpar_fit_predict): the batched fit, then each output's prediction at its fitted theta,
     reusing the fit's Gram at that theta for q(u) when the problem has qu_kuu_noise.
 
     Device problems (make_problem on torch tensors): t_star a device vector, V_stars[i] output
     i's test inputs (N* x D_i tensor, rows = points); returns (FitResult, means, stds) with
-    means/stds lists of device tensors.  Host problems: numpy t_star and D_i x N* ColVecs."""
+    means/stds lists of device tensors.  Host problems: numpy t_star and D_i x N* ColVecs.
+
+    Chained inference inputs (gpar_fit_predict_chain; GPAR_scaled_examples.jl:172 feeds y2's
+    predicted means to y3): `chain` is an N* x K matrix (numpy C-order array for host problems, a
+    device tensor with unit column stride otherwise), `chain_cols[i]` the column output i's
+    predicted mean is written to after its prediction (-1: none).  V_stars[i] = None reads output
+    i's inputs from chain's first D_i columns, as they stand when its prediction runs (columns of
+    earlier outputs hold their predicted means, the others what the caller put there)."""
     ctx = context(device)
     lib = _lib.load()
     P = len(problems)
     keep = keep if keep is not None else _Keep()
+    if chain is not None:
+        if chain_cols is None or len(chain_cols) != P:
+            raise _arg_error("chain_cols needs one entry per problem")
+        K = chain.shape[1]
+        if any(c >= K for c in chain_cols):
+            raise _arg_error("chain_cols entries must be < chain.shape[1]")
+        if _is_torch(chain):
+            if chain.stride(1) != 1 or chain.dtype != __import__("torch").float64:
+                raise _arg_error("chain must be a float64 tensor with unit column stride")
+            chain_ptr, ld_chain = chain.data_ptr(), chain.stride(0)
+        else:
+            if not (isinstance(chain, np.ndarray) and chain.dtype == np.float64 and chain.flags.c_contiguous):
+                raise _arg_error("chain must be a C-contiguous float64 numpy array")
+            chain_ptr, ld_chain = chain.ctypes.data, K
+    elif any(v is None for v in V_stars):
+        raise _arg_error("V_stars[i] = None needs a chain")
     arr = (GparProblem * P)(*problems)
     x0 = np.ascontiguousarray(np.asarray(log_theta0, dtype=np.float64).reshape(P, 5))
     opts = GparFitOptions(int(max_evals), int(max_iterations), float(g_tol), float(time_limit))
@@ -270,6 +293,8 @@ def fit_predict_batch(problems, log_theta0, t_star, V_stars, max_evals=0, max_it
         import torch
         tsp = _dev_vec(t_star, keep)
         for i, Vs in enumerate(V_stars):
+            if Vs is None:
+                Vs = chain[:, : problems[i].d]
             p_, ld_, ns, ds = _dev_points(Vs, keep)
             if ns != n_star or ds != problems[i].d:
                 raise _arg_error(f"V_stars[{i}] must be N* x D = {n_star} x {problems[i].d}")
@@ -282,7 +307,12 @@ def fit_predict_batch(problems, log_theta0, t_star, V_stars, max_evals=0, max_it
     else:
         tsp = _host_vec(t_star, keep)
         for i, Vs in enumerate(V_stars):
-            p_, ld_, ns, ds = _host_points(Vs, keep)
+            if Vs is None:   # read in place from the chain (aliasing is the point)
+                if problems[i].d > chain.shape[1] or chain.shape[0] != n_star:
+                    raise _arg_error(f"chain must be N* x K with K >= D_{i}")
+                p_, ld_, ns, ds = chain.ctypes.data, chain.shape[1], chain.shape[0], problems[i].d
+            else:
+                p_, ld_, ns, ds = _host_points(Vs, keep)
             if ns != n_star or ds != problems[i].d:
                 raise _arg_error(f"V_stars[{i}] must be D x N* = {problems[i].d} x {n_star}")
             vptr.append(p_)
@@ -299,10 +329,29 @@ def fit_predict_batch(problems, log_theta0, t_star, V_stars, max_evals=0, max_it
     MP = (C.c_void_p * P)(*mp_)
     SP = (C.c_void_p * P)(*sp_)
     md = _lib.GPAR_PREDICT_MC if mode == "mc" else _lib.GPAR_PREDICT_ANALYTIC
-    ctx.check(lib.gpar_fit_predict(ctx.h, arr, P, _ptr(x0), C.byref(opts), ns, tsp, VP, LD, md,
-                                   int(samples), int(seed), _ptr(theta), _ptr(nlml), _ptr(evals),
-                                   MP, SP))
+    if chain is None:
+        ctx.check(lib.gpar_fit_predict(ctx.h, arr, P, _ptr(x0), C.byref(opts), ns, tsp, VP, LD, md,
+                                       int(samples), int(seed), _ptr(theta), _ptr(nlml), _ptr(evals),
+                                       MP, SP))
+    else:
+        if dev and chain.shape[0] != n_star:
+            raise _arg_error("chain must have N* rows")
+        CC = (C.c_int32 * P)(*[int(c) for c in chain_cols])
+        ctx.check(lib.gpar_fit_predict_chain(ctx.h, arr, P, _ptr(x0), C.byref(opts), ns, tsp, VP, LD,
+                                             md, int(samples), int(seed), C.c_void_p(chain_ptr),
+                                             int(ld_chain), CC, _ptr(theta), _ptr(nlml),
+                                             _ptr(evals), MP, SP))
     return FitResult(theta, nlml, evals), means, stds
+
+
+def mc_normals(samples, m, seed, device=0):
+    """The standard-normal draws MC-mode prediction uses for (samples, m, seed), samples x m
+    (gpar_mc_normals): draw s maps to the pseudo-point sample m_e + chol(inv(D)).L xi_s
+    (gpar_scaled_inference.jl:103,185).  fit_predict_batch draws output i with seed + i."""
+    ctx = context(device)
+    xi = np.zeros((int(samples), int(m)))
+    ctx.check(_lib.load().gpar_mc_normals(ctx.h, int(samples), int(m), int(seed), _ptr(xi)))
+    return xi
 
 
 def get_optim_scaled_gpar_params(input_locations, pseudo_input_locations, time_loc, outputs,

@@ -155,11 +155,19 @@ int32_t gpar_q_u(gpar_ctx* ctx, const gpar_problem* prob, const double* theta,
  * Cf*u, LGSSM with R = sigma^2 (train) / 1e10 (test), RTS smoothing.
  * t_star [n_star], v_star point k dim i at v_star[k*ldvs + i]; in prob->mem.
  * mean/std [n_star] in prob->mem.  ANALYTIC: mean and std of the latent f (the MC
- * estimator's S -> infinity limit); MC: `samples` draws with the given seed, mean and
- * Bessel-corrected std over samples as the reference does. */
+ * estimator's S -> infinity limit); MC: `samples` (2..65536; the reference takes 100) draws with
+ * the given seed (gpar_mc_normals), mean and Bessel-corrected std over samples as the reference
+ * does. */
 int32_t gpar_predict(gpar_ctx* ctx, const gpar_problem* prob, const double* theta,
                      int64_t n_star, const double* t_star, const double* v_star, int64_t ldvs,
                      int32_t mode, int32_t samples, uint64_t seed, double* mean, double* std);
+
+/* The standard-normal draws MC mode uses for (samples, m, seed): xi_out[s*m + j] is the j-th
+ * coordinate of draw s (host, samples x m).  The m_e sample of draw s is m_e + chol(inv(D)).L
+ * xi_s, as Distributions' rand(MvNormal(m_e, Symmetric(inv(D)))) maps a standard-normal vector
+ * (gpar_scaled_inference.jl:103,185), so a host-side restatement fed these draws reproduces the
+ * device's MC estimate.  gpar_fit_predict draws output i with seed + i. */
+int32_t gpar_mc_normals(gpar_ctx* ctx, int32_t samples, int64_t m, uint64_t seed, double* xi_out);
 
 /* ---------------------------------------------------------------- fit + predict
  * Replaces get_gpar_scaled_predictions (src/gp/gpar_scaled_inference.jl:20-136) -- the fit of
@@ -177,6 +185,22 @@ int32_t gpar_fit_predict(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob
                          int32_t mode, int32_t samples, uint64_t seed, double* theta_out,
                          double* nlml_out, int32_t* evals_out, double* const* mean_out,
                          double* const* std_out);
+
+/* Same, with chained inference inputs (examples/GPAR_scaled_examples.jl:172 passes y2's predicted
+ * means as y3's inference inputs; examples/eeg.jl:249,274 likewise): the fit is batched as above,
+ * the predictions then run in output order i = 0..nprob-1, and after output i's prediction its
+ * mean is also written to column chain_col[i] of `chain` (point k at chain[k*ld_chain + col];
+ * chain_col[i] < 0: not written).  A later output's v_star may point into `chain` (e.g. v_star[i] =
+ * chain, ldvs[i] = ld_chain, its first d columns holding earlier outputs' predicted means) and
+ * then reads them.  chain in probs[0].mem; device writes are stream-ordered before the next
+ * prediction reads them.  Order outputs so that every producer precedes its consumers. */
+int32_t gpar_fit_predict_chain(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                               const double* log_theta0, const gpar_fit_options* opts,
+                               int64_t n_star, const double* t_star, const double* const* v_star,
+                               const int64_t* ldvs, int32_t mode, int32_t samples, uint64_t seed,
+                               double* chain, int64_t ld_chain, const int32_t* chain_col,
+                               double* theta_out, double* nlml_out, int32_t* evals_out,
+                               double* const* mean_out, double* const* std_out);
 
 /* ---------------------------------------------------------------- temporal-only (LGSSM) chains
  * `nchains` independent chains sharing the time grid t [n] (ascending); chain c's
