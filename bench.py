@@ -74,6 +74,10 @@ def main():
                     help="HIP streams a batched objective alternates outputs over (gpar_ctx_set_lanes); "
                          "2 overlaps one output's whitening with another's Gram (+2%% throughput, but "
                          "per-launch kernel durations then include the sharing)")
+    ap.add_argument("--inference", default="given", choices=["given", "chained"],
+                    help="test inputs of output p: 'given' = the noiseless previous outputs at t* "
+                         "(GPAR_scaled_examples.jl:139); 'chained' = output 1's true values and the "
+                         "PREDICTED means of outputs 2..p-1 (GPAR_scaled_examples.jl:172, eeg.jl:249)")
     ap.add_argument("--stub", action="store_true",
                     help="launcher check without a GPU: ranks join a gloo group, take their output "
                          "shards and report them; no compute (tests/test_bench_launch.py)")
@@ -153,10 +157,38 @@ def main():
 
     ctx = G.context(local)
     ctx.set_lanes(args.lanes)
+    chained = args.inference == "chained" and not temporal
+    if chained:
+        # inference inputs: column 0 = output 1's true values at t*, column p-1 = output p's
+        # predicted mean, written as the predictions run in output order
+        chain_d = Fs_d.clone()
+        owners = S.owners_of(shards)
+        gpar_all = list(range(2, P + 1))
 
     def step():
         res = {}
-        if problems and not args.separate_predict:
+        if chained and world == 1:
+            fr, _, _ = G.fit_predict_batch(problems, x0, ts_d, [None] * len(problems),
+                                           max_evals=EV, g_tol=-1.0, mode=args.predict, samples=100,
+                                           seed=gpar_out[0], device=local, chain=chain_d,
+                                           chain_cols=[p - 1 for p in gpar_out])
+            for i, p in enumerate(gpar_out):
+                res[p] = fr.theta[i]
+        elif chained:
+            # independent fits per rank, then the ordered prediction sweep across ranks: each
+            # predicted mean is broadcast by its owner as soon as it is ready (shard.py)
+            if problems:
+                fr = G.fit_batch(problems, x0, max_evals=EV, g_tol=-1.0, device=local)
+                for i, p in enumerate(gpar_out):
+                    res[p] = fr.theta[i]
+            S.chained_predictions(
+                gpar_all, owners,
+                lambda p, c: G.predict_scaled(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], res[p], ts_d,
+                                              c[:, : p - 1], cfg["out_kernel"], "matern52",
+                                              mode=args.predict, samples=100, seed=p, device=local,
+                                              qu_kuu_noise=True),
+                chain_d)
+        elif problems and not args.separate_predict:
             # get_gpar_scaled_predictions for every owned output: batched fit, then predictions
             fr, _, _ = G.fit_predict_batch(problems, x0, ts_d, [Fs_d[:, : p - 1] for p in gpar_out],
                                            max_evals=EV, g_tol=-1.0, mode=args.predict, samples=100,
@@ -232,7 +264,7 @@ def main():
                        "M": M, "P": P, "evals_per_output": EV, "predict": args.predict,
                        "out_kernel": cfg["out_kernel"], "time_kernel": "matern52",
                        "parallelism": f"outputs sharded over {world} GPU(s)",
-                       "outputs_per_rank": shards},
+                       "outputs_per_rank": shards, "inference": args.inference},
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic, "kernel": "gram2_kernel (beta^T beta, fp64 MFMA)",

@@ -66,3 +66,37 @@ def gather_thetas(local: dict, P: int, device=None) -> np.ndarray:
         dist.all_reduce(tt)
         th = tt.cpu().numpy()
     return th
+
+
+def owners_of(shards: list[list[int]]) -> dict[int, int]:
+    """Output -> owning rank, from an assign_outputs() partition."""
+    return {p: r for r, owned in enumerate(shards) for p in owned}
+
+
+def chained_predictions(outputs, owners: dict, predict_fn, chain):
+    """Predictions with chained inference inputs across ranks (GPAR_scaled_examples.jl:172,
+    eeg.jl:249,274: output p's inference inputs include the predicted means of earlier outputs).
+
+    `chain` (N* x K tensor, same contents on every rank) holds the inference inputs: columns the
+    caller fills (observed / true inputs) and one column p - 1 per output p in `outputs`, written
+    here.  Outputs are taken in the given order; the owner of p calls predict_fn(p, chain) ->
+    (mean, std) and then broadcasts the mean (8 N* bytes over RCCL / gloo) from itself, and every
+    rank stores it in chain[:, p - 1] before the next output starts.  The fits are independent
+    and run before this on each rank; only this ordered sweep is serial across ranks.
+    Returns {p: (mean, std)} for this rank's outputs."""
+    import torch
+    import torch.distributed as dist
+    on = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    rank = dist.get_rank() if on else 0
+    col = torch.empty(chain.shape[0], dtype=chain.dtype, device=chain.device)
+    mine = {}
+    for p in outputs:
+        owner = owners[p]
+        if owner == rank:
+            mean, std = predict_fn(p, chain)
+            mine[p] = (mean, std)
+            col.copy_(torch.as_tensor(mean, dtype=chain.dtype).to(chain.device))
+        if on:
+            dist.broadcast(col, owner)
+        chain[:, p - 1].copy_(col)
+    return mine

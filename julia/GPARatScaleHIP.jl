@@ -1,0 +1,356 @@
+#=
+GPARatScaleHIP -- the reference's scaled-GPAR hot path on MI355X through libgparhip.so.
+
+A drop-in for the functions of GPARatScale's hot path (BASELINE.json north_star): same names,
+positional arguments, keywords and return shapes as
+
+  compute_gpar_dtc_objective    src/gp/dtc.jl:83-128          -> (dtc, A)
+  get_optim_scaled_gpar_params  src/gp/dtc.jl:11-77           -> (time_l, time_var, out_l, out_var, noise_sigma)
+  compute_q_u                   src/gp/gpar_scaled_inference.jl:141-196 -> (q_u::MvNormal, U_u)
+  get_gpar_scaled_predictions   src/gp/gpar_scaled_inference.jl:20-136  -> (means, stds)
+  get_sde_predictions           src/gp/temporal_gp_inference.jl:45-114  -> (lgssm, marginals)
+
+with every number computed by the gfx950 kernels behind include/gpar_hip.h.  A caller switches
+`using GPARatScale` to `using GPARatScale, GPARatScaleHIP` and qualifies these five names (or
+imports them from GPARatScaleHIP).  The reference's helpers (to_ColVecs, unpack_gpar,
+unpack_gp, parse_initial_gpar_params, parse_initial_gp_params, create_lgssm) are used as they are.
+
+Julia is absent from the image this was written in, so this file has not been run; its ccall
+argument tuples and struct layouts are checked against include/gpar_hip.h by
+tests/test_julia_shim.py.  Stheno kernel introspection (_kernel_params) follows the Stheno
+0.6-era types the reference's `kernel(k; l, s)` builds (SURVEY §8c: versions unpinned).
+=#
+module GPARatScaleHIP
+
+using LinearAlgebra
+using Random
+using Distributions: MvNormal
+using Stheno
+using Stheno: Matern12, Matern32, Matern52, EQ
+using TemporalGPs: SArrayStorage
+import GPARatScale
+using GPARatScale: to_ColVecs, unpack_gpar, unpack_gp, parse_initial_gpar_params,
+                   parse_initial_gp_params
+
+export compute_gpar_dtc_objective, get_optim_scaled_gpar_params, compute_q_u,
+       get_gpar_scaled_predictions, get_sde_predictions
+
+const libgpar = get(ENV, "GPAR_HIP_LIB", "libgparhip.so")
+
+# ------------------------------------------------------------------ include/gpar_hip.h constants
+const GPAR_ABI_VERSION = Int32(1)
+const GPAR_OK, GPAR_ERR_ARG, GPAR_ERR_NOT_PD = Int32(0), Int32(1), Int32(2)
+const GPAR_MEM_HOST = Int32(0)
+const GPAR_PREDICT_ANALYTIC, GPAR_PREDICT_MC = Int32(0), Int32(1)
+
+kernel_id(::Matern12) = Int32(0)
+kernel_id(::Matern32) = Int32(1)
+kernel_id(::Matern52) = Int32(2)
+kernel_id(::EQ) = Int32(3)
+
+# struct gpar_problem (field order and widths as in the header)
+struct GparProblem
+    n::Int64
+    m::Int64
+    d::Int64
+    t::Ptr{Float64}
+    v::Ptr{Float64}
+    ldv::Int64
+    z::Ptr{Float64}
+    ldz::Int64
+    y::Ptr{Float64}
+    out_kernel::Int32
+    time_kernel::Int32
+    kuu_noise::Int32
+    mem::Int32
+    qu_kuu_noise::Int32
+end
+
+# struct gpar_fit_options
+struct GparFitOptions
+    max_evals::Int32
+    max_iterations::Int32
+    g_tol::Float64
+    time_limit::Float64
+end
+
+# ------------------------------------------------------------------ context and errors
+mutable struct Ctx
+    h::Ptr{Cvoid}
+    function Ctx(device::Integer = 0)
+        v = ccall((:gpar_abi_version, libgpar), Int32, ())
+        v == GPAR_ABI_VERSION || error("libgparhip ABI $v, this binding expects $GPAR_ABI_VERSION")
+        r = Ref{Ptr{Cvoid}}(C_NULL)
+        st = ccall((:gpar_ctx_create, libgpar), Int32, (Int32, Ptr{Ptr{Cvoid}}), device, r)
+        st == GPAR_OK || error("gpar_ctx_create($device) failed ($st): no MI355X visible?")
+        c = new(r[])
+        finalizer(c) do c
+            ccall((:gpar_ctx_destroy, libgpar), Int32, (Ptr{Cvoid},), c.h)
+        end
+    end
+end
+
+const CTX = Ref{Union{Nothing,Ctx}}(nothing)
+ctx() = something(CTX[], (CTX[] = Ctx(parse(Int, get(ENV, "GPAR_HIP_DEVICE", "0")))))
+
+function check(c::Ctx, st)
+    st == GPAR_OK && return nothing
+    msg = unsafe_string(ccall((:gpar_last_error, libgpar), Cstring, (Ptr{Cvoid},), c.h))
+    st == GPAR_ERR_NOT_PD && throw(PosDefException(0))      # as `cholesky` at dtc.jl:119-120
+    st == GPAR_ERR_ARG && throw(DomainError(msg))            # as util.jl:112-117
+    error("libgparhip: $msg")
+end
+
+# ------------------------------------------------------------------ Stheno objects -> numbers
+# kernel(k; l, s) (Stheno 0.6) builds s * stretch(k, 1 / l): Scaled{σ², Stretched{a, base}}.
+_base(k::Union{Matern12,Matern32,Matern52,EQ}) = (k, 1.0, 1.0)
+function _base(k::Stheno.Stretched)
+    b, a, s = _base(k.k)
+    return b, a * only(k.a), s
+end
+function _base(k::Stheno.Scaled)
+    b, a, s = _base(k.k)
+    return b, a, s * only(k.σ²)
+end
+"(structure, lengthscale l, variance s) of kernel(structure; l, s)."
+function _kernel_params(k)
+    b, a, s = _base(k)
+    return b, 1.0 / a, s
+end
+
+# ColVecs (util.jl:16-31) is D x N column-major: point k is column k, so ldv = D.
+_colmat(x) = Matrix{Float64}(to_ColVecs(x).X)
+
+function problem(V::Matrix{Float64}, Z::Matrix{Float64}, t::Vector{Float64}, y::Vector{Float64},
+                 out_kernel, time_kernel; kuu_noise::Bool = true, qu_kuu_noise::Bool = false)
+    size(V, 1) == size(Z, 1) || throw(DomainError(size(Z, 1), "V and Z dimensions differ"))
+    length(t) == length(y) == size(V, 2) || throw(DomainError(length(t), "t, y, V lengths differ"))
+    return GparProblem(length(t), size(Z, 2), size(V, 1), pointer(t), pointer(V), size(V, 1),
+                       pointer(Z), size(Z, 1), pointer(y), kernel_id(out_kernel),
+                       kernel_id(time_kernel), Int32(kuu_noise), GPAR_MEM_HOST, Int32(qu_kuu_noise))
+end
+
+# Optim.Options(time_limit = ...) of dtc.jl:58-61: iterations 1000, g_tol 1e-8, no eval budget
+fit_options(time_limit) = GparFitOptions(Int32(0), Int32(1000), 1e-8, Float64(time_limit))
+
+# ------------------------------------------------------------------ dtc.jl:83-128
+"""
+compute_gpar_dtc_objective(f, u, time_loc, outputs; time_kernel, temporal_noise_sigma, storage)
+
+f = GP(k_o)(V, σ²) and u = GP(k_o)(Z, σ²) as get_optim_scaled_gpar_params builds them
+(dtc.jl:35-36).  Returns (dtc, A) like dtc.jl:127; A (M x N) is materialised only with
+`materialize_A = true` (every caller in the reference discards it), else `nothing`.
+"""
+function compute_gpar_dtc_objective(f, u, time_loc, outputs;
+                                    time_kernel = Matern52(), temporal_noise_sigma = 0.04,
+                                    storage = SArrayStorage(Float64), materialize_A::Bool = false)
+    ok, l_o, s_o = _kernel_params(f.f.k)
+    tk, l_t, s_t = _kernel_params(time_kernel)
+    σ = Float64(temporal_noise_sigma)
+    # the library adds σ² to cov(u) itself (dtc.jl:35,119: u = gp_prior(Z, noise_sigma^2))
+    all(≈(σ^2), diag(u.Σy)) || throw(ArgumentError("cov(u) jitter must be temporal_noise_sigma^2"))
+    V, Z = _colmat(f.x), _colmat(u.x)
+    t = Vector{Float64}(time_loc)
+    y = Vector{Float64}(outputs .- mean(f))                  # dtc.jl:106 decorrelates outputs - mean(f)
+    th = [l_t, sqrt(s_t), l_o, sqrt(s_o), σ]                  # natural units, variances squared inside
+    c = ctx()
+    out = zeros(1)
+    A = materialize_A ? zeros(size(Z, 2), length(t)) : nothing
+    GC.@preserve V Z t y th begin
+        p = Ref(problem(V, Z, t, y, ok, tk))
+        if materialize_A
+            check(c, ccall((:gpar_dtc_objective_A, libgpar), Int32,
+                           (Ptr{Cvoid}, Ref{GparProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                           c.h, p, th, out, A))
+        else
+            check(c, ccall((:gpar_dtc_objective, libgpar), Int32,
+                           (Ptr{Cvoid}, Ref{GparProblem}, Int32, Ptr{Float64}, Ptr{Float64}),
+                           c.h, p, Int32(1), th, out))
+        end
+    end
+    return out[1], A
+end
+
+# ------------------------------------------------------------------ dtc.jl:11-77
+function get_optim_scaled_gpar_params(input_locations, pseudo_input_locations, time_loc, outputs;
+        out_kernel = Matern52(), time_kernel = Matern52(),
+        i_log_time_l = nothing, i_log_time_var = nothing, i_log_out_l = nothing,
+        i_log_out_var = nothing, i_log_noise_sigma = nothing,
+        optimization_time_limit = 1000.0, show_optimization_trace = false, debug::Bool = false,
+        storage = SArrayStorage(Float64))
+    # show_optimization_trace and storage are accepted for signature parity: the simplex runs
+    # inside the library (nelder_mead.hpp) and the state-space storage is the kernels' own.
+    V = _colmat(input_locations)
+    Z = _colmat(pseudo_input_locations)
+    t = Vector{Float64}(time_loc)
+    y = Vector{Float64}(outputs)
+    x0 = Vector{Float64}(parse_initial_gpar_params(i_log_time_l, i_log_time_var, i_log_out_l,
+                                                   i_log_out_var, i_log_noise_sigma))
+    if debug
+        i_time_l, i_time_var, i_out_l, i_out_var, i_noise_sigma = unpack_gpar(x0)
+        println("Generating scaled GPAR with initial parameters:")
+        println("\ti_time_l=$(i_time_l); i_time_var=$(i_time_var); i_out_l=$(i_out_l); i_out_var=$(i_out_var); i_noise_sigma=$(i_noise_sigma)")
+    end
+    c = ctx()
+    θ = zeros(5)
+    nlml = zeros(1)
+    ev = zeros(Int32, 1)
+    opts = Ref(fit_options(optimization_time_limit))
+    GC.@preserve V Z t y x0 begin
+        p = Ref(problem(V, Z, t, y, out_kernel, time_kernel))
+        check(c, ccall((:gpar_fit, libgpar), Int32,
+                       (Ptr{Cvoid}, Ref{GparProblem}, Int32, Ptr{Float64}, Ref{GparFitOptions},
+                        Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
+                       c.h, p, Int32(1), x0, opts, θ, nlml, ev))
+    end
+    opt_params = Tuple(θ)
+    if debug
+        println("Finished optimizing parameters:")
+        println("\tOptimum time L: $(θ[1]) ")
+        println("\tOptimum time var: $(θ[2])")
+        println("\tOptimum outputs l: $(θ[3])")
+        println("\tOptimum outputs var: $(θ[4])")
+        println("\tOptimum Noise std: $(θ[5])")
+        println()
+    end
+    return opt_params
+end
+
+# ------------------------------------------------------------------ gpar_scaled_inference.jl:141-196
+function compute_q_u(input_locations, pseudo_input_locations, time_loc, outputs;
+                     out_kernel = Matern52(), time_kernel = Matern52(),
+                     temporal_noise_sigma = 0.05, debug::Bool = false,
+                     storage = SArrayStorage(Float64))
+    ok, l_o, s_o = _kernel_params(out_kernel)
+    tk, l_t, s_t = _kernel_params(time_kernel)
+    V = _colmat(input_locations)
+    Z = _colmat(pseudo_input_locations)
+    t = Vector{Float64}(time_loc)
+    y = Vector{Float64}(outputs)
+    th = [l_t, sqrt(s_t), l_o, sqrt(s_o), Float64(temporal_noise_sigma)]
+    M = size(Z, 2)
+    me = zeros(M)
+    cov = zeros(M, M)
+    U = zeros(M, M)
+    c = ctx()
+    GC.@preserve V Z t y th begin
+        p = Ref(problem(V, Z, t, y, ok, tk))
+        check(c, ccall((:gpar_q_u, libgpar), Int32,
+                       (Ptr{Cvoid}, Ref{GparProblem}, Ptr{Float64}, Ptr{Float64}, Ptr{Float64},
+                        Ptr{Float64}),
+                       c.h, p, th, me, cov, U))
+    end
+    return MvNormal(me, Symmetric(cov)), UpperTriangular(U)
+end
+
+# ------------------------------------------------------------------ gpar_scaled_inference.jl:20-136
+"""
+Same signature and result as the reference: the fit (Matern52 for both kernels, as :48-49
+hard-codes), q(u) and the 100-sample Monte Carlo at the inference locations.  Extra keywords:
+`mode = :mc` (the reference's estimator) or `:analytic` (its S -> infinity limit), `samples`,
+`seed` (default: drawn from the global RNG, so repeated calls vary as the reference's do).
+"""
+function get_gpar_scaled_predictions(input_locations, pseudo_input_locations, time_loc, outputs,
+        inference_time_loc, inference_input_locations;
+        out_kernel_structure = Matern52(), time_kernel_structure = Matern52(),
+        i_log_time_l = nothing, i_log_time_var = nothing, i_log_out_l = nothing,
+        i_log_out_var = nothing, i_log_noise_sigma = nothing,
+        optimization_time_limit = 1000.0, debug::Bool = false,
+        storage = SArrayStorage(Float64),
+        mode::Symbol = :mc, samples::Integer = 100, seed::UInt64 = rand(UInt64))
+    V = _colmat(input_locations)
+    Z = _colmat(pseudo_input_locations)
+    Vs = _colmat(inference_input_locations)
+    t = Vector{Float64}(time_loc)
+    y = Vector{Float64}(outputs)
+    ts = Vector{Float64}(inference_time_loc)
+    md = mode === :mc ? GPAR_PREDICT_MC : GPAR_PREDICT_ANALYTIC
+    x0 = Vector{Float64}(parse_initial_gpar_params(i_log_time_l, i_log_time_var, i_log_out_l,
+                                                   i_log_out_var, i_log_noise_sigma))
+    debug && println("Starting optimization")
+    c = ctx()
+    θ = zeros(5)
+    nlml = zeros(1)
+    ev = zeros(Int32, 1)
+    ns = length(ts)
+    means = zeros(ns)
+    stds = zeros(ns)
+    opts = Ref(fit_options(optimization_time_limit))
+    GC.@preserve V Z Vs t y ts x0 θ means stds begin
+        pfit = Ref(problem(V, Z, t, y, Matern52(), Matern52()))
+        if out_kernel_structure isa Matern52 && time_kernel_structure isa Matern52
+            # one call: batched fit, then q(u) and prediction at the fitted theta
+            vsp = Ref(pointer(Vs))
+            lds = Ref(Int64(size(Vs, 1)))
+            mp = Ref(pointer(means))
+            sp = Ref(pointer(stds))
+            check(c, ccall((:gpar_fit_predict, libgpar), Int32,
+                           (Ptr{Cvoid}, Ref{GparProblem}, Int32, Ptr{Float64}, Ref{GparFitOptions},
+                            Int64, Ptr{Float64}, Ref{Ptr{Float64}}, Ref{Int64}, Int32, Int32, UInt64,
+                            Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ref{Ptr{Float64}},
+                            Ref{Ptr{Float64}}),
+                           c.h, pfit, Int32(1), x0, opts, ns, ts, vsp, lds, md, Int32(samples),
+                           seed, θ, nlml, ev, mp, sp))
+        else
+            check(c, ccall((:gpar_fit, libgpar), Int32,
+                           (Ptr{Cvoid}, Ref{GparProblem}, Int32, Ptr{Float64}, Ref{GparFitOptions},
+                            Ptr{Float64}, Ptr{Float64}, Ptr{Int32}),
+                           c.h, pfit, Int32(1), x0, opts, θ, nlml, ev))
+            ppred = Ref(problem(V, Z, t, y, out_kernel_structure, time_kernel_structure))
+            check(c, ccall((:gpar_predict, libgpar), Int32,
+                           (Ptr{Cvoid}, Ref{GparProblem}, Ptr{Float64}, Int64, Ptr{Float64},
+                            Ptr{Float64}, Int64, Int32, Int32, UInt64, Ptr{Float64}, Ptr{Float64}),
+                           c.h, ppred, θ, ns, ts, Vs, Int64(size(Vs, 1)), md, Int32(samples), seed,
+                           means, stds))
+        end
+    end
+    return means, stds
+end
+
+# ------------------------------------------------------------------ temporal_gp_inference.jl:45-114
+"Marginal of the latent f at one output location: `.m[1]` mean, `.P[1]` variance."
+struct Marginal
+    m::Vector{Float64}
+    P::Matrix{Float64}
+end
+
+function get_sde_predictions(data_locations, data_outputs, output_locations;
+        kernel_structure::Kernel = Matern52(), sde_storage::SArrayStorage = SArrayStorage(Float64),
+        i_log_time_l = nothing, i_log_time_var = nothing, i_log_noise_sigma = nothing,
+        debug::Bool = true)
+    t = Vector{Float64}(data_locations)
+    y = Vector{Float64}(data_outputs)
+    ts = Vector{Float64}(output_locations)
+    x0 = Vector{Float64}(parse_initial_gp_params(i_log_time_l, i_log_time_var, i_log_noise_sigma))
+    θ = zeros(3)
+    m = zeros(length(ts))
+    v = zeros(length(ts))
+    # Optim.optimize(nlml, params, NelderMead()) with default Options (:82)
+    opts = Ref(fit_options(0.0))
+    c = ctx()
+    GC.@preserve t y ts x0 begin
+        check(c, ccall((:gpar_sde_predictions, libgpar), Int32,
+                       (Ptr{Cvoid}, Int32, Int64, Ptr{Float64}, Ptr{Float64}, Int64, Int64,
+                        Ptr{Float64}, Int32, Ptr{Float64}, Ref{GparFitOptions}, Int32,
+                        Ptr{Float64}, Ptr{Float64}, Ptr{Float64}),
+                       c.h, Int32(1), length(t), t, y, Int64(length(t)), length(ts), ts,
+                       kernel_id(kernel_structure), x0, opts, GPAR_MEM_HOST, θ, m, v))
+    end
+    opt_l, opt_process_var, opt_noise_sigma = θ
+    if debug
+        println("Finished optimizing parameters:")
+        println("\tOptimum L: $(opt_l) ")
+        println("\tOptimum Process Variance: $(opt_process_var)")
+        println("\tOptimum noise: $(opt_noise_sigma)")
+        println()
+    end
+    # the model object the reference returns (:97-105), built by its own create_lgssm (no compute)
+    latent = vcat(t, ts)
+    perm = sortperm(latent)
+    noise_vector = vcat(fill(opt_noise_sigma^2, length(t)), fill(1e10, length(ts)))[perm]
+    opt_lgssm = GPARatScale.create_lgssm(latent[perm], opt_l, opt_process_var, opt_noise_sigma,
+                                         kernel_structure; noise_vector = noise_vector)
+    return opt_lgssm, [Marginal([m[k]], fill(v[k], 1, 1)) for k in eachindex(ts)]
+end
+
+end # module

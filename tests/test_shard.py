@@ -78,3 +78,61 @@ def test_sharded_fit_equals_serial(tmp_path):
     for p in range(1, P + 1):
         ref = _fit(t, Y, p)
         np.testing.assert_array_equal(th[p - 1, : ref.shape[0]], ref)
+
+
+X0 = np.array([0.0, 0.0, 0.0, 0.0, -2.0])
+NS, MC, EVC = 60, 8, 10
+
+
+def _chain_inputs():
+    t, Y = O.synthetic_gpar(N, P, seed=9, noise=0.3)
+    ts = np.sort(np.random.default_rng(10).uniform(t[0], t[-1], NS))
+    F = np.column_stack([np.interp(ts, t, Y[:, q]) for q in range(P)])
+    return t, Y, ts, F
+
+
+def _chain_predict(t, Y, ts, p, chain):
+    """Output p fitted and predicted by the oracle (the stand-in worker), inference inputs read
+    from the chain's first p - 1 columns as they stand."""
+    V = np.ascontiguousarray(Y[:, : p - 1].T)
+    Z = O.pick_pseudo_inputs(V, MC, p)
+    Vs = np.ascontiguousarray(np.asarray(chain)[:, : p - 1].T)
+    m, s, _ = O.get_gpar_scaled_predictions(V, Z, t, Y[:, p - 1], ts, Vs, log_theta0=X0,
+                                            max_evals=EVC, g_tol=-1.0, qu_kuu_noise=True)
+    return m, s
+
+
+def _chain_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "gpar-at-scale_amd", "python"))
+    from gparatscale import shard as S
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t, Y, ts, F = _chain_inputs()
+        chain = torch.zeros((NS, P), dtype=torch.float64)
+        chain[:, 0] = torch.from_numpy(F[:, 0])         # test_y1: the true first output
+        owners = S.owners_of(S.assign_outputs(P, world))
+        mine = S.chained_predictions(range(2, P + 1), owners,
+                                     lambda p, c: _chain_predict(t, Y, ts, p, c.numpy()), chain)
+        assert all(owners[p] == rank for p in mine)
+        if rank == 0:
+            np.save(out, chain.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_chained_predictions_sharded_equal_serial(tmp_path):
+    """world_size 2 over gloo: each predicted mean is broadcast by its owner as soon as it is ready;
+    the chain every rank ends with equals the serial reference chain (GPAR_scaled_examples.jl:172)."""
+    out = str(tmp_path / "chain.npy")
+    mp.start_processes(_chain_worker, args=(2, _free_port(), out), nprocs=2, join=True,
+                       start_method="spawn")
+    got = np.load(out)
+    t, Y, ts, F = _chain_inputs()
+    chain = F[:, :1].copy()
+    for p in range(2, P + 1):
+        m, _ = _chain_predict(t, Y, ts, p, chain)
+        chain = np.column_stack([chain, m])
+    np.testing.assert_array_equal(got, chain)
