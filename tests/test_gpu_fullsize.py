@@ -138,3 +138,47 @@ def test_config5_stress_properties():
     assert np.isfinite(got).all()
     assert got[0] == got[1]
     assert _rel(got[2], got[0]) <= 1e-11, got
+
+
+def test_config5_wide_mixed_batch_properties():
+    """Config 5 at its real width: N = 1e7, M = 1024 and inputs up to D = 255 (P = 256 outputs),
+    HBM-resident (V a column slice of an N x 256 matrix, ldv = 256).  One batched call holds
+    D = 255 (twice, and once with permuted pseudo-inputs), 8, 64 (the fused path's widest) and 65
+    (the distance pass's narrowest): permutation invariance rel <= 1e-11, the repeated problem
+    bit-identical, and each narrower output equal to its own single-problem evaluation."""
+    import torch
+    n, M = 10_000_000, 1024
+    ds = D.gpar_dataset(n, 9, seed=5, observation_noise=0.8)
+    dev = torch.device("cuda", 0)
+    Yb = torch.from_numpy(ds["Y"]).to(dev)
+    t = torch.from_numpy(ds["t"]).to(dev)
+    # 256 input columns from the 8 observed outputs: scaled / shifted copies, as distinct as the
+    # properties need (they hold for any inputs)
+    W = torch.empty((n, 256), dtype=torch.float64, device=dev)
+    for q in range(256):
+        W[:, q] = Yb[:, q % 8] * (1.0 + 0.013 * (q // 8)) + 0.05 * (q // 8)
+    y = Yb[:, 8].contiguous()
+    rows = torch.from_numpy(np.random.default_rng(11).choice(n, M, replace=False)).to(dev)
+    Zfull = W[rows].contiguous()
+    perm = torch.from_numpy(np.random.default_rng(7).permutation(M)).to(dev)
+
+    def prob(d, Z):
+        return G.make_problem(W[:, :d], Z[:, :d].contiguous(), t, y)
+
+    p255, k1 = prob(255, Zfull)
+    p255p, k2 = prob(255, Zfull[perm])
+    p8, k3 = prob(8, Zfull)
+    p64, k4 = prob(64, Zfull)
+    p65, k5 = prob(65, Zfull)
+    theta = np.array([(1.0, 1.0, 6.0 + 0.02 * i, 1.0, 0.25) for i in range(6)])
+    theta[5] = theta[0]
+    got = G.dtc_objective_batch([p255, p8, p255p, p64, p65, p255], theta)
+    assert np.isfinite(got).all(), got
+    assert got[5] == got[0]
+    th2 = theta.copy()
+    th2[2] = theta[0]
+    got2 = G.dtc_objective_batch([p255, p255p], th2[[0, 2]])
+    assert _rel(got2[1], got2[0]) <= 1e-11, got2
+    for j, p in ((1, p8), (3, p64), (4, p65)):
+        single = G.dtc_objective_batch([p], theta[j:j + 1])[0]
+        assert _rel(single, got[j]) <= 1e-12, (j, single, got[j])

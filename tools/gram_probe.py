@@ -27,12 +27,25 @@ def main():
     from gparatscale import data as D
 
     P = a.d + 1
-    ds = D.gpar_dataset(a.n, P, seed=0, observation_noise=0.8)
     dev = torch.device("cuda", 0)
-    t = torch.from_numpy(ds["t"]).to(dev)
-    Y = torch.from_numpy(ds["Y"]).to(dev)
+    if P <= 64:
+        ds = D.gpar_dataset(a.n, P, seed=0, observation_noise=0.8)
+        t = torch.from_numpy(ds["t"]).to(dev)
+        Y = torch.from_numpy(ds["Y"]).to(dev)
+        Z = torch.from_numpy(D.pseudo_inputs(ds["Y"][:, : P - 1], a.m, seed=P)).to(dev)
+    else:
+        # wide inputs (config 5, D up to 255): scaled / shifted copies of 8 observed outputs,
+        # built on the device (a 256-output dataset at N = 1e7 takes minutes on the host)
+        ds = D.gpar_dataset(a.n, 9, seed=0, observation_noise=0.8)
+        t = torch.from_numpy(ds["t"]).to(dev)
+        Yb = torch.from_numpy(ds["Y"]).to(dev)
+        Y = torch.empty((a.n, P), dtype=torch.float64, device=dev)
+        for q in range(P - 1):
+            Y[:, q] = Yb[:, q % 8] * (1.0 + 0.013 * (q // 8)) + 0.05 * (q // 8)
+        Y[:, P - 1] = Yb[:, 8]
+        rows = torch.from_numpy(np.random.default_rng(P).choice(a.n, a.m, replace=False)).to(dev)
+        Z = Y[rows, : P - 1].contiguous()
     y = Y[:, P - 1].contiguous()
-    Z = torch.from_numpy(D.pseudo_inputs(ds["Y"][:, : P - 1], a.m, seed=P)).to(dev)
     pr, keep = G.make_problem(Y[:, : P - 1], Z, t, y, a.kernel, "matern52")
     ctx = G.context(0)
     theta = np.array([[1.0, 1.0, 1.0, 1.0, 0.2]])
