@@ -52,6 +52,37 @@ __device__ __forceinline__ double exp_neg(double x) {
   return ldexp(p, (int)nf);
 }
 
+// exp_neg with its constants handed in by the caller: passed as a kernel argument they live in
+// SGPRs and feed the FMAs directly (a 64-bit literal cannot be an f64 VALU operand, so the
+// inline-constant form re-materialises each one with a v_mov_b64 per evaluation).
+struct ExpNegConsts {
+  double c[12];                 // degree-11 polynomial, highest first (exp_neg's coefficients)
+  double log2e, ln2hi, ln2lo, lo;
+};
+inline ExpNegConsts exp_neg_consts() {
+  return ExpNegConsts{{2.5110037605963777e-08, 2.763263963904103e-07, 2.755724091857897e-06,
+                       2.4801485482328494e-05, 0.00019841269890047113, 0.0013888888952314775,
+                       0.008333333333319601, 0.0416666666664881, 0.1666666666666668,
+                       0.5000000000000019, 1.0, 1.0},
+                      1.4426950408889634074, 6.93147180369123816490e-01,
+                      1.90821492927058770002e-10, -745.5};
+}
+__device__ __forceinline__ double exp_neg_k(double x, const ExpNegConsts& k) {
+  const double y = fmax(-x, k.lo);
+  const double nf = rint(y * k.log2e);
+  double r = fma(-nf, k.ln2hi, y);
+  r = fma(-nf, k.ln2lo, r);
+  double p = k.c[0];
+#pragma unroll
+  for (int i = 1; i < 12; ++i) p = fma(p, r, k.c[i]);
+  return ldexp(p, (int)nf);
+}
+
+// s * kappa(sqrt(d2) / l) with the exp constants from the caller (see ExpNegConsts)
+template <int KIND>
+__device__ __forceinline__ double skappa_sq_k(double d2, double inv_l, double s,
+                                              const ExpNegConsts& k);
+
 // sqrt for x >= 0 (squared distances): v_rsq_f64 seed (~2^-24), one Goldschmidt step for
 // g ~ sqrt(x) (~2^-47), one Newton correction g += (x - g^2) h with the unrefined half-reciprocal
 // h = rsq/2 (its 2^-24 error enters only at second order).  No denormal rescaling or inf/nan
@@ -108,6 +139,22 @@ __device__ __forceinline__ double skappa_sq(double d2, double inv_l, double s) {
   } else {
     const double x = kSqrt5 * inv_l * sqrt_pos(d2);
     return fma(x, fma(x, s * (1.0 / 3.0), s), s) * exp_neg(x);
+  }
+}
+
+template <int KIND>
+__device__ __forceinline__ double skappa_sq_k(double d2, double inv_l, double s,
+                                              const ExpNegConsts& k) {
+  if constexpr (KIND == KEQ) {
+    return s * exp_neg_k(0.5 * d2 * inv_l * inv_l, k);
+  } else if constexpr (KIND == KM12) {
+    return s * exp_neg_k(sqrt_pos(d2) * inv_l, k);
+  } else if constexpr (KIND == KM32) {
+    const double x = kSqrt3 * inv_l * sqrt_pos(d2);
+    return fma(s, x, s) * exp_neg_k(x, k);
+  } else {
+    const double x = kSqrt5 * inv_l * sqrt_pos(d2);
+    return fma(x, fma(x, s * (1.0 / 3.0), s), s) * exp_neg_k(x, k);
   }
 }
 

@@ -31,6 +31,7 @@ struct gpar_ctx {
   hipStream_t input_stream = nullptr;
   hipEvent_t ev_input = nullptr;
   int lanes = 1;                  // gpar_ctx_set_lanes: streams a batch's outputs alternate over
+  int64_t dist_cache_bytes = -1;  // gpar_ctx_set_dist_cache: -1 auto, 0 off, else a byte budget
   std::string err;
   struct Buf {
     void* p = nullptr;
@@ -177,6 +178,9 @@ struct DevProblem {
   const double* zc;      // centres of the pseudo-input column groups (MFMA whitening), per problem
   int64_t ldv, ldz;
   int ok, tk, sdim, kuu_noise, qu_noise;
+  // squared distances |v_k - z_c|^2 (n x mp, ld mp), theta-independent: computed once per fit
+  // when the distance cache holds this output (fit_impl), else null
+  const double* d2 = nullptr;
 };
 
 static void check_sorted_host(const double* t, int64_t n) {
@@ -315,7 +319,10 @@ static void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const double* rec, 
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
                            int64_t ldb, double* send, const double* g, double* hsum) {
   const double s_o = th.sv_o * th.sv_o;
-  if (p.d > kFusedMaxD) {
+  if (p.d2 && v == p.v) {   // the fit's training inputs, distances cached (fit_impl)
+    launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, p.d2, p.mp, p.m, p.mp, n, kChunk, nch,
+                         1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum);
+  } else if (p.d > kFusedMaxD) {
     launch_dist2(c->stream, p.ok, v, ldv, n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, beta, ldb);
     launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, beta, ldb, p.m, p.mp, n, kChunk, nch,
                          1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum);
@@ -1038,6 +1045,13 @@ int32_t gpar_ctx_set_lanes(gpar_ctx* ctx, int32_t lanes) {
   return GPAR_OK;
 }
 
+int32_t gpar_ctx_set_dist_cache(gpar_ctx* ctx, int64_t bytes) {
+  API_BEGIN(ctx)
+  ARGCHECK(bytes >= -1, "bytes must be -1 (auto), 0 (off) or a budget");
+  ctx->dist_cache_bytes = bytes;
+  API_END(ctx)
+}
+
 int32_t gpar_ctx_reset_stats(gpar_ctx* ctx) {
   API_BEGIN(ctx)
   flush_stats(ctx);
@@ -1069,9 +1083,50 @@ struct FitKeep {
   std::vector<char> valid;
 };
 
-static void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P, const double* log_theta0,
+// Distance cache: the squared distances |v_k - z_c|^2 do not depend on theta, so for the
+// outputs it holds they are computed once per fit (dist2, k_dist.hip) and every evaluation's
+// whitening reads them (whiten_kfu_d2, memory-bound) instead of rebuilding the distance
+// contraction on MFMA inside the fused kernel, whose cost grows with D.  Measured at N = 1e6,
+// M = 512: fused 1.62 / 2.13 / 2.6 / 3.2 ms at D = 16 / 32 / 48 / 63, cached 1.75 ms at any D;
+// so outputs with D >= kDistCacheMinD are cached, widest first, while the budget lasts
+// (gpar_ctx_set_dist_cache; default: the free HBM less a reserve).  n x mp doubles each.
+constexpr int64_t kDistCacheMinD = 17;
+
+static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<DevProblem>& P) {
+  std::vector<DevProblem> Q = P;
+  if (c->dist_cache_bytes == 0) return Q;
+  int64_t budget = c->dist_cache_bytes;
+  if (budget < 0) {   // auto: free HBM (the cache buffers already held count as free) - reserve
+    size_t fr = 0, tot = 0;
+    HIPCHECK(hipMemGetInfo(&fr, &tot));
+    int64_t held = 0;
+    for (auto& kv : c->bufs)
+      if (kv.first.rfind("distcache", 0) == 0) held += (int64_t)kv.second.bytes;
+    const int64_t reserve = std::max<int64_t>((int64_t)16 << 30, (int64_t)(tot / 10));
+    budget = std::max<int64_t>(0, (int64_t)fr + held - reserve);
+  }
+  std::vector<int> order(P.size());
+  for (size_t i = 0; i < P.size(); ++i) order[i] = (int)i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return P[a].d > P[b].d; });
+  int slot = 0;
+  for (int i : order) {
+    const DevProblem& p = P[i];
+    if (p.d < kDistCacheMinD) continue;
+    const int64_t bytes = p.n * p.mp * (int64_t)sizeof(double);
+    if (bytes > budget) continue;
+    budget -= bytes;
+    double* d2 = ws<double>(c, "distcache" + std::to_string(slot++), (size_t)p.n * p.mp);
+    launch_dist2(c->stream, p.ok, p.v, p.ldv, p.n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, d2, p.mp);
+    check_launch("dist2 (cache)");
+    Q[i].d2 = d2;
+  }
+  return Q;
+}
+
+static void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* log_theta0,
                      const gpar_fit_options& o, double* theta_out, double* nlml_out,
                      int32_t* evals_out, FitKeep* keep) {
+  const std::vector<DevProblem> P = attach_dist_cache(ctx, P0);
   const int nprob = (int)P.size();
   std::vector<NelderMead> nm;
   nm.reserve(nprob);

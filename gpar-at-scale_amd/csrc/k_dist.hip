@@ -13,9 +13,11 @@
 // with g the centre of the 256-pseudo-input group of column c (zcenter, the same centring the
 // fused kernel uses: Distances.jl's Gram form with the cancellation of the shared offset removed,
 // SURVEY §8a a1).  Matern-1/2 needs direct differences (its kernel is not smooth in d^2 at 0), so
-// it gets a VALU tile kernel instead.  The distances are theta-independent; whiten_kfu_d2 then
-// evaluates Kfu = s_o kappa(sqrt(d2) / l_o) on the fly, runs the chunk-local Kalman filter and
-// overwrites d2 with beta_loc in place (one read + one write of N x Mp doubles).
+// it gets a VALU tile kernel instead.  whiten_kfu_d2x2 then evaluates Kfu = s_o kappa(sqrt(d2) /
+// l_o) on the fly, runs the chunk-local Kalman filter and writes beta_loc (one read + one write of
+// N x Mp doubles): in place over d2 for D > 64, or from the fit's distance cache -- the distances
+// are theta-independent, so gpar_host.cpp (attach_dist_cache) computes them once per fit for the
+// outputs it caches and every objective evaluation reads them.
 #include "device_common.hpp"
 
 namespace gpar {
@@ -186,95 +188,127 @@ __global__ __launch_bounds__(256) void dist2_direct_kernel(
 
 // ---------------------------------------------------------------------------- whitening from d2
 // beta_loc[k][c] = chunk-local whitened Kfu column c, Kfu[k][c] = s_o kappa(sqrt(d2[k][c]) / l_o),
-// reading d2 from `src` (ld lds) and writing beta (ld ldb; in place when src == beta: every
-// thread reads only rows ahead of the ones it has written, of its own column).  grid (nch,
-// ceil(mp / 256)), one column per thread; per 16-step sub-tile the gains records and fix-up rows
-// are staged in LDS (uniform, read back as broadcasts) and the next sub-tile's 16 d2 values are
-// prefetched into registers, so the loads of sub-tile s + 1 are in flight under the kernel
-// evaluations and the filter recursion of sub-tile s.  Outputs as whiten_kfu (send, hsum).
-constexpr int kWT = 16;
+// reading d2 from `src` (ld lds) and writing beta (ld ldb; in place when src == beta: each thread
+// reads only rows ahead of the ones it has written, of its own columns).  Laid out for issue
+// efficiency: each thread runs TWO adjacent columns (16-byte d2 loads and beta stores; every gains
+// record read from LDS serves both recursions, which also interleave), and the whole chunk's
+// records and fix-up rows (L <= 256 steps, 40 KB) are staged in LDS once, so the chunk runs with
+// no workgroup barrier after the first.  grid (nch, ceil(mp / 512)); the next kW2T rows' d2 pairs
+// are prefetched into registers under the current rows' kernel evaluations and recursions; the
+// exp constants come in as a kernel argument (SGPR operands, see ExpNegConsts).  Outputs as
+// whiten_kfu (send, hsum).  Measured at N = 1e6, M = 512: 1.74 ms = 4.7 TB/s of d2 read + beta
+// write (8.2 GB); the single-column form with per-16-row staging took 2.13 ms; occupancy 3
+// (4-row tiles) and inline exp constants measured the same.  Requires L <= kW2MaxL, even lds /
+// ldb, 16-byte aligned src / beta (mp is a multiple of 128).
+constexpr int kW2MaxL = 256;
+
+constexpr int kW2T = 8;
 
 template <int TK, int OK>
-__global__ __launch_bounds__(256) void whiten_kfu_d2(
+__global__ __launch_bounds__(256, 2) void whiten_kfu_d2x2(
     const double* __restrict__ rec, const double* src, int64_t lds, int64_t m, int64_t mp,
     int64_t n, int L, double inv_lo, double s_o, double* beta, int64_t ldb,
     double* __restrict__ send, int64_t mc, const double* __restrict__ g,
-    double* __restrict__ hsum) {
+    double* __restrict__ hsum, ExpNegConsts ek) {
   constexpr int SD = Sde<TK>::d;
   constexpr int RS = Rec<SD>::size;
-  __shared__ __attribute__((aligned(16))) double rl[kWT * RS];
-  __shared__ __attribute__((aligned(16))) double gl[kWT * kGStride];
+  __shared__ __attribute__((aligned(16))) double rl[kW2MaxL * RS];
+  __shared__ __attribute__((aligned(16))) double gl[kW2MaxL * kGStride];
   const int tid = threadIdx.x;
   const int64_t j = blockIdx.x;
-  const int64_t c = (int64_t)blockIdx.y * 256 + tid;
-  const bool colv = c < m, cola = c < mp;
+  const int64_t c = ((int64_t)blockIdx.y * 256 + tid) * 2;   // first of the thread's two columns
+  const bool cola = c < mp;                                  // mp even: both or neither
+  const bool v0 = c < m, v1 = c + 1 < m;
   const int64_t cc = cola ? c : 0;
   const int64_t k0 = j * L;
   const int64_t k1 = (k0 + L < n) ? k0 + L : n;
-  double mst[SD], hs[SD];
+  const int nk = (int)(k1 - k0);
+  // the chunk's records and fix-up rows, once
+  for (int e = tid; e < nk * RS; e += 256) rl[e] = rec[k0 * RS + e];
+  for (int e = tid; e < nk * kGStride; e += 256) gl[e] = g[k0 * kGStride + e];
+  double ma[SD], mb[SD], ha[SD], hb[SD];
 #pragma unroll
-  for (int i = 0; i < SD; ++i) mst[i] = hs[i] = 0.0;
-  double px[kWT], pr, pg;
-  auto prefetch = [&](int64_t kt_) __attribute__((always_inline)) {
+  for (int i = 0; i < SD; ++i) ma[i] = mb[i] = ha[i] = hb[i] = 0.0;
+  const double* sp = src + k0 * lds + cc;
+  double* bp = beta + k0 * ldb + cc;
+  double2 px[kW2T];
+  auto prefetch = [&](int r0) __attribute__((always_inline)) {
 #pragma unroll
-    for (int r = 0; r < kWT; ++r) {
-      const int64_t k = (kt_ + r < n) ? kt_ + r : n - 1;
-      px[r] = src[k * lds + cc];
+    for (int r = 0; r < kW2T; ++r) {
+      const int rr = (r0 + r < nk) ? r0 + r : nk - 1;
+      px[r] = *reinterpret_cast<const double2*>(sp + (int64_t)rr * lds);
     }
-    const int64_t ir = kt_ * RS + tid;
-    pr = rec[ir < n * RS ? ir : n * RS - 1];
-    const int64_t ig = kt_ * kGStride + tid;
-    pg = g[ig < n * kGStride ? ig : n * kGStride - 1];
   };
-  if (k0 < k1) prefetch(k0);
-  for (int64_t kt = k0; kt < k1; kt += kWT) {
-    const int nt = (kt + kWT <= k1) ? kWT : (int)(k1 - kt);
-    __syncthreads();
-    if (tid < kWT * RS) rl[tid] = tid < nt * RS ? pr : 0.0;
-    if (tid < kWT * kGStride) gl[tid] = tid < nt * kGStride ? pg : 0.0;
-    double x[kWT];
+  if (nk > 0) prefetch(0);
+  __syncthreads();
+  for (int r0 = 0; r0 < nk; r0 += kW2T) {
+    double2 x[kW2T];
 #pragma unroll
-    for (int r = 0; r < kWT; ++r) x[r] = px[r];
-    __syncthreads();
-    if (kt + kWT < k1) prefetch(kt + kWT);
+    for (int r = 0; r < kW2T; ++r) x[r] = px[r];
+    if (r0 + kW2T < nk) prefetch(r0 + kW2T);
 #pragma unroll
-    for (int r = 0; r < kWT; ++r) {
-      double d2 = x[r];
-      if constexpr (OK == KEQ) d2 = d2 > 0.0 ? d2 : 0.0;   // the Matern forms clamp in sqrt_pos
-      x[r] = colv ? skappa_sq<OK>(d2, inv_lo, s_o) : 0.0;
+    for (int r = 0; r < kW2T; ++r) {
+      double a = x[r].x, b = x[r].y;
+      if constexpr (OK == KEQ) {
+        a = a > 0.0 ? a : 0.0;
+        b = b > 0.0 ? b : 0.0;
+      }
+      x[r].x = v0 ? skappa_sq_k<OK>(a, inv_lo, s_o, ek) : 0.0;
+      x[r].y = v1 ? skappa_sq_k<OK>(b, inv_lo, s_o, ek) : 0.0;
     }
-    auto step = [&](int kk) __attribute__((always_inline)) {
-      const double* rr = rl + kk * RS;
-      double mm[SD];
+    auto step = [&](int r) __attribute__((always_inline)) {
+      const double* rr = rl + (r0 + r) * RS;
+      const double* gg = gl + (r0 + r) * kGStride;
+      double pa[SD], pb[SD];
 #pragma unroll
       for (int i = 0; i < SD; ++i) {
-        double a2 = 0.0;
+        double sa = 0.0, sb = 0.0;
 #pragma unroll
-        for (int q = 0; q < SD; ++q) a2 = fma(rr[i * SD + q], mst[q], a2);
-        mm[i] = a2;
+        for (int q = 0; q < SD; ++q) {
+          sa = fma(rr[i * SD + q], ma[q], sa);
+          sb = fma(rr[i * SD + q], mb[q], sb);
+        }
+        pa[i] = sa;
+        pb[i] = sb;
       }
-      const double ev = x[kk] - mm[0];
-      const double al = ev * rr[SD * SD + SD];
+      const double ea = x[r].x - pa[0], eb = x[r].y - pb[0];
+      const double rs = rr[SD * SD + SD];
+      const double aa = ea * rs, ab = eb * rs;
 #pragma unroll
-      for (int i = 0; i < SD; ++i) mst[i] = fma(rr[SD * SD + i], ev, mm[i]);
-#pragma unroll
-      for (int i = 0; i < SD; ++i) hs[i] = fma(al, gl[kk * kGStride + i], hs[i]);
-      if (cola) beta[(kt + kk) * ldb + c] = al;
+      for (int i = 0; i < SD; ++i) {
+        const double kg = rr[SD * SD + i];
+        ma[i] = fma(kg, ea, pa[i]);
+        mb[i] = fma(kg, eb, pb[i]);
+        const double gi = gg[i];
+        ha[i] = fma(aa, gi, ha[i]);
+        hb[i] = fma(ab, gi, hb[i]);
+      }
+      if (cola) {
+        double2 o;
+        o.x = aa;
+        o.y = ab;
+        *reinterpret_cast<double2*>(bp + (int64_t)(r0 + r) * ldb) = o;
+      }
     };
-    if (nt == kWT) {
+    if (r0 + kW2T <= nk) {
 #pragma unroll
-      for (int kk = 0; kk < kWT; ++kk) step(kk);
-    } else {
+      for (int r = 0; r < kW2T; ++r) step(r);
+    } else {   // the chunk's last rows (n not a multiple of 8): unrolled, uniform predicate
+      const int nr = nk - r0;
 #pragma unroll
-      for (int kk = 0; kk < kWT; ++kk)
-        if (kk < nt) step(kk);
+      for (int r = 0; r < kW2T; ++r)
+        if (r < nr) step(r);
     }
   }
   if (cola) {
 #pragma unroll
     for (int i = 0; i < SD; ++i) {
-      send[(j * mc + c) * kSStride + i] = mst[i];
-      if (hsum) hsum[(j * mc + c) * kSStride + i] = hs[i];
+      send[(j * mc + c) * kSStride + i] = ma[i];
+      send[(j * mc + c + 1) * kSStride + i] = mb[i];
+      if (hsum) {
+        hsum[(j * mc + c) * kSStride + i] = ha[i];
+        hsum[(j * mc + c + 1) * kSStride + i] = hb[i];
+      }
     }
   }
 }
@@ -299,6 +333,7 @@ __global__ __launch_bounds__(256) void zcenter_wide_kernel(const double* __restr
 
 // ============================================================================ launch wrappers
 #include "launch.hpp"
+#include <stdexcept>
 
 namespace gpar {
 
@@ -330,8 +365,10 @@ static void launch_wd2_k(hipStream_t st, dim3 grid, const double* rec, const dou
                          int64_t lds, int64_t m, int64_t mp, int64_t n, int L, double inv_lo,
                          double s_o, double* beta, int64_t ldb, double* send, int64_t mc,
                          const double* g, double* hsum) {
-  whiten_kfu_d2<TK, OK><<<grid, 256, 0, st>>>(rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb,
-                                              send, mc, g, hsum);
+  if (L > kW2MaxL || (lds & 1) || (ldb & 1))
+    throw std::runtime_error("whiten_kfu_d2x2: chunk length > 256 or odd leading dimension");
+  whiten_kfu_d2x2<TK, OK><<<grid, 256, 0, st>>>(rec, src, lds, m, mp, n, L, inv_lo, s_o, beta,
+                                                ldb, send, mc, g, hsum, exp_neg_consts());
 }
 
 template <int TK>
@@ -351,7 +388,7 @@ void launch_whiten_kfu_d2(hipStream_t st, int time_kind, int out_kind, const dou
                           const double* src, int64_t lds, int64_t m, int64_t mp, int64_t n, int L,
                           int64_t nch, double inv_lo, double s_o, double* beta, int64_t ldb,
                           double* send, int64_t mc, const double* g, double* hsum) {
-  dim3 grid((unsigned)nch, (unsigned)((mp + 255) / 256));
+  dim3 grid((unsigned)nch, (unsigned)((mp + 511) / 512));
   switch (time_kind) {
     case KM12: launch_wd2_t<KM12>(st, out_kind, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
     case KM32: launch_wd2_t<KM32>(st, out_kind, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;

@@ -27,7 +27,7 @@ EXPORTED = (
     "gpar_fit", "gpar_fit_predict", "gpar_fit_predict_chain", "gpar_mc_normals", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
     "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_reset_stats",
-    "gpar_ctx_set_lanes", "gpar_ctx_set_input_stream", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
+    "gpar_ctx_set_lanes", "gpar_ctx_set_dist_cache", "gpar_ctx_set_input_stream", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
 )
 
 
@@ -95,6 +95,7 @@ def load(path: str | None = None):
             "gpar_ctx_kernel_stats": (i32, [vp, C.c_char_p, C.POINTER(i64), C.POINTER(C.c_double)]),
             "gpar_ctx_reset_stats": (i32, [vp]),
             "gpar_ctx_set_lanes": (i32, [vp, i32]),
+            "gpar_ctx_set_dist_cache": (i32, [vp, i64]),
             "gpar_ctx_set_input_stream": (i32, [vp, vp, i32]),
             "gpar_dtc_objective": (i32, [vp, C.POINTER(GparProblem), i32, dp, dp]),
             "gpar_dtc_objective_A": (i32, [vp, C.POINTER(GparProblem), dp, dp, dp]),
@@ -206,6 +207,10 @@ class Context:
 
     def reset_stats(self):
         self.check(load().gpar_ctx_reset_stats(self.h))
+
+    def set_dist_cache(self, nbytes=-1):
+        """Byte budget of the fit's distance cache (gpar_ctx_set_dist_cache): -1 auto, 0 off."""
+        self.check(load().gpar_ctx_set_dist_cache(self.h, int(nbytes)))
 
     def set_lanes(self, lanes):
         """1 (the default): serial batched evaluation; 2: outputs alternate over two HIP streams."""

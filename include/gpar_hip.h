@@ -112,6 +112,13 @@ int32_t gpar_ctx_reset_stats(gpar_ctx* ctx);
  * one output's whitening overlaps another's Gram (~1 % faster at N = 1e6, M = 512, two beta
  * buffers); 1 (the default) serialises them on the context stream. */
 int32_t gpar_ctx_set_lanes(gpar_ctx* ctx, int32_t lanes);
+/* Distance cache of gpar_fit / gpar_fit_predict: the squared input distances |v_k - z_c|^2 are
+ * theta-independent, so for outputs with D >= 17 they are computed once per fit call (N x Mp
+ * doubles per output, widest outputs first) and every objective evaluation's whitening reads them
+ * instead of rebuilding them.  bytes = -1 (the default): budget = free device memory less a
+ * reserve (max(16 GiB, 10 % of HBM)); 0: off; > 0: that budget.  The buffers stay in the
+ * context's workspace (gpar_ctx_trim releases them). */
+int32_t gpar_ctx_set_dist_cache(gpar_ctx* ctx, int64_t bytes);
 /* Producer ordering for GPAR_MEM_DEVICE inputs: with enable = 1, every later call on ctx first
  * makes its streams wait (device side, hipStreamWaitEvent) for all work queued so far on
  * `stream` (a hipStream_t; 0 = the null stream), e.g. the copies that produced its device inputs
