@@ -52,6 +52,8 @@ CONFIGS = {
 # (SQ_VALU_MFMA_BUSY_CYCLES / SQ_INSTS_MFMA = 64, profiles/) x 2.4 GHz = 78.6 TF/s (AMD spec value)
 FP64_MFMA_PEAK_TFLOPS = 78.6
 HBM_PEAK_GBS = 8000.0
+# HBM bytes per launch from the PMC passes of this round's sources (tools/pmc_passes.sh, D = 32)
+PMC_FILE = "pmc_gram_whiten_r02.json"
 
 
 def log(*a):
@@ -234,17 +236,21 @@ def main():
         el = float(e[0])
     gram_n, gram_ms = ctx.kernel_stats("gram")
     wh_n, wh_ms = ctx.kernel_stats("whiten")
+    gram_work = ctx.kernel_work("gram")      # flops, N*M*(M+1) per launch
+    wh_work = ctx.kernel_work("whiten")      # algorithmic HBM bytes (include/gpar_hip.h)
     out = None
     if rank == 0:
         value = n_eff * P / (el / 1e3)
         flops = float(n_eff) * M * (M + 1)       # N*M*(M+1) per Gram launch
         avg = gram_ms / max(gram_n, 1)
-        achieved = flops / (avg * 1e-3) / 1e12 if gram_n else None
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "pmc_gram2_whiten_r01i.json")   # tools/pmc_passes.sh at the north config
+        achieved = gram_work / (gram_ms * 1e-3) / 1e12 if gram_n else None
+        traffic = wtraffic = None
+        pmc = os.path.join(ROOT, "profiles", PMC_FILE)   # tools/pmc_passes.sh at the north config
         if args.config == "north" and os.path.exists(pmc):
             with open(pmc) as f:
-                traffic = json.load(f).get("hbm_bytes_per_launch")
+                pj = json.load(f)
+            traffic = pj.get("hbm_bytes_per_launch")
+            wtraffic = pj.get("whiten_hbm_bytes_per_launch")
         out = {
             # BASELINE.json's metric string (north), the same wording at the other configs' sizes
             "metric": "GPAR fit+predict wall-clock (ms) and pts\u00b7outputs/sec, "
@@ -273,6 +279,21 @@ def main():
             "kernels": {"gram_ms_per_step": gram_ms / args.steps, "whiten_ms_per_step": wh_ms / args.steps,
                         "whiten_launches": wh_n},
         }
+        if wh_n:
+            wa = wh_work / (wh_ms * 1e-3) / 1e9
+            out["roofline_whiten"] = {
+                "bound": "hbm", "achieved": wa, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": wa / HBM_PEAK_GBS, "traffic": wtraffic, "launches": wh_n,
+                "avg_ms": wh_ms / wh_n, "bytes_per_launch": wh_work / wh_n,
+                "kernel": "Kfu assembly + Kalman whitening (whiten_kfu_d2x2 from the fit's distance "
+                          "cache for D >= 17, fused whiten_kfu_mfma below)",
+                "bytes": "8 N (D + M + 20) per launch (M for D when cached), include/gpar_hip.h"}
+        if gram_n:
+            # the whole job against its dominant kernel's floor: every Gram launch at the fp64
+            # MFMA peak, nothing else, vs the measured step
+            floor_ms = gram_work / args.steps / (FP64_MFMA_PEAK_TFLOPS * 1e12) * 1e3
+            out["job_vs_gram_floor"] = {"floor_ms_per_step": floor_ms, "frac": floor_ms / el,
+                                        "note": "Gram launches of one step at 78.6 TF/s / measured step"}
         if args.lanes > 1 and out["roofline"]:
             # two streams overlap launches: event spans are not the kernel's own duration
             out["roofline"].update(achieved=None, frac=None,

@@ -40,10 +40,15 @@ struct gpar_ctx {
   std::unordered_map<std::string, Buf> bufs;
   // event-based kernel timing (gpar_ctx_set_profiling)
   bool profiling = false;
+  struct Pending {
+    hipEvent_t e0, e1;
+    double work;   // algorithmic work of the timed launches (flops or HBM bytes, per family)
+  };
   struct Stat {
-    std::vector<std::pair<hipEvent_t, hipEvent_t>> pending;
+    std::vector<Pending> pending;
     int64_t launches = 0;
     double ms = 0.0;
+    double work = 0.0;
   };
   std::unordered_map<std::string, Stat> stats;
 };
@@ -77,17 +82,18 @@ static void check_launch(const char* what) {
 }
 
 // RAII timing scope: records HIP events around the enclosed launches on the ctx stream.
+// work: the algorithmic work of the enclosed launches (gpar_ctx_kernel_work).
 struct Timed {
   gpar_ctx* c;
   const char* name;
   hipEvent_t e1 = nullptr;
-  Timed(gpar_ctx* c_, const char* n) : c(c_), name(n) {
+  Timed(gpar_ctx* c_, const char* n, double work = 0.0) : c(c_), name(n) {
     if (!c->profiling) return;
     hipEvent_t e0;
     (void)hipEventCreate(&e0);
     (void)hipEventCreate(&e1);
     (void)hipEventRecord(e0, c->stream);
-    c->stats[name].pending.push_back({e0, e1});
+    c->stats[name].pending.push_back({e0, e1, work});
   }
   ~Timed() {
     if (e1) (void)hipEventRecord(e1, c->stream);
@@ -99,12 +105,13 @@ static void flush_stats(gpar_ctx* c) {
   for (auto& kv : c->stats) {
     for (auto& pr : kv.second.pending) {
       float ms = 0.f;
-      if (hipEventElapsedTime(&ms, pr.first, pr.second) == hipSuccess) {
+      if (hipEventElapsedTime(&ms, pr.e0, pr.e1) == hipSuccess) {
         kv.second.ms += ms;
         kv.second.launches += 1;
+        kv.second.work += pr.work;
       }
-      (void)hipEventDestroy(pr.first);
-      (void)hipEventDestroy(pr.second);
+      (void)hipEventDestroy(pr.e0);
+      (void)hipEventDestroy(pr.e1);
     }
     kv.second.pending.clear();
   }
@@ -450,7 +457,10 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     }
     const double s_o = th[i].sv_o * th[i].sv_o;
     {
-      Timed tm_(c, "whiten");
+      // algorithmic HBM bytes: the inputs (V, or the cached distances), the gains records and
+      // fix-up rows (16 + 4 doubles per step), beta written (m columns)
+      const double in_cols = p.d2 ? (double)p.m : (double)p.d;
+      Timed tm_(c, "whiten", 8.0 * (double)n * (in_cols + (double)p.m + 20.0));
       whiten_kfu_any(c, p, g.rec, p.v, p.ldv, n, nch, th[i], beta, p.mp, send, g.g, hsum);
     }
     check_launch("whiten_kfu");
@@ -478,7 +488,7 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     double* rpart = ws<double>(c, "gram_rpart" + sfx, (size_t)plan.rpart_doubles);
     HIPCHECK(hipMemsetAsync(beta + (size_t)n * p.mp, 0, (size_t)16 * p.mp * sizeof(double), c->stream));
     {
-      Timed tm_(c, "gram");
+      Timed tm_(c, "gram", (double)n * (double)p.m * (double)(p.m + 1));   // flops of beta^T beta
       launch_gram(c->stream, p.sdim, plan, beta, p.mp, n, fix_beta ? nullptr : hsum, cin, qv,
                   p.mc, kChunk, alpha, part, rpart, o.G + (size_t)i * mpmax * mpmax, mpmax,
                   o.r + (size_t)i * mpmax);
@@ -1025,6 +1035,15 @@ int32_t gpar_ctx_kernel_stats(gpar_ctx* ctx, const char* name, int64_t* launches
   auto it = ctx->stats.find(name);
   *launches = it == ctx->stats.end() ? 0 : it->second.launches;
   *total_ms = it == ctx->stats.end() ? 0.0 : it->second.ms;
+  API_END(ctx)
+}
+
+int32_t gpar_ctx_kernel_work(gpar_ctx* ctx, const char* name, double* work) {
+  API_BEGIN(ctx)
+  ARGCHECK(name && work, "null argument");
+  flush_stats(ctx);
+  auto it = ctx->stats.find(name);
+  *work = it == ctx->stats.end() ? 0.0 : it->second.work;
   API_END(ctx)
 }
 

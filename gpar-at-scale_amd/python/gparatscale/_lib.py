@@ -26,7 +26,7 @@ EXPORTED = (
     "gpar_ctx_workspace_bytes", "gpar_ctx_trim", "gpar_dtc_objective", "gpar_dtc_objective_A",
     "gpar_fit", "gpar_fit_predict", "gpar_fit_predict_chain", "gpar_mc_normals", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
-    "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_reset_stats",
+    "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_kernel_work", "gpar_ctx_reset_stats",
     "gpar_ctx_set_lanes", "gpar_ctx_set_dist_cache", "gpar_ctx_set_input_stream", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
 )
 
@@ -94,6 +94,7 @@ def load(path: str | None = None):
             "gpar_ctx_set_profiling": (i32, [vp, i32]),
             "gpar_ctx_kernel_stats": (i32, [vp, C.c_char_p, C.POINTER(i64), C.POINTER(C.c_double)]),
             "gpar_ctx_reset_stats": (i32, [vp]),
+            "gpar_ctx_kernel_work": (i32, [vp, C.c_char_p, C.POINTER(C.c_double)]),
             "gpar_ctx_set_lanes": (i32, [vp, i32]),
             "gpar_ctx_set_dist_cache": (i32, [vp, i64]),
             "gpar_ctx_set_input_stream": (i32, [vp, vp, i32]),
@@ -199,6 +200,13 @@ class Context:
         ms = C.c_double()
         self.check(load().gpar_ctx_kernel_stats(self.h, name.encode(), C.byref(n), C.byref(ms)))
         return int(n.value), float(ms.value)
+
+    def kernel_work(self, name):
+        """Algorithmic work of the timed launches of a family since the last reset
+        (gpar_ctx_kernel_work): flops for "gram", HBM bytes for "whiten"."""
+        w = C.c_double()
+        self.check(load().gpar_ctx_kernel_work(self.h, name.encode(), C.byref(w)))
+        return float(w.value)
 
     def follow_stream(self, stream_ptr):
         """Order every later call after the work queued on `stream_ptr` (a hipStream_t handle,

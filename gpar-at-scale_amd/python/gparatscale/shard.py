@@ -13,18 +13,22 @@ import heapq
 
 import numpy as np
 
-# Per-objective-evaluation cost model of output p (ms at N=1e6, M=512 on one MI355X, profiles/):
-# the Gram beta^T beta is independent of the input dimension D = p - 1, the whitening grows with
-# it, the temporal-only output 1 is ~20x cheaper.  Only relative sizes matter.
-GRAM_MS = 6.9
-WHITEN_MS0, WHITEN_MS_PER_D = 1.3, 0.033
+# Per-objective-evaluation cost model of output p (ms at N=1e6, M=512 on one MI355X,
+# profiles/rocprof_bench_r02f_north_stats.csv): the Gram beta^T beta is independent of the input
+# dimension D = p - 1; the whitening is the fused kernel for D <= 16 and reads the fit's distance
+# cache above (D-independent, plus the one-off distance pass spread over the fit's evaluations);
+# the dense tail, carries and gains add ~0.9; the temporal-only output 1 is ~20x cheaper.  Only
+# relative sizes matter.
+GRAM_MS = 4.4
+WHITEN_FUSED_MS, WHITEN_CACHED_MS = 1.50, 1.56
+OTHER_MS = 0.9
 SDE_MS = 0.4
 
 
 def output_cost(p: int) -> float:
     if p == 1:
         return SDE_MS
-    return GRAM_MS + WHITEN_MS0 + WHITEN_MS_PER_D * (p - 1)
+    return GRAM_MS + OTHER_MS + (WHITEN_FUSED_MS if p - 1 < 17 else WHITEN_CACHED_MS)
 
 
 def assign_outputs(P: int, world: int) -> list[list[int]]:

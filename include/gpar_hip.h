@@ -107,6 +107,11 @@ int32_t gpar_ctx_trim(gpar_ctx* ctx);
 int32_t gpar_ctx_set_profiling(gpar_ctx* ctx, int32_t on);
 int32_t gpar_ctx_kernel_stats(gpar_ctx* ctx, const char* name, int64_t* launches, double* total_ms);
 int32_t gpar_ctx_reset_stats(gpar_ctx* ctx);
+/* Algorithmic work of the timed launches of a family since the last reset (for rooflines):
+ * "gram": flops, N M (M + 1) per launch; "whiten": HBM bytes, 8 N (D + M + 20) per launch (V read,
+ * gains records + fix-up rows, beta written), with M in place of D when the distances come from the
+ * fit's cache. */
+int32_t gpar_ctx_kernel_work(gpar_ctx* ctx, const char* name, double* work);
 /* Concurrency of batched calls (gpar_dtc_objective / gpar_fit with nprob > 1): lanes = 2
  * alternates the outputs' whitening + Gram between two HIP streams with separate workspaces so
  * one output's whitening overlaps another's Gram (~1 % faster at N = 1e6, M = 512, two beta

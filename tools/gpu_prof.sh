@@ -1,12 +1,10 @@
+# Round profile: PMC passes (Gram + whitening traffic, SQ counters), then rocprofv3 kernel stats of
+# the default north bench (1 warm-up + 1 timed step), then the plain bench line.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for k in 0 1 2 3 4; do
-  if [ $k = 0 ]; then unset GPAR_LIB_PATH; else export GPAR_LIB_PATH=$PWD/gpar-at-scale_amd/abl/libgparhip_WHITEN_ABL$k.so; fi
-  echo "ABL=$k" >> gpurun_out/abl.txt
-  timeout -k 10 200 python tools/gram_probe.py --evals 10 >> gpurun_out/abl.txt 2>&1 || exit 1
-done
-unset GPAR_LIB_PATH
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_r01d -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/bench_rocprof.json 2> gpurun_out/bench_rocprof.err || exit 1
-cat gpurun_out/abl.txt; cat gpurun_out/bench_rocprof.json
+bash tools/pmc_passes.sh > gpurun_out/pmc_summary.txt 2>&1 || { echo PMC FAILED; tail -20 gpurun_out/pmc_summary.txt; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/bench_rocprof.json 2> gpurun_out/bench_rocprof.err || { echo ROCPROF BENCH FAILED; tail -20 gpurun_out/bench_rocprof.err; exit 1; }
+timeout -k 10 400 python bench.py --no-cpu-baseline > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH FAILED; tail -20 gpurun_out/bench.err; exit 1; }
+cat gpurun_out/bench.json

@@ -20,6 +20,9 @@ def main():
     ap.add_argument("--d", type=int, default=32)
     ap.add_argument("--evals", type=int, default=3)
     ap.add_argument("--kernel", default="matern52")
+    ap.add_argument("--fit", action="store_true",
+                    help="time gpar_fit (max_evals = --evals) instead of objective calls: the fit's "
+                         "distance cache is used for D >= 17")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -57,6 +60,23 @@ def main():
                 raise
             return [float("nan")]
 
+    if a.fit:
+        x0 = np.array([[0.0, 0.0, 0.0, 0.0, -2.0]])
+        G.fit_batch([pr], x0, max_evals=2, g_tol=-1.0)
+        ctx.set_profiling(True)
+        ctx.reset_stats()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        fr = G.fit_batch([pr], x0, max_evals=a.evals, g_tol=-1.0)
+        torch.cuda.synchronize()
+        el = (time.perf_counter() - t0) * 1e3 / a.evals
+        out = [f"N={a.n} M={a.m} D={a.d} fit ms/eval={el:.3f} nlml={fr.nlml[0]:.6f}"]
+        for k in ("gram", "whiten", "gains", "dense"):
+            n, ms = ctx.kernel_stats(k)
+            if n:
+                out.append(f"{k}: {n} launches avg {ms / n:.4f} ms")
+        print("; ".join(out))
+        return
     ev(theta)
     ctx.set_profiling(True)
     ctx.reset_stats()

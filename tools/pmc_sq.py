@@ -21,7 +21,12 @@ def load(d):
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
-            k = "gram" if ("gram" in name and "_kernel" in name) else "whiten"
+            if "gram" in name and "_kernel" in name:
+                k = "gram"
+            elif "whiten_kfu" in name:
+                k = "whiten"
+            else:
+                continue
             key = (k, r["Dispatch_Id"])
             per[key][r["Counter_Name"]] += float(r["Counter_Value"])
             if "Start_Timestamp" in r and r.get("End_Timestamp"):
@@ -42,7 +47,8 @@ def avg(x):
 
 def main(root):
     res = {"source": "tools/pmc_passes.sh: rocprofv3 --pmc passes over tools/gram_probe.py "
-                     f"--evals 2 (N={N}, M={M}, D={D}); per-dispatch averages"}
+                     f"--fit --evals 4 (N={N}, M={M}, D={D}; the whitening reads the fit's distance "
+                     "cache: whiten_kfu_d2x2); per-dispatch averages"}
     sq, dsq = load(root + "/sq1")
     fe, _ = load(root + "/fetch")
     wr, _ = load(root + "/write")
@@ -72,8 +78,12 @@ def main(root):
     g = res["gram"]
     if g.get("hbm_read_bytes") is not None and g.get("hbm_write_bytes") is not None:
         res["hbm_bytes_per_launch"] = g["hbm_read_bytes"] + g["hbm_write_bytes"]   # bench.py traffic
-    res["whiten"]["algorithmic"] = {"bytes": N * D * 8 + N * 16 * 8 + N * M * 8,
-                                    "note": "V read, gains records read, beta written"}
+    res["whiten"]["algorithmic"] = {"bytes": 8 * N * (M + M + 20),
+                                    "note": "cached distances read, gains records + fix-up rows "
+                                            "read, beta written (include/gpar_hip.h)"}
+    w = res["whiten"]
+    if w.get("hbm_read_bytes") is not None and w.get("hbm_write_bytes") is not None:
+        res["whiten_hbm_bytes_per_launch"] = w["hbm_read_bytes"] + w["hbm_write_bytes"]
     print(json.dumps(res, indent=1))
 
 
