@@ -258,8 +258,6 @@ def fit_predict_batch(problems, log_theta0, t_star, V_stars, max_evals=0, max_it
     predicted mean is written to after its prediction (-1: none).  V_stars[i] = None reads output
     i's inputs from chain's first D_i columns, as they stand when its prediction runs (columns of
     earlier outputs hold their predicted means, the others what the caller put there)."""
-    ctx = context(device)
-    lib = _lib.load()
     P = len(problems)
     keep = keep if keep is not None else _Keep()
     if chain is not None:
@@ -322,6 +320,7 @@ def fit_predict_batch(problems, log_theta0, t_star, V_stars, max_evals=0, max_it
         mp_ = [m.ctypes.data for m in means]
         sp_ = [x.ctypes.data for x in stds]
     ns = n_star
+    ctx, lib = context(device), _lib.load()
     if dev:
         _order_after_torch(ctx)
     VP = (C.c_void_p * P)(*vptr)
@@ -437,8 +436,6 @@ def predict_scaled(input_locations, pseudo_input_locations, time_loc, outputs, t
     given theta.  Returns (mean, std) at the inference locations, in their input order.
     mode="mc" reproduces the reference's 100-sample Monte Carlo estimator; "analytic" is its
     S -> infinity limit."""
-    ctx = context(device)
-    lib = _lib.load()
     p, keep = make_problem(input_locations, pseudo_input_locations, time_loc, outputs,
                            out_kernel, time_kernel, qu_kuu_noise=qu_kuu_noise)
     th = np.ascontiguousarray(np.asarray(theta, dtype=np.float64).reshape(5))
@@ -449,6 +446,7 @@ def predict_scaled(input_locations, pseudo_input_locations, time_loc, outputs, t
         tsp = _dev_vec(inference_time_loc, keep)
         if ns != inference_time_loc.numel() or ds != p.d:
             raise _arg_error("inference inputs must be N* x D with N* = len(inference_time_loc)")
+        ctx, lib = context(device), _lib.load()
         _order_after_torch(ctx)
         mean = torch.empty(ns, dtype=torch.float64, device=inference_time_loc.device)
         std = torch.empty(ns, dtype=torch.float64, device=inference_time_loc.device)
@@ -460,6 +458,7 @@ def predict_scaled(input_locations, pseudo_input_locations, time_loc, outputs, t
     if ds != p.d or ns != len(np.asarray(inference_time_loc)):
         raise _arg_error("inference inputs must have the training dimension and one point per "
                          "inference time")
+    ctx, lib = context(device), _lib.load()
     mean = np.zeros(ns)
     std = np.zeros(ns)
     ctx.check(lib.gpar_predict(ctx.h, C.byref(p), _ptr(th), ns, tsp, vsp, ldvs, md, int(samples),

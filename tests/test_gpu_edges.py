@@ -114,3 +114,41 @@ def test_dtc_small_noise_ill_conditioned_kuu(sigma):
     got = G.compute_gpar_dtc_objective(V, Z, t, y, theta, "eq", "matern52")
     tol = max(1e-10, 1e-14 * np.linalg.cond(parts["Kuu"]))
     assert abs(got - ref) <= tol * abs(ref), (got, ref, abs(got - ref) / abs(ref), tol)
+
+
+def test_device_size_checks():
+    """HBM inputs: the C side cannot see buffer lengths, so mismatches must raise before launch."""
+    import torch
+    dev = torch.device("cuda", 0)
+    t, Y = O.synthetic_gpar(300, 3, seed=2, noise=0.3)
+    Yd, td = torch.from_numpy(Y).to(dev), torch.from_numpy(t).to(dev)
+    Zd = Yd[:20, :2].contiguous()
+    with pytest.raises(G.DomainError):
+        G.make_problem(Yd[:, :2], Zd, td[:-1], Yd[:, 2].contiguous())
+    ts = td[:40] + 0.01
+    with pytest.raises(G.DomainError):
+        G.predict_scaled(Yd[:, :2], Zd, td, Yd[:, 2].contiguous(), (1.0, 1.0, 1.0, 1.0, 0.2), ts,
+                         Yd[:39, :2])
+    pr, k = G.make_problem(Yd[:, :2], Zd, td, Yd[:, 2].contiguous())
+    with pytest.raises(G.DomainError):
+        G.fit_predict_batch([pr], np.zeros((1, 5)), ts, [Yd[:41, :2]], max_evals=3)
+
+
+def test_fresh_noncontiguous_device_inputs():
+    """Inputs written by torch kernels just before the call, passed as strided views (the
+    binding's .contiguous() copies run on torch's stream; the library orders itself after it):
+    the same objective as from host memory."""
+    import torch
+    dev = torch.device("cuda", 0)
+    t, Y = O.synthetic_gpar(4000, 4, seed=3, noise=0.3)
+    V = np.ascontiguousarray(Y[:, :3].T)
+    Z = O.pick_pseudo_inputs(V, 40, 1)
+    theta = (1.1, 0.9, 1.2, 1.0, 0.25)
+    host = G.compute_gpar_dtc_objective(V, Z, t, Y[:, 3], theta)
+    for _ in range(3):
+        base = torch.from_numpy(np.ascontiguousarray(Y.T)).to(dev) * 2.0   # fresh, 4 x N
+        Yt = (base * 0.5).T                                                  # N x 4, strided
+        Zt = torch.from_numpy(np.ascontiguousarray(Z)).to(dev).T             # M x 3, strided
+        tt = torch.from_numpy(t).to(dev) + 0.0
+        got = G.compute_gpar_dtc_objective(Yt[:, :3], Zt, tt, Yt[:, 3], theta)
+        assert abs(got - host) <= 1e-12 * abs(host), (got, host)
