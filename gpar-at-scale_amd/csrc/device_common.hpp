@@ -142,6 +142,22 @@ __device__ __forceinline__ double skappa_sq(double d2, double inv_l, double s) {
   }
 }
 
+// s * kappa(r / l) from the distance r = sqrt_pos(d2) itself (the Matern forms; the fit's
+// distance cache stores r, so the square root is taken once per fit, bit-identical to skappa_sq_k)
+template <int KIND>
+__device__ __forceinline__ double skappa_r_k(double r, double inv_l, double s,
+                                             const ExpNegConsts& k) {
+  if constexpr (KIND == KM12) {
+    return s * exp_neg_k(r * inv_l, k);
+  } else if constexpr (KIND == KM32) {
+    const double x = kSqrt3 * inv_l * r;
+    return fma(s, x, s) * exp_neg_k(x, k);
+  } else {
+    const double x = kSqrt5 * inv_l * r;
+    return fma(x, fma(x, s * (1.0 / 3.0), s), s) * exp_neg_k(x, k);
+  }
+}
+
 template <int KIND>
 __device__ __forceinline__ double skappa_sq_k(double d2, double inv_l, double s,
                                               const ExpNegConsts& k) {

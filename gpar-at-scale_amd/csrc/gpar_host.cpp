@@ -185,9 +185,11 @@ struct DevProblem {
   const double* zc;      // centres of the pseudo-input column groups (MFMA whitening), per problem
   int64_t ldv, ldz;
   int ok, tk, sdim, kuu_noise, qu_noise;
-  // squared distances |v_k - z_c|^2 (n x mp, ld mp), theta-independent: computed once per fit
-  // when the distance cache holds this output (fit_impl), else null
+  // distances (n x mp, ld mp), theta-independent: computed once per fit when the distance cache
+  // holds this output (fit_impl), else null.  Squared for EQ, r = |v_k - z_c| for the Matern
+  // kernels (d2_is_r), so their square root is taken once per fit, not per evaluation
   const double* d2 = nullptr;
+  bool d2_is_r = false;
 };
 
 static void check_sorted_host(const double* t, int64_t n) {
@@ -328,7 +330,7 @@ static void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const double* rec, 
   const double s_o = th.sv_o * th.sv_o;
   if (p.d2 && v == p.v) {   // the fit's training inputs, distances cached (fit_impl)
     launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, p.d2, p.mp, p.m, p.mp, n, kChunk, nch,
-                         1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum);
+                         1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum, p.d2_is_r);
   } else if (p.d > kFusedMaxD) {
     launch_dist2(c->stream, p.ok, v, ldv, n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, beta, ldb);
     launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, beta, ldb, p.m, p.mp, n, kChunk, nch,
@@ -483,7 +485,8 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
       launch_beta_fix(c->stream, p.sdim, beta, p.mp, n, g.g, cin, p.mc, kChunk);
       check_launch("beta_fix");
     }
-    GramPlan plan = gram_plan(n, p.mp);
+    // two lanes: one Gram workgroup per CU, so the other lane's whitening runs beside it
+    GramPlan plan = gram_plan(n, p.mp, nlanes > 1);
     double* part = ws<double>(c, "gram_part" + sfx, (size_t)plan.part_doubles);
     double* rpart = ws<double>(c, "gram_rpart" + sfx, (size_t)plan.rpart_doubles);
     HIPCHECK(hipMemsetAsync(beta + (size_t)n * p.mp, 0, (size_t)16 * p.mp * sizeof(double), c->stream));
@@ -1136,8 +1139,10 @@ static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<
     budget -= bytes;
     double* d2 = ws<double>(c, "distcache" + std::to_string(slot++), (size_t)p.n * p.mp);
     launch_dist2(c->stream, p.ok, p.v, p.ldv, p.n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, d2, p.mp);
+    if (p.ok != GPAR_EQ) launch_sqrt_inplace(c->stream, d2, p.n * p.mp);
     check_launch("dist2 (cache)");
     Q[i].d2 = d2;
+    Q[i].d2_is_r = p.ok != GPAR_EQ;
   }
   return Q;
 }

@@ -204,7 +204,8 @@ constexpr int kW2MaxL = 256;
 
 constexpr int kW2T = 8;
 
-template <int TK, int OK>
+// RIN: src holds the distances r = sqrt_pos(d2) (the fit's cache, Matern kernels) instead of d2.
+template <int TK, int OK, bool RIN>
 __global__ __launch_bounds__(256, 2) void whiten_kfu_d2x2(
     const double* __restrict__ rec, const double* src, int64_t lds, int64_t m, int64_t mp,
     int64_t n, int L, double inv_lo, double s_o, double* beta, int64_t ldb,
@@ -253,8 +254,13 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_d2x2(
         a = a > 0.0 ? a : 0.0;
         b = b > 0.0 ? b : 0.0;
       }
-      x[r].x = v0 ? skappa_sq_k<OK>(a, inv_lo, s_o, ek) : 0.0;
-      x[r].y = v1 ? skappa_sq_k<OK>(b, inv_lo, s_o, ek) : 0.0;
+      if constexpr (RIN) {
+        x[r].x = v0 ? skappa_r_k<OK>(a, inv_lo, s_o, ek) : 0.0;
+        x[r].y = v1 ? skappa_r_k<OK>(b, inv_lo, s_o, ek) : 0.0;
+      } else {
+        x[r].x = v0 ? skappa_sq_k<OK>(a, inv_lo, s_o, ek) : 0.0;
+        x[r].y = v1 ? skappa_sq_k<OK>(b, inv_lo, s_o, ek) : 0.0;
+      }
     }
     auto step = [&](int r) __attribute__((always_inline)) {
       const double* rr = rl + (r0 + r) * RS;
@@ -360,40 +366,64 @@ void launch_dist2(hipStream_t st, int out_kind, const double* v, int64_t ldv, in
   }
 }
 
-template <int TK, int OK>
+template <int TK, int OK, bool RIN>
 static void launch_wd2_k(hipStream_t st, dim3 grid, const double* rec, const double* src,
                          int64_t lds, int64_t m, int64_t mp, int64_t n, int L, double inv_lo,
                          double s_o, double* beta, int64_t ldb, double* send, int64_t mc,
                          const double* g, double* hsum) {
   if (L > kW2MaxL || (lds & 1) || (ldb & 1))
     throw std::runtime_error("whiten_kfu_d2x2: chunk length > 256 or odd leading dimension");
-  whiten_kfu_d2x2<TK, OK><<<grid, 256, 0, st>>>(rec, src, lds, m, mp, n, L, inv_lo, s_o, beta,
-                                                ldb, send, mc, g, hsum, exp_neg_consts());
+  whiten_kfu_d2x2<TK, OK, RIN><<<grid, 256, 0, st>>>(rec, src, lds, m, mp, n, L, inv_lo, s_o, beta,
+                                                     ldb, send, mc, g, hsum, exp_neg_consts());
 }
 
 template <int TK>
-static void launch_wd2_t(hipStream_t st, int ok, dim3 grid, const double* rec, const double* src,
-                         int64_t lds, int64_t m, int64_t mp, int64_t n, int L, double inv_lo,
-                         double s_o, double* beta, int64_t ldb, double* send, int64_t mc,
-                         const double* g, double* hsum) {
-  switch (ok) {
-    case KM12: launch_wd2_k<TK, KM12>(st, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
-    case KM32: launch_wd2_k<TK, KM32>(st, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
-    case KEQ: launch_wd2_k<TK, KEQ>(st, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
-    default: launch_wd2_k<TK, KM52>(st, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+static void launch_wd2_t(hipStream_t st, int ok, bool rin, dim3 grid, const double* rec,
+                         const double* src, int64_t lds, int64_t m, int64_t mp, int64_t n, int L,
+                         double inv_lo, double s_o, double* beta, int64_t ldb, double* send,
+                         int64_t mc, const double* g, double* hsum) {
+#define WD2_ARGS st, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum
+  if (rin) {
+    switch (ok) {
+      case KM12: launch_wd2_k<TK, KM12, true>(WD2_ARGS); break;
+      case KM32: launch_wd2_k<TK, KM32, true>(WD2_ARGS); break;
+      case KEQ: throw std::runtime_error("whiten_kfu_d2x2: EQ takes squared distances");
+      default: launch_wd2_k<TK, KM52, true>(WD2_ARGS); break;
+    }
+  } else {
+    switch (ok) {
+      case KM12: launch_wd2_k<TK, KM12, false>(WD2_ARGS); break;
+      case KM32: launch_wd2_k<TK, KM32, false>(WD2_ARGS); break;
+      case KEQ: launch_wd2_k<TK, KEQ, false>(WD2_ARGS); break;
+      default: launch_wd2_k<TK, KM52, false>(WD2_ARGS); break;
+    }
   }
+#undef WD2_ARGS
+}
+
+// r = sqrt_pos(d2) in place (the distance cache of the Matern kernels)
+__global__ void sqrt_inplace_kernel(double* __restrict__ a, int64_t count) {
+  const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
+  if (i < count) a[i] = sqrt_pos(a[i]);
+}
+
+void launch_sqrt_inplace(hipStream_t st, double* a, int64_t count) {
+  if (count <= 0) return;
+  sqrt_inplace_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(a, count);
 }
 
 void launch_whiten_kfu_d2(hipStream_t st, int time_kind, int out_kind, const double* rec,
                           const double* src, int64_t lds, int64_t m, int64_t mp, int64_t n, int L,
                           int64_t nch, double inv_lo, double s_o, double* beta, int64_t ldb,
-                          double* send, int64_t mc, const double* g, double* hsum) {
+                          double* send, int64_t mc, const double* g, double* hsum, bool src_is_r) {
   dim3 grid((unsigned)nch, (unsigned)((mp + 511) / 512));
+#define WD2T_ARGS st, out_kind, src_is_r, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum
   switch (time_kind) {
-    case KM12: launch_wd2_t<KM12>(st, out_kind, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
-    case KM32: launch_wd2_t<KM32>(st, out_kind, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
-    default: launch_wd2_t<KM52>(st, out_kind, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case KM12: launch_wd2_t<KM12>(WD2T_ARGS); break;
+    case KM32: launch_wd2_t<KM32>(WD2T_ARGS); break;
+    default: launch_wd2_t<KM52>(WD2T_ARGS); break;
   }
+#undef WD2T_ARGS
 }
 
 }  // namespace gpar

@@ -329,7 +329,11 @@ __device__ __forceinline__ constexpr int d2_tile(int ia, int c) {
   return t + c;
 }
 
-template <int D>
+// PF: operand fragments of k-substep ks + 1 are read from LDS while substep ks's MFMAs issue
+// (two fragment sets in registers).  Used by the one-workgroup-per-CU mode, where each SIMD has a
+// single Gram wave and nothing else of the Gram to hide LDS latency behind; the two-per-CU kernel
+// (PF = false) keeps reading each substep's fragments just before its MFMAs.
+template <int D, bool PF>
 __global__ __launch_bounds__(256, 2) void gram2_kernel(
     const double* __restrict__ beta, int64_t ldb, int64_t n, const double* __restrict__ ecor,
     const double* __restrict__ cin, const double* __restrict__ qv, int64_t mc, int L,
@@ -459,6 +463,29 @@ __global__ __launch_bounds__(256, 2) void gram2_kernel(
     for (int s = 0; s < nsteps; ++s) {
       if (s + 1 < nsteps) issue(s + 1);
       const double* base = smem + (s & 1) * 4 * kPanelD;
+      if constexpr (PF) {
+        double fa[2][4], fb[2][4];
+#pragma unroll
+        for (int a = 0; a < 4; ++a) { fa[0][a] = base[offa[a]]; fb[0][a] = base[offb[a]]; }
+#pragma unroll
+        for (int ks = 0; ks < kBK / 4; ++ks) {
+          const int cur = ks & 1;
+          if (ks + 1 < kBK / 4) {
+#pragma unroll
+            for (int a = 0; a < 4; ++a) {
+              fa[cur ^ 1][a] = base[offa[a] + (ks + 1) * 4 * kPW];
+              fb[cur ^ 1][a] = base[offb[a] + (ks + 1) * 4 * kPW];
+            }
+          }
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int a = 0; a < 4; ++a)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+              acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[cur][a], fb[cur][c], acc[a][c], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
+        }
+      } else {
 #pragma unroll
       for (int ks = 0; ks < kBK / 4; ++ks) {
         double fa[4], fb[4];
@@ -473,6 +500,7 @@ __global__ __launch_bounds__(256, 2) void gram2_kernel(
           for (int c = 0; c < 4; ++c)
             acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[c], acc[a][c], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
+      }
       }
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -533,6 +561,31 @@ __global__ __launch_bounds__(256, 2) void gram2_kernel(
     for (int s = 0; s < nsteps; ++s) {
       if (s + 1 < nsteps) issue(s + 1);
       const double* base = smem + (s & 1) * 4 * kPanelD;
+      if constexpr (PF) {
+        double fa[2][NA], fb[2][NB];
+#pragma unroll
+        for (int ia = 0; ia < NA; ++ia) fa[0][ia] = base[offa[ia]];
+#pragma unroll
+        for (int c = 0; c < NB; ++c) fb[0][c] = base[offb[c]];
+#pragma unroll
+        for (int ks = 0; ks < kBK / 4; ++ks) {
+          const int cur = ks & 1;
+          if (ks + 1 < kBK / 4) {
+#pragma unroll
+            for (int ia = 0; ia < NA; ++ia) fa[cur ^ 1][ia] = base[offa[ia] + (ks + 1) * 4 * kPW];
+#pragma unroll
+            for (int c = 0; c < NB; ++c) fb[cur ^ 1][c] = base[offb[c] + (ks + 1) * 4 * kPW];
+          }
+          __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+          for (int ia = 0; ia < NA; ++ia)
+#pragma unroll
+            for (int c = 0; c <= d2_row<H>(ia); ++c)
+              acc[d2_tile<H>(ia, c)] = __builtin_amdgcn_mfma_f64_16x16x4f64(
+                  fa[cur][ia], fb[cur][c], acc[d2_tile<H>(ia, c)], 0, 0, 0);
+          __builtin_amdgcn_s_setprio(0);
+        }
+      } else {
 #pragma unroll
       for (int ks = 0; ks < kBK / 4; ++ks) {
         double fa[NA], fb[NB];
@@ -548,6 +601,7 @@ __global__ __launch_bounds__(256, 2) void gram2_kernel(
             acc[d2_tile<H>(ia, c)] =
                 __builtin_amdgcn_mfma_f64_16x16x4f64(fa[ia], fb[c], acc[d2_tile<H>(ia, c)], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
+      }
       }
       if (owns_r) r_update(s, base);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -734,7 +788,9 @@ namespace gpar {
 // ceil(workgroups / 256) x max(16 x rows_off, 18 x rows_dg), at most 512 workgroups (2 per CU);
 // at M = 512, N = 1e6: 6 x 62 OFF + 2 x 70 DG = 512 workgroups, 16 x 16144 vs 18 x 14288
 // tile-rows per wave (v1: 16 x 17872).
-static void gram2_plan(int64_t n, int64_t mp, GramPlan& p) {
+static void gram2_plan(int64_t n, int64_t mp, GramPlan& p, bool one_per_cu) {
+  const int slots = one_per_cu ? 256 : 512;   // co-resident workgroups the splits should fill
+  p.one_per_cu = one_per_cu ? 1 : 0;
   const int nbk = (int)(mp / 128);
   p.v2 = 1;
   p.npan = 2 * nbk;
@@ -746,9 +802,9 @@ static void gram2_plan(int64_t n, int64_t mp, GramPlan& p) {
   auto rows_of = [&](int64_t s) { return (((n + s - 1) / s + kBK - 1) / kBK) * kBK; };
   double best = 1e300;
   int bo = 1, bd = 1, bw = 0;
-  for (int so = (p.noff ? 1 : 0); so <= (p.noff ? 512 : 0); ++so) {
+  for (int so = (p.noff ? 1 : 0); so <= (p.noff ? slots : 0); ++so) {
     if (so > maxs) break;
-    const int left = 512 - p.noff * so;
+    const int left = slots - p.noff * so;
     if (left < p.ndg) break;
     for (int sd = 1; sd <= left / p.ndg && sd <= maxs; ++sd) {
       const int wgs = p.noff * so + p.ndg * sd;
@@ -756,7 +812,8 @@ static void gram2_plan(int64_t n, int64_t mp, GramPlan& p) {
       const double wd = 18.0 * (double)rows_of(sd);
       // one workgroup per CU leaves one wave per SIMD, with nothing to hide its barrier and LDS
       // waits behind: priced 15 % worse than the same work spread two per CU
-      const double cost = (double)((wgs + 255) / 256) * (wo > wd ? wo : wd) * (wgs > 384 ? 1.0 : 1.15);
+      const double cost = (double)((wgs + 255) / 256) * (wo > wd ? wo : wd) *
+                          (one_per_cu ? 1.0 : (wgs > 384 ? 1.0 : 1.15));
       if (cost < best * (1.0 - 1e-9) || (cost <= best * (1.0 + 1e-9) && wgs > bw)) {
         best = cost; bo = so; bd = sd; bw = wgs;
       }
@@ -771,10 +828,10 @@ static void gram2_plan(int64_t n, int64_t mp, GramPlan& p) {
   p.rpart_doubles = (int64_t)p.sdg * mp;
 }
 
-GramPlan gram_plan(int64_t n, int64_t mp) {
+GramPlan gram_plan(int64_t n, int64_t mp, bool one_per_cu) {
   GramPlan p;
   if (!GRAM_V1) {
-    gram2_plan(n, mp, p);
+    gram2_plan(n, mp, p, one_per_cu);
     return p;
   }
   p.npan = (int)(mp / kPW);
@@ -815,11 +872,25 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
                  int64_t ldg, double* r) {
   if (plan.v2) {
     const int nwg = ((plan.noff * plan.soff + plan.ndg * plan.sdg + 7) / 8) * 8;   // XCD deal
-    switch (sdim) {
-      case 1: gram2_kernel<1><<<nwg, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, plan.rows_off, plan.rows_dg, part, rpart); break;
-      case 2: gram2_kernel<2><<<nwg, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, plan.rows_off, plan.rows_dg, part, rpart); break;
-      default: gram2_kernel<3><<<nwg, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, plan.rows_off, plan.rows_dg, part, rpart); break;
+#define GRAM2_ARGS beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.noff, plan.ndg, \
+                   plan.soff, plan.sdg, plan.rows_off, plan.rows_dg, part, rpart
+    if (plan.one_per_cu) {
+      // 65 KB static + 24 KB padding: a second Gram workgroup no longer fits a CU (160 KB), the
+      // other lane's whitening (40 KB, 216 VGPRs beside the Gram's 239) does
+      const size_t pad = 24 * 1024;
+      switch (sdim) {
+        case 1: gram2_kernel<1, true><<<nwg, 256, pad, st>>>(GRAM2_ARGS); break;
+        case 2: gram2_kernel<2, true><<<nwg, 256, pad, st>>>(GRAM2_ARGS); break;
+        default: gram2_kernel<3, true><<<nwg, 256, pad, st>>>(GRAM2_ARGS); break;
+      }
+    } else {
+      switch (sdim) {
+        case 1: gram2_kernel<1, false><<<nwg, 256, 0, st>>>(GRAM2_ARGS); break;
+        case 2: gram2_kernel<2, false><<<nwg, 256, 0, st>>>(GRAM2_ARGS); break;
+        default: gram2_kernel<3, false><<<nwg, 256, 0, st>>>(GRAM2_ARGS); break;
+      }
     }
+#undef GRAM2_ARGS
     const int nrows = plan.noff * 4 * 16 + plan.ndg * 4 * kD2T + 1;
     gram2_reduce<<<nrows, 256, 0, st>>>(part, rpart, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, G, ldg, r);
     return;

@@ -72,6 +72,9 @@ struct GramPlan {
   // v2 decomposition (k_gram.hip): OFF / DG workgroup counts, their time splits and rows
   int v2 = 0, noff = 0, ndg = 0, soff = 0, sdg = 0;
   int64_t rows_off = 0, rows_dg = 0;
+  // one workgroup per CU (gram_plan(..., one_per_cu)): launched with padding LDS so a second Gram
+  // workgroup cannot join, leaving each CU room for the other stream lane's whitening
+  int one_per_cu = 0;
 };
 
 constexpr int kGramTile = 128;
@@ -111,11 +114,14 @@ void launch_zcenter_wide(hipStream_t st, const double* z, int64_t ldz, int d, in
 void launch_dist2(hipStream_t st, int out_kind, const double* v, int64_t ldv, int64_t n,
                   const double* z, int64_t ldz, int64_t m, int64_t mp, int d, const double* zc,
                   double* out, int64_t ldo);
-// whiten_kfu from precomputed squared distances (src may equal beta: in place)
+// whiten_kfu from precomputed squared distances (src may equal beta: in place), or from the
+// distances themselves (src_is_r: the fit's cache for the Matern kernels)
 void launch_whiten_kfu_d2(hipStream_t st, int time_kind, int out_kind, const double* rec,
                           const double* src, int64_t lds, int64_t m, int64_t mp, int64_t n, int L,
                           int64_t nch, double inv_lo, double s_o, double* beta, int64_t ldb,
-                          double* send, int64_t mc, const double* g, double* hsum);
+                          double* send, int64_t mc, const double* g, double* hsum,
+                          bool src_is_r = false);
+void launch_sqrt_inplace(hipStream_t st, double* a, int64_t count);
 void launch_whiten_vec(hipStream_t st, int sdim, const double* rec, int64_t recstride,
                        const double* y, int64_t ldy, int64_t n, int L, int64_t nch, int nchains,
                        double* alpha, int64_t lda, double* send, int64_t sendstride, int64_t mc,
@@ -157,7 +163,7 @@ void launch_chain_lml(hipStream_t st, const double* logs, int64_t nch, const dou
                       int64_t npart, int64_t n, int nchains, double* lml);
 
 // k_gram.hip
-GramPlan gram_plan(int64_t n, int64_t mp);
+GramPlan gram_plan(int64_t n, int64_t mp, bool one_per_cu = false);
 // ecor: E_j (nch x mc x 4, vec_fix), cin: C_j (carry), qv: q_j (nch x 4, vec_fix)
 void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* beta,
                  int64_t ldb, int64_t n, const double* ecor, const double* cin, const double* qv,
