@@ -80,13 +80,17 @@ def main():
                     help="test inputs of output p: 'given' = the noiseless previous outputs at t* "
                          "(GPAR_scaled_examples.jl:139); 'chained' = output 1's true values and the "
                          "PREDICTED means of outputs 2..p-1 (GPAR_scaled_examples.jl:172, eeg.jl:249)")
+    ap.add_argument("--rehearse", action="store_true",
+                    help="multi-rank rehearsal on ONE GPU: every rank uses device 0 and the gloo "
+                         "backend (RCCL runs one rank per device); exercises the launcher, sharding, "
+                         "broadcasts and gathers with the real kernels -- not a scaling measurement")
     ap.add_argument("--stub", action="store_true",
                     help="launcher check without a GPU: ranks join a gloo group, take their output "
                          "shards and report them; no compute (tests/test_bench_launch.py)")
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
-        sys.exit(launch_ranks(args.gpus, sys.argv[1:], stub=args.stub))
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], stub=args.stub or args.rehearse))
     if args.stub:
         return stub_rank(args)
 
@@ -106,11 +110,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         log(f"[rank {rank}] note: --gpus {args.gpus} but WORLD_SIZE={world}; n_gpus reports WORLD_SIZE")
+    if args.rehearse:
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=dev)
+        if args.rehearse:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=dev)
 
     # ---------------------------------------------------------------- inputs (untimed)
     t0 = time.perf_counter()
@@ -271,6 +280,8 @@ def main():
                        "out_kernel": cfg["out_kernel"], "time_kernel": "matern52",
                        "parallelism": f"outputs sharded over {world} GPU(s)",
                        "outputs_per_rank": shards, "inference": args.inference},
+            **({"rehearsal": "all ranks on one GPU over gloo: not a scaling measurement"}
+               if args.rehearse else {}),
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic, "kernel": "gram2_kernel (beta^T beta, fp64 MFMA)",
