@@ -351,8 +351,8 @@ def launch_ranks(n, argv, stub=False):
                                       text=True))
     out0, _ = procs[0].communicate()
     codes = [procs[0].returncode] + [p.wait() for p in procs[1:]]
-    for line in out0.splitlines():
-        print(line, flush=True)
+    for line in out0.splitlines():   # the JSON line to stdout, anything a library printed to stderr
+        print(line, file=sys.stdout if line.startswith("{") else sys.stderr, flush=True)
     bad = [c for c in codes if c != 0]
     if bad:
         log(f"bench: rank exit statuses {codes}")
