@@ -18,15 +18,9 @@
 // global -> LDS by LDS-DMA (no VGPRs), double buffered; each wave stages one 64-column panel.
 #include <type_traits>
 
-#include "device_common.hpp"
+#include "gram_common.hpp"
 
 namespace gpar {
-
-typedef double d4 __attribute__((ext_vector_type(4)));
-
-constexpr int kPW = 64;               // panel width (columns of beta / of G)
-constexpr int kBK = 16;               // time rows per K-step
-constexpr int kPanelD = kBK * kPW;    // doubles per staged panel
 #ifndef GRAM_ABL
 #define GRAM_ABL 0   // timing ablations only: 2 no LDS-DMA, 3 no MFMA, 5 no chunk-correction tail
 #endif
@@ -314,20 +308,7 @@ __global__ __launch_bounds__(256, 2) void gram_kernel(
 // gram2_plan picks the split counts so the per-wave work (tiles x rows) of the two types
 // matches and the workgroups fill the 512 co-resident slots.  DG also owns r = beta^T alpha
 // (every panel is staged by exactly one DG workgroup per split).
-constexpr int kD2T = 18;   // tiles per DG wave (accumulators: 72 doubles)
-
-template <int H>
-__device__ __forceinline__ constexpr int d2_row(int ia) { return H == 0 ? (ia < 4 ? ia : 7) : 4 + ia; }
-template <int H>
-__device__ __forceinline__ constexpr int d2_na() { return H == 0 ? 5 : 3; }
-template <int H>
-__device__ __forceinline__ constexpr int d2_nb() { return H == 0 ? 8 : 7; }
-template <int H>
-__device__ __forceinline__ constexpr int d2_tile(int ia, int c) {
-  int t = 0;
-  for (int i = 0; i < ia; ++i) t += d2_row<H>(i) + 1;
-  return t + c;
-}
+// (kD2T and the d2_* tile maps: gram_common.hpp)
 
 // PF: operand fragments of k-substep ks + 1 are read from LDS while substep ks's MFMAs issue
 // (two fragment sets in registers).  Used by the one-workgroup-per-CU mode, where each SIMD has a
@@ -659,6 +640,194 @@ __global__ __launch_bounds__(256, 2) void gram2_kernel(
   }
 }
 
+// ============================================================================ v3: fat waves
+// One wave per SIMD with twice the tiles.  A workgroup is 2 waves (128 threads), two workgroups
+// per CU, in three launches:
+//   * OFF(a, b), a > b (gram3_off_kernel, here): the whole off-diagonal 128 x 128 block; wave w
+//     takes row panel 2a + w against both column panels 2b, 2b + 1: 4 x 8 = 32 tiles, whose
+//     accumulators fill the 256 AGPRs.  Four panels per K-step, two staged by each wave (slots w
+//     and 2 + w);
+//   * DG(q) (gram3_dg_kernel, k_gram3v.hip): ONE diagonal 128-block q, its lower triangle's 36
+//     tiles split 18 + 18 over the two waves as in v2 (local tile rows {0, 1, 2, 3, 7} |
+//     {4, 5, 6}); wave h stages panel 2q + h.  DG also owns r = beta^T alpha (each panel is
+//     staged by exactly one DG workgroup per split);
+//   * the chunk correction sum_j (E_j C_j^T + C_j E_j^T) and r's sum_j C_j q_j
+//     (gram3_corr_kernel, k_gram3v.hip) as extra "splits" of the same partial-tile layout.
+// Per K-step an OFF wave issues 128 MFMAs between barriers, twice v2's, from 12 fragment reads
+// per 32 MFMAs (v2: 8 per 16), and the next k-substep's fragments are read under the current
+// substep's MFMAs.  A pure 4 x 8-tile wave loop measured 67 TF/s on MI355X (0.85 of the fp64
+// peak) with one wave per SIMD, against v2's ~60 TF/s in the job.  The three kernels are
+// separate because the register allocator keeps loop-carried accumulators in place only in a
+// kernel with one accumulation loop: with the correction tail (or the DG path) in the same
+// function it parks tiles in VGPRs and copies all of them every K-step.  The DG and correction
+// kernels fit their accumulators in VGPRs and are compiled with VGPR-form MFMAs (Makefile).
+//
+// Partial-tile layout (part): workgroup slot w, wave h, tile t at ((w * 2 + h) * kF3T + t) * 256
+// (16 x 16 row-major).  OFF slots: gid + s * noff for s < soff + ncs (ncs correction splits
+// after the soff time splits); DG slots from noff * (soff + ncs): gid + s * ndg, s < sdg + ncs.
+// rpart: (sdg + ncs) x Mp.
+__global__ __launch_bounds__(128) void gram3_off_kernel(const double* __restrict__ beta,
+                                                        int64_t ldb, int64_t n, int noff,
+                                                        int soff, int64_t rows,
+                                                        double* __restrict__ part) {
+  __shared__ __attribute__((aligned(16))) double smem[8 * kPanelD];
+
+  const int nty = noff * soff;
+  const int per = (nty + 7) >> 3;
+  const int b = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);   // XCD-major deal
+  if (b >= nty) return;
+  const int gid = b % noff, split = b / noff;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  int a = 1;
+  while (a * (a + 1) / 2 <= gid) ++a;
+  const int bo = gid - a * (a - 1) / 2;
+  const int pA = 2 * a + wave, pB = 2 * bo + wave;   // panels this wave stages
+
+  const int64_t kb = (int64_t)split * rows;
+  int64_t ke = kb + rows;
+  if (ke > n) ke = n;
+  const int nsteps = (int)(ke > kb ? (ke - kb + kBK - 1) / kBK : 0);
+
+  const int hl = lane >> 5, cl2 = (lane & 31) * 2;
+  const int64_t lrow = (int64_t)hl * ldb;
+  const uint32_t boffA = (uint32_t)((lrow + (int64_t)pA * kPW + (cl2 ^ (hl << 4))) * 8);
+  const uint32_t boffB = (uint32_t)((lrow + (int64_t)pB * kPW + (cl2 ^ (hl << 4))) * 8);
+  const char* bbase = reinterpret_cast<const char*>(beta);
+  // wave w stages its A panel into slot w and its B panel into slot 2 + w
+  auto issue = [&](int s) __attribute__((always_inline)) {
+    const int64_t k0 = kb + (int64_t)s * kBK;
+    double* imgA = smem + ((s & 1) * 4 + wave) * kPanelD;
+    double* imgB = smem + ((s & 1) * 4 + 2 + wave) * kPanelD;
+#pragma unroll
+    for (int i = 0; i < kBK / 2; ++i) {
+      const char* rowp = bbase + (k0 + 2 * i) * ldb * 8;
+      __builtin_amdgcn_global_load_lds(rowp + boffA, imgA + 2 * i * kPW, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(rowp + boffB, imgB + 2 * i * kPW, 16, 0, 0);
+    }
+  };
+  const int frow = lane >> 4, fcol = lane & 15;
+  const int par = frow & 1;
+  auto foff = [&](int sl, int t) __attribute__((always_inline)) {
+    return sl * kPanelD + frow * kPW + ((t ^ par) << 4) + fcol;
+  };
+
+  if (nsteps > 0) issue(0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // rows = tiles 0..3 of slot `wave`, columns = tiles 0..3 of slots 2, 3
+  d4 acc[4][8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int c = 0; c < 8; ++c) acc[i][c] = d4{0.0, 0.0, 0.0, 0.0};
+  int offa[4], offb[8];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) offa[i] = foff(wave, i);
+#pragma unroll
+  for (int c = 0; c < 8; ++c) offb[c] = foff(2 + (c >> 2), c & 3);
+  for (int s = 0; s < nsteps; ++s) {
+    if (s + 1 < nsteps) issue(s + 1);
+    const double* base = smem + (s & 1) * 4 * kPanelD;
+    double fa[2][4], fb[2][8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[0][i] = base[offa[i]];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) fb[0][c] = base[offb[c]];
+#pragma unroll
+    for (int ks = 0; ks < kBK / 4; ++ks) {
+      const int cur = ks & 1;
+      if (ks + 1 < kBK / 4) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fa[cur ^ 1][i] = base[offa[i] + (ks + 1) * 4 * kPW];
+#pragma unroll
+        for (int c = 0; c < 8; ++c) fb[cur ^ 1][c] = base[offb[c] + (ks + 1) * 4 * kPW];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int c = 0; c < 8; ++c)
+          acc[i][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[cur][i], fb[cur][c], acc[i][c], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+  double* ptile = part + (((int64_t)b * 2 + wave) * kF3T) * 256;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int c = 0; c < 8; ++c)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        ptile[(i * 8 + c) * 256 + (frow + 4 * r) * 16 + fcol] = acc[i][c][r];
+}
+
+// v3 reduction: one grid row per (workgroup of the first split, wave, tile), summed over the
+// type's time splits then its ncs correction splits, in order (deterministic); writes G and its
+// mirror.  The last row sums r.
+__global__ __launch_bounds__(256) void gram3_reduce(const double* __restrict__ part,
+                                                    const double* __restrict__ rpart, int npan,
+                                                    int noff, int ndg, int soff, int sdg, int ncs,
+                                                    double* __restrict__ G, int64_t ldg,
+                                                    double* __restrict__ r) {
+  const int e = threadIdx.x;
+  const int y = blockIdx.x;
+  const int nrow_off = noff * 2 * kF3T, nrow_dg = ndg * 2 * kD2T;
+  if (y == nrow_off + nrow_dg) {
+    const int mp = npan * kPW;
+    for (int c = e; c < mp; c += 256) {
+      double s = 0.0;
+#pragma unroll 8
+      for (int sp = 0; sp < sdg + ncs; ++sp) s += rpart[(int64_t)sp * mp + c];
+      r[c] = s;
+    }
+    return;
+  }
+  int64_t grow, gcol, wb;
+  int w, t, nsp, stride;
+  bool diag_tile = false;
+  if (y < nrow_off) {
+    const int gid = y / (2 * kF3T), rem = y % (2 * kF3T);
+    w = rem / kF3T; t = rem % kF3T;
+    int a = 1;
+    while (a * (a + 1) / 2 <= gid) ++a;
+    const int bo = gid - a * (a - 1) / 2;
+    const int i = t / 8, c = t % 8;
+    grow = (int64_t)(2 * a + w) * kPW + i * 16;
+    gcol = (int64_t)(2 * bo + (c >> 2)) * kPW + (c & 3) * 16;
+    wb = gid; nsp = soff + ncs; stride = noff;
+  } else {
+    const int yy = y - nrow_off;
+    const int gid = yy / (2 * kD2T), rem = yy % (2 * kD2T);
+    w = rem / kD2T; t = rem % kD2T;
+    const int H = w;
+    int ia = 0, tt = t, rr = 0;
+    for (;;) {
+      rr = (H == 0) ? (ia < 4 ? ia : 7) : 4 + ia;
+      if (tt <= rr) break;
+      tt -= rr + 1;
+      ++ia;
+    }
+    grow = (int64_t)2 * gid * kPW + rr * 16;
+    gcol = (int64_t)2 * gid * kPW + tt * 16;
+    diag_tile = rr == tt;
+    wb = (int64_t)noff * (soff + ncs) + gid; nsp = sdg + ncs; stride = ndg;
+  }
+  const int er = e / 16, ec = e % 16;
+  if (diag_tile && er < ec) return;
+  const double* pp = part + ((wb * 2 + w) * kF3T + t) * 256 + e;
+  const int64_t pstride = (int64_t)stride * 2 * kF3T * 256;
+  double s = 0.0;
+#pragma unroll 8
+  for (int sp = 0; sp < nsp; ++sp) s += pp[sp * pstride];
+  const int64_t gr = grow + er, gc = gcol + ec;
+  G[gr * ldg + gc] = s;
+  G[gc * ldg + gr] = s;
+}
+
 // v2 reduction: one grid row per (workgroup of the first split, wave, tile); sums that tile's
 // partials over the type's splits in split order and writes G (and its mirror).  The last grid
 // row sums r over the DG splits.
@@ -828,10 +997,55 @@ static void gram2_plan(int64_t n, int64_t mp, GramPlan& p, bool one_per_cu) {
   p.rpart_doubles = (int64_t)p.sdg * mp;
 }
 
+#ifndef GRAM_V3
+#define GRAM_V3 1   // 0: the v2 kernel at two workgroups per CU as well (A/B)
+#endif
+#ifndef GRAM3_DG_SLOTS
+#define GRAM3_DG_SLOTS 1024
+#endif
+
+// v3: split counts for OFF (32 tiles per wave) and DG (18 tiles per wave, one diagonal block per
+// workgroup), two launches of up to 512 workgroups each (two per CU, one wave per SIMD).
+static void gram3_plan(int64_t n, int64_t mp, GramPlan& p) {
+  const int nbk = (int)(mp / 128);
+  p.v2 = 1;
+  p.v3 = 1;
+  p.npan = 2 * nbk;
+  p.noff = nbk * (nbk - 1) / 2;
+  p.ndg = nbk;
+  const int64_t maxs = (n + 255) / 256 > 8 ? (n + 255) / 256 : 8;
+  auto rows_of = [&](int64_t sp) { return (((n + sp - 1) / sp + kBK - 1) / kBK) * kBK; };
+  // OFF and DG run as two launches, each filling the 512 slots (two workgroups per CU) alone:
+  // the most splits <= 512 / groups, and >= 8
+  auto splits = [&](int groups, int slots) {
+    int sp = slots / groups;
+    if (sp < 1) sp = 1;
+    if (sp > maxs) sp = (int)maxs;
+    return sp;
+  };
+  p.soff = p.noff ? splits(p.noff, 512) : 0;
+  // DG (238 VGPRs, 33 KB LDS) runs two waves per SIMD: 1024 slots
+  p.sdg = splits(p.ndg, GRAM3_DG_SLOTS);
+  p.rows_off = p.noff ? rows_of(p.soff) : 0;
+  p.rows_dg = rows_of(p.sdg);
+  p.nsplit = p.sdg;
+  // chunk-correction splits: (noff + ndg) x ncs four-wave workgroups, two per CU
+  const int64_t nch = (n + 255) / 256;
+  int ncs = 512 / (p.noff + p.ndg);
+  if (ncs < 1) ncs = 1;
+  if (ncs > nch) ncs = (int)(nch > 0 ? nch : 1);
+  p.ncs = ncs;
+  p.part_doubles = (int64_t)(p.noff * (p.soff + ncs) + p.ndg * (p.sdg + ncs)) * 2 * kF3T * 256;
+  p.rpart_doubles = (int64_t)(p.sdg + ncs) * mp;
+}
+
 GramPlan gram_plan(int64_t n, int64_t mp, bool one_per_cu) {
   GramPlan p;
   if (!GRAM_V1) {
-    gram2_plan(n, mp, p, one_per_cu);
+    if (GRAM_V3 && !one_per_cu)
+      gram3_plan(n, mp, p);
+    else
+      gram2_plan(n, mp, p, one_per_cu);
     return p;
   }
   p.npan = (int)(mp / kPW);
@@ -870,6 +1084,22 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
                  int64_t ldb, int64_t n, const double* ecor, const double* cin, const double* qv,
                  int64_t mc, int L, const double* alpha, double* part, double* rpart, double* G,
                  int64_t ldg, double* r) {
+  if (plan.v3) {
+    const int ncs = ecor ? plan.ncs : 0;
+    const int noffw = ((plan.noff * plan.soff + 7) / 8) * 8;   // XCD deal
+    const int ndgw = ((plan.ndg * plan.sdg + 7) / 8) * 8;
+    if (noffw > 0)
+      gram3_off_kernel<<<noffw, 128, 0, st>>>(beta, ldb, n, plan.noff, plan.soff, plan.rows_off, part);
+    launch_gram3_dg(st, ndgw, beta, ldb, n, alpha, plan.npan, plan.ndg, plan.sdg, plan.rows_dg,
+                    (int64_t)plan.noff * (plan.soff + ncs), part, rpart);
+    if (ncs)
+      launch_gram3_corr(st, sdim, ecor, cin, qv, mc, (n + L - 1) / L, plan.npan, plan.noff,
+                        plan.ndg, plan.soff, plan.sdg, ncs, part, rpart);
+    const int nrows = plan.noff * 2 * kF3T + plan.ndg * 2 * kD2T + 1;
+    gram3_reduce<<<nrows, 256, 0, st>>>(part, rpart, plan.npan, plan.noff, plan.ndg, plan.soff,
+                                        plan.sdg, ncs, G, ldg, r);
+    return;
+  }
   if (plan.v2) {
     const int nwg = ((plan.noff * plan.soff + plan.ndg * plan.sdg + 7) / 8) * 8;   // XCD deal
 #define GRAM2_ARGS beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.noff, plan.ndg, \

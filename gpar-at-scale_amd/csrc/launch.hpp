@@ -75,6 +75,8 @@ struct GramPlan {
   // one workgroup per CU (gram_plan(..., one_per_cu)): launched with padding LDS so a second Gram
   // workgroup cannot join, leaving each CU room for the other stream lane's whitening
   int one_per_cu = 0;
+  int v3 = 0;   // fat-wave kernels (gram3_*: 2-wave workgroups, 32-tile OFF waves)
+  int ncs = 0;  // v3 chunk-correction splits
 };
 
 constexpr int kGramTile = 128;
