@@ -284,7 +284,7 @@ def main():
                if args.rehearse else {}),
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
-                         "traffic": traffic, "kernel": "gram2_kernel (beta^T beta, fp64 MFMA)",
+                         "traffic": traffic, "kernel": "Gram beta^T beta + beta^T alpha, fp64 MFMA (v3: gram3_off + gram3_dg + gram3_corr + gram3_reduce per launch; lanes=2: gram2)",
                          "launches": gram_n, "avg_ms": avg, "flops_per_launch": flops,
                          "lanes": args.lanes},
             "kernels": {"gram_ms_per_step": gram_ms / args.steps, "whiten_ms_per_step": wh_ms / args.steps,

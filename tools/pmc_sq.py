@@ -15,47 +15,63 @@ N, M, D = 1_000_000, 512, 32
 SIMDS = 1024
 
 
+def avg(x):
+    return sum(x) / len(x) if x else None
+
+
 def load(d):
-    per = defaultdict(lambda: defaultdict(float))   # (kernel, dispatch) -> counter -> value
+    """-> (counters, durations): k -> counter -> per-launch value, k -> per-launch seconds, where
+    a Gram "launch" is one launch_gram call (v3: gram3_off + gram3_dg + gram3_corr + gram3_reduce
+    dispatches; v2: gram2_kernel + gram2_reduce): per-kernel averages summed over its kernels."""
+    per = defaultdict(lambda: defaultdict(float))   # (k, kernel, dispatch) -> counter -> value
     dur = {}
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
-            if "gram" in name and "_kernel" in name:
+            if "gram" in name:
                 k = "gram"
             elif "whiten_kfu" in name:
                 k = "whiten"
             else:
                 continue
-            key = (k, r["Dispatch_Id"])
+            sub = name.split("(")[0]
+            key = (k, sub, r["Dispatch_Id"])
             per[key][r["Counter_Name"]] += float(r["Counter_Value"])
             if "Start_Timestamp" in r and r.get("End_Timestamp"):
                 dur[key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-    out = defaultdict(lambda: defaultdict(list))
-    for (k, _), cs in per.items():
+    by = defaultdict(lambda: defaultdict(list))     # (k, kernel) -> counter -> [values]
+    for (k, sub, _), cs in per.items():
         for c, v in cs.items():
-            out[k][c].append(v)
+            by[(k, sub)][c].append(v)
+    dby = defaultdict(list)
+    for (k, sub, _), t in dur.items():
+        dby[(k, sub)].append(t)
+    out = defaultdict(lambda: defaultdict(list))
+    for (k, sub), cs in by.items():
+        for c, v in cs.items():
+            out[k][c].append(avg(v))                 # one entry per kernel: summed below
     durs = defaultdict(list)
-    for (k, _), t in dur.items():
-        durs[k].append(t)
-    return out, durs
-
-
-def avg(x):
-    return sum(x) / len(x) if x else None
+    for (k, sub), ts in dby.items():
+        durs[k].append(avg(ts))
+    kernels = defaultdict(list)
+    for (k, sub) in by:
+        kernels[k].append(sub)
+    return out, durs, kernels
 
 
 def main(root):
     res = {"source": "tools/pmc_passes.sh: rocprofv3 --pmc passes over tools/gram_probe.py "
                      f"--fit --evals 4 (N={N}, M={M}, D={D}; the whitening reads the fit's distance "
-                     "cache: whiten_kfu_d2x2); per-dispatch averages"}
-    sq, dsq = load(root + "/sq1")
-    fe, _ = load(root + "/fetch")
-    wr, _ = load(root + "/write")
+                     "cache: whiten_kfu_d2x2); per-launch values: each kernel's per-dispatch "
+                     "average, summed over the kernels of one launch (Gram v3: OFF + DG + "
+                     "correction + reduction)"}
+    sq, dsq, kn = load(root + "/sq1")
+    fe, _, _ = load(root + "/fetch")
+    wr, _, _ = load(root + "/write")
     for k in ("gram", "whiten"):
-        c = {n: avg(v) for n, v in sq[k].items()}
-        t = avg(dsq[k])
-        e = {"counters": c, "kernel_s_under_pmc": t}
+        c = {n: sum(v) for n, v in sq[k].items()}     # per launch, summed over its kernels
+        t = sum(dsq[k]) if dsq[k] else None
+        e = {"kernels": sorted(kn[k]), "counters": c, "kernel_s_under_pmc": t}
         if t and c.get("GRBM_GUI_ACTIVE"):
             clk = c["GRBM_GUI_ACTIVE"] / 8 / t
             e["effective_clock_GHz"] = clk / 1e9
@@ -68,8 +84,8 @@ def main(root):
             e["wave_time_fraction"] = {"active_inst_any": c.get("SQ_ACTIVE_INST_ANY", 0) / w,
                                        "wait_inst_any (issue stall)": c.get("SQ_WAIT_INST_ANY", 0) / w,
                                        "wait_any (waitcnt/barrier)": c.get("SQ_WAIT_ANY", 0) / w}
-        f = avg(fe[k].get("FETCH_SIZE", []))
-        wb = avg(wr[k].get("WRITE_SIZE", []))
+        f = sum(fe[k]["FETCH_SIZE"]) if fe[k].get("FETCH_SIZE") else None
+        wb = sum(wr[k]["WRITE_SIZE"]) if wr[k].get("WRITE_SIZE") else None
         e["hbm_read_bytes"] = f * 1024 * 2 if f is not None else None
         e["hbm_write_bytes"] = wb * 1024 if wb is not None else None
         res[k] = e
