@@ -80,6 +80,11 @@ def main():
                     help="test inputs of output p: 'given' = the noiseless previous outputs at t* "
                          "(GPAR_scaled_examples.jl:139); 'chained' = output 1's true values and the "
                          "PREDICTED means of outputs 2..p-1 (GPAR_scaled_examples.jl:172, eeg.jl:249)")
+    ap.add_argument("--inputs", default="device", choices=["device", "host"],
+                    help="'device': inputs resident in HBM before the timed region (the bench "
+                         "contract's value); 'host': numpy inputs and outputs through the C-ABI's "
+                         "host-memory mode (the Julia binding's case), so every step includes the "
+                         "library's H2D / D2H copies over PCIe")
     ap.add_argument("--rehearse", action="store_true",
                     help="multi-rank rehearsal on ONE GPU: every rank uses device 0 and the gloo "
                          "backend (RCCL runs one rank per device); exercises the launcher, sharding, "
@@ -161,6 +166,22 @@ def main():
     y1 = Y_d[:, 0].contiguous() if 1 in mine else None
     if temporal:   # every owned output is a temporal-only chain (rows of one contiguous block)
         y1 = Y_d[:, [p - 1 for p in mine]].T.contiguous() if mine else None
+    host = args.inputs == "host"
+    if host:
+        if world > 1 or args.inference != "given" or temporal or args.separate_predict:
+            sys.exit("--inputs host: one rank, given inference inputs, the GPAR configs only")
+        # the same problems from host (numpy) buffers: D x N ColVecs, as the Julia shim passes them
+        Yh_all = Y_d.cpu().numpy()
+        t_hh, ts_hh, Fs_hh = t_d.cpu().numpy(), ts_d.cpu().numpy(), Fs_d.cpu().numpy()
+        problems, keep = [], []
+        for p in gpar_out:
+            pr, k = G.make_problem(np.ascontiguousarray(Yh_all[:, : p - 1].T), Zs[p].cpu().numpy().T,
+                                   t_hh, np.ascontiguousarray(Yh_all[:, p - 1]), cfg["out_kernel"],
+                                   "matern52", qu_kuu_noise=True)
+            problems.append(pr)
+            keep.append(k)
+        Vs_h = [np.ascontiguousarray(Fs_hh[:, : p - 1].T) for p in gpar_out]
+        y1_h = np.ascontiguousarray(Yh_all[:, 0]) if y1 is not None else None
     x0 = np.tile(np.array([0.0, 0.0, 0.0, 0.0, -2.0]), (len(problems), 1))
     torch.cuda.synchronize()
     log(f"[rank {rank}] inputs ready in {time.perf_counter() - t0:.1f}s: N={n_eff} N*={ns_eff} "
@@ -178,6 +199,19 @@ def main():
 
     def step():
         res = {}
+        if host:
+            if problems:
+                fr, _, _ = G.fit_predict_batch(problems, x0, ts_hh, Vs_h, max_evals=EV, g_tol=-1.0,
+                                               mode=args.predict, samples=100, seed=gpar_out[0],
+                                               device=local)
+                for i, p in enumerate(gpar_out):
+                    res[p] = fr.theta[i]
+            if y1_h is not None:
+                th1, _, _ = G.get_sde_predictions(t_hh, y1_h, ts_hh, "matern52", i_log_time_l=0.0,
+                                                  i_log_time_var=0.0, i_log_noise_sigma=-2.0,
+                                                  max_evals=EV, g_tol=-1.0, device=local)
+                res[1] = np.array(list(th1) + [0.0, 0.0])
+            return S.gather_thetas(res, P, dev)
         if chained and world == 1:
             fr, _, _ = G.fit_predict_batch(problems, x0, ts_d, [None] * len(problems),
                                            max_evals=EV, g_tol=-1.0, mode=args.predict, samples=100,
@@ -279,7 +313,8 @@ def main():
                        "M": M, "P": P, "evals_per_output": EV, "predict": args.predict,
                        "out_kernel": cfg["out_kernel"], "time_kernel": "matern52",
                        "parallelism": f"outputs sharded over {world} GPU(s)",
-                       "outputs_per_rank": shards, "inference": args.inference},
+                       "outputs_per_rank": shards, "inference": args.inference,
+                       "inputs": args.inputs},
             **({"rehearsal": "all ranks on one GPU over gloo: not a scaling measurement"}
                if args.rehearse else {}),
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,

@@ -141,6 +141,17 @@ static void d2h(gpar_ctx* c, T* dst, const T* src, size_t count) {
   if (count) HIPCHECK(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyDeviceToHost, c->stream));
 }
 static void sync(gpar_ctx* c) { HIPCHECK(hipStreamSynchronize(c->stream)); }
+// rows x width doubles from a host matrix with leading dimension ld into a packed device matrix:
+// one linear copy when the rows are already packed (a pitched copy from pageable memory goes row
+// by row: 10^6 rows of a few doubles took seconds)
+static void h2d_rows(gpar_ctx* c, double* dst, const double* src, int64_t ld, int64_t width,
+                     int64_t rows) {
+  if (ld == width)
+    h2d(c, dst, src, (size_t)rows * width);
+  else
+    HIPCHECK(hipMemcpy2DAsync(dst, width * sizeof(double), src, ld * sizeof(double),
+                              width * sizeof(double), rows, hipMemcpyHostToDevice, c->stream));
+}
 
 // Route the launches of a scope to another stream (all helpers launch on c->stream).
 struct OnStream {
@@ -259,10 +270,8 @@ static DevProblem prepare_problem(gpar_ctx* c, const gpar_problem& p, int idx) {
   double* y = ws<double>(c, k + "_y", p.n);
   h2d(c, t, p.t, p.n);
   h2d(c, y, p.y, p.n);
-  HIPCHECK(hipMemcpy2DAsync(v, p.d * sizeof(double), p.v, p.ldv * sizeof(double),
-                            p.d * sizeof(double), p.n, hipMemcpyHostToDevice, c->stream));
-  HIPCHECK(hipMemcpy2DAsync(z, p.d * sizeof(double), p.z, p.ldz * sizeof(double),
-                            p.d * sizeof(double), p.m, hipMemcpyHostToDevice, c->stream));
+  h2d_rows(c, v, p.v, p.ldv, p.d, p.n);
+  h2d_rows(c, z, p.z, p.ldz, p.d, p.m);
   d.t = t; d.v = v; d.z = z; d.y = y;
   d.ldv = p.d; d.ldz = p.d;
   centres();
@@ -729,19 +738,24 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
   const double* vs = v_star_in;
   int64_t ldv_s = ldvs;
   if (mem == GPAR_MEM_HOST) {
-    perm.resize(n_star);
-    for (int64_t i = 0; i < n_star; ++i) perm[i] = i;
-    std::stable_sort(perm.begin(), perm.end(),
-                     [&](int64_t a, int64_t b) { return t_star_in[a] < t_star_in[b]; });
-    std::vector<double> tsh(n_star), vsh((size_t)n_star * d);
-    for (int64_t i = 0; i < n_star; ++i) {
-      tsh[i] = t_star_in[perm[i]];
-      for (int64_t q = 0; q < d; ++q) vsh[i * d + q] = v_star_in[perm[i] * ldvs + q];
-    }
     double* dts = ws<double>(c, "pr_ts", n_star);
     double* dvs = ws<double>(c, "pr_vs", (size_t)n_star * d);
-    h2d(c, dts, tsh.data(), n_star);
-    h2d(c, dvs, vsh.data(), (size_t)n_star * d);
+    if (std::is_sorted(t_star_in, t_star_in + n_star)) {   // already ascending: no permutation
+      h2d(c, dts, t_star_in, n_star);
+      h2d_rows(c, dvs, v_star_in, ldvs, d, n_star);
+    } else {
+      perm.resize(n_star);
+      for (int64_t i = 0; i < n_star; ++i) perm[i] = i;
+      std::stable_sort(perm.begin(), perm.end(),
+                       [&](int64_t a, int64_t b) { return t_star_in[a] < t_star_in[b]; });
+      std::vector<double> tsh(n_star), vsh((size_t)n_star * d);
+      for (int64_t i = 0; i < n_star; ++i) {
+        tsh[i] = t_star_in[perm[i]];
+        for (int64_t q = 0; q < d; ++q) vsh[i * d + q] = v_star_in[perm[i] * ldvs + q];
+      }
+      h2d(c, dts, tsh.data(), n_star);
+      h2d(c, dvs, vsh.data(), (size_t)n_star * d);
+    }
     sync(c);
     ts = dts;
     vs = dvs;
@@ -861,6 +875,10 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
   if (mem == GPAR_MEM_DEVICE) {
     HIPCHECK(hipMemcpyAsync(mean_out, dmean, n_star * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
     HIPCHECK(hipMemcpyAsync(std_out, dstd, n_star * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+    sync(c);
+  } else if (perm.empty()) {   // t* was ascending: straight into the caller's buffers
+    d2h(c, mean_out, dmean, n_star);
+    d2h(c, std_out, dstd, n_star);
     sync(c);
   } else {
     std::vector<double> hm(n_star), hs(n_star);
