@@ -503,7 +503,8 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
       Timed tm_(c, "gram", (double)n * (double)p.m * (double)(p.m + 1));   // flops of beta^T beta
       launch_gram(c->stream, p.sdim, plan, beta, p.mp, n, fix_beta ? nullptr : hsum, cin, qv,
                   p.mc, kChunk, alpha, part, rpart, o.G + (size_t)i * mpmax * mpmax, mpmax,
-                  o.r + (size_t)i * mpmax);
+                  o.r + (size_t)i * mpmax, nlanes == 1 ? c->side : nullptr, c->ev_fork,
+                  c->ev_join);
     }
     check_launch("gram");
   }

@@ -1000,6 +1000,10 @@ static void gram2_plan(int64_t n, int64_t mp, GramPlan& p, bool one_per_cu) {
 #ifndef GRAM_V3
 #define GRAM_V3 1   // 0: the v2 kernel at two workgroups per CU as well (A/B)
 #endif
+#ifndef GRAM3_CORUN
+#define GRAM3_CORUN 1   // 1: the chunk correction runs beside the OFF kernel on a second stream
+#endif
+#define HIPCHECK_G(x) do { if ((x) != hipSuccess) throw std::runtime_error("launch_gram: " #x); } while (0)
 #ifndef GRAM3_DG_SLOTS
 #define GRAM3_DG_SLOTS 1024
 #endif
@@ -1035,8 +1039,14 @@ static void gram3_plan(int64_t n, int64_t mp, GramPlan& p) {
   if (ncs < 1) ncs = 1;
   if (ncs > nch) ncs = (int)(nch > 0 ? nch : 1);
   p.ncs = ncs;
-  p.part_doubles = (int64_t)(p.noff * (p.soff + ncs) + p.ndg * (p.sdg + ncs)) * 2 * kF3T * 256;
-  p.rpart_doubles = (int64_t)(p.sdg + ncs) * mp;
+  // co-run: the slim correction's 8 waves per (group, split), at most one per SIMD beside OFF
+  int ncs2 = 1024 / (8 * (p.noff + p.ndg));
+  if (ncs2 < 1) ncs2 = 1;
+  if (ncs2 > nch) ncs2 = (int)(nch > 0 ? nch : 1);
+  p.ncs_slim = ncs2;
+  const int nc = ncs > ncs2 ? ncs : ncs2;
+  p.part_doubles = (int64_t)(p.noff * (p.soff + nc) + p.ndg * (p.sdg + nc)) * 2 * kF3T * 256;
+  p.rpart_doubles = (int64_t)(p.sdg + nc) * mp;
 }
 
 GramPlan gram_plan(int64_t n, int64_t mp, bool one_per_cu) {
@@ -1083,18 +1093,31 @@ GramPlan gram_plan(int64_t n, int64_t mp, bool one_per_cu) {
 void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* beta,
                  int64_t ldb, int64_t n, const double* ecor, const double* cin, const double* qv,
                  int64_t mc, int L, const double* alpha, double* part, double* rpart, double* G,
-                 int64_t ldg, double* r) {
+                 int64_t ldg, double* r, hipStream_t side, hipEvent_t ev_a, hipEvent_t ev_b) {
   if (plan.v3) {
-    const int ncs = ecor ? plan.ncs : 0;
+    const bool corun = GRAM3_CORUN && ecor && side && plan.noff > 0;
+    const int ncs = ecor ? (corun ? plan.ncs_slim : plan.ncs) : 0;
     const int noffw = ((plan.noff * plan.soff + 7) / 8) * 8;   // XCD deal
     const int ndgw = ((plan.ndg * plan.sdg + 7) / 8) * 8;
+    const int64_t nchk = (n + L - 1) / L;
+    if (corun) {   // the slim correction beside the OFF kernel, on the second stream
+      HIPCHECK_G(hipEventRecord(ev_a, st));
+      HIPCHECK_G(hipStreamWaitEvent(side, ev_a, 0));
+    }
     if (noffw > 0)
       gram3_off_kernel<<<noffw, 128, 0, st>>>(beta, ldb, n, plan.noff, plan.soff, plan.rows_off, part);
+    if (corun)
+      launch_gram3_corr_slim(side, sdim, ecor, cin, qv, mc, nchk, plan.npan, plan.noff, plan.ndg,
+                             plan.soff, plan.sdg, ncs, part, rpart);
     launch_gram3_dg(st, ndgw, beta, ldb, n, alpha, plan.npan, plan.ndg, plan.sdg, plan.rows_dg,
                     (int64_t)plan.noff * (plan.soff + ncs), part, rpart);
-    if (ncs)
-      launch_gram3_corr(st, sdim, ecor, cin, qv, mc, (n + L - 1) / L, plan.npan, plan.noff,
-                        plan.ndg, plan.soff, plan.sdg, ncs, part, rpart);
+    if (corun) {
+      HIPCHECK_G(hipEventRecord(ev_b, side));
+      HIPCHECK_G(hipStreamWaitEvent(st, ev_b, 0));
+    } else if (ncs) {
+      launch_gram3_corr(st, sdim, ecor, cin, qv, mc, nchk, plan.npan, plan.noff, plan.ndg,
+                        plan.soff, plan.sdg, ncs, part, rpart);
+    }
     const int nrows = plan.noff * 2 * kF3T + plan.ndg * 2 * kD2T + 1;
     gram3_reduce<<<nrows, 256, 0, st>>>(part, rpart, plan.npan, plan.noff, plan.ndg, plan.soff,
                                         plan.sdg, ncs, G, ldg, r);

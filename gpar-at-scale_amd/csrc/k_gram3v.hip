@@ -273,6 +273,140 @@ __global__ __launch_bounds__(256) void gram3_corr_kernel(
   }
 }
 
+// Slim chunk correction, for running CONCURRENTLY with gram3_off_kernel on a second stream: a
+// wave owns 2 x 4 tiles (64 accumulator VGPRs) and stays within the <= 124 registers per lane that
+// the OFF wave (132 VGPRs + 256 AGPRs) leaves free on its SIMD, and it uses no LDS.  Grid:
+// (noff + ndg) groups x 2 workgroups x ncs chunk splits, 4 waves each; the 8 waves of a group
+// cover its 8 x 8 tiles as 2 x 4 blocks (row pair wg >> 1, column half wg & 1).  DG groups skip
+// the two blocks above the diagonal and every wave sums r's chunk term for 16 of the block's
+// columns.  Partial slots as gram3_corr_kernel.
+template <int D>
+__global__ __launch_bounds__(256) void gram3_corr_slim_kernel(
+    const double* __restrict__ ecor, const double* __restrict__ cin, const double* __restrict__ qv,
+    int64_t mc, int64_t nch, int npan, int noff, int ndg, int soff, int sdg, int ncs,
+    double* __restrict__ part, double* __restrict__ rpart) {
+  const int ng = noff + ndg;
+  const int g = (int)blockIdx.x % ng;
+  const int hw = ((int)blockIdx.x / ng) & 1, cs = (int)blockIdx.x / (2 * ng);
+  const int64_t j0 = (int64_t)cs * nch / ncs, j1 = (int64_t)(cs + 1) * nch / ncs;
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+  const int wg = hw * 4 + wave;           // 0..7 within the group
+  const int rb = wg >> 1, cb = wg & 1;    // row tiles 2 rb, 2 rb + 1; column tiles 4 cb .. 4 cb + 3
+  const int lq = lane >> 4, lc = lane & 15;
+  const bool cv = lq < D;
+  const int64_t cstride = mc * kSStride;
+
+  const bool is_dg = g >= noff;
+  int64_t base_r, base_c;   // G row / column of local tile 0
+  if (!is_dg) {
+    int a = 1;
+    while (a * (a + 1) / 2 <= g) ++a;
+    const int bo = g - a * (a - 1) / 2;
+    base_r = (int64_t)(2 * a) * kPW;
+    base_c = (int64_t)(2 * bo) * kPW;
+  } else {
+    base_r = base_c = (int64_t)2 * (g - noff) * kPW;
+  }
+  const bool active = !is_dg || !(cb == 1 && rb < 2);
+
+  d4 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[i][c] = d4{0.0, 0.0, 0.0, 0.0};
+  double racc = 0.0;
+  // K-lane packing: chunk j contributes 2 d rank-1 terms, sum_q E[:, q] C[:, q]^T and
+  // sum_q C[:, q] E[:, q]^T; two chunks' 4 d terms fill d MFMAs of K = 4 exactly (slot
+  // s = 4 m + lane's k: chunk j + s / 2d, term u = s % 2d: u < d -> (E_u, C_u), else (C_u-d, E_u-d))
+  // instead of 4 MFMAs with the state lanes q >= d zero.
+  const int64_t ra = (base_r + rb * 32 + lc) * kSStride;   // row operand, column offset
+  const int64_t rbo = (base_c + cb * 64 + lc) * kSStride;  // column operand
+  const int64_t orr = (base_c + wg * 16 + lc) * kSStride + lq;
+  for (int64_t jj = j0; jj < j1; jj += 2) {
+    if (active) {
+#pragma unroll
+      for (int m = 0; m < D; ++m) {
+        const int sl = 4 * m + lq;
+        const int64_t ch = jj + sl / (2 * D);
+        const int u = sl % (2 * D);
+        const bool ok = ch < j1;
+        const int q = u < D ? u : u - D;
+        const double* srcA = (u < D ? ecor : cin) + (ok ? ch : jj) * cstride + q;
+        const double* srcB = (u < D ? cin : ecor) + (ok ? ch : jj) * cstride + q;
+        double fa[2], fb[4];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) fa[t] = ok ? srcA[ra + t * 16 * kSStride] : 0.0;
+#pragma unroll
+        for (int t = 0; t < 4; ++t) fb[t] = ok ? srcB[rbo + t * 16 * kSStride] : 0.0;
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int c = 0; c < 4; ++c)
+            acc[i][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[i], fb[c], acc[i][c], 0, 0, 0);
+      }
+    }
+    if (is_dg) {
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        if (jj + k < j1) {
+          const double cr = cv ? cin[(jj + k) * cstride + orr] : 0.0;
+          const double qq = cv ? qv[(jj + k) * 4 + lq] : 0.0;
+          racc = fma(cr, qq, racc);
+        }
+      }
+    }
+  }
+
+  const int frow = lane >> 4, fcol = lane & 15;
+  if (!is_dg) {
+    const int64_t slot = (int64_t)g + (int64_t)(soff + cs) * noff;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rr = rb * 2 + i;   // local row tile 0..7: OFF wave rr >> 2, tile row rr & 3
+      double* prow = part + ((slot * 2 + (rr >> 2)) * kF3T + (rr & 3) * 8 + cb * 4) * 256;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) prow[c * 256 + (frow + 4 * r) * 16 + fcol] = acc[i][c][r];
+    }
+    return;
+  }
+  const int64_t slot = (int64_t)noff * (soff + ncs) + (g - noff) + (int64_t)(sdg + cs) * ndg;
+  if (active) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int rr = rb * 2 + i;
+      const int h = d2_half_of(rr), tb = d2_base_of(rr);
+      double* prow = part + ((slot * 2 + h) * kF3T + tb) * 256;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        const int cc = cb * 4 + c;
+        if (cc > rr) continue;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) prow[cc * 256 + (frow + 4 * r) * 16 + fcol] = acc[i][c][r];
+      }
+    }
+  }
+  double v = racc;
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  if (lq == 0) rpart[(int64_t)(sdg + cs) * npan * kPW + base_c + wg * 16 + lc] = v;
+}
+
+void launch_gram3_corr_slim(hipStream_t st, int sdim, const double* ecor, const double* cin,
+                            const double* qv, int64_t mc, int64_t nch, int npan, int noff, int ndg,
+                            int soff, int sdg, int ncs, double* part, double* rpart) {
+  const int nwg = (noff + ndg) * 2 * ncs;
+#define GRAM3C_ARGS ecor, cin, qv, mc, nch, npan, noff, ndg, soff, sdg, ncs, part, rpart
+  switch (sdim) {
+    case 1: gram3_corr_slim_kernel<1><<<nwg, 256, 0, st>>>(GRAM3C_ARGS); break;
+    case 2: gram3_corr_slim_kernel<2><<<nwg, 256, 0, st>>>(GRAM3C_ARGS); break;
+    default: gram3_corr_slim_kernel<3><<<nwg, 256, 0, st>>>(GRAM3C_ARGS); break;
+  }
+#undef GRAM3C_ARGS
+}
+
 void launch_gram3_dg(hipStream_t st, int nwg, const double* beta, int64_t ldb, int64_t n,
                      const double* alpha, int npan, int ndg, int sdg, int64_t rows,
                      int64_t slot0, double* part, double* rpart) {

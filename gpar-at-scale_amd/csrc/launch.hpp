@@ -77,6 +77,7 @@ struct GramPlan {
   int one_per_cu = 0;
   int v3 = 0;   // fat-wave kernels (gram3_*: 2-wave workgroups, 32-tile OFF waves)
   int ncs = 0;  // v3 chunk-correction splits
+  int ncs_slim = 0;  // ... of the slim correction that runs beside the OFF kernel
 };
 
 constexpr int kGramTile = 128;
@@ -170,7 +171,8 @@ GramPlan gram_plan(int64_t n, int64_t mp, bool one_per_cu = false);
 void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* beta,
                  int64_t ldb, int64_t n, const double* ecor, const double* cin, const double* qv,
                  int64_t mc, int L, const double* alpha, double* part, double* rpart, double* G,
-                 int64_t ldg, double* r);
+                 int64_t ldg, double* r, hipStream_t side = nullptr,
+                 hipEvent_t ev_a = nullptr, hipEvent_t ev_b = nullptr);
 void launch_beta_fix(hipStream_t st, int sdim, double* beta, int64_t ldb, int64_t n,
                      const double* g, const double* cin, int64_t mc, int L);
 
