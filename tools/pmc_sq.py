@@ -49,9 +49,13 @@ def load(d):
     out = defaultdict(lambda: defaultdict(list))
     for (k, sub), cs in by.items():
         for c, v in cs.items():
+            if "corr_slim" in sub and c.startswith("GRBM_"):
+                continue   # elapsed-cycle counter of a kernel that overlaps gram3_off_kernel
             out[k][c].append(avg(v))                 # one entry per kernel: summed below
     durs = defaultdict(list)
     for (k, sub), ts in dby.items():
+        if "corr_slim" in sub:   # runs concurrently with gram3_off_kernel: adds no time
+            continue
         durs[k].append(avg(ts))
     kernels = defaultdict(list)
     for (k, sub) in by:
