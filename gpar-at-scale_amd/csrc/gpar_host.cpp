@@ -1157,8 +1157,8 @@ static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<
     if (bytes > budget) continue;
     budget -= bytes;
     double* d2 = ws<double>(c, "distcache" + std::to_string(slot++), (size_t)p.n * p.mp);
-    launch_dist2(c->stream, p.ok, p.v, p.ldv, p.n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, d2, p.mp);
-    if (p.ok != GPAR_EQ) launch_sqrt_inplace(c->stream, d2, p.n * p.mp);
+    launch_dist2(c->stream, p.ok, p.v, p.ldv, p.n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, d2, p.mp,
+                 /*take_sqrt=*/p.ok != GPAR_EQ);
     check_launch("dist2 (cache)");
     Q[i].d2 = d2;
     Q[i].d2_is_r = p.ok != GPAR_EQ;

@@ -34,7 +34,7 @@ constexpr int kDT = 128, kDBK = 16, kDLds = 136;
 __global__ __launch_bounds__(256, 2) void dist2_mfma_kernel(
     const double* __restrict__ v, int64_t ldv, int64_t n, const double* __restrict__ z,
     int64_t ldz, int64_t m, int64_t mp, int d, const double* __restrict__ zc, int64_t zld,
-    double* __restrict__ out, int64_t ldo) {
+    double* __restrict__ out, int64_t ldo, int rout) {
   __shared__ __attribute__((aligned(16))) double smem[2 * 2 * kDBK * kDLds];
   __shared__ double vn_s[kDT], zn_s[kDT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -124,7 +124,10 @@ __global__ __launch_bounds__(256, 2) void dist2_mfma_kernel(
       for (int c = 0; c < 4; ++c) {
         const int cl = wc * 64 + c * 16 + fcol;
         const int64_t col = c0 + cl;
-        if (col < mp) out[row * ldo + col] = col < m ? vn + zn_s[cl] - 2.0 * acc[a][c][r] : 0.0;
+        if (col < mp) {
+          const double d2 = col < m ? vn + zn_s[cl] - 2.0 * acc[a][c][r] : 0.0;
+          out[row * ldo + col] = rout ? sqrt_pos(d2) : d2;
+        }
       }
     }
 }
@@ -138,7 +141,7 @@ constexpr int kDRows = 64, kDDim = 16;
 
 __global__ __launch_bounds__(256) void dist2_direct_kernel(
     const double* __restrict__ v, int64_t ldv, int64_t n, const double* __restrict__ z,
-    int64_t ldz, int64_t m, int64_t mp, int d, double* __restrict__ out, int64_t ldo) {
+    int64_t ldz, int64_t m, int64_t mp, int d, double* __restrict__ out, int64_t ldo, int rout) {
   __shared__ double vs[kDRows][kDDim + 1];
   const int tid = threadIdx.x;
   const int64_t c = (int64_t)blockIdx.y * 256 + tid;
@@ -181,7 +184,10 @@ __global__ __launch_bounds__(256) void dist2_direct_kernel(
 #pragma unroll
     for (int r = 0; r < kDRows; ++r) {
       const int64_t k = k0 + r;
-      if (k < n) out[k * ldo + c] = cv ? acc[r] : 0.0;
+      if (k < n) {
+        const double d2 = cv ? acc[r] : 0.0;
+        out[k * ldo + c] = rout ? sqrt_pos(d2) : d2;
+      }
     }
   }
 }
@@ -375,14 +381,16 @@ void launch_zcenter_wide(hipStream_t st, const double* z, int64_t ldz, int d, in
 
 void launch_dist2(hipStream_t st, int out_kind, const double* v, int64_t ldv, int64_t n,
                   const double* z, int64_t ldz, int64_t m, int64_t mp, int d, const double* zc,
-                  double* out, int64_t ldo) {
+                  double* out, int64_t ldo, bool take_sqrt) {
   if (n <= 0) return;
+  const int rout = take_sqrt ? 1 : 0;
   if (out_kind == KM12) {
     dim3 grid((unsigned)((n + kDRows - 1) / kDRows), (unsigned)((mp + 255) / 256));
-    dist2_direct_kernel<<<grid, 256, 0, st>>>(v, ldv, n, z, ldz, m, mp, d, out, ldo);
+    dist2_direct_kernel<<<grid, 256, 0, st>>>(v, ldv, n, z, ldz, m, mp, d, out, ldo, rout);
   } else {
     dim3 grid((unsigned)((n + kDT - 1) / kDT), (unsigned)((mp + kDT - 1) / kDT));
-    dist2_mfma_kernel<<<grid, 256, 0, st>>>(v, ldv, n, z, ldz, m, mp, d, zc, zc_stride(d), out, ldo);
+    dist2_mfma_kernel<<<grid, 256, 0, st>>>(v, ldv, n, z, ldz, m, mp, d, zc, zc_stride(d), out, ldo,
+                                            rout);
   }
 }
 
@@ -421,16 +429,6 @@ static void launch_wd2_t(hipStream_t st, int ok, bool rin, dim3 grid, const doub
 #undef WD2_ARGS
 }
 
-// r = sqrt_pos(d2) in place (the distance cache of the Matern kernels)
-__global__ void sqrt_inplace_kernel(double* __restrict__ a, int64_t count) {
-  const int64_t i = blockIdx.x * (int64_t)256 + threadIdx.x;
-  if (i < count) a[i] = sqrt_pos(a[i]);
-}
-
-void launch_sqrt_inplace(hipStream_t st, double* a, int64_t count) {
-  if (count <= 0) return;
-  sqrt_inplace_kernel<<<(unsigned)((count + 255) / 256), 256, 0, st>>>(a, count);
-}
 
 void launch_whiten_kfu_d2(hipStream_t st, int time_kind, int out_kind, const double* rec,
                           const double* src, int64_t lds, int64_t m, int64_t mp, int64_t n, int L,

@@ -113,10 +113,11 @@ int64_t zc_stride(int d);
 void launch_zcenter_wide(hipStream_t st, const double* z, int64_t ldz, int d, int64_t m,
                          int64_t mp, double* zc);
 // d2[k][c] (k < n, c < mp; 0 for c >= m) into out (ld ldo): MFMA Gram form, centred per 256-column
-// group (smooth kernels), or direct differences (out_kind = Matern-1/2)
+// group (smooth kernels), or direct differences (out_kind = Matern-1/2); take_sqrt: r = sqrt_pos(d2)
+// instead (the Matern kernels' distance cache)
 void launch_dist2(hipStream_t st, int out_kind, const double* v, int64_t ldv, int64_t n,
                   const double* z, int64_t ldz, int64_t m, int64_t mp, int d, const double* zc,
-                  double* out, int64_t ldo);
+                  double* out, int64_t ldo, bool take_sqrt = false);
 // whiten_kfu from precomputed squared distances (src may equal beta: in place), or from the
 // distances themselves (src_is_r: the fit's cache for the Matern kernels)
 void launch_whiten_kfu_d2(hipStream_t st, int time_kind, int out_kind, const double* rec,
@@ -124,7 +125,6 @@ void launch_whiten_kfu_d2(hipStream_t st, int time_kind, int out_kind, const dou
                           int64_t nch, double inv_lo, double s_o, double* beta, int64_t ldb,
                           double* send, int64_t mc, const double* g, double* hsum,
                           bool src_is_r = false);
-void launch_sqrt_inplace(hipStream_t st, double* a, int64_t count);
 void launch_whiten_vec(hipStream_t st, int sdim, const double* rec, int64_t recstride,
                        const double* y, int64_t ldy, int64_t n, int L, int64_t nch, int nchains,
                        double* alpha, int64_t lda, double* send, int64_t sendstride, int64_t mc,
