@@ -320,6 +320,10 @@ def main():
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
                          "traffic": traffic, "kernel": "Gram beta^T beta + beta^T alpha, fp64 MFMA (v3: gram3_off + gram3_dg + gram3_corr + gram3_reduce per launch; lanes=2: gram2)",
+                         "note": "avg_ms spans one Gram launch (HIP events): gram3_off_kernel, then "
+                                 "gram3_dg_kernel and gram3_reduce; gram3_corr_slim_kernel runs "
+                                 "concurrently with gram3_off_kernel on a second stream, so rocprof's "
+                                 "averages of the three sequential kernels add up to avg_ms",
                          "launches": gram_n, "avg_ms": avg, "flops_per_launch": flops,
                          "lanes": args.lanes},
             "kernels": {"gram_ms_per_step": gram_ms / args.steps, "whiten_ms_per_step": wh_ms / args.steps,
