@@ -333,9 +333,6 @@ static GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
 // Inputs wider than kFusedMaxD (the fused kernels keep a column's pseudo-input in registers):
 // the squared distances are a separate MFMA (or direct-difference) pass into beta itself, which
 // the whitening then reads and overwrites in place (k_dist.hip).
-#ifndef WHITEN_VX
-#define WHITEN_VX 0   // 1: D <= 16 through whiten_kfu_vx2 (direct differences); 0: the MFMA-form fused kernel
-#endif
 static void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const double* rec, const double* v,
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
                            int64_t ldb, double* send, const double* g, double* hsum) {
@@ -343,9 +340,6 @@ static void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const double* rec, 
   if (p.d2 && v == p.v) {   // the fit's training inputs, distances cached (fit_impl)
     launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, p.d2, p.mp, p.m, p.mp, n, kChunk, nch,
                          1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum, p.d2_is_r);
-  } else if (WHITEN_VX && p.d <= 16) {   // narrow inputs: direct differences on the VALU
-    launch_whiten_kfu_vx(c->stream, p.tk, p.ok, rec, v, ldv, (int)p.d, p.z, p.ldz, p.m, p.mp, n,
-                         kChunk, nch, 1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum);
   } else if (p.d > kFusedMaxD) {
     launch_dist2(c->stream, p.ok, v, ldv, n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, beta, ldb);
     launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, beta, ldb, p.m, p.mp, n, kChunk, nch,

@@ -345,173 +345,6 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_d2x2(
   }
 }
 
-// ---------------------------------------------------------------------------- narrow inputs
-// Kfu + whitening for inputs with D <= 16, distances by direct differences on the VALU: the
-// d2x2 layout (two adjacent columns per thread, the chunk's records and fix-up rows staged in LDS
-// once) with the chunk's V rows staged beside them (256 x DP doubles, read back as broadcasts)
-// and each thread's two pseudo-inputs in registers.  d2 = sum_i (v_i - z_i)^2 over DP dimensions
-// (the ones past d are zero in both), so the distance work scales with D, where the MFMA form's
-// 16-step sub-tiles, transposes and barriers cost the same at D = 1 as at D = 16.  Direct
-// differences are also the oracle's form (no Gram-form cancellation).  Reads only V (N x D);
-// writes beta.  DP in {4, 8, 16}.
-template <int TK, int OK, int DP>
-__global__ __launch_bounds__(256, 2) void whiten_kfu_vx2(
-    const double* __restrict__ rec, const double* __restrict__ v, int64_t ldv, int d,
-    const double* __restrict__ z, int64_t ldz, int64_t m, int64_t mp, int64_t n, int L,
-    double inv_lo, double s_o, double* __restrict__ beta, int64_t ldb,
-    double* __restrict__ send, int64_t mc, const double* __restrict__ g,
-    double* __restrict__ hsum, ExpNegConsts ek) {
-  constexpr int SD = Sde<TK>::d;
-  constexpr int RS = Rec<SD>::size;
-  __shared__ __attribute__((aligned(16))) double rl[kW2MaxL * RS];
-  __shared__ __attribute__((aligned(16))) double gl[kW2MaxL * kGStride];
-  __shared__ __attribute__((aligned(16))) double vl[kW2MaxL * DP];
-  const int tid = threadIdx.x;
-  const int64_t j = blockIdx.x;
-  const int64_t c = ((int64_t)blockIdx.y * 256 + tid) * 2;   // first of the thread's two columns
-  const bool cola = c < mp;                                  // mp even: both or neither
-  const bool v0 = c < m, v1 = c + 1 < m;
-  const int64_t k0 = j * L;
-  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
-  const int nk = (int)(k1 - k0);
-  for (int e = tid; e < nk * RS; e += 256) rl[e] = rec[k0 * RS + e];
-  for (int e = tid; e < nk * kGStride; e += 256) gl[e] = g[k0 * kGStride + e];
-  for (int e = tid; e < nk * DP; e += 256) {
-    const int r = e / DP, i = e % DP;
-    vl[e] = i < d ? v[(k0 + r) * ldv + i] : 0.0;
-  }
-  double za[DP], zb[DP];
-#pragma unroll
-  for (int i = 0; i < DP; ++i) {
-    za[i] = (v0 && i < d) ? z[c * ldz + i] : 0.0;
-    zb[i] = (v1 && i < d) ? z[(c + 1) * ldz + i] : 0.0;
-  }
-  double ma[SD], mb[SD], ha[SD], hb[SD];
-#pragma unroll
-  for (int i = 0; i < SD; ++i) ma[i] = mb[i] = ha[i] = hb[i] = 0.0;
-  double* bp = beta + k0 * ldb + (cola ? c : 0);
-  __syncthreads();
-  for (int r0 = 0; r0 < nk; r0 += kW2T) {
-    double2 x[kW2T];
-#pragma unroll
-    for (int r = 0; r < kW2T; ++r) {
-      const int rw = (r0 + r < nk) ? r0 + r : nk - 1;
-      const double* vr = vl + rw * DP;
-      double sa = 0.0, sb = 0.0;
-#pragma unroll
-      for (int i = 0; i < DP; ++i) {   // d2 += diff * diff, each rounded (no fma): the
-        const double vi = vr[i];         // oracle's (and numpy's) order, so d2 is bit-identical
-        const double da = vi - za[i], db = vi - zb[i];
-        sa = __dadd_rn(sa, __dmul_rn(da, da));
-        sb = __dadd_rn(sb, __dmul_rn(db, db));
-      }
-      x[r].x = v0 ? skappa_sq_k<OK>(sa, inv_lo, s_o, ek) : 0.0;
-      x[r].y = v1 ? skappa_sq_k<OK>(sb, inv_lo, s_o, ek) : 0.0;
-    }
-    auto step = [&](int r) __attribute__((always_inline)) {
-      const double* rr = rl + (r0 + r) * RS;
-      const double* gg = gl + (r0 + r) * kGStride;
-      double pa[SD], pb[SD];
-#pragma unroll
-      for (int i = 0; i < SD; ++i) {
-        double sa = 0.0, sb = 0.0;
-#pragma unroll
-        for (int q = 0; q < SD; ++q) {
-          sa = fma(rr[i * SD + q], ma[q], sa);
-          sb = fma(rr[i * SD + q], mb[q], sb);
-        }
-        pa[i] = sa;
-        pb[i] = sb;
-      }
-      const double ea = x[r].x - pa[0], eb = x[r].y - pb[0];
-      const double rs = rr[SD * SD + SD];
-      const double aa = ea * rs, ab = eb * rs;
-#pragma unroll
-      for (int i = 0; i < SD; ++i) {
-        const double kg = rr[SD * SD + i];
-        ma[i] = fma(kg, ea, pa[i]);
-        mb[i] = fma(kg, eb, pb[i]);
-        const double gi = gg[i];
-        ha[i] = fma(aa, gi, ha[i]);
-        hb[i] = fma(ab, gi, hb[i]);
-      }
-      if (cola) {
-        typedef double v2d __attribute__((ext_vector_type(2)));
-        v2d t;
-        t.x = aa;
-        t.y = ab;
-        __builtin_nontemporal_store(t, reinterpret_cast<v2d*>(bp + (int64_t)(r0 + r) * ldb));
-      }
-    };
-    if (r0 + kW2T <= nk) {
-#pragma unroll
-      for (int r = 0; r < kW2T; ++r) step(r);
-    } else {
-      const int nr = nk - r0;
-#pragma unroll
-      for (int r = 0; r < kW2T; ++r)
-        if (r < nr) step(r);
-    }
-  }
-  if (cola) {
-#pragma unroll
-    for (int i = 0; i < SD; ++i) {
-      send[(j * mc + c) * kSStride + i] = ma[i];
-      send[(j * mc + c + 1) * kSStride + i] = mb[i];
-      if (hsum) {
-        hsum[(j * mc + c) * kSStride + i] = ha[i];
-        hsum[(j * mc + c + 1) * kSStride + i] = hb[i];
-      }
-    }
-  }
-}
-
-template <int TK, int OK>
-static void launch_wvx_k(hipStream_t st, dim3 grid, int dp, const double* rec, const double* v,
-                         int64_t ldv, int d, const double* z, int64_t ldz, int64_t m, int64_t mp,
-                         int64_t n, int L, double inv_lo, double s_o, double* beta, int64_t ldb,
-                         double* send, int64_t mc, const double* g, double* hsum) {
-#define WVX_ARGS rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum, exp_neg_consts()
-  switch (dp) {
-    case 4: whiten_kfu_vx2<TK, OK, 4><<<grid, 256, 0, st>>>(WVX_ARGS); break;
-    case 8: whiten_kfu_vx2<TK, OK, 8><<<grid, 256, 0, st>>>(WVX_ARGS); break;
-    default: whiten_kfu_vx2<TK, OK, 16><<<grid, 256, 0, st>>>(WVX_ARGS); break;
-  }
-#undef WVX_ARGS
-}
-
-template <int TK>
-static void launch_wvx_t(hipStream_t st, int ok, dim3 grid, int dp, const double* rec,
-                         const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
-                         int64_t m, int64_t mp, int64_t n, int L, double inv_lo, double s_o,
-                         double* beta, int64_t ldb, double* send, int64_t mc, const double* g,
-                         double* hsum) {
-#define WVXT_ARGS st, grid, dp, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum
-  switch (ok) {
-    case KM12: launch_wvx_k<TK, KM12>(WVXT_ARGS); break;
-    case KM32: launch_wvx_k<TK, KM32>(WVXT_ARGS); break;
-    case KEQ: launch_wvx_k<TK, KEQ>(WVXT_ARGS); break;
-    default: launch_wvx_k<TK, KM52>(WVXT_ARGS); break;
-  }
-#undef WVXT_ARGS
-}
-
-void launch_whiten_kfu_vx(hipStream_t st, int time_kind, int out_kind, const double* rec,
-                          const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
-                          int64_t m, int64_t mp, int64_t n, int L, int64_t nch, double inv_lo,
-                          double s_o, double* beta, int64_t ldb, double* send, int64_t mc,
-                          const double* g, double* hsum) {
-  if (L > kW2MaxL || (ldb & 1) || d > 16)
-    throw std::runtime_error("whiten_kfu_vx2: chunk length > 256, odd ldb or d > 16");
-  const dim3 grid((unsigned)nch, (unsigned)((mp + 511) / 512));
-  const int dp = d <= 4 ? 4 : (d <= 8 ? 8 : 16);
-  switch (time_kind) {
-    case KM12: launch_wvx_t<KM12>(st, out_kind, grid, dp, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
-    case KM32: launch_wvx_t<KM32>(st, out_kind, grid, dp, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
-    default: launch_wvx_t<KM52>(st, out_kind, grid, dp, rec, v, ldv, d, z, ldz, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
-  }
-}
-
 // ---------------------------------------------------------------------------- wide centres
 // zc[g * zld + i] = mean over the group's (<= 256) pseudo-inputs of z[c][i], any d (one thread per
 // dimension, the group's columns summed in order).

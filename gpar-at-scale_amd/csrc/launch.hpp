@@ -118,12 +118,6 @@ void launch_zcenter_wide(hipStream_t st, const double* z, int64_t ldz, int d, in
 void launch_dist2(hipStream_t st, int out_kind, const double* v, int64_t ldv, int64_t n,
                   const double* z, int64_t ldz, int64_t m, int64_t mp, int d, const double* zc,
                   double* out, int64_t ldo, bool take_sqrt = false);
-// Kfu + whitening for d <= 16 with the distances by direct differences (k_dist.hip)
-void launch_whiten_kfu_vx(hipStream_t st, int time_kind, int out_kind, const double* rec,
-                          const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
-                          int64_t m, int64_t mp, int64_t n, int L, int64_t nch, double inv_lo,
-                          double s_o, double* beta, int64_t ldb, double* send, int64_t mc,
-                          const double* g, double* hsum);
 // whiten_kfu from precomputed squared distances (src may equal beta: in place), or from the
 // distances themselves (src_is_r: the fit's cache for the Matern kernels)
 void launch_whiten_kfu_d2(hipStream_t st, int time_kind, int out_kind, const double* rec,
