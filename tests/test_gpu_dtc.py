@@ -33,6 +33,11 @@ CASES = [
     # a diagonal group whose second block is missing
     (800, 3, 300, 12, ("matern52", "matern52"), (1.2, 0.9, 1.0, 1.1, 0.25)),
     (600, 3, 600, 13, ("matern32", "matern52"), (0.9, 1.1, 1.4, 0.9, 0.3)),
+    # Gram v3's correction beside the OFF kernel with its K lanes packed over chunk pairs: state
+    # dimension 2 (Matern-3/2 time) and 1 (Matern-1/2), odd chunk counts (6 and 5 chunks of 256,
+    # the last one short), off-diagonal groups present (Mp = 384)
+    (1297, 3, 260, 14, ("matern52", "matern32"), (1.0, 1.2, 1.1, 0.9, 0.2)),
+    (1041, 2, 300, 15, ("eq", "matern12"), (1.4, 0.7, 1.6, 1.3, 0.3)),
 ]
 
 
