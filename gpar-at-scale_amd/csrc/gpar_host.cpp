@@ -9,6 +9,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <stdexcept>
@@ -25,6 +26,8 @@ struct gpar_ctx {
   hipStream_t main = nullptr;     // the context's stream
   hipStream_t side = nullptr;     // second stream: alternate outputs of a batch run here
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+  hipEvent_t ev_pw = nullptr, ev_pc[2] = {nullptr, nullptr};   // the fit's pipelined Gram stage
+  bool pipeline = true;           // GPAR_PIPELINE=0 turns the pipelined Gram stage off (A/B)
   // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
   // the caller's stream, e.g. the copies that produce its device inputs
   bool has_input_stream = false;
@@ -165,6 +168,7 @@ constexpr int kChunk = 256;   // time-chunk length of the Kalman sweeps (power o
 static_assert(kChunk == 256, "vec_fix runs one 256-thread block per chunk");
 constexpr int kSStride = 4;   // chunk state vectors padded to 4 doubles (device_common.hpp)
 constexpr int64_t kFusedMaxD = 64;   // widest input the fused Kfu + whitening kernels take
+constexpr int64_t kPipeMaxBetaBytes = (int64_t)8 << 30;   // second beta buffer of the pipelined fit
 
 static int sde_dim(int kind) {
   if (kind == GPAR_MATERN12) return 1;
@@ -426,13 +430,22 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   // beta / alpha / carry workspace, so one output's (VALU-bound) whitening overlaps another's
   // (MFMA-bound) Gram.  Gains are shared: the side stream waits for them (fork event).
   const int nlanes = (np > 1 && !fix_beta && c->lanes > 1) ? 2 : 1;
+  // One lane, pipelined (the batched fit): the big kernels stay in order on the context stream,
+  // whitening(i + 1) issued ahead of Gram(i), and output i's short chain between them (alpha's end
+  // states, the chunk carry, vec_fix, the beta tail) runs on the side stream beside a whitening
+  // instead of on the critical path.  Two beta / carry buffers, so only when a second beta fits
+  // comfortably (the north job: 4.1 GB; the N = 1e7, M = 1024 stress config's 82 GB does not).
+  const int64_t beta_bytes = (n + 16) * mpmax * (int64_t)sizeof(double);
+  const bool pipe = nlanes == 1 && np > 1 && shared && !fix_beta && c->pipeline &&
+                    beta_bytes <= kPipeMaxBetaBytes;
+  const int nbuf = (nlanes > 1 || pipe) ? 2 : 1;
   double* beta_l[2];
   double* alpha_l[2];
   double* send_l[2];
   double* cin_l[2];
   double* hsum_l[2];
   double* qv_l[2];
-  for (int l = 0; l < nlanes; ++l) {
+  for (int l = 0; l < nbuf; ++l) {
     const std::string sfx = l ? "_1" : "";
     beta_l[l] = ws<double>(c, "beta" + sfx, (size_t)(n + 16) * mpmax);
     alpha_l[l] = ws<double>(c, "alpha" + sfx, (size_t)n);
@@ -445,68 +458,104 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     HIPCHECK(hipEventRecord(c->ev_fork, c->stream));
     HIPCHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
   }
-  for (int i = 0; i < np; ++i) {
+  std::vector<GainsOut> gi(np);
+  auto alpha_of = [&](int i) { return shared ? alpha_all + (size_t)i * n : alpha_l[i % nbuf]; };
+  // Kfu assembly + whitening of output i into buffer i % nbuf, on c->stream
+  auto whiten_stage = [&](int i) {
     const DevProblem& p = P[i];
-    const int lane = i % nlanes;
-    OnStream on_(c, lane ? c->side : c->main);
-    const std::string sfx = lane ? "_1" : "";
-    double* beta = beta_l[lane];
-    double* alpha = shared ? alpha_all + (size_t)i * n : alpha_l[lane];
-    double* send = send_l[lane];
-    double* cin = cin_l[lane];
-    double* hsum = hsum_l[lane];
-    double* qv = qv_l[lane];
-    GainsOut g;
+    const int b = i % nbuf;
+    const std::string sfx = b ? "_1" : "";
     if (shared) {
-      g = gains[i];
+      gi[i] = gains[i];
     } else {
       std::vector<ChainParamsHost> cps(1);
       cps[0] = {1.0 / th[i].l_t, th[i].l_t, th[i].sv_t * th[i].sv_t, th[i].sigma * th[i].sigma};
-      g = run_gains(c, p.sdim, p.t, n, cps, nullptr, false, "fit1" + sfx);
-      HIPCHECK(hipMemcpyAsync(o.logs + (size_t)i * nch, g.logs, nch * sizeof(double),
+      gi[i] = run_gains(c, p.sdim, p.t, n, cps, nullptr, false, "fit1" + sfx);
+      HIPCHECK(hipMemcpyAsync(o.logs + (size_t)i * nch, gi[i].logs, nch * sizeof(double),
                               hipMemcpyDeviceToDevice, c->stream));
     }
-    const double s_o = th[i].sv_o * th[i].sv_o;
-    {
-      // algorithmic HBM bytes: the inputs (V, or the cached distances), the gains records and
-      // fix-up rows (16 + 4 doubles per step), beta written (m columns)
-      const double in_cols = p.d2 ? (double)p.m : (double)p.d;
-      Timed tm_(c, "whiten", 8.0 * (double)n * (in_cols + (double)p.m + 20.0));
-      whiten_kfu_any(c, p, g.rec, p.v, p.ldv, n, nch, th[i], beta, p.mp, send, g.g, hsum);
-    }
+    // algorithmic HBM bytes: the inputs (V, or the cached distances), the gains records and
+    // fix-up rows (16 + 4 doubles per step), beta written (m columns)
+    const double in_cols = p.d2 ? (double)p.m : (double)p.d;
+    Timed tm_(c, "whiten", 8.0 * (double)n * (in_cols + (double)p.m + 20.0));
+    whiten_kfu_any(c, p, gi[i].rec, p.v, p.ldv, n, nch, th[i], beta_l[b], p.mp, send_l[b], gi[i].g,
+                   hsum_l[b]);
     check_launch("whiten_kfu");
+  };
+  // the short chain between output i's whitening and its Gram, on c->stream
+  auto post_stage = [&](int i) {
+    const DevProblem& p = P[i];
+    const int b = i % nbuf;
+    const std::string sfx = b ? "_1" : "";
+    double* send = send_l[b];
     if (shared) {   // alpha's chunk end states -> column mp of the carry input
       HIPCHECK(hipMemcpy2DAsync(send + (size_t)p.mp * kSStride, (size_t)p.mc * kSStride * sizeof(double),
                                 asend_all + (size_t)i * nch * kSStride, kSStride * sizeof(double),
                                 kSStride * sizeof(double), nch, hipMemcpyDeviceToDevice, c->stream));
     } else {
-      launch_whiten_vec(c->stream, p.sdim, g.rec, 0, p.y, 0, n, kChunk, nch, 1, alpha, 0, send, 0,
-                        p.mc, p.mp);
+      launch_whiten_vec(c->stream, p.sdim, gi[i].rec, 0, p.y, 0, n, kChunk, nch, 1, alpha_of(i), 0,
+                        send, 0, p.mc, p.mp);
     }
     check_launch("whiten_vec");
-    run_carry(c, p.sdim, g.phi, 0, send, cin, 0, nch, p.mc, p.mc, 1, "fitc" + sfx);
+    run_carry(c, p.sdim, gi[i].phi, 0, send, cin_l[b], 0, nch, p.mc, p.mc, 1, "fitc" + sfx);
     check_launch("carry");
     // alpha fix-up, plus the Gram's chunk correction E_j = H_j + W_j C_j / 2 and q_j
-    launch_vec_fix(c->stream, p.sdim, alpha, 0, g.g, 0, cin, 0, p.mc, p.mp, n, kChunk, 1,
-                   o.a2part + (size_t)i * npart, fix_beta ? nullptr : hsum, p.mp, qv);
+    launch_vec_fix(c->stream, p.sdim, alpha_of(i), 0, gi[i].g, 0, cin_l[b], 0, p.mc, p.mp, n, kChunk,
+                   1, o.a2part + (size_t)i * npart, fix_beta ? nullptr : hsum_l[b], p.mp, qv_l[b]);
     check_launch("vec_fix");
     if (fix_beta) {
-      launch_beta_fix(c->stream, p.sdim, beta, p.mp, n, g.g, cin, p.mc, kChunk);
+      launch_beta_fix(c->stream, p.sdim, beta_l[b], p.mp, n, gi[i].g, cin_l[b], p.mc, kChunk);
       check_launch("beta_fix");
     }
+    HIPCHECK(hipMemsetAsync(beta_l[b] + (size_t)n * p.mp, 0, (size_t)16 * p.mp * sizeof(double), c->stream));
+  };
+  auto gram_stage = [&](int i) {
+    const DevProblem& p = P[i];
+    const int b = i % nbuf;
+    const std::string sfx = (nlanes > 1 && b) ? "_1" : "";
     // two lanes: one Gram workgroup per CU, so the other lane's whitening runs beside it
     GramPlan plan = gram_plan(n, p.mp, nlanes > 1);
     double* part = ws<double>(c, "gram_part" + sfx, (size_t)plan.part_doubles);
     double* rpart = ws<double>(c, "gram_rpart" + sfx, (size_t)plan.rpart_doubles);
-    HIPCHECK(hipMemsetAsync(beta + (size_t)n * p.mp, 0, (size_t)16 * p.mp * sizeof(double), c->stream));
     {
       Timed tm_(c, "gram", (double)n * (double)p.m * (double)(p.m + 1));   // flops of beta^T beta
-      launch_gram(c->stream, p.sdim, plan, beta, p.mp, n, fix_beta ? nullptr : hsum, cin, qv,
-                  p.mc, kChunk, alpha, part, rpart, o.G + (size_t)i * mpmax * mpmax, mpmax,
-                  o.r + (size_t)i * mpmax, nlanes == 1 ? c->side : nullptr, c->ev_fork,
+      launch_gram(c->stream, p.sdim, plan, beta_l[b], p.mp, n, fix_beta ? nullptr : hsum_l[b], cin_l[b],
+                  qv_l[b], p.mc, kChunk, alpha_of(i), part, rpart, o.G + (size_t)i * mpmax * mpmax,
+                  mpmax, o.r + (size_t)i * mpmax, nlanes == 1 ? c->side : nullptr, c->ev_fork,
                   c->ev_join);
     }
     check_launch("gram");
+  };
+  if (pipe) {
+    // main: W0 W1 G0 W2 G1 W3 G2 ...; side: P0 after W0, P(i+1) after G(i), so P(i+1) runs beside
+    // W(i+2) and G(i+1) waits for it.  (P(i+1) right after W(i+1) would start with G(i) and queue
+    // G(i)'s co-running correction behind it on the side stream: 4.17 -> 4.93 ms per Gram.)
+    auto issue_post = [&](int i) {
+      HIPCHECK(hipEventRecord(c->ev_pw, c->main));
+      HIPCHECK(hipStreamWaitEvent(c->side, c->ev_pw, 0));
+      {
+        OnStream on_(c, c->side);
+        post_stage(i);
+      }
+      HIPCHECK(hipEventRecord(c->ev_pc[i & 1], c->side));
+    };
+    whiten_stage(0);
+    issue_post(0);
+    for (int i = 0; i < np; ++i) {
+      if (i + 1 < np) whiten_stage(i + 1);
+      HIPCHECK(hipStreamWaitEvent(c->main, c->ev_pc[i & 1], 0));
+      gram_stage(i);
+      if (i + 1 < np) issue_post(i + 1);
+    }
+    // every side-stream item has been waited for: P(np-1) by G(np-1), the corrections by their Gram
+    return o;
+  }
+  for (int i = 0; i < np; ++i) {
+    const int lane = i % nlanes;
+    OnStream on_(c, lane ? c->side : c->main);
+    whiten_stage(i);
+    post_stage(i);
+    gram_stage(i);
   }
   if (nlanes > 1) {   // join: the dense tail on the context stream needs every G
     HIPCHECK(hipEventRecord(c->ev_join, c->side));
@@ -1001,11 +1050,15 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
       hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&c->ev_input, hipEventDisableTiming) != hipSuccess) {
+      hipEventCreateWithFlags(&c->ev_input, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_pw, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_pc[0], hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&c->ev_pc[1], hipEventDisableTiming) != hipSuccess) {
     delete c;
     return GPAR_ERR_HIP;
   }
   c->stream = c->main;
+  if (const char* e = std::getenv("GPAR_PIPELINE")) c->pipeline = std::atoi(e) != 0;
   *out = c;
   return GPAR_OK;
 }
@@ -1020,6 +1073,9 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev_fork);
   (void)hipEventDestroy(ctx->ev_join);
   (void)hipEventDestroy(ctx->ev_input);
+  (void)hipEventDestroy(ctx->ev_pw);
+  (void)hipEventDestroy(ctx->ev_pc[0]);
+  (void)hipEventDestroy(ctx->ev_pc[1]);
   (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->main);
   delete ctx;
