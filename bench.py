@@ -76,6 +76,9 @@ def main():
                     help="HIP streams a batched objective alternates outputs over (gpar_ctx_set_lanes); "
                          "2 overlaps one output's whitening with another's Gram (+2%% throughput, but "
                          "per-launch kernel durations then include the sharing)")
+    ap.add_argument("--cu-split", type=int, default=None,
+                    help="CUs per XCD that whiten beside the Gram in the batched fit "
+                         "(gpar_ctx_set_cu_split; default: the library's, 8); 0 = whole-chip kernels")
     ap.add_argument("--inference", default="given", choices=["given", "chained"],
                     help="test inputs of output p: 'given' = the noiseless previous outputs at t* "
                          "(GPAR_scaled_examples.jl:139); 'chained' = output 1's true values and the "
@@ -189,6 +192,9 @@ def main():
 
     ctx = G.context(local)
     ctx.set_lanes(args.lanes)
+    if args.cu_split is not None:
+        ctx.set_cu_split(args.cu_split)
+    cu_split = ctx.cu_split()
     chained = args.inference == "chained" and not temporal
     if chained:
         # inference inputs: column 0 = output 1's true values at t*, column p-1 = output p's
@@ -314,7 +320,7 @@ def main():
                        "out_kernel": cfg["out_kernel"], "time_kernel": "matern52",
                        "parallelism": f"outputs sharded over {world} GPU(s)",
                        "outputs_per_rank": shards, "inference": args.inference,
-                       "inputs": args.inputs},
+                       "inputs": args.inputs, "cu_split": cu_split},
             **({"rehearsal": "all ranks on one GPU over gloo: not a scaling measurement"}
                if args.rehearse else {}),
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
@@ -322,8 +328,8 @@ def main():
                          "traffic": traffic, "kernel": "Gram beta^T beta + beta^T alpha, fp64 MFMA (v3: gram3_off + gram3_dg + gram3_corr + gram3_reduce per launch; lanes=2: gram2)",
                          "note": "avg_ms spans one Gram launch (HIP events): gram3_off_kernel, then "
                                  "gram3_dg_kernel and gram3_reduce; gram3_corr_slim_kernel runs "
-                                 "concurrently with gram3_off_kernel on a second stream, so rocprof's "
-                                 "averages of the three sequential kernels add up to avg_ms",
+                                 "concurrently with gram3_off_kernel on a second stream (and with "
+                                 "cu_split, part of gram3_dg_kernel on the whitening CUs)",
                          "launches": gram_n, "avg_ms": avg, "flops_per_launch": flops,
                          "lanes": args.lanes},
             "kernels": {"gram_ms_per_step": gram_ms / args.steps, "whiten_ms_per_step": wh_ms / args.steps,
@@ -344,6 +350,22 @@ def main():
             floor_ms = gram_work / args.steps / (FP64_MFMA_PEAK_TFLOPS * 1e12) * 1e3
             out["job_vs_gram_floor"] = {"floor_ms_per_step": floor_ms, "frac": floor_ms / el,
                                         "note": "Gram launches of one step at 78.6 TF/s / measured step"}
+        if cu_split and args.lanes == 1 and gram_n and wh_n:
+            # CU split: the fit's Gram runs on (32 - w) of every XCD's 32 CUs, the whitening on
+            # the other w, concurrently; the fractions above are against the whole chip's peaks
+            share = (32 - cu_split) / 32.0
+            out["roofline"]["cu_split"] = {
+                "gram_cus": 8 * (32 - cu_split), "whiten_cus": 8 * cu_split,
+                "frac_vs_masked_peak": out["roofline"]["frac"] / share,
+                "note": f"the fit's Gram launches run on {8 * (32 - cu_split)} CUs while the next "
+                        f"output's whitening runs on the other {8 * cu_split} (CU-masked streams); "
+                        f"{cu_split}/32 of the Gram's diagonal-block items run on the whitening CUs "
+                        "after it, so avg_ms spans the whole Gram including that share, and "
+                        "frac_vs_masked_peak (peak x the Gram's CU share) is an upper bound; "
+                        "the prediction's Gram-free kernels and q(u) use the whole chip"}
+            out["roofline_whiten"]["note"] = (
+                f"fit launches run on {8 * cu_split} of 256 CUs beside the Gram (HBM shared), "
+                "so per-launch time is not the whole-chip kernel's")
         if args.lanes > 1 and out["roofline"]:
             # two streams overlap launches: event spans are not the kernel's own duration
             out["roofline"].update(achieved=None, frac=None,

@@ -6,6 +6,7 @@
 #include "gpar_hip.h"
 
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <algorithm>
 #include <cmath>
@@ -28,6 +29,12 @@ struct gpar_ctx {
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_pw = nullptr, ev_pc[2] = {nullptr, nullptr};   // the fit's pipelined Gram stage
   bool pipeline = true;           // GPAR_PIPELINE=0 turns the pipelined Gram stage off (A/B)
+  // gpar_ctx_set_cu_split(w): the pipelined fit's whitening runs on w CUs of every XCD and the
+  // Gram (its co-running correction too) on the other 32 - w, concurrently (CU-masked streams)
+  int split_w = 0, split_mask_w = 0;
+  bool split_dgw = true;          // a w/32 share of the DG items on the whitening CUs
+  hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr;
+  hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
   // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
   // the caller's stream, e.g. the copies that produce its device inputs
   bool has_input_stream = false;
@@ -169,6 +176,9 @@ static_assert(kChunk == 256, "vec_fix runs one 256-thread block per chunk");
 constexpr int kSStride = 4;   // chunk state vectors padded to 4 doubles (device_common.hpp)
 constexpr int64_t kFusedMaxD = 64;   // widest input the fused Kfu + whitening kernels take
 constexpr int64_t kPipeMaxBetaBytes = (int64_t)8 << 30;   // second beta buffer of the pipelined fit
+// default gpar_ctx_set_cu_split width: 8 of every XCD's 32 CUs whiten beside the Gram (north job
+// 20.66 -> 19.69 s per job in same-box pairs; 4 starves the whitening: 28.4 s)
+constexpr int kDefaultCuSplit = 8;
 
 static int sde_dim(int kind) {
   if (kind == GPAR_MATERN12) return 1;
@@ -509,23 +519,63 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     }
     HIPCHECK(hipMemsetAsync(beta_l[b] + (size_t)n * p.mp, 0, (size_t)16 * p.mp * sizeof(double), c->stream));
   };
-  auto gram_stage = [&](int i) {
+  // cus: the CUs c->stream may use; st_w: the first w_frac32 / 32 of the DG kernel's work items
+  // run there (ev_w joins them)
+  auto gram_stage = [&](int i, hipStream_t side, int cus, hipStream_t st_w = nullptr,
+                        hipEvent_t ev_w = nullptr, int w_frac32 = 0) {
     const DevProblem& p = P[i];
     const int b = i % nbuf;
     const std::string sfx = (nlanes > 1 && b) ? "_1" : "";
     // two lanes: one Gram workgroup per CU, so the other lane's whitening runs beside it
-    GramPlan plan = gram_plan(n, p.mp, nlanes > 1);
+    GramPlan plan = gram_plan(n, p.mp, nlanes > 1, cus, st_w ? 256 : cus);
+    const int w_items = st_w ? plan.ndg * plan.sdg * w_frac32 / 32 : 0;
     double* part = ws<double>(c, "gram_part" + sfx, (size_t)plan.part_doubles);
     double* rpart = ws<double>(c, "gram_rpart" + sfx, (size_t)plan.rpart_doubles);
     {
       Timed tm_(c, "gram", (double)n * (double)p.m * (double)(p.m + 1));   // flops of beta^T beta
       launch_gram(c->stream, p.sdim, plan, beta_l[b], p.mp, n, fix_beta ? nullptr : hsum_l[b], cin_l[b],
                   qv_l[b], p.mc, kChunk, alpha_of(i), part, rpart, o.G + (size_t)i * mpmax * mpmax,
-                  mpmax, o.r + (size_t)i * mpmax, nlanes == 1 ? c->side : nullptr, c->ev_fork,
-                  c->ev_join);
+                  mpmax, o.r + (size_t)i * mpmax, side, c->ev_fork, c->ev_join, st_w, ev_w,
+                  w_items);
     }
     check_launch("gram");
   };
+  if (pipe && c->split_w) {
+    // Whitening + short chain on w CUs of every XCD (s_w), concurrently with the Gram on the other
+    // 32 - w (s_g, its co-running correction on s_g2): W(i+1) P(i+1) beside G(i).  A w/32 share of
+    // G(i)'s DG items runs on s_w after P(i+1), so both sides end together.  W(i+1) waits for
+    // G(i-1) (same buffers), G(i) for P(i), and s_w's DG share of G(i) for G(i-1)'s reduction
+    // (the partial slots are reused).
+    const int gcus = 8 * (32 - c->split_w);
+    HIPCHECK(hipEventRecord(c->ev_sp, c->main));
+    HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_sp, 0));
+    HIPCHECK(hipStreamWaitEvent(c->s_g, c->ev_sp, 0));
+    HIPCHECK(hipStreamWaitEvent(c->s_g2, c->ev_sp, 0));
+    auto wp = [&](int i) {
+      OnStream on_(c, c->s_w);
+      if (i >= 2) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[i & 1], 0));
+      whiten_stage(i);
+      post_stage(i);
+      HIPCHECK(hipEventRecord(c->ev_pc[i & 1], c->s_w));
+    };
+    wp(0);
+    for (int i = 0; i < np; ++i) {
+      if (i + 1 < np) wp(i + 1);
+      OnStream on_(c, c->s_g);
+      HIPCHECK(hipStreamWaitEvent(c->s_g, c->ev_pc[i & 1], 0));
+      if (c->split_dgw) {
+        if (i >= 1) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[(i - 1) & 1], 0));
+        gram_stage(i, c->s_g2, gcus, c->s_w, c->ev_pw, c->split_w);
+      } else {
+        gram_stage(i, c->s_g2, gcus);
+      }
+      HIPCHECK(hipEventRecord(c->ev_gd[i & 1], c->s_g));
+    }
+    // the last Gram follows every P, DG share and correction: the context stream joins s_g
+    HIPCHECK(hipEventRecord(c->ev_sp, c->s_g));
+    HIPCHECK(hipStreamWaitEvent(c->main, c->ev_sp, 0));
+    return o;
+  }
   if (pipe) {
     // main: W0 W1 G0 W2 G1 W3 G2 ...; side: P0 after W0, P(i+1) after G(i), so P(i+1) runs beside
     // W(i+2) and G(i+1) waits for it.  (P(i+1) right after W(i+1) would start with G(i) and queue
@@ -544,7 +594,7 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     for (int i = 0; i < np; ++i) {
       if (i + 1 < np) whiten_stage(i + 1);
       HIPCHECK(hipStreamWaitEvent(c->main, c->ev_pc[i & 1], 0));
-      gram_stage(i);
+      gram_stage(i, c->side, 256);
       if (i + 1 < np) issue_post(i + 1);
     }
     // every side-stream item has been waited for: P(np-1) by G(np-1), the corrections by their Gram
@@ -555,7 +605,7 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     OnStream on_(c, lane ? c->side : c->main);
     whiten_stage(i);
     post_stage(i);
-    gram_stage(i);
+    gram_stage(i, nlanes == 1 ? c->side : nullptr, 256);
   }
   if (nlanes > 1) {   // join: the dense tail on the context stream needs every G
     HIPCHECK(hipEventRecord(c->ev_join, c->side));
@@ -1014,6 +1064,8 @@ static int fail(gpar_ctx* c, int code, const char* what) {
   c->stream = c->main;
   (void)hipStreamSynchronize(c->main);
   (void)hipStreamSynchronize(c->side);
+  for (hipStream_t st : {c->s_w, c->s_g, c->s_g2})
+    if (st) (void)hipStreamSynchronize(st);
   (void)hipGetLastError();
   return code;
 }
@@ -1032,6 +1084,34 @@ static int fail(gpar_ctx* c, int code, const char* what) {
     return fail((ctx), GPAR_ERR_HIP, e.what());                 \
   }                                                             \
   return GPAR_OK;
+
+// CU split of the pipelined fit (gpar_ctx_set_cu_split): CU-masked streams for the whitening
+// (mask bits [0, 8w): bit i is a CU of XCD i % 8, the bits of one XCD walk its four SEs in turn,
+// tools/ubench/cumask_probe.cpp) and for the Gram (the other bits).  w a multiple of 4 keeps every
+// SE of both sides equally wide: workgroups are dealt to the SEs evenly, so an SE with fewer CUs
+// than its neighbours sets the pace (w = 6 measured slower than w = 4).
+static int set_cu_split(gpar_ctx* c, int w) {
+  if (w < 0 || w >= 32 || w % 4) return GPAR_ERR_ARG;
+  if (w > 0 && !c->s_w) {
+    hipDeviceProp_t pr;
+    if (hipGetDeviceProperties(&pr, c->device) != hipSuccess) return GPAR_ERR_HIP;
+    if (pr.multiProcessorCount != 256) return GPAR_ERR_UNSUPPORTED;   // the MI355X layout only
+    uint32_t mw[8] = {0}, mg[8] = {0};
+    for (int i = 0; i < 256; ++i) (i < 8 * w ? mw : mg)[i / 32] |= 1u << (i % 32);
+    // the masks are fixed per stream: the split streams carry w's mask from their creation
+    if (hipExtStreamCreateWithCUMask(&c->s_w, 8, mw) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&c->s_g, 8, mg) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&c->s_g2, 8, mg) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gd[0], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_gd[1], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_sp, hipEventDisableTiming) != hipSuccess)
+      return GPAR_ERR_HIP;
+    c->split_mask_w = w;
+  }
+  if (w > 0 && w != c->split_mask_w) return GPAR_ERR_ARG;   // one split width per context
+  c->split_w = w;
+  return GPAR_OK;
+}
 
 extern "C" {
 
@@ -1059,6 +1139,11 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
   }
   c->stream = c->main;
   if (const char* e = std::getenv("GPAR_PIPELINE")) c->pipeline = std::atoi(e) != 0;
+  // A/B knobs: GPAR_SPLIT_CUS overrides the default CU split, GPAR_SPLIT_DGW=0 keeps the DG
+  // kernel off the whitening CUs
+  if (const char* e = std::getenv("GPAR_SPLIT_DGW")) c->split_dgw = std::atoi(e) != 0;
+  const char* e_split = std::getenv("GPAR_SPLIT_CUS");
+  (void)set_cu_split(c, e_split ? std::atoi(e_split) : kDefaultCuSplit);   // 0 where unsupported
   *out = c;
   return GPAR_OK;
 }
@@ -1076,6 +1161,15 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev_pw);
   (void)hipEventDestroy(ctx->ev_pc[0]);
   (void)hipEventDestroy(ctx->ev_pc[1]);
+  if (ctx->s_w) {
+    for (hipStream_t st : {ctx->s_w, ctx->s_g, ctx->s_g2})
+      if (st) {
+        (void)hipStreamSynchronize(st);
+        (void)hipStreamDestroy(st);
+      }
+    for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp})
+      if (ev) (void)hipEventDestroy(ev);
+  }
   (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->main);
   delete ctx;
@@ -1139,6 +1233,23 @@ int32_t gpar_ctx_set_lanes(gpar_ctx* ctx, int32_t lanes) {
     return GPAR_ERR_ARG;
   }
   ctx->lanes = lanes;
+  return GPAR_OK;
+}
+
+int32_t gpar_ctx_set_cu_split(gpar_ctx* ctx, int32_t cus_per_xcd) {
+  if (!ctx) return GPAR_ERR_STATE;
+  (void)hipSetDevice(ctx->device);
+  const int rc = set_cu_split(ctx, cus_per_xcd);
+  if (rc != GPAR_OK)
+    ctx->err = "gpar_ctx_set_cu_split: cus_per_xcd must be 0 or a multiple of 4 below 32 (one "
+               "nonzero width per context, 256-CU devices)";
+  return rc;
+}
+
+int32_t gpar_ctx_get_cu_split(const gpar_ctx* ctx, int32_t* cus_per_xcd) {
+  if (!ctx) return GPAR_ERR_STATE;
+  if (!cus_per_xcd) return GPAR_ERR_ARG;
+  *cus_per_xcd = ctx->split_w;
   return GPAR_OK;
 }
 

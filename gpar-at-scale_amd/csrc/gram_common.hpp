@@ -41,7 +41,7 @@ constexpr int kF3T = 32;
 // v3 launchers living in k_gram3v.hip (VGPR-form MFMA accumulators)
 void launch_gram3_dg(hipStream_t st, int nwg, const double* beta, int64_t ldb, int64_t n,
                      const double* alpha, int npan, int ndg, int sdg, int64_t rows,
-                     int64_t slot0, double* part, double* rpart);
+                     int64_t slot0, double* part, double* rpart, int bt_lo = 0, int bt_cnt = -1);
 void launch_gram3_corr_slim(hipStream_t st, int sdim, const double* ecor, const double* cin,
                             const double* qv, int64_t mc, int64_t nch, int npan, int noff, int ndg,
                             int soff, int sdg, int ncs, double* part, double* rpart);

@@ -1010,7 +1010,7 @@ static void gram2_plan(int64_t n, int64_t mp, GramPlan& p, bool one_per_cu) {
 
 // v3: split counts for OFF (32 tiles per wave) and DG (18 tiles per wave, one diagonal block per
 // workgroup), two launches of up to 512 workgroups each (two per CU, one wave per SIMD).
-static void gram3_plan(int64_t n, int64_t mp, GramPlan& p) {
+static void gram3_plan(int64_t n, int64_t mp, GramPlan& p, int cus, int dg_cus) {
   const int nbk = (int)(mp / 128);
   p.v2 = 1;
   p.v3 = 1;
@@ -1027,20 +1027,20 @@ static void gram3_plan(int64_t n, int64_t mp, GramPlan& p) {
     if (sp > maxs) sp = (int)maxs;
     return sp;
   };
-  p.soff = p.noff ? splits(p.noff, 512) : 0;
+  p.soff = p.noff ? splits(p.noff, 2 * cus) : 0;
   // DG (238 VGPRs, 33 KB LDS) runs two waves per SIMD: 1024 slots
-  p.sdg = splits(p.ndg, GRAM3_DG_SLOTS);
+  p.sdg = splits(p.ndg, GRAM3_DG_SLOTS * dg_cus / 256);
   p.rows_off = p.noff ? rows_of(p.soff) : 0;
   p.rows_dg = rows_of(p.sdg);
   p.nsplit = p.sdg;
   // chunk-correction splits: (noff + ndg) x ncs four-wave workgroups, two per CU
   const int64_t nch = (n + 255) / 256;
-  int ncs = 512 / (p.noff + p.ndg);
+  int ncs = 2 * cus / (p.noff + p.ndg);
   if (ncs < 1) ncs = 1;
   if (ncs > nch) ncs = (int)(nch > 0 ? nch : 1);
   p.ncs = ncs;
   // co-run: the slim correction's 8 waves per (group, split), at most one per SIMD beside OFF
-  int ncs2 = 1024 / (8 * (p.noff + p.ndg));
+  int ncs2 = 4 * cus / (8 * (p.noff + p.ndg));
   if (ncs2 < 1) ncs2 = 1;
   if (ncs2 > nch) ncs2 = (int)(nch > 0 ? nch : 1);
   p.ncs_slim = ncs2;
@@ -1049,11 +1049,11 @@ static void gram3_plan(int64_t n, int64_t mp, GramPlan& p) {
   p.rpart_doubles = (int64_t)(p.sdg + nc) * mp;
 }
 
-GramPlan gram_plan(int64_t n, int64_t mp, bool one_per_cu) {
+GramPlan gram_plan(int64_t n, int64_t mp, bool one_per_cu, int cus, int dg_cus) {
   GramPlan p;
   if (!GRAM_V1) {
     if (GRAM_V3 && !one_per_cu)
-      gram3_plan(n, mp, p);
+      gram3_plan(n, mp, p, cus, dg_cus > 0 ? dg_cus : cus);
     else
       gram2_plan(n, mp, p, one_per_cu);
     return p;
@@ -1093,7 +1093,8 @@ GramPlan gram_plan(int64_t n, int64_t mp, bool one_per_cu) {
 void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* beta,
                  int64_t ldb, int64_t n, const double* ecor, const double* cin, const double* qv,
                  int64_t mc, int L, const double* alpha, double* part, double* rpart, double* G,
-                 int64_t ldg, double* r, hipStream_t side, hipEvent_t ev_a, hipEvent_t ev_b) {
+                 int64_t ldg, double* r, hipStream_t side, hipEvent_t ev_a, hipEvent_t ev_b,
+                 hipStream_t st_w, hipEvent_t ev_w, int w_items) {
   if (plan.v3) {
     const bool corun = GRAM3_CORUN && ecor && side && plan.noff > 0;
     const int ncs = ecor ? (corun ? plan.ncs_slim : plan.ncs) : 0;
@@ -1109,8 +1110,18 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
     if (corun)
       launch_gram3_corr_slim(side, sdim, ecor, cin, qv, mc, nchk, plan.npan, plan.noff, plan.ndg,
                              plan.soff, plan.sdg, ncs, part, rpart);
-    launch_gram3_dg(st, ndgw, beta, ldb, n, alpha, plan.npan, plan.ndg, plan.sdg, plan.rows_dg,
-                    (int64_t)plan.noff * (plan.soff + ncs), part, rpart);
+    const int64_t dslot0 = (int64_t)plan.noff * (plan.soff + ncs);
+    if (st_w && w_items > 0) {   // the first w_items DG items on another stream (other CUs)
+      launch_gram3_dg(st_w, 0, beta, ldb, n, alpha, plan.npan, plan.ndg, plan.sdg, plan.rows_dg,
+                      dslot0, part, rpart, 0, w_items);
+      HIPCHECK_G(hipEventRecord(ev_w, st_w));
+      launch_gram3_dg(st, 0, beta, ldb, n, alpha, plan.npan, plan.ndg, plan.sdg, plan.rows_dg,
+                      dslot0, part, rpart, w_items, -1);
+      HIPCHECK_G(hipStreamWaitEvent(st, ev_w, 0));
+    } else {
+      launch_gram3_dg(st, ndgw, beta, ldb, n, alpha, plan.npan, plan.ndg, plan.sdg, plan.rows_dg,
+                      dslot0, part, rpart);
+    }
     if (corun) {
       HIPCHECK_G(hipEventRecord(ev_b, side));
       HIPCHECK_G(hipStreamWaitEvent(st, ev_b, 0));

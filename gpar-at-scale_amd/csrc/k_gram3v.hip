@@ -14,14 +14,15 @@ namespace gpar {
 __global__ __launch_bounds__(128) void gram3_dg_kernel(
     const double* __restrict__ beta, int64_t ldb, int64_t n, const double* __restrict__ alpha,
     int npan, int ndg, int sdg, int64_t rows, int64_t slot0, double* __restrict__ part,
-    double* __restrict__ rpart) {
+    double* __restrict__ rpart, int bt_lo, int bt_cnt) {
   __shared__ __attribute__((aligned(16))) double smem[4 * kPanelD + 2 * 2 * kBK];
   double* ringa = smem + 4 * kPanelD;
 
-  const int nty = ndg * sdg;
-  const int per = (nty + 7) >> 3;
-  const int bt = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);   // XCD-major deal
-  if (bt >= nty) return;
+  // work items [bt_lo, bt_lo + bt_cnt) of the ndg x sdg (group, split) items
+  const int per = (bt_cnt + 7) >> 3;
+  const int lb = ((int)blockIdx.x & 7) * per + ((int)blockIdx.x >> 3);   // XCD-major deal
+  if (lb >= bt_cnt) return;
+  const int bt = bt_lo + lb;
   const int gid = bt % ndg, split = bt / ndg;
 
   const int tid = threadIdx.x;
@@ -409,9 +410,12 @@ void launch_gram3_corr_slim(hipStream_t st, int sdim, const double* ecor, const 
 
 void launch_gram3_dg(hipStream_t st, int nwg, const double* beta, int64_t ldb, int64_t n,
                      const double* alpha, int npan, int ndg, int sdg, int64_t rows,
-                     int64_t slot0, double* part, double* rpart) {
+                     int64_t slot0, double* part, double* rpart, int bt_lo, int bt_cnt) {
+  if (bt_cnt < 0) bt_cnt = ndg * sdg - bt_lo;
+  if (bt_cnt <= 0) return;
+  if (nwg <= 0) nwg = ((bt_cnt + 7) / 8) * 8;
   gram3_dg_kernel<<<nwg, 128, 0, st>>>(beta, ldb, n, alpha, npan, ndg, sdg, rows, slot0, part,
-                                       rpart);
+                                       rpart, bt_lo, bt_cnt);
 }
 
 void launch_gram3_corr(hipStream_t st, int sdim, const double* ecor, const double* cin,

@@ -166,13 +166,16 @@ void launch_chain_lml(hipStream_t st, const double* logs, int64_t nch, const dou
                       int64_t npart, int64_t n, int nchains, double* lml);
 
 // k_gram.hip
-GramPlan gram_plan(int64_t n, int64_t mp, bool one_per_cu = false);
+// cus: the CUs the Gram's stream may use (v3 plan; 256 = the whole chip)
+// dg_cus: the CUs the v3 DG kernel's items are planned for (0: cus)
+GramPlan gram_plan(int64_t n, int64_t mp, bool one_per_cu = false, int cus = 256, int dg_cus = 0);
 // ecor: E_j (nch x mc x 4, vec_fix), cin: C_j (carry), qv: q_j (nch x 4, vec_fix)
 void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* beta,
                  int64_t ldb, int64_t n, const double* ecor, const double* cin, const double* qv,
                  int64_t mc, int L, const double* alpha, double* part, double* rpart, double* G,
                  int64_t ldg, double* r, hipStream_t side = nullptr,
-                 hipEvent_t ev_a = nullptr, hipEvent_t ev_b = nullptr);
+                 hipEvent_t ev_a = nullptr, hipEvent_t ev_b = nullptr,
+                 hipStream_t st_w = nullptr, hipEvent_t ev_w = nullptr, int w_items = 0);
 void launch_beta_fix(hipStream_t st, int sdim, double* beta, int64_t ldb, int64_t n,
                      const double* g, const double* cin, int64_t mc, int L);
 

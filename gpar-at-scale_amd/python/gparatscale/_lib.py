@@ -27,7 +27,7 @@ EXPORTED = (
     "gpar_fit", "gpar_fit_predict", "gpar_fit_predict_chain", "gpar_mc_normals", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
     "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_kernel_work", "gpar_ctx_reset_stats",
-    "gpar_ctx_set_lanes", "gpar_ctx_set_dist_cache", "gpar_ctx_set_input_stream", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
+    "gpar_ctx_set_lanes", "gpar_ctx_set_cu_split", "gpar_ctx_get_cu_split", "gpar_ctx_set_dist_cache", "gpar_ctx_set_input_stream", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
 )
 
 
@@ -96,6 +96,8 @@ def load(path: str | None = None):
             "gpar_ctx_reset_stats": (i32, [vp]),
             "gpar_ctx_kernel_work": (i32, [vp, C.c_char_p, C.POINTER(C.c_double)]),
             "gpar_ctx_set_lanes": (i32, [vp, i32]),
+            "gpar_ctx_set_cu_split": (i32, [vp, i32]),
+            "gpar_ctx_get_cu_split": (i32, [vp, C.POINTER(C.c_int32)]),
             "gpar_ctx_set_dist_cache": (i32, [vp, i64]),
             "gpar_ctx_set_input_stream": (i32, [vp, vp, i32]),
             "gpar_dtc_objective": (i32, [vp, C.POINTER(GparProblem), i32, dp, dp]),
@@ -223,6 +225,17 @@ class Context:
     def set_lanes(self, lanes):
         """1 (the default): serial batched evaluation; 2: outputs alternate over two HIP streams."""
         self.check(load().gpar_ctx_set_lanes(self.h, int(lanes)))
+
+    def set_cu_split(self, cus_per_xcd):
+        """CUs per XCD for the batched fit's whitening beside the Gram (0: whole-chip kernels)."""
+        self.check(load().gpar_ctx_set_cu_split(self.h, int(cus_per_xcd)))
+        self._cu_split = int(cus_per_xcd)
+
+    def cu_split(self):
+        """The CU split in effect (gpar_ctx_get_cu_split)."""
+        v = C.c_int32(0)
+        self.check(load().gpar_ctx_get_cu_split(self.h, C.byref(v)))
+        return int(v.value)
 
 
 _ctx: dict[int, Context] = {}

@@ -117,6 +117,16 @@ int32_t gpar_ctx_kernel_work(gpar_ctx* ctx, const char* name, double* work);
  * one output's whitening overlaps another's Gram (~1 % faster at N = 1e6, M = 512, two beta
  * buffers); 1 (the default) serialises them on the context stream. */
 int32_t gpar_ctx_set_lanes(gpar_ctx* ctx, int32_t lanes);
+/* CU split of the batched fit (one lane): with cus_per_xcd = w > 0, each output's Kfu assembly +
+ * whitening runs on w CUs of every XCD while the previous output's Gram runs on the other 32 - w
+ * (CU-masked HIP streams; a w/32 share of the Gram's diagonal-block work also goes to the
+ * whitening side).  w = 0: whole-chip kernels, one after the other.  w must be a multiple of 4
+ * below 32 (equal SE widths); one nonzero w per context.  Default 8 (0 on devices without 256
+ * CUs; the environment variable GPAR_SPLIT_CUS overrides the default at context creation).  Results are identical either way up to
+ * the Gram's split plan (deterministic for a given w).  256-CU devices only. */
+int32_t gpar_ctx_set_cu_split(gpar_ctx* ctx, int32_t cus_per_xcd);
+/* The CU split in effect (0 when off or unsupported). */
+int32_t gpar_ctx_get_cu_split(const gpar_ctx* ctx, int32_t* cus_per_xcd);
 /* Distance cache of gpar_fit / gpar_fit_predict: the squared input distances |v_k - z_c|^2 are
  * theta-independent, so for outputs with D >= 17 they are computed once per fit call (N x Mp
  * doubles per output, widest outputs first) and every objective evaluation's whitening reads them
