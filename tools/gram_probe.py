@@ -23,6 +23,9 @@ def main():
     ap.add_argument("--fit", action="store_true",
                     help="time gpar_fit (max_evals = --evals) instead of objective calls: the fit's "
                          "distance cache is used for D >= 17")
+    ap.add_argument("--batch", type=int, default=1,
+                    help="fit / evaluate this many copies of the output in one batched call (>= 2 "
+                         "runs the batched fit's pipelined, CU-split Gram stage)")
     a = ap.parse_args()
     import numpy as np
     import torch
@@ -50,27 +53,28 @@ def main():
         Z = Y[rows, : P - 1].contiguous()
     y = Y[:, P - 1].contiguous()
     pr, keep = G.make_problem(Y[:, : P - 1], Z, t, y, a.kernel, "matern52")
+    prs = [pr] * a.batch
     ctx = G.context(0)
-    theta = np.array([[1.0, 1.0, 1.0, 1.0, 0.2]])
+    theta = np.tile(np.array([[1.0, 1.0, 1.0, 1.0, 0.2]]), (a.batch, 1))
     def ev(th):
         try:
-            return G.dtc_objective_batch([pr], th)
+            return G.dtc_objective_batch(prs, th)
         except G.GparError:   # timing ablations (GPAR_LIB_PATH) compute garbage on purpose
             if not os.environ.get("GPAR_LIB_PATH"):
                 raise
             return [float("nan")]
 
     if a.fit:
-        x0 = np.array([[0.0, 0.0, 0.0, 0.0, -2.0]])
-        G.fit_batch([pr], x0, max_evals=2, g_tol=-1.0)
+        x0 = np.tile(np.array([[0.0, 0.0, 0.0, 0.0, -2.0]]), (a.batch, 1))
+        G.fit_batch(prs, x0, max_evals=2, g_tol=-1.0)
         ctx.set_profiling(True)
         ctx.reset_stats()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        fr = G.fit_batch([pr], x0, max_evals=a.evals, g_tol=-1.0)
+        fr = G.fit_batch(prs, x0, max_evals=a.evals, g_tol=-1.0)
         torch.cuda.synchronize()
         el = (time.perf_counter() - t0) * 1e3 / a.evals
-        out = [f"N={a.n} M={a.m} D={a.d} fit ms/eval={el:.3f} nlml={fr.nlml[0]:.6f}"]
+        out = [f"N={a.n} M={a.m} D={a.d} batch={a.batch} fit ms/eval={el:.3f} nlml={fr.nlml[0]:.6f}"]
         for k in ("gram", "whiten", "gains", "dense"):
             n, ms = ctx.kernel_stats(k)
             if n:

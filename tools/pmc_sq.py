@@ -20,9 +20,12 @@ def avg(x):
 
 
 def load(d):
-    """-> (counters, durations): k -> counter -> per-launch value, k -> per-launch seconds, where
-    a Gram "launch" is one launch_gram call (v3: gram3_off + gram3_dg + gram3_corr + gram3_reduce
-    dispatches; v2: gram2_kernel + gram2_reduce): per-kernel averages summed over its kernels."""
+    """-> (counters, durations, kernels): k -> counter -> per-launch value, k -> per-launch
+    seconds, where a Gram "launch" is one launch_gram call (v3: gram3_off + gram3_dg (one or two
+    dispatches: with the CU split a share runs on the whitening CUs) + gram3_corr + gram3_reduce;
+    v2: gram2_kernel + gram2_reduce) and a whitening launch one dispatch: each kernel's counters
+    summed over its dispatches, divided by the number of launches (the reduction's dispatches for
+    the Gram).  Under --pmc the dispatches are serialised, so the durations add."""
     per = defaultdict(lambda: defaultdict(float))   # (k, kernel, dispatch) -> counter -> value
     dur = {}
     for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
@@ -39,43 +42,43 @@ def load(d):
             per[key][r["Counter_Name"]] += float(r["Counter_Value"])
             if "Start_Timestamp" in r and r.get("End_Timestamp"):
                 dur[key] = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) * 1e-9
-    by = defaultdict(lambda: defaultdict(list))     # (k, kernel) -> counter -> [values]
+    disp = defaultdict(set)
+    for (k, sub, di) in per:
+        disp[(k, sub)].add(di)
+    nl = {}
+    for k in ("gram", "whiten"):
+        red = [len(v) for (kk, sub), v in disp.items() if kk == k and "reduce" in sub]
+        nl[k] = max(red) if red else sum(len(v) for (kk, _), v in disp.items() if kk == k)
+    out = defaultdict(lambda: defaultdict(float))
     for (k, sub, _), cs in per.items():
-        for c, v in cs.items():
-            by[(k, sub)][c].append(v)
-    dby = defaultdict(list)
-    for (k, sub, _), t in dur.items():
-        dby[(k, sub)].append(t)
-    out = defaultdict(lambda: defaultdict(list))
-    for (k, sub), cs in by.items():
         for c, v in cs.items():
             if "corr_slim" in sub and c.startswith("GRBM_"):
                 continue   # elapsed-cycle counter of a kernel that overlaps gram3_off_kernel
-            out[k][c].append(avg(v))                 # one entry per kernel: summed below
-    durs = defaultdict(list)
-    for (k, sub), ts in dby.items():
-        if "corr_slim" in sub:   # runs concurrently with gram3_off_kernel: adds no time
+            out[k][c] += v / nl[k]
+    durs = defaultdict(float)
+    for (k, sub, _), t in dur.items():
+        if "corr_slim" in sub:   # runs concurrently with gram3_off_kernel outside --pmc
             continue
-        durs[k].append(avg(ts))
+        durs[k] += t / nl[k]
     kernels = defaultdict(list)
-    for (k, sub) in by:
+    for (k, sub) in disp:
         kernels[k].append(sub)
-    return out, durs, kernels
+    return out, durs, kernels, nl
 
 
 def main(root):
     res = {"source": "tools/pmc_passes.sh: rocprofv3 --pmc passes over tools/gram_probe.py "
-                     f"--fit --evals 4 (N={N}, M={M}, D={D}; the whitening reads the fit's distance "
-                     "cache: whiten_kfu_d2x2); per-launch values: each kernel's per-dispatch "
-                     "average, summed over the kernels of one launch (Gram v3: OFF + DG + "
-                     "correction + reduction)"}
-    sq, dsq, kn = load(root + "/sq1")
-    fe, _, _ = load(root + "/fetch")
-    wr, _, _ = load(root + "/write")
+                     f"--fit --evals 4 --batch 3 (N={N}, M={M}, D={D}; the batched fit's CU-split "
+                     "Gram stage; the whitening reads the fit's distance cache: whiten_kfu_d2x2); "
+                     "per-launch values: counters summed over every dispatch of the family, divided "
+                     "by the launches (Gram v3: OFF + DG share(s) + correction + reduction)"}
+    sq, dsq, kn, nl = load(root + "/sq1")
+    fe, _, _, _ = load(root + "/fetch")
+    wr, _, _, _ = load(root + "/write")
     for k in ("gram", "whiten"):
-        c = {n: sum(v) for n, v in sq[k].items()}     # per launch, summed over its kernels
-        t = sum(dsq[k]) if dsq[k] else None
-        e = {"kernels": sorted(kn[k]), "counters": c, "kernel_s_under_pmc": t}
+        c = dict(sq[k])                                # per launch, summed over its kernels
+        t = dsq[k] or None
+        e = {"kernels": sorted(kn[k]), "launches": nl[k], "counters": c, "kernel_s_under_pmc": t}
         if t and c.get("GRBM_GUI_ACTIVE"):
             clk = c["GRBM_GUI_ACTIVE"] / 8 / t
             e["effective_clock_GHz"] = clk / 1e9
@@ -88,8 +91,8 @@ def main(root):
             e["wave_time_fraction"] = {"active_inst_any": c.get("SQ_ACTIVE_INST_ANY", 0) / w,
                                        "wait_inst_any (issue stall)": c.get("SQ_WAIT_INST_ANY", 0) / w,
                                        "wait_any (waitcnt/barrier)": c.get("SQ_WAIT_ANY", 0) / w}
-        f = sum(fe[k]["FETCH_SIZE"]) if fe[k].get("FETCH_SIZE") else None
-        wb = sum(wr[k]["WRITE_SIZE"]) if wr[k].get("WRITE_SIZE") else None
+        f = fe[k].get("FETCH_SIZE")
+        wb = wr[k].get("WRITE_SIZE")
         e["hbm_read_bytes"] = f * 1024 * 2 if f is not None else None
         e["hbm_write_bytes"] = wb * 1024 if wb is not None else None
         res[k] = e
