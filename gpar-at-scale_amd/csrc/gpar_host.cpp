@@ -1299,6 +1299,14 @@ struct FitKeep {
 // so outputs with D >= kDistCacheMinD are cached, widest first, while the budget lasts
 // (gpar_ctx_set_dist_cache; default: the free HBM less a reserve).  n x mp doubles each.
 constexpr int64_t kDistCacheMinD = 17;
+// With the CU split the whitening runs on a quarter of the chip, where the fused kernel is
+// compute-bound (D <= 16: 5.05 ms per launch on 64 CUs against 3.62 ms for the cached one), so a
+// batched fit over long series caches outputs down to D = 3 (the narrowest stay fused: they fit
+// last).  Short series (N < 2^16) keep the D >= 17 rule: there the fused kernel is latency-bound
+// either way, and the small-D fits then stay on the arithmetic a single-output q(u) recomputes
+// (gpar_fit_predict's reused Gram stays bit-identical to gpar_predict's).
+constexpr int64_t kDistCacheMinDSplit = 3;
+constexpr int64_t kDistCacheSplitMinN = (int64_t)1 << 16;
 
 static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<DevProblem>& P) {
   std::vector<DevProblem> Q = P;
@@ -1316,10 +1324,12 @@ static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<
   std::vector<int> order(P.size());
   for (size_t i = 0; i < P.size(); ++i) order[i] = (int)i;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return P[a].d > P[b].d; });
+  const int64_t min_d = (c->split_w && c->lanes == 1 && P.size() > 1 && P[0].n >= kDistCacheSplitMinN)
+                            ? kDistCacheMinDSplit : kDistCacheMinD;
   int slot = 0;
   for (int i : order) {
     const DevProblem& p = P[i];
-    if (p.d < kDistCacheMinD) continue;
+    if (p.d < min_d) continue;
     const int64_t bytes = p.n * p.mp * (int64_t)sizeof(double);
     if (bytes > budget) continue;
     budget -= bytes;
