@@ -78,7 +78,8 @@ def main():
                          "per-launch kernel durations then include the sharing)")
     ap.add_argument("--cu-split", type=int, default=None,
                     help="CUs per XCD that whiten beside the Gram in the batched fit "
-                         "(gpar_ctx_set_cu_split; default: the library's, 8); 0 = whole-chip kernels")
+                         "(gpar_ctx_set_cu_split; default: the library's, 8 where N Mp^2 >= 1e11); "
+                         "0 = whole-chip kernels")
     ap.add_argument("--inference", default="given", choices=["given", "chained"],
                     help="test inputs of output p: 'given' = the noiseless previous outputs at t* "
                          "(GPAR_scaled_examples.jl:139); 'chained' = output 1's true values and the "
@@ -195,6 +196,10 @@ def main():
     if args.cu_split is not None:
         ctx.set_cu_split(args.cu_split)
     cu_split = ctx.cu_split()
+    # the default split applies only to batched fits with N Mp^2 >= 1e11 (include/gpar_hip.h)
+    mp = (M + 127) // 128 * 128
+    if args.cu_split is None and float(N) * mp * mp < 1e11:
+        cu_split = 0
     chained = args.inference == "chained" and not temporal
     if chained:
         # inference inputs: column 0 = output 1's true values at t*, column p-1 = output p's

@@ -32,6 +32,7 @@ struct gpar_ctx {
   // gpar_ctx_set_cu_split(w): the pipelined fit's whitening runs on w CUs of every XCD and the
   // Gram (its co-running correction too) on the other 32 - w, concurrently (CU-masked streams)
   int split_w = 0, split_mask_w = 0;
+  bool split_forced = false;      // set explicitly: no problem-size gate (split_active)
   bool split_dgw = true;          // a w/32 share of the DG items on the whitening CUs
   hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr;
   hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
@@ -179,6 +180,14 @@ constexpr int64_t kPipeMaxBetaBytes = (int64_t)8 << 30;   // second beta buffer 
 // default gpar_ctx_set_cu_split width: 8 of every XCD's 32 CUs whiten beside the Gram (north job
 // 20.66 -> 19.69 s per job in same-box pairs; 4 starves the whitening: 28.4 s)
 constexpr int kDefaultCuSplit = 8;
+// the default split applies to batched fits whose Gram is big enough to amortise it: N Mp^2 >= 1e11
+// (north, N = 1e6, M = 512: 2.6e11; the N = 1e5 configs measured slower split: dtc 389 vs 297 ms
+// per job, eeg 3.09 vs 3.07 s)
+constexpr double kSplitMinWork = 1e11;
+static bool split_active(const gpar_ctx* c, int64_t n, int64_t mp) {
+  return c->split_w > 0 && c->lanes == 1 &&
+         (c->split_forced || (double)n * (double)mp * (double)mp >= kSplitMinWork);
+}
 
 static int sde_dim(int kind) {
   if (kind == GPAR_MATERN12) return 1;
@@ -540,7 +549,7 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     }
     check_launch("gram");
   };
-  if (pipe && c->split_w) {
+  if (pipe && split_active(c, n, mpmax)) {
     // Whitening + short chain on w CUs of every XCD (s_w), concurrently with the Gram on the other
     // 32 - w (s_g, its co-running correction on s_g2): W(i+1) P(i+1) beside G(i).  A w/32 share of
     // G(i)'s DG items runs on s_w after P(i+1), so both sides end together.  W(i+1) waits for
@@ -1090,26 +1099,36 @@ static int fail(gpar_ctx* c, int code, const char* what) {
 // tools/ubench/cumask_probe.cpp) and for the Gram (the other bits).  w a multiple of 4 keeps every
 // SE of both sides equally wide: workgroups are dealt to the SEs evenly, so an SE with fewer CUs
 // than its neighbours sets the pace (w = 6 measured slower than w = 4).
-static int set_cu_split(gpar_ctx* c, int w) {
+static int set_cu_split(gpar_ctx* c, int w, bool forced) {
   if (w < 0 || w >= 32 || w % 4) return GPAR_ERR_ARG;
-  if (w > 0 && !c->s_w) {
+  if (w > 0 && w != c->split_mask_w) {
     hipDeviceProp_t pr;
     if (hipGetDeviceProperties(&pr, c->device) != hipSuccess) return GPAR_ERR_HIP;
     if (pr.multiProcessorCount != 256) return GPAR_ERR_UNSUPPORTED;   // the MI355X layout only
+    // a stream's CU mask is fixed at its creation: a new width gets new streams
+    for (hipStream_t* st : {&c->s_w, &c->s_g, &c->s_g2})
+      if (*st) {
+        (void)hipStreamSynchronize(*st);
+        (void)hipStreamDestroy(*st);
+        *st = nullptr;
+      }
+    c->split_mask_w = 0;
+    c->split_w = 0;
     uint32_t mw[8] = {0}, mg[8] = {0};
     for (int i = 0; i < 256; ++i) (i < 8 * w ? mw : mg)[i / 32] |= 1u << (i % 32);
-    // the masks are fixed per stream: the split streams carry w's mask from their creation
     if (hipExtStreamCreateWithCUMask(&c->s_w, 8, mw) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&c->s_g, 8, mg) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&c->s_g2, 8, mg) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_gd[0], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_gd[1], hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_sp, hipEventDisableTiming) != hipSuccess)
+        hipExtStreamCreateWithCUMask(&c->s_g2, 8, mg) != hipSuccess)
+      return GPAR_ERR_HIP;
+    if (!c->ev_sp &&
+        (hipEventCreateWithFlags(&c->ev_gd[0], hipEventDisableTiming) != hipSuccess ||
+         hipEventCreateWithFlags(&c->ev_gd[1], hipEventDisableTiming) != hipSuccess ||
+         hipEventCreateWithFlags(&c->ev_sp, hipEventDisableTiming) != hipSuccess))
       return GPAR_ERR_HIP;
     c->split_mask_w = w;
   }
-  if (w > 0 && w != c->split_mask_w) return GPAR_ERR_ARG;   // one split width per context
   c->split_w = w;
+  c->split_forced = forced;
   return GPAR_OK;
 }
 
@@ -1143,7 +1162,10 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
   // kernel off the whitening CUs
   if (const char* e = std::getenv("GPAR_SPLIT_DGW")) c->split_dgw = std::atoi(e) != 0;
   const char* e_split = std::getenv("GPAR_SPLIT_CUS");
-  (void)set_cu_split(c, e_split ? std::atoi(e_split) : kDefaultCuSplit);   // 0 where unsupported
+  if (e_split)
+    (void)set_cu_split(c, std::atoi(e_split), true);
+  else
+    (void)set_cu_split(c, kDefaultCuSplit, false);   // stays 0 where unsupported
   *out = c;
   return GPAR_OK;
 }
@@ -1161,7 +1183,7 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev_pw);
   (void)hipEventDestroy(ctx->ev_pc[0]);
   (void)hipEventDestroy(ctx->ev_pc[1]);
-  if (ctx->s_w) {
+  {
     for (hipStream_t st : {ctx->s_w, ctx->s_g, ctx->s_g2})
       if (st) {
         (void)hipStreamSynchronize(st);
@@ -1239,10 +1261,12 @@ int32_t gpar_ctx_set_lanes(gpar_ctx* ctx, int32_t lanes) {
 int32_t gpar_ctx_set_cu_split(gpar_ctx* ctx, int32_t cus_per_xcd) {
   if (!ctx) return GPAR_ERR_STATE;
   (void)hipSetDevice(ctx->device);
-  const int rc = set_cu_split(ctx, cus_per_xcd);
+  // -1: back to the default (kDefaultCuSplit, gated by problem size); else that width, always
+  const int rc = cus_per_xcd == -1 ? set_cu_split(ctx, kDefaultCuSplit, false)
+                                   : set_cu_split(ctx, cus_per_xcd, true);
   if (rc != GPAR_OK)
-    ctx->err = "gpar_ctx_set_cu_split: cus_per_xcd must be 0 or a multiple of 4 below 32 (one "
-               "nonzero width per context, 256-CU devices)";
+    ctx->err = "gpar_ctx_set_cu_split: cus_per_xcd must be -1 (default), 0 or a multiple of 4 "
+               "below 32 (256-CU devices)";
   return rc;
 }
 
@@ -1324,7 +1348,9 @@ static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<
   std::vector<int> order(P.size());
   for (size_t i = 0; i < P.size(); ++i) order[i] = (int)i;
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return P[a].d > P[b].d; });
-  const int64_t min_d = (c->split_w && c->lanes == 1 && P.size() > 1 && P[0].n >= kDistCacheSplitMinN)
+  int64_t mpmax = 0;
+  for (auto& p : P) mpmax = std::max(mpmax, p.mp);
+  const int64_t min_d = (P.size() > 1 && split_active(c, P[0].n, mpmax) && P[0].n >= kDistCacheSplitMinN)
                             ? kDistCacheMinDSplit : kDistCacheMinD;
   int slot = 0;
   for (int i : order) {

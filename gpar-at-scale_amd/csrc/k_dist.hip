@@ -211,11 +211,15 @@ constexpr int kW2MaxL = 256;
 #define D2_NT 1   // non-temporal d2 loads and beta stores (streamed once): 1.656 -> 1.575 ms at D = 32
 #endif
 
-constexpr int kW2T = 8;
+#ifndef W2V
+#define W2V 0   // A/B: 1 = 4-row prefetch at three workgroups per CU
+#endif
+constexpr int kW2T = W2V ? 4 : 8;
+constexpr int kW2Occ = W2V ? 3 : 2;
 
 // RIN: src holds the distances r = sqrt_pos(d2) (the fit's cache, Matern kernels) instead of d2.
 template <int TK, int OK, bool RIN>
-__global__ __launch_bounds__(256, 2) void whiten_kfu_d2x2(
+__global__ __launch_bounds__(256, kW2Occ) void whiten_kfu_d2x2(
     const double* __restrict__ rec, const double* src, int64_t lds, int64_t m, int64_t mp,
     int64_t n, int L, double inv_lo, double s_o, double* beta, int64_t ldb,
     double* __restrict__ send, int64_t mc, const double* __restrict__ g,

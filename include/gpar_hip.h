@@ -121,9 +121,11 @@ int32_t gpar_ctx_set_lanes(gpar_ctx* ctx, int32_t lanes);
  * whitening runs on w CUs of every XCD while the previous output's Gram runs on the other 32 - w
  * (CU-masked HIP streams; a w/32 share of the Gram's diagonal-block work also goes to the
  * whitening side).  w = 0: whole-chip kernels, one after the other.  w must be a multiple of 4
- * below 32 (equal SE widths); one nonzero w per context.  Default 8 (0 on devices without 256
- * CUs; the environment variable GPAR_SPLIT_CUS overrides the default at context creation).  Results are identical either way up to
- * the Gram's split plan (deterministic for a given w).  256-CU devices only. */
+ * below 32 (equal SE widths).  An explicit w applies to every batched
+ * fit; -1 restores the default: w = 8 for batched fits with N * Mp^2 >= 1e11 (smaller Grams run
+ * whole-chip), 0 on devices without 256 CUs; the environment variable GPAR_SPLIT_CUS sets an
+ * explicit width at context creation.  Results agree with the whole-chip schedule up to the
+ * Gram's split plan (last bits; deterministic for a given w). */
 int32_t gpar_ctx_set_cu_split(gpar_ctx* ctx, int32_t cus_per_xcd);
 /* The CU split in effect (0 when off or unsupported). */
 int32_t gpar_ctx_get_cu_split(const gpar_ctx* ctx, int32_t* cus_per_xcd);
