@@ -1335,15 +1335,18 @@ constexpr int64_t kDistCacheSplitMinN = (int64_t)1 << 16;
 static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<DevProblem>& P) {
   std::vector<DevProblem> Q = P;
   if (c->dist_cache_bytes == 0) return Q;
+  // explicit budget: total cache bytes.  auto: new allocations take at most the free HBM less a
+  // reserve, and cache buffers the context already holds (an earlier call's) are reused at no
+  // cost -- counting them against the reserve again would drop outputs from the cache on every
+  // call after the first, once later phases (the predictions) have taken their workspace.
   int64_t budget = c->dist_cache_bytes;
-  if (budget < 0) {   // auto: free HBM (the cache buffers already held count as free) - reserve
+  int64_t fresh = INT64_MAX;
+  if (budget < 0) {
     size_t fr = 0, tot = 0;
     HIPCHECK(hipMemGetInfo(&fr, &tot));
-    int64_t held = 0;
-    for (auto& kv : c->bufs)
-      if (kv.first.rfind("distcache", 0) == 0) held += (int64_t)kv.second.bytes;
     const int64_t reserve = std::max<int64_t>((int64_t)16 << 30, (int64_t)(tot / 10));
-    budget = std::max<int64_t>(0, (int64_t)fr + held - reserve);
+    fresh = std::max<int64_t>(0, (int64_t)fr - reserve);
+    budget = INT64_MAX;
   }
   std::vector<int> order(P.size());
   for (size_t i = 0; i < P.size(); ++i) order[i] = (int)i;
@@ -1357,9 +1360,15 @@ static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<
     const DevProblem& p = P[i];
     if (p.d < min_d) continue;
     const int64_t bytes = p.n * p.mp * (int64_t)sizeof(double);
-    if (bytes > budget) continue;
+    const std::string name = "distcache" + std::to_string(slot);
+    const auto it = c->bufs.find(name);
+    const int64_t held = it != c->bufs.end() ? (int64_t)it->second.bytes : 0;
+    const int64_t need = held >= bytes ? 0 : bytes - held;   // ws() frees the smaller one first
+    if (bytes > budget || need > fresh) continue;
     budget -= bytes;
-    double* d2 = ws<double>(c, "distcache" + std::to_string(slot++), (size_t)p.n * p.mp);
+    fresh -= need;
+    ++slot;
+    double* d2 = ws<double>(c, name, (size_t)p.n * p.mp);
     launch_dist2(c->stream, p.ok, p.v, p.ldv, p.n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, d2, p.mp,
                  /*take_sqrt=*/p.ok != GPAR_EQ);
     check_launch("dist2 (cache)");
