@@ -292,6 +292,29 @@ def main():
     wh_n, wh_ms = ctx.kernel_stats("whiten")
     gram_work = ctx.kernel_work("gram")      # flops, N*M*(M+1) per launch
     wh_work = ctx.kernel_work("whiten")      # algorithmic HBM bytes (include/gpar_hip.h)
+    probe = None
+    if rank == 0 and cu_split and problems and not host and args.lanes == 1:
+        # after the timed region: the same kernels whole-chip (gpar_ctx_set_cu_split(ctx, 0)) in
+        # a batched fit of four outputs around D = 32 (pipelined, distance cache), so the line
+        # also carries the kernels' own fractions next to the split job's.  (A one-output fit
+        # idles the GPU between evaluations and measures ~10 % slower Grams: cold clocks.)
+        i = max(0, min(len(problems) - 4, 30))
+        sub = problems[i:i + 4]
+        ctx.set_cu_split(0)
+        ctx.reset_stats()
+        G.fit_batch(sub, x0[: len(sub)], max_evals=8, g_tol=-1.0, device=local)
+        ctx.set_cu_split(-1 if args.cu_split is None else args.cu_split)
+        pg_n, pg_ms = ctx.kernel_stats("gram")
+        pw_n, pw_ms = ctx.kernel_stats("whiten")
+        if pg_n and pw_n:
+            pg = ctx.kernel_work("gram") / (pg_ms * 1e-3) / 1e12
+            pw = ctx.kernel_work("whiten") / (pw_ms * 1e-3) / 1e9
+            probe = {"outputs": gpar_out[i:i + len(sub)], "evals": 8,
+                     "gram": {"avg_ms": pg_ms / pg_n, "achieved_tflops": pg,
+                              "frac": pg / FP64_MFMA_PEAK_TFLOPS},
+                     "whiten": {"avg_ms": pw_ms / pw_n, "achieved_gbs": pw, "frac": pw / HBM_PEAK_GBS},
+                     "note": "untimed, after the timed steps: a batched fit of these outputs with "
+                             "the CU split off (whole-chip kernels), HIP events as above"}
     out = None
     if rank == 0:
         value = n_eff * P / (el / 1e3)
@@ -371,6 +394,8 @@ def main():
             out["roofline_whiten"]["note"] = (
                 f"fit launches run on {8 * cu_split} of 256 CUs beside the Gram (HBM shared), "
                 "so per-launch time is not the whole-chip kernel's")
+        if probe:
+            out["roofline_whole_chip_probe"] = probe
         if args.lanes > 1 and out["roofline"]:
             # two streams overlap launches: event spans are not the kernel's own duration
             out["roofline"].update(achieved=None, frac=None,
