@@ -479,6 +479,24 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   }
   std::vector<GainsOut> gi(np);
   auto alpha_of = [&](int i) { return shared ? alpha_all + (size_t)i * n : alpha_l[i % nbuf]; };
+  // the Gram partials, sized once for the batch's largest plan (any of the plans below): growing
+  // them mid-batch would free a buffer another stream's kernels may still be using
+  {
+    int64_t pd = 0, rd = 0;
+    for (const auto& p : P)
+      for (int cus : {256, 8 * (32 - c->split_w)})
+        for (int dgc : {cus, 256}) {
+          if (cus <= 0) continue;
+          const GramPlan pl = gram_plan(n, p.mp, nlanes > 1, cus, dgc);
+          pd = std::max(pd, pl.part_doubles);
+          rd = std::max(rd, pl.rpart_doubles);
+        }
+    for (int l = 0; l < nlanes; ++l) {
+      const std::string sfx = l ? "_1" : "";
+      (void)ws<double>(c, "gram_part" + sfx, (size_t)pd);
+      (void)ws<double>(c, "gram_rpart" + sfx, (size_t)rd);
+    }
+  }
   // Kfu assembly + whitening of output i into buffer i % nbuf, on c->stream
   auto whiten_stage = [&](int i) {
     const DevProblem& p = P[i];
