@@ -292,6 +292,13 @@ def main():
     wh_n, wh_ms = ctx.kernel_stats("whiten")
     gram_work = ctx.kernel_work("gram")      # flops, N*M*(M+1) per launch
     wh_work = ctx.kernel_work("whiten")      # algorithmic HBM bytes (include/gpar_hip.h)
+    try:   # telemetry only: never fails the line
+        free_b, total_b = torch.cuda.mem_get_info(dev)
+        memory = {"library_workspace_gb": ctx.workspace_bytes() / 1e9, "device_free_gb": free_b / 1e9,
+                  "device_total_gb": total_b / 1e9,
+                  "note": "after the timed steps; the workspace includes the fit's distance cache"}
+    except Exception as e:   # noqa: BLE001
+        memory = {"error": repr(e)}
     probe = None
     if rank == 0 and cu_split and problems and not host and args.lanes == 1:
         # after the timed region: the same kernels whole-chip (gpar_ctx_set_cu_split(ctx, 0)) in
@@ -394,6 +401,7 @@ def main():
             out["roofline_whiten"]["note"] = (
                 f"fit launches run on {8 * cu_split} of 256 CUs beside the Gram (HBM shared), "
                 "so per-launch time is not the whole-chip kernel's")
+        out["memory"] = memory
         if probe:
             out["roofline_whole_chip_probe"] = probe
         if args.lanes > 1 and out["roofline"]:
