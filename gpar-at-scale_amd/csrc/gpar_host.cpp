@@ -1343,11 +1343,12 @@ struct FitKeep {
 constexpr int64_t kDistCacheMinD = 17;
 // With the CU split the whitening runs on a quarter of the chip, where the fused kernel is
 // compute-bound (D <= 16: 5.05 ms per launch on 64 CUs against 3.62 ms for the cached one), so a
-// batched fit over long series caches outputs down to D = 3 (the narrowest stay fused: they fit
-// last).  Short series (N < 2^16) keep the D >= 17 rule: there the fused kernel is latency-bound
-// either way, and the small-D fits then stay on the arithmetic a single-output q(u) recomputes
-// (gpar_fit_predict's reused Gram stays bit-identical to gpar_predict's).
-constexpr int64_t kDistCacheMinDSplit = 3;
+// batched fit over long series caches every output the budget holds (the narrowest fit last; at
+// the north config all 63: 258 GB, 10 GB of the 309 GB left free after the predictions).  Short
+// series (N < 2^16) keep the D >= 17 rule: there the fused kernel is latency-bound either way, and
+// the small-D fits then stay on the arithmetic a single-output q(u) recomputes (gpar_fit_predict's
+// reused Gram stays bit-identical to gpar_predict's).
+constexpr int64_t kDistCacheMinDSplit = 1;
 constexpr int64_t kDistCacheSplitMinN = (int64_t)1 << 16;
 
 static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<DevProblem>& P) {
