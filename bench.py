@@ -93,6 +93,26 @@ def main():
                     help="multi-rank rehearsal on ONE GPU: every rank uses device 0 and the gloo "
                          "backend (RCCL runs one rank per device); exercises the launcher, sharding, "
                          "broadcasts and gathers with the real kernels -- not a scaling measurement")
+    ap.add_argument("--qu-noise-free", action="store_true",
+                    help="q(u) with the reference's noise-free Cuu (gpar_scaled_inference.jl:157) "
+                         "instead of Cuu + sigma^2 I (qu_kuu_noise, the default here: the noise-free "
+                         "Cuu of M=512 pseudo-inputs drawn from the data is numerically singular)")
+    ap.add_argument("--api", default="batched", choices=["batched", "per-output"],
+                    help="'batched': one gpar_fit_predict call for all owned outputs (the library's "
+                         "multi-output driver); 'per-output': one single-output gpar_fit_predict call "
+                         "per output, as a reference caller's loop through the Julia shim's "
+                         "get_gpar_scaled_predictions makes them (GPAR_scaled_examples.jl:132-175)")
+    ap.add_argument("--shard", default=None,
+                    help="R/W: run exactly rank R's outputs of the W-way output assignment "
+                         "(gparatscale.shard.assign_outputs) on this one GPU, the code path of one "
+                         "rank of a W-GPU job, to predict the per-rank step time")
+    ap.add_argument("--dist-cache", default="keep", choices=["keep", "release"],
+                    help="'keep' (the bench default): the fit's distance-cache buffers stay allocated "
+                         "between calls (gpar_ctx_set_dist_cache_keep; the distances themselves are "
+                         "recomputed by every fit, nothing is carried across steps) -- re-allocating "
+                         "258 GB per step costs ~5.8 s on MI355X (fresh VRAM is cleared); 'release': "
+                         "the library default, freed when each fit call returns")
+    ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--stub", action="store_true",
                     help="launcher check without a GPU: ranks join a gloo group, take their output "
                          "shards and report them; no compute (tests/test_bench_launch.py)")
@@ -102,6 +122,16 @@ def main():
         sys.exit(launch_ranks(args.gpus, sys.argv[1:], stub=args.stub or args.rehearse))
     if args.stub:
         return stub_rank(args)
+    if args.cpu_baseline_child:
+        return cpu_baseline_child(args)
+    world0 = int(os.environ.get("WORLD_SIZE", "1"))
+    cfg0 = CONFIGS[args.config]
+    # the CPU baseline runs in a child process started before anything touches the GPU, so it
+    # overlaps the inputs and the warm-up steps; it is joined before the timed region
+    cpu_child = None
+    if (world0 == 1 and not args.no_cpu_baseline and not cfg0.get("temporal", False)
+            and args.shard is None and args.api == "batched"):
+        cpu_child = start_cpu_baseline(args)
 
     import torch
     import torch.distributed as dist
@@ -154,17 +184,26 @@ def main():
     shards = S.assign_outputs(P, world) if not temporal else \
         [[p for p in range(1, P + 1) if (p - 1) % world == r] for r in range(world)]
     mine = shards[rank]
+    shard_of = None
+    if args.shard:
+        if world > 1 or temporal:
+            sys.exit("--shard R/W: one process, the GPAR configs")
+        r_, w_ = (int(x) for x in args.shard.split("/"))
+        shard_of = (r_, w_)
+        shards = S.assign_outputs(P, w_)
+        mine = shards[r_]
     gpar_out = [p for p in mine if p >= 2] if not temporal else []
     Yh = Y_d.cpu().numpy() if gpar_out else None
-    # q(u) with Kuu + sigma^2 I (qu_kuu_noise): the reference's jitter-free Cuu
-    # (gpar_scaled_inference.jl:157) is numerically singular for M=512 pseudo-inputs drawn from
-    # the data at fitted lengthscales; the objective itself is unchanged (dtc.jl:35,119).
+    # q(u) with Kuu + sigma^2 I (qu_kuu_noise) unless --qu-noise-free: the reference's jitter-free
+    # Cuu (gpar_scaled_inference.jl:157) is numerically singular for M=512 pseudo-inputs drawn
+    # from the data at fitted lengthscales; the objective itself is unchanged (dtc.jl:35,119).
+    qn = not args.qu_noise_free
     problems, keep, ycols, Zs = [], [], {}, {}
     for p in gpar_out:
         ycols[p] = Y_d[:, p - 1].contiguous()
         Zs[p] = torch.from_numpy(D.pseudo_inputs(Yh[:, : p - 1], M, seed=p)).to(dev)
         pr, k = G.make_problem(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], cfg["out_kernel"], "matern52",
-                               qu_kuu_noise=True)
+                               qu_kuu_noise=qn)
         problems.append(pr)
         keep.append(k)
     y1 = Y_d[:, 0].contiguous() if 1 in mine else None
@@ -174,6 +213,8 @@ def main():
     if host:
         if world > 1 or args.inference != "given" or temporal or args.separate_predict:
             sys.exit("--inputs host: one rank, given inference inputs, the GPAR configs only")
+    if args.api == "per-output" and (args.inference != "given" or temporal or args.separate_predict):
+        sys.exit("--api per-output: given inference inputs, the GPAR configs only")
         # the same problems from host (numpy) buffers: D x N ColVecs, as the Julia shim passes them
         Yh_all = Y_d.cpu().numpy()
         t_hh, ts_hh, Fs_hh = t_d.cpu().numpy(), ts_d.cpu().numpy(), Fs_d.cpu().numpy()
@@ -181,7 +222,7 @@ def main():
         for p in gpar_out:
             pr, k = G.make_problem(np.ascontiguousarray(Yh_all[:, : p - 1].T), Zs[p].cpu().numpy().T,
                                    t_hh, np.ascontiguousarray(Yh_all[:, p - 1]), cfg["out_kernel"],
-                                   "matern52", qu_kuu_noise=True)
+                                   "matern52", qu_kuu_noise=qn)
             problems.append(pr)
             keep.append(k)
         Vs_h = [np.ascontiguousarray(Fs_hh[:, : p - 1].T) for p in gpar_out]
@@ -208,13 +249,32 @@ def main():
         owners = S.owners_of(shards)
         gpar_all = list(range(2, P + 1))
 
+    ctx.set_dist_cache_keep(args.dist_cache == "keep")
+    per_output = args.api == "per-output"
+    last = {}   # the last step's FitResult per output (the self-check after the timed region)
+
+    def fit_predict_outputs(ts, Vs):
+        """get_gpar_scaled_predictions for every owned GPAR output: one batched call, or one
+        single-output call per output (--api per-output)."""
+        if not per_output:
+            fr, _, _ = G.fit_predict_batch(problems, x0, ts, Vs, max_evals=EV, g_tol=-1.0,
+                                           mode=args.predict, samples=100, seed=gpar_out[0],
+                                           device=local)
+            return fr
+        th, nl = np.zeros((len(problems), 5)), np.zeros(len(problems))
+        for i in range(len(problems)):
+            fr, _, _ = G.fit_predict_batch(problems[i:i + 1], x0[i:i + 1], ts, Vs[i:i + 1],
+                                           max_evals=EV, g_tol=-1.0, mode=args.predict, samples=100,
+                                           seed=gpar_out[0] + i, device=local)
+            th[i], nl[i] = fr.theta[0], fr.nlml[0]
+        return G.FitResult(th, nl, np.full(len(problems), EV, dtype=np.int32))
+
     def step():
         res = {}
         if host:
             if problems:
-                fr, _, _ = G.fit_predict_batch(problems, x0, ts_hh, Vs_h, max_evals=EV, g_tol=-1.0,
-                                               mode=args.predict, samples=100, seed=gpar_out[0],
-                                               device=local)
+                fr = fit_predict_outputs(ts_hh, Vs_h)
+                last["fit"] = fr
                 for i, p in enumerate(gpar_out):
                     res[p] = fr.theta[i]
             if y1_h is not None:
@@ -242,13 +302,12 @@ def main():
                 lambda p, c: G.predict_scaled(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], res[p], ts_d,
                                               c[:, : p - 1], cfg["out_kernel"], "matern52",
                                               mode=args.predict, samples=100, seed=p, device=local,
-                                              qu_kuu_noise=True),
+                                              qu_kuu_noise=qn),
                 chain_d)
         elif problems and not args.separate_predict:
             # get_gpar_scaled_predictions for every owned output: batched fit, then predictions
-            fr, _, _ = G.fit_predict_batch(problems, x0, ts_d, [Fs_d[:, : p - 1] for p in gpar_out],
-                                           max_evals=EV, g_tol=-1.0, mode=args.predict, samples=100,
-                                           seed=gpar_out[0], device=local)
+            fr = fit_predict_outputs(ts_d, [Fs_d[:, : p - 1] for p in gpar_out])
+            last["fit"] = fr
             for i, p in enumerate(gpar_out):
                 res[p] = fr.theta[i]
         elif problems:
@@ -267,11 +326,14 @@ def main():
         for i, p in enumerate(gpar_out if args.separate_predict else []):
             G.predict_scaled(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], res[p], ts_d, Fs_d[:, : p - 1],
                              cfg["out_kernel"], "matern52", mode=args.predict, samples=100,
-                             seed=p, device=local, qu_kuu_noise=True)
+                             seed=p, device=local, qu_kuu_noise=qn)
         return S.gather_thetas(res, P, dev)   # fitted hyperparameters, P x 5 (tiny)
 
     for _ in range(args.warmup):
         step()
+    cpu_res = None
+    if cpu_child is not None:   # joined before the timed region (untimed)
+        cpu_res = join_cpu_baseline(cpu_child)
     ctx.set_profiling(True)
     ctx.reset_stats()
     if world > 1:
@@ -294,9 +356,13 @@ def main():
     wh_work = ctx.kernel_work("whiten")      # algorithmic HBM bytes (include/gpar_hip.h)
     try:   # telemetry only: never fails the line
         free_b, total_b = torch.cuda.mem_get_info(dev)
+        cached, evictions, held = ctx.dist_cache_stats()
         memory = {"library_workspace_gb": ctx.workspace_bytes() / 1e9, "device_free_gb": free_b / 1e9,
                   "device_total_gb": total_b / 1e9,
-                  "note": "after the timed steps; the workspace includes the fit's distance cache"}
+                  "dist_cache": {"outputs_cached_last_fit": cached, "oom_evictions": evictions,
+                                 "held_gb": held / 1e9, "keep": args.dist_cache == "keep"},
+                  "note": "after the timed steps; the workspace includes the fit's distance cache "
+                          "only with keep (else it is released when each fit call returns)"}
     except Exception as e:   # noqa: BLE001
         memory = {"error": repr(e)}
     probe = None
@@ -322,9 +388,28 @@ def main():
                      "whiten": {"avg_ms": pw_ms / pw_n, "achieved_gbs": pw, "frac": pw / HBM_PEAK_GBS},
                      "note": "untimed, after the timed steps: a batched fit of these outputs with "
                              "the CU split off (whole-chip kernels), HIP events as above"}
+    self_check = None
+    if rank == 0 and problems and "fit" in last:
+        # the timed steps' own outputs: each checked output's -nlml (the objective value the
+        # split, cached, pipelined batched fit reached at its returned theta) against a fresh
+        # single-output whole-chip evaluation at that theta (no split, no cache, no pipeline)
+        fr = last["fit"]
+        idx = sorted({0, len(problems) // 2, len(problems) - 1})
+        saved = ctx.cu_split()
+        ctx.set_cu_split(0)
+        rels = []
+        for i in idx:
+            v = G.dtc_objective_batch([problems[i]], fr.theta[i:i + 1], device=local)[0]
+            rels.append(abs(-v - fr.nlml[i]) / abs(v))
+        ctx.set_cu_split(-1 if args.cu_split is None else saved)
+        self_check = {"outputs": [gpar_out[i] for i in idx], "max_rel": max(rels),
+                      "ok": bool(max(rels) <= 1e-9),
+                      "what": "-nlml of the timed run's last step at its fitted theta vs a fresh "
+                              "whole-chip single-output gpar_dtc_objective there (rel <= 1e-9)"}
     out = None
     if rank == 0:
-        value = n_eff * P / (el / 1e3)
+        P_work = len(mine) if shard_of else P
+        value = n_eff * P_work / (el / 1e3)
         flops = float(n_eff) * M * (M + 1)       # N*M*(M+1) per Gram launch
         avg = gram_ms / max(gram_n, 1)
         achieved = gram_work / (gram_ms * 1e-3) / 1e12 if gram_n else None
@@ -355,7 +440,15 @@ def main():
                        "out_kernel": cfg["out_kernel"], "time_kernel": "matern52",
                        "parallelism": f"outputs sharded over {world} GPU(s)",
                        "outputs_per_rank": shards, "inference": args.inference,
-                       "inputs": args.inputs, "cu_split": cu_split},
+                       "inputs": args.inputs, "cu_split": cu_split, "qu_kuu_noise": qn,
+                       "api": args.api, "dist_cache": args.dist_cache,
+                       **({"shard": f"{shard_of[0]}/{shard_of[1]}", "shard_outputs": mine}
+                          if shard_of else {})},
+            "qu_convention": ("q(u) and the predictions factor Cuu + sigma^2 I (qu_kuu_noise), the "
+                              "objective's regularised Kuu (dtc.jl:35,119), not the reference's "
+                              "noise-free Cuu (gpar_scaled_inference.jl:157)" if qn else
+                              "q(u) factors the reference's noise-free Cuu "
+                              "(gpar_scaled_inference.jl:157)"),
             **({"rehearsal": "all ranks on one GPU over gloo: not a scaling measurement"}
                if args.rehearse else {}),
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
@@ -402,6 +495,8 @@ def main():
                 f"fit launches run on {8 * cu_split} of 256 CUs beside the Gram (HBM shared), "
                 "so per-launch time is not the whole-chip kernel's")
         out["memory"] = memory
+        if self_check:
+            out["self_check"] = self_check
         if probe:
             out["roofline_whole_chip_probe"] = probe
         if args.lanes > 1 and out["roofline"]:
@@ -414,8 +509,8 @@ def main():
             out["roofline"] = None
             out["config"]["workload"] = f"temporal-only chains fit+smooth ({args.config})"
             out["config"]["time_kernel"] = cfg["out_kernel"]
-        if world == 1 and not args.no_cpu_baseline and not temporal:
-            out["cpu_baseline"] = cpu_baseline(n_eff, ns_eff, M, P, EV, cfg["out_kernel"])
+        if cpu_res is not None:
+            out["cpu_baseline"] = cpu_res
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
@@ -480,7 +575,76 @@ def stub_rank(args):
         print(json.dumps({"stub": True, "n_gpus": world, "P": P, "ranks": got}), flush=True)
 
 
-def _cpu_sample(CR, O, n, ns, M, d, out_kernel, theta):
+def _cpu_model():
+    """The host CPU's model name (/proc/cpuinfo, as lscpu reports it) and the CPUs this process
+    may use (its affinity mask; os.cpu_count() shows the whole machine on a shared box)."""
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = os.cpu_count()
+    return {"model": model, "machine_cpus": os.cpu_count(), "affinity_cpus": avail,
+            "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
+
+
+def _cpu_threads():
+    """Threads for the CPU baseline: the box's CPU share (OMP_NUM_THREADS, else the affinity mask)
+    less one, which the GPU process's host thread keeps while the baseline runs beside its
+    warm-up."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    try:
+        share = int(env) if env else len(os.sched_getaffinity(0))
+    except (ValueError, AttributeError, OSError):
+        share = os.cpu_count() or 1
+    return max(1, share - 1)
+
+
+def start_cpu_baseline(args):
+    """Start the CPU baseline (cpu_baseline below) in a child process, before this process touches
+    the GPU: it then runs beside the inputs and the warm-up steps instead of after the timed region.
+    Returns the Popen (joined by join_cpu_baseline before the timed region)."""
+    th = _cpu_threads()
+    env = dict(os.environ, OMP_NUM_THREADS=str(th), OPENBLAS_NUM_THREADS=str(th))
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--config", args.config]
+    if args.evals:
+        cmd += ["--evals", str(args.evals)]
+    if args.qu_noise_free:
+        cmd += ["--qu-noise-free"]
+    log(f"cpu_baseline: child process with {th} threads beside the warm-up")
+    return subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+
+
+def join_cpu_baseline(child, timeout=900):
+    try:
+        out, _ = child.communicate(timeout=timeout)
+    except subprocess.TimeoutExpired:
+        child.kill()
+        child.communicate()
+        return {"value": None, "error": f"cpu baseline child exceeded {timeout}s"}
+    for line in out.splitlines()[::-1]:
+        if line.startswith("{"):
+            return json.loads(line)
+    return {"value": None, "error": f"cpu baseline child exited {child.returncode} without a result"}
+
+
+def cpu_baseline_child(args):
+    cfg = dict(CONFIGS[args.config])
+    if args.evals:
+        cfg["evals"] = args.evals
+    res = cpu_baseline(cfg["N"], cfg["N"], cfg["M"], cfg["P"], cfg["evals"], cfg["out_kernel"],
+                       qu_kuu_noise=not args.qu_noise_free)
+    print(json.dumps(res), flush=True)
+
+
+def _cpu_sample(CR, O, n, ns, M, d, out_kernel, theta, qu_kuu_noise=True):
     """One DTC objective evaluation and one analytic prediction of the C port at n training /
     ns test points (D = d inputs), seconds each."""
     t, Y = O.synthetic_gpar(n, d + 1, seed=1, noise=0.8)
@@ -494,22 +658,23 @@ def _cpu_sample(CR, O, n, ns, M, d, out_kernel, theta):
     Vs = np.vstack([np.interp(ts, t, V[q]) for q in range(d)])
     t0 = time.perf_counter()
     CR.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, out_kernel, "matern52",
-                                         qu_kuu_noise=True)
+                                         qu_kuu_noise=qu_kuu_noise)
     return t_eval, time.perf_counter() - t0
 
 
-def cpu_baseline(N, NS, M, P, EV, out_kernel, d_sample=32, single_ns=(20_000, 40_000, 80_000)):
+def cpu_baseline(N, NS, M, P, EV, out_kernel, d_sample=32, n_ratio=100_000, qu_kuu_noise=True):
     """Time the C/OpenMP CPU restatement of the reference path (oracle/cpu_ref.{c,py}, SURVEY §8d
     "cpu_ref": kernel assembly, Kalman gains and per-column decorrelate sweeps, RTS smoother in C;
     cholesky / trsm / gemm in OpenBLAS, as the reference leaves them to Julia's OpenBLAS; "port").
 
-    Threaded leg (all OpenMP / OpenBLAS threads): one DTC objective evaluation and one analytic
-    prediction at the job's own sizes (N training points, N* = NS test points, M, D = d_sample),
-    so nothing is extrapolated in N: job = (P - 1) outputs x (EV evaluations + 1 prediction).
-    One-thread leg (the reference's sequential column loop, dtc.jl:110-117): the same two pieces
-    at three smaller sizes under threadpoolctl's limit of 1; cost = a + b*N is fitted on the two
-    larger and checked on the smallest (any check off by more than 5 % is reported in
-    `warnings`), then evaluated at the job's sizes."""
+    Threaded leg (the OpenMP / OpenBLAS threads this process was given): one DTC objective
+    evaluation and one analytic prediction at the job's own sizes (N training points, N* = NS test
+    points, M, D = d_sample), so nothing is extrapolated in N: job = (P - 1) outputs x (EV
+    evaluations + 1 prediction).
+    One-thread figure (the reference's sequential column loop, dtc.jl:110-117): the same two
+    pieces at N = N* = n_ratio with all threads and with one (threadpoolctl's limit of 1); the
+    one-thread job is the threaded job scaled by those measured ratios (assumption: the thread
+    speed-up at n_ratio holds at the job's N)."""
     sys.path.insert(0, ROOT)
     from oracle import gpar_oracle as O
     from oracle import cpu_ref as CR
@@ -520,41 +685,27 @@ def cpu_baseline(N, NS, M, P, EV, out_kernel, d_sample=32, single_ns=(20_000, 40
         blas = 1
     cores = max(CR.threads(), blas)
     theta = (2.0, 2.0, 2.0, 2.0, float(np.exp(-2.0) + 1e-3))
-    warnings = []
-    t_eval, t_pred = _cpu_sample(CR, O, N, NS, M, d_sample, out_kernel, theta)
+    _cpu_sample(CR, O, 4096, 1024, M, d_sample, out_kernel, theta, qu_kuu_noise)   # warm-up, untimed
+    t_eval, t_pred = _cpu_sample(CR, O, N, NS, M, d_sample, out_kernel, theta, qu_kuu_noise)
     t_job = (P - 1) * (EV * t_eval + t_pred)
     single = None
     try:
         from threadpoolctl import threadpool_limits
-        per = []
+        n_ratio = min(n_ratio, N)
+        em, pm = _cpu_sample(CR, O, n_ratio, n_ratio, M, d_sample, out_kernel, theta, qu_kuu_noise)
         with threadpool_limits(limits=1):
-            for n1 in single_ns:
-                e1, p1 = _cpu_sample(CR, O, n1, n1 // 4, M, d_sample, out_kernel, theta)
-                per.append((n1, e1, p1))
-        # cost = a + b n (the M^3 dense tail does not scale with n): fit on the two larger
-        # sizes, check on the smallest, extrapolate to the job's N
-        (n0, e0, p0), (na, ea, pa), (n1, e1, p1) = per
-        def affine(x0, y0, x1, y1, x):
-            return y1 + (y1 - y0) / (x1 - x0) * (x - x1)
-        chk_e = affine(na, ea, n1, e1, n0) / e0
-        chk_p = affine(na + na // 4, pa, n1 + n1 // 4, p1, n0 + n0 // 4) / p0
-        for what, r in (("one-thread eval", chk_e), ("one-thread predict", chk_p)):
-            if abs(r - 1.0) > 0.05:
-                warnings.append(f"{what}: affine fit on N={na},{n1} predicts N={n0} at x{r:.3f} "
-                                f"of the measured time (> 5 %)")
-        e_job = affine(na, ea, n1, e1, N)
-        p_job = affine(na + na // 4, pa, n1 + n1 // 4, p1, N + NS)
-        tj1 = (P - 1) * (EV * e_job + p_job)
+            e1, p1 = _cpu_sample(CR, O, n_ratio, n_ratio, M, d_sample, out_kernel, theta, qu_kuu_noise)
+        re_, rp_ = e1 / em, p1 / pm
+        tj1 = (P - 1) * (EV * t_eval * re_ + t_pred * rp_)
         single = {"value": N * P / tj1, "cores": 1,
-                  "sample": "1 thread: 1 eval + 1 predict (N* = N/4) at " +
-                            ", ".join(f"N={a} ({b:.2f}s + {c:.2f}s)" for a, b, c in per) +
-                            f"; cost = a + b*N fitted on the two larger, checked on the smallest "
-                            f"(eval x{chk_e:.3f}, predict x{chk_p:.3f}); at the job's sizes 1 eval = "
-                            f"{e_job:.1f}s, 1 predict = {p_job:.1f}s: est {tj1:.0f}s per job"}
+                  "sample": f"N = N* = {n_ratio}: 1 eval {em:.2f}s with {int(cores)} threads, {e1:.2f}s "
+                            f"with 1 (x{re_:.2f}); 1 predict {pm:.2f}s / {p1:.2f}s (x{rp_:.2f}); the "
+                            f"threaded job scaled by these ratios: est {tj1:.0f}s per job"}
     except Exception as exc:   # threadpoolctl missing: report the threaded figure only
         single = {"value": None, "error": repr(exc)}
-    return {"value": N * P / t_job, "unit": "pts\u00b7outputs/s", "cores": int(cores), "kind": "port",
-            "single_thread": single, "warnings": warnings,
+    return {"value": N * P / t_job, "unit": "pts·outputs/s", "cores": int(cores), "kind": "port",
+            "host_cpu": _cpu_model(), "single_thread": single,
+            "ran": "in a child process beside the GPU warm-up (joined before the timed region)",
             "sample": f"C/OpenMP + OpenBLAS restatement (oracle/cpu_ref), {int(cores)} threads, at the job's "
                       f"own sizes: 1 DTC objective eval (N={N}, M={M}, D={d_sample}) = {t_eval:.2f}s + "
                       f"1 analytic predict (N={N}, N*={NS}) = {t_pred:.2f}s; job = {P - 1} outputs x "

@@ -43,6 +43,13 @@ struct gpar_ctx {
   hipEvent_t ev_input = nullptr;
   int lanes = 1;                  // gpar_ctx_set_lanes: streams a batch's outputs alternate over
   int64_t dist_cache_bytes = -1;  // gpar_ctx_set_dist_cache: -1 auto, 0 off, else a byte budget
+  bool dist_cache_keep = false;   // gpar_ctx_set_dist_cache_keep: hold the cache past the fit call
+  // per distance-cache slot ("distcache<i>"): still resident.  An allocation that runs out of
+  // memory evicts the whole cache (ws) and clears these, so the fit's later launches fall back to
+  // the fused kernel instead of failing (the cache is recomputable, never required)
+  std::vector<char> cache_valid;
+  int32_t cache_outputs = 0;      // outputs the last fit call cached
+  int32_t cache_evictions = 0;    // OOM evictions since the context was created
   std::string err;
   struct Buf {
     void* p = nullptr;
@@ -128,19 +135,66 @@ static void flush_stats(gpar_ctx* c) {
   }
 }
 
-template <class T>
-static T* ws(gpar_ctx* c, const std::string& name, size_t count) {
-  size_t bytes = count * sizeof(T);
+static bool is_cache_buf(const std::string& name) { return name.rfind("distcache", 0) == 0; }
+
+static void sync_all(gpar_ctx* c) {
+  for (hipStream_t st : {c->main, c->side, c->s_w, c->s_g, c->s_g2})
+    if (st) HIPCHECK(hipStreamSynchronize(st));
+}
+
+// Free distance-cache buffers, the highest slots first, until at least `bytes` are released
+// (INT64_MAX: all of them), once all queued work is done (nothing in flight can still read
+// them), and mark those slots gone: whiten_kfu_any checks the slot before every launch.
+// Returns the bytes freed.
+static int64_t release_dist_cache(gpar_ctx* c, int64_t bytes = INT64_MAX) {
+  int64_t freed = 0;
+  bool synced = false;
+  for (int s = (int)c->cache_valid.size() - 1; s >= 0 && freed < bytes; --s) {
+    auto it = c->bufs.find("distcache" + std::to_string(s));
+    if (it == c->bufs.end()) continue;
+    if (!synced) sync_all(c);
+    synced = true;
+    if (it->second.p) HIPCHECK(hipFree(it->second.p));
+    freed += (int64_t)it->second.bytes;
+    c->bufs.erase(it);
+    c->cache_valid[s] = 0;
+  }
+  return freed;
+}
+
+// Grow-only named workspace.  Out of memory: the distance cache is the one optional holder, so
+// its slots are evicted (the last ones first, as many as the request needs) and the allocation
+// retried (not for the cache's own buffers, which must not evict their siblings).
+static void* ws_bytes(gpar_ctx* c, const std::string& name, size_t bytes) {
   if (bytes == 0) bytes = 16;
+  const bool evict = !is_cache_buf(name);   // eviction erases cache entries (b below)
   auto& b = c->bufs[name];
   if (b.bytes < bytes) {
     if (b.p) HIPCHECK(hipFree(b.p));
     b.p = nullptr;
     b.bytes = 0;
-    HIPCHECK(hipMalloc(&b.p, bytes));
+    hipError_t e = hipMalloc(&b.p, bytes);
+    while (e == hipErrorOutOfMemory && evict) {
+      (void)hipGetLastError();
+      b.p = nullptr;
+      if (release_dist_cache(c, (int64_t)bytes) == 0) break;
+      ++c->cache_evictions;
+      e = hipMalloc(&b.p, bytes);
+    }
+    if (e != hipSuccess) {
+      (void)hipGetLastError();
+      b.p = nullptr;
+      throw Error(e == hipErrorOutOfMemory ? GPAR_ERR_OOM : GPAR_ERR_HIP,
+                  "hipMalloc(" + name + ", " + std::to_string(bytes) + " B): " + hipGetErrorString(e));
+    }
     b.bytes = bytes;
   }
-  return reinterpret_cast<T*>(b.p);
+  return b.p;
+}
+
+template <class T>
+static T* ws(gpar_ctx* c, const std::string& name, size_t count) {
+  return reinterpret_cast<T*>(ws_bytes(c, name, count * sizeof(T)));
 }
 
 template <class T>
@@ -224,7 +278,33 @@ struct DevProblem {
   // kernels (d2_is_r), so their square root is taken once per fit, not per evaluation
   const double* d2 = nullptr;
   bool d2_is_r = false;
+  int cache_slot = -1;   // its gpar_ctx::cache_valid entry (an OOM eviction clears it)
 };
+
+// The cached distances of p if they are still resident, else null (fused kernel).
+static const double* cached_d2(const gpar_ctx* c, const DevProblem& p) {
+  if (!p.d2 || p.cache_slot < 0 || p.cache_slot >= (int)c->cache_valid.size()) return nullptr;
+  return c->cache_valid[p.cache_slot] ? p.d2 : nullptr;
+}
+
+// Every problem of the batch shares the time grid (same caller pointer, n and SDE order): one
+// batched gains launch serves them all.
+static bool shares_grid(const std::vector<DevProblem>& P) {
+  for (auto& p : P)
+    if (p.t_user != P[0].t_user || p.n != P[0].n || p.sdim != P[0].sdim) return false;
+  return true;
+}
+
+// The one-lane pipelined Gram stage (run_gram_stage): several outputs on one grid, two beta
+// buffers (only when a second beta fits comfortably: the north job's 4.1 GB, not the N = 1e7,
+// M = 1024 stress config's 82 GB).  The CU split and the all-D distance cache apply only on top of it.
+static bool fit_pipelined(const gpar_ctx* c, const std::vector<DevProblem>& P, bool fix_beta = false) {
+  int64_t mpmax = 0;
+  for (auto& p : P) mpmax = std::max(mpmax, p.mp);
+  const int64_t beta_bytes = (P[0].n + 16) * mpmax * (int64_t)sizeof(double);
+  return P.size() > 1 && !fix_beta && c->lanes == 1 && shares_grid(P) && c->pipeline &&
+         beta_bytes <= kPipeMaxBetaBytes;
+}
 
 static void check_sorted_host(const double* t, int64_t n) {
   for (int64_t k = 1; k < n; ++k)
@@ -360,8 +440,9 @@ static void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const double* rec, 
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
                            int64_t ldb, double* send, const double* g, double* hsum) {
   const double s_o = th.sv_o * th.sv_o;
-  if (p.d2 && v == p.v) {   // the fit's training inputs, distances cached (fit_impl)
-    launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, p.d2, p.mp, p.m, p.mp, n, kChunk, nch,
+  const double* d2 = cached_d2(c, p);
+  if (d2 && v == p.v) {   // the fit's training inputs, distances cached (fit_impl)
+    launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, d2, p.mp, p.m, p.mp, n, kChunk, nch,
                          1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum, p.d2_is_r);
   } else if (p.d > kFusedMaxD) {
     launch_dist2(c->stream, p.ok, v, ldv, n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, beta, ldb);
@@ -413,9 +494,7 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     }
 
   // group problems sharing (t, n, time kernel) into one batched gains launch
-  bool shared = true;
-  for (auto& p : P)
-    if (p.t_user != P[0].t_user || p.n != n || p.sdim != P[0].sdim) shared = false;
+  const bool shared = shares_grid(P);
   std::vector<GainsOut> gains(np);
   // shared gains: every output's alpha_loc (y filtered from zero per chunk) comes out of the
   // gains pass itself; only its chunk end states are copied into the carry's alpha column
@@ -452,11 +531,8 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   // One lane, pipelined (the batched fit): the big kernels stay in order on the context stream,
   // whitening(i + 1) issued ahead of Gram(i), and output i's short chain between them (alpha's end
   // states, the chunk carry, vec_fix, the beta tail) runs on the side stream beside a whitening
-  // instead of on the critical path.  Two beta / carry buffers, so only when a second beta fits
-  // comfortably (the north job: 4.1 GB; the N = 1e7, M = 1024 stress config's 82 GB does not).
-  const int64_t beta_bytes = (n + 16) * mpmax * (int64_t)sizeof(double);
-  const bool pipe = nlanes == 1 && np > 1 && shared && !fix_beta && c->pipeline &&
-                    beta_bytes <= kPipeMaxBetaBytes;
+  // instead of on the critical path.  Two beta / carry buffers (fit_pipelined).
+  const bool pipe = fit_pipelined(c, P, fix_beta);
   const int nbuf = (nlanes > 1 || pipe) ? 2 : 1;
   double* beta_l[2];
   double* alpha_l[2];
@@ -513,7 +589,7 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     }
     // algorithmic HBM bytes: the inputs (V, or the cached distances), the gains records and
     // fix-up rows (16 + 4 doubles per step), beta written (m columns)
-    const double in_cols = p.d2 ? (double)p.m : (double)p.d;
+    const double in_cols = cached_d2(c, p) ? (double)p.m : (double)p.d;
     Timed tm_(c, "whiten", 8.0 * (double)n * (in_cols + (double)p.m + 20.0));
     whiten_kfu_any(c, p, gi[i].rec, p.v, p.ldv, n, nch, th[i], beta_l[b], p.mp, send_l[b], gi[i].g,
                    hsum_l[b]);
@@ -1228,9 +1304,11 @@ int64_t gpar_ctx_workspace_bytes(const gpar_ctx* ctx) {
 int32_t gpar_ctx_trim(gpar_ctx* ctx) {
   API_BEGIN(ctx)
   HIPCHECK(hipStreamSynchronize(ctx->stream));
+  sync_all(ctx);
   for (auto& kv : ctx->bufs)
     if (kv.second.p) HIPCHECK(hipFree(kv.second.p));
   ctx->bufs.clear();
+  std::fill(ctx->cache_valid.begin(), ctx->cache_valid.end(), 0);
   API_END(ctx)
 }
 
@@ -1302,6 +1380,42 @@ int32_t gpar_ctx_set_dist_cache(gpar_ctx* ctx, int64_t bytes) {
   API_END(ctx)
 }
 
+int32_t gpar_ctx_set_dist_cache_keep(gpar_ctx* ctx, int32_t keep) {
+  API_BEGIN(ctx)
+  ctx->dist_cache_keep = keep != 0;
+  if (!keep) release_dist_cache(ctx);
+  API_END(ctx)
+}
+
+int32_t gpar_ctx_dist_cache_stats(const gpar_ctx* ctx, int32_t* outputs_cached, int32_t* evictions,
+                                  int64_t* bytes_held) {
+  if (!ctx) return GPAR_ERR_STATE;
+  int64_t held = 0;
+  for (auto& kv : ctx->bufs)
+    if (is_cache_buf(kv.first)) held += (int64_t)kv.second.bytes;
+  if (outputs_cached) *outputs_cached = ctx->cache_outputs;
+  if (evictions) *evictions = ctx->cache_evictions;
+  if (bytes_held) *bytes_held = held;
+  return GPAR_OK;
+}
+
+int32_t gpar_pairwise_distances(gpar_ctx* ctx, const gpar_problem* prob, double* dist_out) {
+  API_BEGIN(ctx)
+  ARGCHECK(prob && dist_out, "null argument");
+  DevProblem p = prepare_problem(ctx, *prob, 0);
+  // the fit's distance-cache kernel, as gpar_fit fills a cache slot (attach_dist_cache)
+  double* d = ws<double>(ctx, "pw_dist", (size_t)p.n * p.mp);
+  launch_dist2(ctx->stream, p.ok, p.v, p.ldv, p.n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, d, p.mp,
+               /*take_sqrt=*/p.ok != GPAR_EQ);
+  check_launch("dist2 (pairwise)");
+  HIPCHECK(hipMemcpy2DAsync(dist_out, p.m * sizeof(double), d, p.mp * sizeof(double),
+                            p.m * sizeof(double), p.n,
+                            prob->mem == GPAR_MEM_DEVICE ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost,
+                            ctx->stream));
+  sync(ctx);
+  API_END(ctx)
+}
+
 int32_t gpar_ctx_reset_stats(gpar_ctx* ctx) {
   API_BEGIN(ctx)
   flush_stats(ctx);
@@ -1351,19 +1465,59 @@ constexpr int64_t kDistCacheMinD = 17;
 constexpr int64_t kDistCacheMinDSplit = 1;
 constexpr int64_t kDistCacheSplitMinN = (int64_t)1 << 16;
 
-static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<DevProblem>& P) {
+// Device bytes a batched fit's evaluations allocate besides the cache (run_gram_stage, run_dense,
+// the kept Grams): the cache's auto budget leaves room for them.
+static int64_t fit_ws_estimate(const gpar_ctx* c, const std::vector<DevProblem>& P) {
+  const int64_t np = (int64_t)P.size(), n = P[0].n, nch = (n + kChunk - 1) / kChunk;
+  int64_t mpmax = 0, rs = 4;
+  for (auto& p : P) {
+    mpmax = std::max(mpmax, p.mp);
+    rs = std::max<int64_t>(rs, rec_size(p.sdim));
+  }
+  const int64_t nbuf = (fit_pipelined(c, P) || c->lanes > 1) ? 2 : 1;
+  const GramPlan pl = gram_plan(n, mpmax, false, 256, 256);
+  const int64_t doubles = nbuf * ((n + 16) * mpmax + n + 3 * nch * (mpmax + 1) * 4)   // beta, carries
+                          + np * n * (rs + 5)                 // gains records, fix-up rows, alpha
+                          + 7 * np * mpmax * mpmax            // G, dense tail, kept Grams
+                          + 2 * (pl.part_doubles + pl.rpart_doubles);
+  return doubles * (int64_t)sizeof(double);
+}
+
+// The same for the prediction of a gpar_fit_predict call (predict_impl, merged grid of n + n_star).
+static int64_t predict_ws_estimate(int64_t n, int64_t n_star, int64_t mp, int64_t d, int mode,
+                                   int samples) {
+  const int64_t nt = n + n_star, nch = (nt + kChunk - 1) / kChunk;
+  int64_t doubles = nt * (mp + 64)                 // whitened Cf*u + y*
+                    + n_star * (mp + 8 + d)        // Q rows, mean / std, sorted test inputs
+                    + nt * (20 + 8 + d)            // gains records, grid, merged inputs
+                    + 4 * nch * (mp + 1) * 4       // carries
+                    + 8 * mp * mp;                 // q(u) dense
+  if (mode == GPAR_PREDICT_MC) doubles += n_star * mp + (int64_t)samples * mp + 2 * n_star * ((samples + 127) / 128);
+  return doubles * (int64_t)sizeof(double);
+}
+
+// later_bytes: what the call allocates after the cache (fit_ws_estimate + predict_ws_estimate).
+static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<DevProblem>& P,
+                                                 int64_t later_bytes) {
   std::vector<DevProblem> Q = P;
+  c->cache_outputs = 0;
   if (c->dist_cache_bytes == 0) return Q;
   // explicit budget: total cache bytes.  auto: new allocations take at most the free HBM less a
-  // reserve, and cache buffers the context already holds (an earlier call's) are reused at no
-  // cost -- counting them against the reserve again would drop outputs from the cache on every
-  // call after the first, once later phases (the predictions) have taken their workspace.
+  // reserve -- 1 % of the part plus the workspace the call still has to allocate (what the
+  // context already holds under other names is reused) -- and cache buffers the context already
+  // holds (gpar_ctx_set_dist_cache_keep) are reused at no cost.  Either way an allocation that
+  // fails stops the cache there, and a later workspace allocation that finds no memory evicts
+  // cache slots (ws_bytes), so the cache never turns into an out-of-memory failure.
   int64_t budget = c->dist_cache_bytes;
   int64_t fresh = INT64_MAX;
   if (budget < 0) {
     size_t fr = 0, tot = 0;
     HIPCHECK(hipMemGetInfo(&fr, &tot));
-    const int64_t reserve = std::max<int64_t>((int64_t)16 << 30, (int64_t)(tot / 10));
+    int64_t held_other = 0;
+    for (auto& kv : c->bufs)
+      if (!is_cache_buf(kv.first)) held_other += (int64_t)kv.second.bytes;
+    const int64_t need = std::max<int64_t>(0, later_bytes - held_other);
+    const int64_t reserve = std::max<int64_t>((int64_t)1 << 30, (int64_t)(tot / 100)) + need;
     fresh = std::max<int64_t>(0, (int64_t)fr - reserve);
     budget = INT64_MAX;
   }
@@ -1372,8 +1526,10 @@ static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<
   std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return P[a].d > P[b].d; });
   int64_t mpmax = 0;
   for (auto& p : P) mpmax = std::max(mpmax, p.mp);
-  const int64_t min_d = (P.size() > 1 && split_active(c, P[0].n, mpmax) && P[0].n >= kDistCacheSplitMinN)
-                            ? kDistCacheMinDSplit : kDistCacheMinD;
+  // every output (D >= 1) only where the whitening runs on the CU split's quarter of the chip,
+  // i.e. the pipelined split schedule actually runs (fit_pipelined && split_active)
+  const int64_t min_d = (fit_pipelined(c, P) && split_active(c, P[0].n, mpmax) &&
+                         P[0].n >= kDistCacheSplitMinN) ? kDistCacheMinDSplit : kDistCacheMinD;
   int slot = 0;
   for (int i : order) {
     const DevProblem& p = P[i];
@@ -1384,23 +1540,46 @@ static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<
     const int64_t held = it != c->bufs.end() ? (int64_t)it->second.bytes : 0;
     const int64_t need = held >= bytes ? 0 : bytes - held;   // ws() frees the smaller one first
     if (bytes > budget || need > fresh) continue;
+    double* d2 = nullptr;
+    try {
+      d2 = reinterpret_cast<double*>(ws_bytes(c, name, (size_t)bytes));
+    } catch (const Error& e) {
+      if (e.code != GPAR_ERR_OOM) throw;
+      c->bufs.erase(name);   // another tenant took the memory: cache what fits so far
+      break;
+    }
     budget -= bytes;
     fresh -= need;
-    ++slot;
-    double* d2 = ws<double>(c, name, (size_t)p.n * p.mp);
+    if ((int)c->cache_valid.size() <= slot) c->cache_valid.resize(slot + 1, 0);
+    c->cache_valid[slot] = 1;
     launch_dist2(c->stream, p.ok, p.v, p.ldv, p.n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, d2, p.mp,
                  /*take_sqrt=*/p.ok != GPAR_EQ);
     check_launch("dist2 (cache)");
     Q[i].d2 = d2;
     Q[i].d2_is_r = p.ok != GPAR_EQ;
+    Q[i].cache_slot = slot;
+    ++slot;
   }
+  c->cache_outputs = slot;
   return Q;
 }
 
 static void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* log_theta0,
                      const gpar_fit_options& o, double* theta_out, double* nlml_out,
-                     int32_t* evals_out, FitKeep* keep) {
-  const std::vector<DevProblem> P = attach_dist_cache(ctx, P0);
+                     int32_t* evals_out, FitKeep* keep, int64_t later_bytes = 0) {
+  // the cache lives for this fit call only, unless the caller keeps it (gpar_ctx_set_dist_cache_keep)
+  struct CacheRelease {
+    gpar_ctx* c;
+    ~CacheRelease() {
+      if (c->dist_cache_keep) return;
+      try {
+        release_dist_cache(c);
+      } catch (...) {
+      }
+    }
+  } release_{ctx};
+  const std::vector<DevProblem> P =
+      attach_dist_cache(ctx, P0, fit_ws_estimate(ctx, P0) + later_bytes);
   const int nprob = (int)P.size();
   std::vector<NelderMead> nm;
   nm.reserve(nprob);
@@ -1509,7 +1688,11 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
   std::vector<DevProblem> P;
   for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
   FitKeep keep;
-  fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, &keep);
+  // the predictions' workspace (named buffers, reused across the outputs: the largest counts)
+  int64_t pred_bytes = 0;
+  for (const auto& p : P)
+    pred_bytes = std::max(pred_bytes, predict_ws_estimate(p.n, n_star, p.mp, p.d, mode, samples));
+  fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, &keep, pred_bytes);
   const int mem = probs[0].mem;
   for (int i = 0; i < nprob; ++i) {
     const double* q = theta_out + 5 * i;

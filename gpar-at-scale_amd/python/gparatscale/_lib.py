@@ -27,7 +27,8 @@ EXPORTED = (
     "gpar_fit", "gpar_fit_predict", "gpar_fit_predict_chain", "gpar_mc_normals", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
     "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_kernel_work", "gpar_ctx_reset_stats",
-    "gpar_ctx_set_lanes", "gpar_ctx_set_cu_split", "gpar_ctx_get_cu_split", "gpar_ctx_set_dist_cache", "gpar_ctx_set_input_stream", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
+    "gpar_ctx_set_lanes", "gpar_ctx_set_cu_split", "gpar_ctx_get_cu_split", "gpar_ctx_set_dist_cache", "gpar_ctx_set_dist_cache_keep", "gpar_ctx_dist_cache_stats",
+    "gpar_pairwise_distances", "gpar_ctx_set_input_stream", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
 )
 
 
@@ -99,6 +100,9 @@ def load(path: str | None = None):
             "gpar_ctx_set_cu_split": (i32, [vp, i32]),
             "gpar_ctx_get_cu_split": (i32, [vp, C.POINTER(C.c_int32)]),
             "gpar_ctx_set_dist_cache": (i32, [vp, i64]),
+            "gpar_ctx_set_dist_cache_keep": (i32, [vp, i32]),
+            "gpar_ctx_dist_cache_stats": (i32, [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i64)]),
+            "gpar_pairwise_distances": (i32, [vp, C.POINTER(GparProblem), dp]),
             "gpar_ctx_set_input_stream": (i32, [vp, vp, i32]),
             "gpar_dtc_objective": (i32, [vp, C.POINTER(GparProblem), i32, dp, dp]),
             "gpar_dtc_objective_A": (i32, [vp, C.POINTER(GparProblem), dp, dp, dp]),
@@ -210,10 +214,12 @@ class Context:
         self.check(load().gpar_ctx_kernel_work(self.h, name.encode(), C.byref(w)))
         return float(w.value)
 
-    def follow_stream(self, stream_ptr):
+    def follow_stream(self, stream_ptr, enable=True):
         """Order every later call after the work queued on `stream_ptr` (a hipStream_t handle,
-        e.g. torch.cuda.current_stream().cuda_stream) at the time of the call."""
-        self.check(load().gpar_ctx_set_input_stream(self.h, C.c_void_p(int(stream_ptr)), 1))
+        e.g. torch.cuda.current_stream().cuda_stream) at the time of the call; enable=False
+        forgets the stream again (the handle is not kept)."""
+        self.check(load().gpar_ctx_set_input_stream(self.h, C.c_void_p(int(stream_ptr or 0)),
+                                                    1 if enable else 0))
 
     def reset_stats(self):
         self.check(load().gpar_ctx_reset_stats(self.h))
@@ -221,6 +227,20 @@ class Context:
     def set_dist_cache(self, nbytes=-1):
         """Byte budget of the fit's distance cache (gpar_ctx_set_dist_cache): -1 auto, 0 off."""
         self.check(load().gpar_ctx_set_dist_cache(self.h, int(nbytes)))
+
+    def set_dist_cache_keep(self, keep=True):
+        """Hold the distance cache past the fit call (gpar_ctx_set_dist_cache_keep); default off."""
+        self.check(load().gpar_ctx_set_dist_cache_keep(self.h, 1 if keep else 0))
+
+    def dist_cache_stats(self):
+        """(outputs cached by the last fit, OOM evictions so far, cache bytes held now)."""
+        o, e, b = C.c_int32(), C.c_int32(), C.c_int64()
+        self.check(load().gpar_ctx_dist_cache_stats(self.h, C.byref(o), C.byref(e), C.byref(b)))
+        return int(o.value), int(e.value), int(b.value)
+
+    def trim(self):
+        """Release the context's device workspace (gpar_ctx_trim)."""
+        self.check(load().gpar_ctx_trim(self.h))
 
     def set_lanes(self, lanes):
         """1 (the default): serial batched evaluation; 2: outputs alternate over two HIP streams."""

@@ -18,6 +18,7 @@ GPAR_MEM_DEVICE without host copies.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 from dataclasses import dataclass
 
@@ -130,11 +131,21 @@ def _dev_vec(x, keep):
     return x.data_ptr()
 
 
-def _order_after_torch(ctx):
+@contextlib.contextmanager
+def _after_torch(ctx, on=True):
     """Device inputs are produced on torch's current stream (a .contiguous() copy above may still
-    be in flight): the library's streams wait for it, device side, before the call's kernels."""
+    be in flight): for the calls inside the block the library's streams wait for it, device side,
+    before their kernels.  The stream is forgotten again on exit, so no later call (host-memory
+    ones included) touches a handle torch may since have freed."""
+    if not on:
+        yield
+        return
     import torch
     ctx.follow_stream(torch.cuda.current_stream(ctx.device).cuda_stream)
+    try:
+        yield
+    finally:
+        ctx.follow_stream(0, enable=False)
 
 
 def _arg_error(msg):
@@ -191,13 +202,12 @@ def compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel="matern52", time_ke
     p, keep = make_problem(V, Z, t, y, out_kernel, time_kernel, kuu_noise)
     th = np.ascontiguousarray(np.asarray(theta, dtype=np.float64).reshape(5))
     out = np.zeros(1)
-    if p.mem == _lib.GPAR_MEM_DEVICE:
-        _order_after_torch(ctx)
-    if return_A:
-        A = np.zeros((p.n, p.m))  # column-major M x N == row-major N x M
-        ctx.check(lib.gpar_dtc_objective_A(ctx.h, C.byref(p), _ptr(th), _ptr(out), _ptr(A)))
-        return float(out[0]), A.T.copy()
-    ctx.check(lib.gpar_dtc_objective(ctx.h, C.byref(p), 1, _ptr(th), _ptr(out)))
+    with _after_torch(ctx, p.mem == _lib.GPAR_MEM_DEVICE):
+        if return_A:
+            A = np.zeros((p.n, p.m))  # column-major M x N == row-major N x M
+            ctx.check(lib.gpar_dtc_objective_A(ctx.h, C.byref(p), _ptr(th), _ptr(out), _ptr(A)))
+            return float(out[0]), A.T.copy()
+        ctx.check(lib.gpar_dtc_objective(ctx.h, C.byref(p), 1, _ptr(th), _ptr(out)))
     return float(out[0])
 
 
@@ -208,9 +218,29 @@ def dtc_objective_batch(problems, thetas, device=0):
     arr = (GparProblem * len(problems))(*problems)
     th = np.ascontiguousarray(np.asarray(thetas, dtype=np.float64).reshape(len(problems), 5))
     out = np.zeros(len(problems))
-    if problems[0].mem == _lib.GPAR_MEM_DEVICE:
-        _order_after_torch(ctx)
-    ctx.check(lib.gpar_dtc_objective(ctx.h, arr, len(problems), _ptr(th), _ptr(out)))
+    with _after_torch(ctx, problems[0].mem == _lib.GPAR_MEM_DEVICE):
+        ctx.check(lib.gpar_dtc_objective(ctx.h, arr, len(problems), _ptr(th), _ptr(out)))
+    return out
+
+
+def pairwise_distances(V, Z, out_kernel="matern52", device=0):
+    """The distances Kfu = pairwise(k_o, V, Z) is built from (dtc.jl:104), as the fit's distance
+    cache holds them (gpar_pairwise_distances): |v_k - z_c| for the Matern kernels, squared for
+    EQ; N x M.  Host V / Z (D x N / D x M ColVecs) or device tensors (rows = points)."""
+    ctx, lib = context(device), _lib.load()
+    if _is_torch(V):
+        import torch
+        n = V.shape[0]
+        t = torch.arange(n, dtype=torch.float64, device=V.device)
+        p, keep = make_problem(V, Z, t, torch.zeros_like(t), out_kernel)
+        out = torch.empty((n, p.m), dtype=torch.float64, device=V.device)
+        with _after_torch(ctx):
+            ctx.check(lib.gpar_pairwise_distances(ctx.h, C.byref(p), C.c_void_p(out.data_ptr())))
+        return out
+    n = to_colvecs(V).shape[1]
+    p, keep = make_problem(V, Z, np.arange(n, dtype=np.float64), np.zeros(n), out_kernel)
+    out = np.zeros((n, p.m))
+    ctx.check(lib.gpar_pairwise_distances(ctx.h, C.byref(p), _ptr(out)))
     return out
 
 
@@ -234,10 +264,9 @@ def fit_batch(problems, log_theta0, max_evals=0, max_iterations=1000, g_tol=1e-8
     theta = np.zeros((P, 5))
     nlml = np.zeros(P)
     evals = np.zeros(P, dtype=np.int32)
-    if problems[0].mem == _lib.GPAR_MEM_DEVICE:
-        _order_after_torch(ctx)
-    ctx.check(lib.gpar_fit(ctx.h, arr, P, _ptr(x0), C.byref(opts), _ptr(theta), _ptr(nlml),
-                           _ptr(evals)))
+    with _after_torch(ctx, problems[0].mem == _lib.GPAR_MEM_DEVICE):
+        ctx.check(lib.gpar_fit(ctx.h, arr, P, _ptr(x0), C.byref(opts), _ptr(theta), _ptr(nlml),
+                               _ptr(evals)))
     return FitResult(theta, nlml, evals)
 
 
@@ -321,25 +350,24 @@ def fit_predict_batch(problems, log_theta0, t_star, V_stars, max_evals=0, max_it
         sp_ = [x.ctypes.data for x in stds]
     ns = n_star
     ctx, lib = context(device), _lib.load()
-    if dev:
-        _order_after_torch(ctx)
     VP = (C.c_void_p * P)(*vptr)
     LD = (C.c_int64 * P)(*ldvs)
     MP = (C.c_void_p * P)(*mp_)
     SP = (C.c_void_p * P)(*sp_)
     md = _lib.GPAR_PREDICT_MC if mode == "mc" else _lib.GPAR_PREDICT_ANALYTIC
-    if chain is None:
-        ctx.check(lib.gpar_fit_predict(ctx.h, arr, P, _ptr(x0), C.byref(opts), ns, tsp, VP, LD, md,
-                                       int(samples), int(seed), _ptr(theta), _ptr(nlml), _ptr(evals),
-                                       MP, SP))
-    else:
-        if dev and chain.shape[0] != n_star:
-            raise _arg_error("chain must have N* rows")
-        CC = (C.c_int32 * P)(*[int(c) for c in chain_cols])
-        ctx.check(lib.gpar_fit_predict_chain(ctx.h, arr, P, _ptr(x0), C.byref(opts), ns, tsp, VP, LD,
-                                             md, int(samples), int(seed), C.c_void_p(chain_ptr),
-                                             int(ld_chain), CC, _ptr(theta), _ptr(nlml),
-                                             _ptr(evals), MP, SP))
+    if chain is not None and dev and chain.shape[0] != n_star:
+        raise _arg_error("chain must have N* rows")
+    with _after_torch(ctx, dev):
+        if chain is None:
+            ctx.check(lib.gpar_fit_predict(ctx.h, arr, P, _ptr(x0), C.byref(opts), ns, tsp, VP, LD,
+                                           md, int(samples), int(seed), _ptr(theta), _ptr(nlml),
+                                           _ptr(evals), MP, SP))
+        else:
+            CC = (C.c_int32 * P)(*[int(c) for c in chain_cols])
+            ctx.check(lib.gpar_fit_predict_chain(ctx.h, arr, P, _ptr(x0), C.byref(opts), ns, tsp, VP,
+                                                 LD, md, int(samples), int(seed),
+                                                 C.c_void_p(chain_ptr), int(ld_chain), CC,
+                                                 _ptr(theta), _ptr(nlml), _ptr(evals), MP, SP))
     return FitResult(theta, nlml, evals), means, stds
 
 
@@ -383,9 +411,8 @@ def compute_q_u(input_locations, pseudo_input_locations, time_loc, outputs, thet
     me = np.zeros(m)
     cov = np.zeros((m, m))
     U = np.zeros((m, m))  # column-major -> read as transposed
-    if p.mem == _lib.GPAR_MEM_DEVICE:
-        _order_after_torch(ctx)
-    ctx.check(lib.gpar_q_u(ctx.h, C.byref(p), _ptr(th), _ptr(me), _ptr(cov), _ptr(U)))
+    with _after_torch(ctx, p.mem == _lib.GPAR_MEM_DEVICE):
+        ctx.check(lib.gpar_q_u(ctx.h, C.byref(p), _ptr(th), _ptr(me), _ptr(cov), _ptr(U)))
     return me, cov, U.T.copy()
 
 
@@ -447,11 +474,11 @@ def predict_scaled(input_locations, pseudo_input_locations, time_loc, outputs, t
         if ns != inference_time_loc.numel() or ds != p.d:
             raise _arg_error("inference inputs must be N* x D with N* = len(inference_time_loc)")
         ctx, lib = context(device), _lib.load()
-        _order_after_torch(ctx)
         mean = torch.empty(ns, dtype=torch.float64, device=inference_time_loc.device)
         std = torch.empty(ns, dtype=torch.float64, device=inference_time_loc.device)
-        ctx.check(lib.gpar_predict(ctx.h, C.byref(p), _ptr(th), ns, tsp, vsp, ldvs, md,
-                                   int(samples), int(seed), mean.data_ptr(), std.data_ptr()))
+        with _after_torch(ctx):
+            ctx.check(lib.gpar_predict(ctx.h, C.byref(p), _ptr(th), ns, tsp, vsp, ldvs, md,
+                                       int(samples), int(seed), mean.data_ptr(), std.data_ptr()))
         return mean, std
     vsp, ldvs, ns, ds = _host_points(inference_input_locations, keep)
     tsp = _host_vec(inference_time_loc, keep)
@@ -555,11 +582,11 @@ def get_sde_predictions_device(t, Y, t_star, kernel_structure="matern52", log_th
         raise _arg_error("t and Y must have the same length")
     ts_ = _dev_vec(t_star, keep)
     tt_ = _dev_vec(t, keep)
-    _order_after_torch(ctx)
-    ctx.check(lib.gpar_sde_predictions(ctx.h, nch, n, tt_, Y2.data_ptr(), n, ns,
-                                       ts_, _kernel_id(kernel_structure),
-                                       _ptr(x0), C.byref(opts), _lib.GPAR_MEM_DEVICE, _ptr(theta),
-                                       mean.data_ptr(), var.data_ptr()))
+    with _after_torch(ctx):
+        ctx.check(lib.gpar_sde_predictions(ctx.h, nch, n, tt_, Y2.data_ptr(), n, ns,
+                                           ts_, _kernel_id(kernel_structure),
+                                           _ptr(x0), C.byref(opts), _lib.GPAR_MEM_DEVICE,
+                                           _ptr(theta), mean.data_ptr(), var.data_ptr()))
     if nch == 1:
         return tuple(theta[0]), mean[0], var[0]
     return theta, mean, var

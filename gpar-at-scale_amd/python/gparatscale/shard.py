@@ -13,22 +13,19 @@ import heapq
 
 import numpy as np
 
-# Per-objective-evaluation cost model of output p (ms at N=1e6, M=512 on one MI355X,
-# profiles/rocprof_bench_r02f_north_stats.csv): the Gram beta^T beta is independent of the input
-# dimension D = p - 1; the whitening is the fused kernel for D <= 16 and reads the fit's distance
-# cache above (D-independent, plus the one-off distance pass spread over the fit's evaluations);
-# the dense tail, carries and gains add ~0.9; the temporal-only output 1 is ~20x cheaper.  Only
-# relative sizes matter.
-GRAM_MS = 4.4
-WHITEN_FUSED_MS, WHITEN_CACHED_MS = 1.50, 1.56
-OTHER_MS = 0.9
+# Per-objective-evaluation cost of output p at the north config on one MI355X (bench r02x,
+# profiles/rocprof_bench_r02x_north_stats.csv): the batched fit whitens every GPAR output beside
+# the previous output's Gram on the CU split, with every output's distances cached (N >= 2^16,
+# include/gpar_hip.h gpar_ctx_set_dist_cache), so one output-evaluation costs the Gram's span,
+# ~5.1 ms, whatever the input dimension D = p - 1; the dense tail, carries and gains add ~0.1.
+# The temporal-only output 1 is ~20x cheaper.  Only relative sizes matter: LPT then deals the
+# GPAR outputs evenly (8 GPUs: seven ranks with 8 of them, one with 7 plus output 1).
+OUTPUT_EVAL_MS = 5.2
 SDE_MS = 0.4
 
 
 def output_cost(p: int) -> float:
-    if p == 1:
-        return SDE_MS
-    return GRAM_MS + OTHER_MS + (WHITEN_FUSED_MS if p - 1 < 17 else WHITEN_CACHED_MS)
+    return SDE_MS if p == 1 else OUTPUT_EVAL_MS
 
 
 def assign_outputs(P: int, world: int) -> list[list[int]]:

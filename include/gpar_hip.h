@@ -3,8 +3,8 @@
  *
  * The reference (TudorParas/GPAR-at-scale) is a Julia package whose hot path is a set
  * of plain Julia functions.  Each entry point below replaces one of them; the Julia
- * `ccall` binding a maintainer would add is in INTEGRATION.md, the Python ctypes
- * mirror is gpar-at-scale_amd/python/gparatscale/.
+ * `ccall` binding a maintainer would add is julia/GPARatScaleHIP.jl (INTEGRATION.md explains
+ * how to wire it in), the Python ctypes mirror is gpar-at-scale_amd/python/gparatscale/.
  *
  * Conventions
  *   - return value: gpar_status (0 = OK); gpar_last_error(ctx) describes the failure.
@@ -129,13 +129,31 @@ int32_t gpar_ctx_set_lanes(gpar_ctx* ctx, int32_t lanes);
 int32_t gpar_ctx_set_cu_split(gpar_ctx* ctx, int32_t cus_per_xcd);
 /* The CU split in effect (0 when off or unsupported). */
 int32_t gpar_ctx_get_cu_split(const gpar_ctx* ctx, int32_t* cus_per_xcd);
-/* Distance cache of gpar_fit / gpar_fit_predict: the squared input distances |v_k - z_c|^2 are
- * theta-independent, so for outputs with D >= 17 they are computed once per fit call (N x Mp
- * doubles per output, widest outputs first) and every objective evaluation's whitening reads them
- * instead of rebuilding them.  bytes = -1 (the default): budget = free device memory less a
- * reserve (max(16 GiB, 10 % of HBM)); 0: off; > 0: that budget.  The buffers stay in the
- * context's workspace (gpar_ctx_trim releases them). */
+/* Distance cache of gpar_fit / gpar_fit_predict: the input distances |v_k - z_c| (squared for EQ)
+ * are theta-independent, so they are computed once per fit call (N x Mp doubles per output, widest
+ * outputs first) and every objective evaluation's whitening reads them instead of rebuilding them
+ * inside the fused kernel.  Which outputs: D >= 17; every output (D >= 1) in a batched fit over
+ * N >= 2^16 points that runs the pipelined CU-split schedule (gpar_ctx_set_cu_split), where the
+ * whitening has a quarter of the chip.  bytes = -1 (the default): the budget is the free device
+ * memory less 1 % of the part and less the workspace the call still has to allocate (the fit's,
+ * and gpar_fit_predict's predictions'); 0: off; > 0: that budget.  A cache allocation that fails
+ * stops the cache there, and a later workspace allocation that finds no memory evicts cache slots
+ * and retries, so the cache never turns into an out-of-memory failure.  The cached distances are
+ * the same Gram-form values the fused kernel builds, in another summation order: results agree
+ * with an uncached fit to the last bits (fitted theta rtol 1e-9), and gpar_fit_predict, which
+ * reuses the fit's Gram at the fitted theta for q(u), can then differ from gpar_predict in the
+ * last bits.  Device memory taken by the cache is not visible to other allocators in the process
+ * (torch's caching allocator) while the fit runs. */
 int32_t gpar_ctx_set_dist_cache(gpar_ctx* ctx, int64_t bytes);
+/* keep = 0 (the default): the cache is released when the fit call returns.  keep = 1: the buffers
+ * stay in the context's workspace and the next fit reuses them (no re-allocation), evictable by
+ * any later allocation that runs out of memory; gpar_ctx_trim or keep = 0 releases them. */
+int32_t gpar_ctx_set_dist_cache_keep(gpar_ctx* ctx, int32_t keep);
+/* outputs_cached: outputs the last fit call cached; evictions: cache slots evicted by
+ * out-of-memory retries since the context was created; bytes_held: cache bytes held now.
+ * Any pointer may be NULL. */
+int32_t gpar_ctx_dist_cache_stats(const gpar_ctx* ctx, int32_t* outputs_cached, int32_t* evictions,
+                                  int64_t* bytes_held);
 /* Producer ordering for GPAR_MEM_DEVICE inputs: with enable = 1, every later call on ctx first
  * makes its streams wait (device side, hipStreamWaitEvent) for all work queued so far on
  * `stream` (a hipStream_t; 0 = the null stream), e.g. the copies that produced its device inputs
@@ -154,6 +172,13 @@ int32_t gpar_dtc_objective(gpar_ctx* ctx, const gpar_problem* probs, int32_t npr
  * Materialises A: intended for parity checks at modest N*M. */
 int32_t gpar_dtc_objective_A(gpar_ctx* ctx, const gpar_problem* prob, const double* theta,
                              double* dtc_out, double* A_out);
+
+/* The distances Kfu = pairwise(k_o, V, Z) is built from (dtc.jl:104; Stheno evaluates k_o on
+ * Distances.jl's pairwise distances), as the fit's distance cache holds them: dist_out[k*m + c] =
+ * |v_k - z_c| for the Matern output kernels (Gram form |v|^2 + |z|^2 - 2 v.z about per-256-column
+ * centres, clamped at 0, for Matern-3/2 / 5/2; direct differences for Matern-1/2) and the squared
+ * distance for EQ.  n x m, in prob->mem.  For parity checks of the cache. */
+int32_t gpar_pairwise_distances(gpar_ctx* ctx, const gpar_problem* prob, double* dist_out);
 
 /* ---------------------------------------------------------------- fit
  * Replaces get_optim_scaled_gpar_params (src/gp/dtc.jl:11-77): Nelder-Mead over the 5

@@ -1,4 +1,4 @@
-"""The fit's distance cache (gpar_ctx_set_dist_cache): the squared input distances are
+"""The fit's distance cache (gpar_ctx_set_dist_cache): the input distances are
 theta-independent, so gpar_fit computes them once per call for outputs with D >= 17 and the
 whitening reads them instead of rebuilding them in the fused kernel.  Same objective to rounding
 (both use the centred Gram form, in a different summation order), so the same Nelder-Mead
@@ -57,3 +57,157 @@ def test_cache_budget_argument():
     ctx = G.context(0)
     with pytest.raises(G.DomainError):
         ctx.set_dist_cache(-2)
+
+
+# ---------------------------------------------------------------- the all-D cache of split fits
+def _split_batch(kernel, n=70_000, m=64, dims=(1, 4, 16)):
+    t, Y = O.synthetic_gpar(n, max(dims) + 1, seed=53, noise=0.3)
+    probs, keep, data = [], [], []
+    for d in dims:
+        V = np.ascontiguousarray(Y[:, :d].T)
+        Z = O.pick_pseudo_inputs(V, m, 100 + d)
+        pr, k = G.make_problem(V, Z, t, Y[:, d], kernel, "matern52")
+        probs.append(pr)
+        keep.append(k)
+        data.append((V, Z, Y[:, d]))
+    return t, probs, keep, data
+
+
+@pytest.mark.parametrize("kernel", ["matern52", "eq", "matern12"])
+def test_split_fit_caches_every_output(kernel):
+    """With the CU split on and N >= 2^16 the fit caches outputs down to D = 1 (gpar_host.cpp
+    attach_dist_cache): the small-D cached path (group-centred Gram-form distances, or direct
+    differences for Matern-1/2) against the same split fit without the cache, and one output's
+    objective at the fitted theta against the C port (dtc.jl:83-128)."""
+    from oracle import cpu_ref as CR
+    CR.load()
+    t, probs, keep, data = _split_batch(kernel)
+    ctx = G.context(0)
+    x0 = np.tile(X0, (len(probs), 1))
+    try:
+        ctx.set_cu_split(8)
+        ctx.set_dist_cache(-1)
+        on = G.fit_batch(probs, x0, max_evals=25, g_tol=-1.0)
+        assert ctx.dist_cache_stats()[0] == len(probs)
+        assert ctx.dist_cache_stats()[2] == 0          # released when the fit returned
+        ctx.set_dist_cache(0)
+        off = G.fit_batch(probs, x0, max_evals=25, g_tol=-1.0)
+        assert ctx.dist_cache_stats()[0] == 0
+    finally:
+        ctx.set_cu_split(-1)
+        ctx.set_dist_cache(-1)
+    np.testing.assert_allclose(on.theta, off.theta, rtol=1e-9)
+    np.testing.assert_allclose(on.nlml, off.nlml, rtol=1e-12)
+    V, Z, y = data[0]                                   # D = 1
+    ref, _ = CR.compute_gpar_dtc_objective(V, Z, t, y, on.theta[0], kernel, "matern52")
+    assert abs(-on.nlml[0] - ref) <= 1e-9 * abs(ref), (-on.nlml[0], ref)
+
+
+@pytest.mark.parametrize("kernel", ["matern52", "eq", "matern12"])
+def test_cached_distances_match_direct_differences(kernel):
+    """gpar_pairwise_distances = the cache's kernel (dist2) at D = 1..16 against direct
+    differences.  The Gram form |v - c|^2 + |z - c|^2 - 2 (v - c).(z - c) about per-256-column
+    centres c loses |r^2| to cancellation by ~eps (|v - c|^2 + |z - c|^2); so r^2 is checked to
+    32 eps of that scale everywhere, and r to rel 1e-12 wherever r^2 >= 1e-3 of it."""
+    t, Y = O.synthetic_gpar(20_000, 17, seed=57, noise=0.3)
+    eps = np.finfo(np.float64).eps
+    for d in range(1, 17):
+        V = np.ascontiguousarray(Y[:, :d].T)
+        Z = O.pick_pseudo_inputs(V, 300, 200 + d)          # Mp = 384: two centre groups
+        got = G.pairwise_distances(V, Z, kernel)
+        diff = V.T[:, None, :] - Z.T[None, :, :]
+        r2 = np.einsum("kcd,kcd->kc", diff, diff)
+        if kernel == "matern12":                            # direct differences on the device too
+            # (sqrt_pos floors r at 1e-100 where v = z: kappa(1e-100 / l) = 1 exactly)
+            np.testing.assert_allclose(got, np.sqrt(r2), rtol=1e-14, atol=2e-100)
+            continue
+        g2 = got if kernel == "eq" else got * got
+        scale = (np.einsum("dk,dk->k", V, V).max() + np.einsum("dc,dc->c", Z, Z).max())
+        assert np.abs(g2 - r2).max() <= 32 * eps * scale, (d, np.abs(g2 - r2).max(), scale)
+        big = r2 >= 1e-3 * scale
+        assert big.mean() > 0.5
+        r_got = np.sqrt(g2[big])
+        np.testing.assert_allclose(r_got, np.sqrt(r2[big]), rtol=1e-12)
+
+
+def test_cache_survives_memory_pressure():
+    """A nearly full device (a blocker tensor) with an oversized explicit cache budget: the cache
+    takes what it can, the fit's own workspace then runs out of memory and evicts cache slots
+    (ws_bytes), and gpar_fit_predict completes with the unconstrained run's results."""
+    import torch
+    n, m = 200_000, 256
+    t, probs, keep, data = _split_batch("matern52", n=n, m=m, dims=(2, 8, 20, 40))
+    ts = np.linspace(t[0], t[-1], 5000) + 1e-3
+    Vs = [np.vstack([np.interp(ts, t, V[q]) for q in range(V.shape[0])]) for V, _, _ in data]
+    x0 = np.tile(X0, (len(probs), 1))
+    ctx = G.context(0)
+    cache_bytes = n * m * 8
+    blocker = None
+    try:
+        ctx.set_cu_split(8)
+        ctx.set_dist_cache(0)
+        ctx.trim()
+        ref, rm, rs = G.fit_predict_batch(probs, x0, ts, Vs, max_evals=12, g_tol=-1.0)
+        work = ctx.workspace_bytes()                  # the call's workspace without the cache
+        ctx.trim()
+        torch.cuda.empty_cache()
+        free = torch.cuda.mem_get_info(0)[0]
+        # leave the workspace plus 1.5 cache slots: the cache fills what it can, the workspace
+        # allocations then evict
+        leave = work + int(1.5 * cache_bytes)
+        blocker = torch.empty(free - leave, dtype=torch.uint8, device="cuda:0")
+        ctx.set_dist_cache(1 << 40)                   # explicit: far more than is free
+        ev0 = ctx.dist_cache_stats()[1]
+        got, gm, gs = G.fit_predict_batch(probs, x0, ts, Vs, max_evals=12, g_tol=-1.0)
+        cached, ev1, held = ctx.dist_cache_stats()
+    finally:
+        del blocker
+        torch.cuda.empty_cache()
+        ctx.set_cu_split(-1)
+        ctx.set_dist_cache(-1)
+        ctx.trim()
+    assert cached >= 1, cached
+    assert ev1 > ev0, (ev0, ev1)
+    np.testing.assert_allclose(got.theta, ref.theta, rtol=1e-9)
+    np.testing.assert_allclose(got.nlml, ref.nlml, rtol=1e-12)
+    for a, b in zip(gm + gs, rm + rs):
+        np.testing.assert_allclose(a, b, rtol=1e-8, atol=1e-10 * np.abs(b).max())
+
+
+def test_cache_auto_budget_under_memory_pressure():
+    """The auto budget reads the free memory net of the workspace the call still needs: with
+    room for the workspace, the 1 % reserve and about two slots, the fit caches what fits, needs no
+    eviction, and matches the uncached run."""
+    import torch
+    n, m = 200_000, 256
+    t, probs, keep, data = _split_batch("matern52", n=n, m=m, dims=(2, 8, 20, 40))
+    x0 = np.tile(X0, (len(probs), 1))
+    ctx = G.context(0)
+    cache_bytes = n * m * 8
+    blocker = None
+    try:
+        ctx.set_cu_split(8)
+        ctx.set_dist_cache(0)
+        ctx.trim()
+        ref = G.fit_batch(probs, x0, max_evals=12, g_tol=-1.0)
+        work = ctx.workspace_bytes()                  # the fit's workspace without the cache
+        ctx.trim()
+        torch.cuda.empty_cache()
+        free, total = torch.cuda.mem_get_info(0)
+        reserve = max(1 << 30, total // 100)
+        leave = reserve + work + int(2.5 * cache_bytes)
+        blocker = torch.empty(free - leave, dtype=torch.uint8, device="cuda:0")
+        ctx.set_dist_cache(-1)
+        ev0 = ctx.dist_cache_stats()[1]
+        got = G.fit_batch(probs, x0, max_evals=12, g_tol=-1.0)
+        cached, ev1, _ = ctx.dist_cache_stats()
+    finally:
+        del blocker
+        torch.cuda.empty_cache()
+        ctx.set_cu_split(-1)
+        ctx.set_dist_cache(-1)
+        ctx.trim()
+    assert 1 <= cached < len(probs), cached
+    assert ev1 == ev0
+    np.testing.assert_allclose(got.theta, ref.theta, rtol=1e-9)
+    np.testing.assert_allclose(got.nlml, ref.nlml, rtol=1e-12)
