@@ -13,6 +13,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <functional>
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
@@ -50,6 +51,18 @@ struct gpar_ctx {
   std::vector<char> cache_valid;
   int32_t cache_outputs = 0;      // outputs the last fit call cached
   int32_t cache_evictions = 0;    // OOM evictions since the context was created
+  // Pinned upload arenas of the round-overlapping fit (fit_overlapped): with `staging` set, h2d
+  // copies through it, so an upload queued behind running work never blocks the host (a
+  // pageable-memory copy may wait for its stream).  One arena per output group, reset when that
+  // group's previous round has been consumed.
+  struct Staging {
+    char* host = nullptr;
+    size_t cap = 0, used = 0;
+  };
+  Staging stage[2];
+  Staging* staging = nullptr;
+  bool overlap = true;            // gpar_ctx_set_fit_overlap (GPAR_OVERLAP=0 at creation): A/B
+  hipEvent_t ev_grp[2] = {nullptr, nullptr};   // fit_overlapped: a group's values are in
   std::string err;
   struct Buf {
     void* p = nullptr;
@@ -199,7 +212,18 @@ static T* ws(gpar_ctx* c, const std::string& name, size_t count) {
 
 template <class T>
 static void h2d(gpar_ctx* c, T* dst, const T* src, size_t count) {
-  if (count) HIPCHECK(hipMemcpyAsync(dst, src, count * sizeof(T), hipMemcpyHostToDevice, c->stream));
+  if (!count) return;
+  const size_t bytes = count * sizeof(T);
+  if (c->staging) {   // through the pinned arena: never waits for the stream
+    gpar_ctx::Staging& s = *c->staging;
+    const size_t off = (s.used + 255) & ~(size_t)255;
+    if (off + bytes > s.cap) throw Error(GPAR_ERR_STATE, "upload staging arena exhausted");
+    std::memcpy(s.host + off, src, bytes);
+    s.used = off + bytes;
+    HIPCHECK(hipMemcpyAsync(dst, s.host + off, bytes, hipMemcpyHostToDevice, c->stream));
+    return;
+  }
+  HIPCHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, c->stream));
 }
 template <class T>
 static void d2h(gpar_ctx* c, T* dst, const T* src, size_t count) {
@@ -463,6 +487,188 @@ struct GramOut {
   int64_t ldg, npart;
 };
 
+// Workspace of one Gram-stage buffer (two when outputs are pipelined or laned): beta (n + 16 rows,
+// the Gram's LDS-DMA reads whole 16-row K-steps), alpha (outputs whose gains are not shared), the
+// chunk states and the Gram's chunk-correction inputs.
+struct StageBufs {
+  int idx;   // 0 / 1: workspace names, carry tags
+  double *beta, *alpha, *send, *cin, *hsum, *qv;
+};
+
+static StageBufs stage_bufs(gpar_ctx* c, int l, int64_t n, int64_t mpmax) {
+  const int64_t nch = (n + kChunk - 1) / kChunk;
+  const std::string sfx = l ? "_1" : "";
+  StageBufs b;
+  b.idx = l;
+  b.beta = ws<double>(c, "beta" + sfx, (size_t)(n + 16) * mpmax);
+  b.alpha = ws<double>(c, "alpha" + sfx, (size_t)n);
+  b.send = ws<double>(c, "send" + sfx, (size_t)nch * (mpmax + 1) * 4);
+  b.cin = ws<double>(c, "cin" + sfx, (size_t)nch * (mpmax + 1) * 4);
+  b.hsum = ws<double>(c, "hsum" + sfx, (size_t)nch * (mpmax + 1) * 4);
+  b.qv = ws<double>(c, "qv" + sfx, (size_t)nch * 4);
+  return b;
+}
+
+// One output-evaluation in the Gram stage: the problem at hyperparameters th with its gains;
+// alpha = L_Sigma^-1 y (asend: its chunk end states from the batched gains pass, which filtered
+// alpha_loc already; null: alpha is whitened in stage_post into alpha); where G / r / the
+// alpha^2 partials go.  group / last: the round-overlapping fit's bookkeeping.
+struct StageJob {
+  const DevProblem* p = nullptr;
+  const Theta* th = nullptr;
+  GainsOut gi{};
+  double* alpha = nullptr;
+  const double* asend = nullptr;
+  double *G = nullptr, *r = nullptr, *a2part = nullptr;
+  int64_t ldg = 0;
+  int group = -1;
+  bool last = false;
+};
+
+// Kfu assembly + chunk-local whitening of j's output into b.beta, on c->stream.
+static void stage_whiten(gpar_ctx* c, const StageJob& j, const StageBufs& b) {
+  const DevProblem& p = *j.p;
+  // algorithmic HBM bytes: the inputs (V, or the cached distances), the gains records and
+  // fix-up rows (16 + 4 doubles per step), beta written (m columns)
+  const double in_cols = cached_d2(c, p) ? (double)p.m : (double)p.d;
+  Timed tm_(c, "whiten", 8.0 * (double)p.n * (in_cols + (double)p.m + 20.0));
+  whiten_kfu_any(c, p, j.gi.rec, p.v, p.ldv, p.n, p.nch, *j.th, b.beta, p.mp, b.send, j.gi.g,
+                 b.hsum);
+  check_launch("whiten_kfu");
+}
+
+// The short chain between a whitening and its Gram, on c->stream: alpha's chunk end states, the
+// chunk carry, vec_fix (alpha fix-up, the Gram's correction E_j = H_j + W_j C_j / 2 and q_j), the
+// beta tail (and the beta fix-up pass when fix_beta).
+static void stage_post(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_beta) {
+  const DevProblem& p = *j.p;
+  const int64_t n = p.n, nch = p.nch;
+  if (j.asend) {   // alpha's chunk end states -> column mp of the carry input
+    HIPCHECK(hipMemcpy2DAsync(b.send + (size_t)p.mp * kSStride, (size_t)p.mc * kSStride * sizeof(double),
+                              j.asend, kSStride * sizeof(double), kSStride * sizeof(double), nch,
+                              hipMemcpyDeviceToDevice, c->stream));
+  } else {
+    launch_whiten_vec(c->stream, p.sdim, j.gi.rec, 0, p.y, 0, n, kChunk, nch, 1, j.alpha, 0, b.send,
+                      0, p.mc, p.mp);
+  }
+  check_launch("whiten_vec");
+  run_carry(c, p.sdim, j.gi.phi, 0, b.send, b.cin, 0, nch, p.mc, p.mc, 1,
+            b.idx ? "fitc_1" : "fitc");
+  check_launch("carry");
+  launch_vec_fix(c->stream, p.sdim, j.alpha, 0, j.gi.g, 0, b.cin, 0, p.mc, p.mp, n, kChunk, 1,
+                 j.a2part, fix_beta ? nullptr : b.hsum, p.mp, b.qv);
+  check_launch("vec_fix");
+  if (fix_beta) {
+    launch_beta_fix(c->stream, p.sdim, b.beta, p.mp, n, j.gi.g, b.cin, p.mc, kChunk);
+    check_launch("beta_fix");
+  }
+  HIPCHECK(hipMemsetAsync(b.beta + (size_t)n * p.mp, 0, (size_t)16 * p.mp * sizeof(double), c->stream));
+}
+
+// G = beta^T beta, r = beta^T alpha of j on c->stream, which may use `cus` CUs; side: the stream of
+// the co-running chunk correction; st_w: the first w_frac32 / 32 of the DG kernel's work items run
+// there (ev_w joins them).  one_per_cu: the two-lane plan (one Gram workgroup per CU).
+static void stage_gram(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_beta,
+                       bool one_per_cu, const std::string& part_sfx, hipStream_t side, int cus,
+                       hipStream_t st_w = nullptr, hipEvent_t ev_w = nullptr, int w_frac32 = 0) {
+  const DevProblem& p = *j.p;
+  const GramPlan plan = gram_plan(p.n, p.mp, one_per_cu, cus, st_w ? 256 : cus);
+  const int w_items = st_w ? plan.ndg * plan.sdg * w_frac32 / 32 : 0;
+  double* part = ws<double>(c, "gram_part" + part_sfx, (size_t)plan.part_doubles);
+  double* rpart = ws<double>(c, "gram_rpart" + part_sfx, (size_t)plan.rpart_doubles);
+  {
+    Timed tm_(c, "gram", (double)p.n * (double)p.m * (double)(p.m + 1));   // flops of beta^T beta
+    launch_gram(c->stream, p.sdim, plan, b.beta, p.mp, p.n, fix_beta ? nullptr : b.hsum, b.cin,
+                b.qv, p.mc, kChunk, j.alpha, part, rpart, j.G, j.ldg, j.r, side, c->ev_fork,
+                c->ev_join, st_w, ev_w, w_items);
+  }
+  check_launch("gram");
+}
+
+// The Gram partials, sized once for the largest plan any problem of the batch can take: growing
+// them mid-batch would free a buffer another stream's kernels may still be using.
+static void reserve_gram_parts(gpar_ctx* c, const std::vector<DevProblem>& P, int nlanes) {
+  int64_t pd = 0, rd = 0;
+  for (const auto& p : P)
+    for (int cus : {256, 8 * (32 - c->split_w)})
+      for (int dgc : {cus, 256}) {
+        if (cus <= 0) continue;
+        const GramPlan pl = gram_plan(p.n, p.mp, nlanes > 1, cus, dgc);
+        pd = std::max(pd, pl.part_doubles);
+        rd = std::max(rd, pl.rpart_doubles);
+      }
+  for (int l = 0; l < nlanes; ++l) {
+    const std::string sfx = l ? "_1" : "";
+    (void)ws<double>(c, "gram_part" + sfx, (size_t)pd);
+    (void)ws<double>(c, "gram_rpart" + sfx, (size_t)rd);
+  }
+}
+
+// The CU-split pipeline: whitening + short chain of job k on w CUs of every XCD (s_w),
+// concurrently with job k-1's Gram on the other 32 - w (s_g, its co-running correction on s_g2).
+// Jobs are numbered across push() calls, so a caller can keep feeding it (the round-overlapping
+// fit does, across Nelder-Mead rounds): beta buffer k & 1; W(k) waits for G(k-2) (same buffers),
+// G(k) for P(k), and a w/32 share of G(k)'s DG items runs on s_w after P(k+1) -- both sides then
+// end together -- once G(k-1)'s reduction is done (the partial slots are reused).
+struct SplitPipe {
+  gpar_ctx* c;
+  StageBufs buf[2];
+  int gcus;
+  int64_t k = 0;              // jobs whitened so far
+  bool has_pending = false;   // job k - 1 whitened, its Gram not yet issued
+  StageJob pending;
+  std::function<void(const StageJob&, int64_t)> on_gram;   // right after job k's Gram is issued
+
+  SplitPipe(gpar_ctx* c_, int64_t n, int64_t mpmax)
+      : c(c_), gcus(8 * (32 - c_->split_w)) {
+    buf[0] = stage_bufs(c, 0, n, mpmax);
+    buf[1] = stage_bufs(c, 1, n, mpmax);
+  }
+  void start() {   // the split streams follow everything queued on the context stream so far
+    HIPCHECK(hipEventRecord(c->ev_sp, c->main));
+    for (hipStream_t st : {c->s_w, c->s_g, c->s_g2}) HIPCHECK(hipStreamWaitEvent(st, c->ev_sp, 0));
+  }
+  void push(const StageJob& j) {
+    {
+      OnStream on_(c, c->s_w);
+      if (k >= 2) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[k & 1], 0));
+      stage_whiten(c, j, buf[k & 1]);
+      stage_post(c, j, buf[k & 1], false);
+      HIPCHECK(hipEventRecord(c->ev_pc[k & 1], c->s_w));
+    }
+    if (has_pending) issue_gram();
+    pending = j;
+    has_pending = true;
+    ++k;
+  }
+  void issue_gram() {
+    const int64_t i = k - 1;
+    {
+      OnStream on_(c, c->s_g);
+      HIPCHECK(hipStreamWaitEvent(c->s_g, c->ev_pc[i & 1], 0));
+      if (c->split_dgw) {
+        if (i >= 1) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[(i - 1) & 1], 0));
+        stage_gram(c, pending, buf[i & 1], false, false, "", c->s_g2, gcus, c->s_w, c->ev_pw,
+                   c->split_w);
+      } else {
+        stage_gram(c, pending, buf[i & 1], false, false, "", c->s_g2, gcus);
+      }
+      HIPCHECK(hipEventRecord(c->ev_gd[i & 1], c->s_g));
+    }
+    has_pending = false;
+    if (on_gram) on_gram(pending, i);
+  }
+  void flush() {
+    if (has_pending) issue_gram();
+  }
+  // stream st waits for every job issued so far (the last Gram follows every P, DG share and
+  // correction)
+  void join(hipStream_t st) {
+    HIPCHECK(hipEventRecord(c->ev_sp, c->s_g));
+    HIPCHECK(hipStreamWaitEvent(st, c->ev_sp, 0));
+  }
+};
+
 // For every problem: G = beta^T beta, r = beta^T alpha, sum alpha^2 partials, sum log S
 // partials, at hyperparameters th.
 // fix_beta = false (the objective): the Gram streams the chunk-local beta and adds the chunk
@@ -522,8 +728,6 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
                             hipMemcpyDeviceToDevice, c->stream));
   }
 
-  // beta carries 16 zero rows past n: the Gram kernel's LDS-DMA reads whole 16-row K-steps
-  // (zeroed right before each Gram launch: the whitening may write its last chunk's tail rows)
   // Outputs alternate between the context stream and a side stream, each with its own
   // beta / alpha / carry workspace, so one output's (VALU-bound) whitening overlaps another's
   // (MFMA-bound) Gram.  Gains are shared: the side stream waits for them (fork event).
@@ -533,151 +737,47 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   // states, the chunk carry, vec_fix, the beta tail) runs on the side stream beside a whitening
   // instead of on the critical path.  Two beta / carry buffers (fit_pipelined).
   const bool pipe = fit_pipelined(c, P, fix_beta);
-  const int nbuf = (nlanes > 1 || pipe) ? 2 : 1;
-  double* beta_l[2];
-  double* alpha_l[2];
-  double* send_l[2];
-  double* cin_l[2];
-  double* hsum_l[2];
-  double* qv_l[2];
-  for (int l = 0; l < nbuf; ++l) {
-    const std::string sfx = l ? "_1" : "";
-    beta_l[l] = ws<double>(c, "beta" + sfx, (size_t)(n + 16) * mpmax);
-    alpha_l[l] = ws<double>(c, "alpha" + sfx, (size_t)n);
-    send_l[l] = ws<double>(c, "send" + sfx, (size_t)nch * (mpmax + 1) * 4);
-    cin_l[l] = ws<double>(c, "cin" + sfx, (size_t)nch * (mpmax + 1) * 4);
-    hsum_l[l] = ws<double>(c, "hsum" + sfx, (size_t)nch * (mpmax + 1) * 4);
-    qv_l[l] = ws<double>(c, "qv" + sfx, (size_t)nch * 4);
-  }
-  if (nlanes > 1) {
-    HIPCHECK(hipEventRecord(c->ev_fork, c->stream));
-    HIPCHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
-  }
-  std::vector<GainsOut> gi(np);
-  auto alpha_of = [&](int i) { return shared ? alpha_all + (size_t)i * n : alpha_l[i % nbuf]; };
-  // the Gram partials, sized once for the batch's largest plan (any of the plans below): growing
-  // them mid-batch would free a buffer another stream's kernels may still be using
-  {
-    int64_t pd = 0, rd = 0;
-    for (const auto& p : P)
-      for (int cus : {256, 8 * (32 - c->split_w)})
-        for (int dgc : {cus, 256}) {
-          if (cus <= 0) continue;
-          const GramPlan pl = gram_plan(n, p.mp, nlanes > 1, cus, dgc);
-          pd = std::max(pd, pl.part_doubles);
-          rd = std::max(rd, pl.rpart_doubles);
-        }
-    for (int l = 0; l < nlanes; ++l) {
-      const std::string sfx = l ? "_1" : "";
-      (void)ws<double>(c, "gram_part" + sfx, (size_t)pd);
-      (void)ws<double>(c, "gram_rpart" + sfx, (size_t)rd);
-    }
-  }
-  // Kfu assembly + whitening of output i into buffer i % nbuf, on c->stream
-  auto whiten_stage = [&](int i) {
-    const DevProblem& p = P[i];
-    const int b = i % nbuf;
-    const std::string sfx = b ? "_1" : "";
+  reserve_gram_parts(c, P, nlanes);
+  // the stage job of output i, its gains (per output unless shared) run on c->stream
+  std::vector<StageJob> jobs(np);
+  std::vector<double*> alpha_own(np, nullptr);
+  auto job = [&](int i, const StageBufs& b) -> const StageJob& {
+    StageJob& j = jobs[i];
+    j.p = &P[i];
+    j.th = &th[i];
     if (shared) {
-      gi[i] = gains[i];
+      j.gi = gains[i];
+      j.alpha = alpha_all + (size_t)i * n;
+      j.asend = asend_all + (size_t)i * nch * kSStride;
     } else {
       std::vector<ChainParamsHost> cps(1);
       cps[0] = {1.0 / th[i].l_t, th[i].l_t, th[i].sv_t * th[i].sv_t, th[i].sigma * th[i].sigma};
-      gi[i] = run_gains(c, p.sdim, p.t, n, cps, nullptr, false, "fit1" + sfx);
-      HIPCHECK(hipMemcpyAsync(o.logs + (size_t)i * nch, gi[i].logs, nch * sizeof(double),
+      j.gi = run_gains(c, P[i].sdim, P[i].t, n, cps, nullptr, false, b.idx ? "fit1_1" : "fit1");
+      HIPCHECK(hipMemcpyAsync(o.logs + (size_t)i * nch, j.gi.logs, nch * sizeof(double),
                               hipMemcpyDeviceToDevice, c->stream));
+      j.alpha = b.alpha;
+      j.asend = nullptr;
     }
-    // algorithmic HBM bytes: the inputs (V, or the cached distances), the gains records and
-    // fix-up rows (16 + 4 doubles per step), beta written (m columns)
-    const double in_cols = cached_d2(c, p) ? (double)p.m : (double)p.d;
-    Timed tm_(c, "whiten", 8.0 * (double)n * (in_cols + (double)p.m + 20.0));
-    whiten_kfu_any(c, p, gi[i].rec, p.v, p.ldv, n, nch, th[i], beta_l[b], p.mp, send_l[b], gi[i].g,
-                   hsum_l[b]);
-    check_launch("whiten_kfu");
-  };
-  // the short chain between output i's whitening and its Gram, on c->stream
-  auto post_stage = [&](int i) {
-    const DevProblem& p = P[i];
-    const int b = i % nbuf;
-    const std::string sfx = b ? "_1" : "";
-    double* send = send_l[b];
-    if (shared) {   // alpha's chunk end states -> column mp of the carry input
-      HIPCHECK(hipMemcpy2DAsync(send + (size_t)p.mp * kSStride, (size_t)p.mc * kSStride * sizeof(double),
-                                asend_all + (size_t)i * nch * kSStride, kSStride * sizeof(double),
-                                kSStride * sizeof(double), nch, hipMemcpyDeviceToDevice, c->stream));
-    } else {
-      launch_whiten_vec(c->stream, p.sdim, gi[i].rec, 0, p.y, 0, n, kChunk, nch, 1, alpha_of(i), 0,
-                        send, 0, p.mc, p.mp);
-    }
-    check_launch("whiten_vec");
-    run_carry(c, p.sdim, gi[i].phi, 0, send, cin_l[b], 0, nch, p.mc, p.mc, 1, "fitc" + sfx);
-    check_launch("carry");
-    // alpha fix-up, plus the Gram's chunk correction E_j = H_j + W_j C_j / 2 and q_j
-    launch_vec_fix(c->stream, p.sdim, alpha_of(i), 0, gi[i].g, 0, cin_l[b], 0, p.mc, p.mp, n, kChunk,
-                   1, o.a2part + (size_t)i * npart, fix_beta ? nullptr : hsum_l[b], p.mp, qv_l[b]);
-    check_launch("vec_fix");
-    if (fix_beta) {
-      launch_beta_fix(c->stream, p.sdim, beta_l[b], p.mp, n, gi[i].g, cin_l[b], p.mc, kChunk);
-      check_launch("beta_fix");
-    }
-    HIPCHECK(hipMemsetAsync(beta_l[b] + (size_t)n * p.mp, 0, (size_t)16 * p.mp * sizeof(double), c->stream));
-  };
-  // cus: the CUs c->stream may use; st_w: the first w_frac32 / 32 of the DG kernel's work items
-  // run there (ev_w joins them)
-  auto gram_stage = [&](int i, hipStream_t side, int cus, hipStream_t st_w = nullptr,
-                        hipEvent_t ev_w = nullptr, int w_frac32 = 0) {
-    const DevProblem& p = P[i];
-    const int b = i % nbuf;
-    const std::string sfx = (nlanes > 1 && b) ? "_1" : "";
-    // two lanes: one Gram workgroup per CU, so the other lane's whitening runs beside it
-    GramPlan plan = gram_plan(n, p.mp, nlanes > 1, cus, st_w ? 256 : cus);
-    const int w_items = st_w ? plan.ndg * plan.sdg * w_frac32 / 32 : 0;
-    double* part = ws<double>(c, "gram_part" + sfx, (size_t)plan.part_doubles);
-    double* rpart = ws<double>(c, "gram_rpart" + sfx, (size_t)plan.rpart_doubles);
-    {
-      Timed tm_(c, "gram", (double)n * (double)p.m * (double)(p.m + 1));   // flops of beta^T beta
-      launch_gram(c->stream, p.sdim, plan, beta_l[b], p.mp, n, fix_beta ? nullptr : hsum_l[b], cin_l[b],
-                  qv_l[b], p.mc, kChunk, alpha_of(i), part, rpart, o.G + (size_t)i * mpmax * mpmax,
-                  mpmax, o.r + (size_t)i * mpmax, side, c->ev_fork, c->ev_join, st_w, ev_w,
-                  w_items);
-    }
-    check_launch("gram");
+    j.G = o.G + (size_t)i * mpmax * mpmax;
+    j.r = o.r + (size_t)i * mpmax;
+    j.a2part = o.a2part + (size_t)i * npart;
+    j.ldg = mpmax;
+    return j;
   };
   if (pipe && split_active(c, n, mpmax)) {
-    // Whitening + short chain on w CUs of every XCD (s_w), concurrently with the Gram on the other
-    // 32 - w (s_g, its co-running correction on s_g2): W(i+1) P(i+1) beside G(i).  A w/32 share of
-    // G(i)'s DG items runs on s_w after P(i+1), so both sides end together.  W(i+1) waits for
-    // G(i-1) (same buffers), G(i) for P(i), and s_w's DG share of G(i) for G(i-1)'s reduction
-    // (the partial slots are reused).
-    const int gcus = 8 * (32 - c->split_w);
-    HIPCHECK(hipEventRecord(c->ev_sp, c->main));
-    HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_sp, 0));
-    HIPCHECK(hipStreamWaitEvent(c->s_g, c->ev_sp, 0));
-    HIPCHECK(hipStreamWaitEvent(c->s_g2, c->ev_sp, 0));
-    auto wp = [&](int i) {
-      OnStream on_(c, c->s_w);
-      if (i >= 2) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[i & 1], 0));
-      whiten_stage(i);
-      post_stage(i);
-      HIPCHECK(hipEventRecord(c->ev_pc[i & 1], c->s_w));
-    };
-    wp(0);
-    for (int i = 0; i < np; ++i) {
-      if (i + 1 < np) wp(i + 1);
-      OnStream on_(c, c->s_g);
-      HIPCHECK(hipStreamWaitEvent(c->s_g, c->ev_pc[i & 1], 0));
-      if (c->split_dgw) {
-        if (i >= 1) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[(i - 1) & 1], 0));
-        gram_stage(i, c->s_g2, gcus, c->s_w, c->ev_pw, c->split_w);
-      } else {
-        gram_stage(i, c->s_g2, gcus);
-      }
-      HIPCHECK(hipEventRecord(c->ev_gd[i & 1], c->s_g));
-    }
-    // the last Gram follows every P, DG share and correction: the context stream joins s_g
-    HIPCHECK(hipEventRecord(c->ev_sp, c->s_g));
-    HIPCHECK(hipStreamWaitEvent(c->main, c->ev_sp, 0));
+    SplitPipe sp(c, n, mpmax);
+    sp.start();
+    for (int i = 0; i < np; ++i) sp.push(job(i, sp.buf[i & 1]));
+    sp.flush();
+    sp.join(c->main);
     return o;
+  }
+  StageBufs bufs[2];
+  const int nbuf = (nlanes > 1 || pipe) ? 2 : 1;
+  for (int l = 0; l < nbuf; ++l) bufs[l] = stage_bufs(c, l, n, mpmax);
+  if (nlanes > 1) {
+    HIPCHECK(hipEventRecord(c->ev_fork, c->stream));
+    HIPCHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
   }
   if (pipe) {
     // main: W0 W1 G0 W2 G1 W3 G2 ...; side: P0 after W0, P(i+1) after G(i), so P(i+1) runs beside
@@ -688,16 +788,16 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
       HIPCHECK(hipStreamWaitEvent(c->side, c->ev_pw, 0));
       {
         OnStream on_(c, c->side);
-        post_stage(i);
+        stage_post(c, jobs[i], bufs[i % nbuf], false);
       }
       HIPCHECK(hipEventRecord(c->ev_pc[i & 1], c->side));
     };
-    whiten_stage(0);
+    stage_whiten(c, job(0, bufs[0]), bufs[0]);
     issue_post(0);
     for (int i = 0; i < np; ++i) {
-      if (i + 1 < np) whiten_stage(i + 1);
+      if (i + 1 < np) stage_whiten(c, job(i + 1, bufs[(i + 1) % nbuf]), bufs[(i + 1) % nbuf]);
       HIPCHECK(hipStreamWaitEvent(c->main, c->ev_pc[i & 1], 0));
-      gram_stage(i, c->side, 256);
+      stage_gram(c, jobs[i], bufs[i % nbuf], false, false, "", c->side, 256);
       if (i + 1 < np) issue_post(i + 1);
     }
     // every side-stream item has been waited for: P(np-1) by G(np-1), the corrections by their Gram
@@ -705,10 +805,13 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   }
   for (int i = 0; i < np; ++i) {
     const int lane = i % nlanes;
+    const StageBufs& b = bufs[i % nbuf];
     OnStream on_(c, lane ? c->side : c->main);
-    whiten_stage(i);
-    post_stage(i);
-    gram_stage(i, nlanes == 1 ? c->side : nullptr, 256);
+    const StageJob& j = job(i, b);
+    stage_whiten(c, j, b);
+    stage_post(c, j, b, fix_beta);
+    stage_gram(c, j, b, fix_beta, nlanes > 1, (nlanes > 1 && lane) ? "_1" : "",
+               nlanes == 1 ? c->side : nullptr, 256);
   }
   if (nlanes > 1) {   // join: the dense tail on the context stream needs every G
     HIPCHECK(hipEventRecord(c->ev_join, c->side));
@@ -1252,6 +1355,7 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
   }
   c->stream = c->main;
   if (const char* e = std::getenv("GPAR_PIPELINE")) c->pipeline = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GPAR_OVERLAP")) c->overlap = std::atoi(e) != 0;
   // A/B knobs: GPAR_SPLIT_CUS overrides the default CU split, GPAR_SPLIT_DGW=0 keeps the DG
   // kernel off the whitening CUs
   if (const char* e = std::getenv("GPAR_SPLIT_DGW")) c->split_dgw = std::atoi(e) != 0;
@@ -1283,8 +1387,10 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
         (void)hipStreamSynchronize(st);
         (void)hipStreamDestroy(st);
       }
-    for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp})
+    for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_grp[0], ctx->ev_grp[1]})
       if (ev) (void)hipEventDestroy(ev);
+    for (auto& s : ctx->stage)
+      if (s.host) (void)hipHostFree(s.host);
   }
   (void)hipStreamDestroy(ctx->side);
   (void)hipStreamDestroy(ctx->main);
@@ -1364,6 +1470,12 @@ int32_t gpar_ctx_set_cu_split(gpar_ctx* ctx, int32_t cus_per_xcd) {
     ctx->err = "gpar_ctx_set_cu_split: cus_per_xcd must be -1 (default), 0 or a multiple of 4 "
                "below 32 (256-CU devices)";
   return rc;
+}
+
+int32_t gpar_ctx_set_fit_overlap(gpar_ctx* ctx, int32_t on) {
+  if (!ctx) return GPAR_ERR_STATE;
+  ctx->overlap = on != 0;
+  return GPAR_OK;
 }
 
 int32_t gpar_ctx_get_cu_split(const gpar_ctx* ctx, int32_t* cus_per_xcd) {
@@ -1564,6 +1676,187 @@ static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<
   return Q;
 }
 
+// ---------------------------------------------------------------- round-overlapping batched fit
+// fit_impl's batched Nelder-Mead evaluates one simplex point per output per round.  Round by
+// round (eval_dtc), every round drains the chip: its first whitening runs alone, its last Gram
+// runs alone, then the next round's gains, the dense tail and a host sync.  On the CU-split
+// schedule with >= 4 outputs, fit_overlapped deals the outputs into two groups that take turns:
+// while the host waits for group A's values (A's dense tail runs on the context stream beside the
+// split streams) and steps A's simplices, group B's whitenings and Grams keep both sides of the
+// split busy, and A's next round (gains on the whitening CUs, then its jobs) is queued behind
+// them -- one drain per fit instead of one per round.  Every output evaluates exactly the points
+// its own simplex asks for, in the same order, with the same kernels and per-problem arithmetic
+// (batched gains and dense-tail launches compute each problem independently), so the fit equals
+// the round-by-round one bit for bit.  Uploads go through pinned arenas (gpar_ctx::staging): a
+// pageable copy queued behind running work could block the host and stall the pipeline.
+struct OverlapGroup {
+  int id = 0;
+  std::vector<int> members;        // output indices dealt to this group
+  std::vector<int> act;            // this round's active members
+  std::vector<Theta> th;           // their hyperparameters this round
+  std::vector<DevProblem> sub;     // their problems (stable while their jobs are queued)
+  GramOut go{};                    // one G / r / alpha^2 / log S slot per member
+  double *alpha_all = nullptr, *asend_all = nullptr, *dout = nullptr;
+  double* hout = nullptr;          // pinned: -dtc values of the round
+  int* hstat = nullptr;            // pinned: Cholesky status flags (2 per output)
+  size_t res_bytes = 0;            // the arena's result prefix
+  bool in_flight = false;
+};
+
+using AcceptFn = std::function<void(int, double, const double*, const double*, int64_t)>;
+
+static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
+                           std::vector<NelderMead>& nm, const AcceptFn& accept) {
+  const int np = (int)P.size();
+  const int64_t n = P[0].n, nch = P[0].nch, npart = vec_fix_blocks(n);
+  int64_t mpmax = 0;
+  for (auto& p : P) mpmax = std::max(mpmax, p.mp);
+  const size_t sq = (size_t)mpmax * mpmax;
+  for (hipEvent_t* ev : {&c->ev_grp[0], &c->ev_grp[1]})
+    if (!*ev) HIPCHECK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+  OverlapGroup grp[2];
+  for (int i = 0; i < np; ++i) grp[i & 1].members.push_back(i);
+  for (int g = 0; g < 2; ++g) {
+    OverlapGroup& G = grp[g];
+    G.id = g;
+    const size_t cap = G.members.size();
+    const std::string sfx = g ? "B" : "A";
+    G.go.ldg = mpmax;
+    G.go.npart = npart;
+    G.go.G = ws<double>(c, "ovG" + sfx, cap * sq);
+    G.go.r = ws<double>(c, "ovr" + sfx, cap * mpmax);
+    G.go.a2part = ws<double>(c, "ova2" + sfx, cap * npart);
+    G.go.logs = ws<double>(c, "ovlogs" + sfx, cap * nch);
+    G.alpha_all = ws<double>(c, "ovalpha" + sfx, cap * n);
+    G.asend_all = ws<double>(c, "ovasend" + sfx, cap * nch * kSStride);
+    G.dout = ws<double>(c, "ovout" + sfx, cap);
+    gpar_ctx::Staging& s = c->stage[g];
+    const size_t vbytes = (cap * sizeof(double) + 255) & ~(size_t)255;
+    G.res_bytes = vbytes + ((2 * cap * sizeof(int) + 255) & ~(size_t)255);
+    const size_t need = G.res_bytes + ((size_t)1 << 20) + cap * 4096;
+    if (s.cap < need) {
+      if (s.host) HIPCHECK(hipHostFree(s.host));
+      s.host = nullptr;
+      s.cap = 0;
+      HIPCHECK(hipHostMalloc((void**)&s.host, need, hipHostMallocDefault));
+      s.cap = need;
+    }
+    G.hout = reinterpret_cast<double*>(s.host);
+    G.hstat = reinterpret_cast<int*>(s.host + vbytes);
+  }
+  reserve_gram_parts(c, P, 1);
+  struct StagingScope {   // h2d through group g's pinned arena inside the scope
+    gpar_ctx* c;
+    StagingScope(gpar_ctx* c_, int g) : c(c_) { c->staging = &c->stage[g]; }
+    ~StagingScope() { c->staging = nullptr; }
+  };
+
+  SplitPipe sp(c, n, mpmax);
+  // a group's dense tail + finish on the context stream as soon as its round's last Gram is
+  // issued; its values land in pinned memory, ev_grp[g] marks them
+  auto issue_dense = [&](OverlapGroup& G, int64_t job) {
+    OnStream on_(c, c->main);
+    StagingScope st_(c, G.id);
+    HIPCHECK(hipStreamWaitEvent(c->main, c->ev_gd[job & 1], 0));
+    const int na = (int)G.act.size();
+    DenseOut dn = run_dense(c, G.sub, G.th, G.go, false);
+    std::vector<Finish2JobHost> fj(na);
+    for (int a = 0; a < na; ++a) fj[a] = finish_job(dn, G.go, G.sub[a], a, nch, G.dout + a, nullptr);
+    auto* dfj = ws<Finish2JobHost>(c, "finishjobs", np);
+    h2d(c, dfj, fj.data(), na);
+    launch_finish2(c->main, dfj, na, dn.ld, dn.nb);
+    check_launch("finish");
+    HIPCHECK(hipMemcpyAsync(G.hout, G.dout, na * sizeof(double), hipMemcpyDeviceToHost, c->main));
+    HIPCHECK(hipMemcpyAsync(G.hstat, dn.status, 2 * na * sizeof(int), hipMemcpyDeviceToHost, c->main));
+    HIPCHECK(hipEventRecord(c->ev_grp[G.id], c->main));
+  };
+  sp.on_gram = [&](const StageJob& j, int64_t job) {
+    if (j.last) issue_dense(grp[j.group], job);
+  };
+  // ask every active member for its next point; queue the group's gains and its jobs
+  auto begin_round = [&](OverlapGroup& G) {
+    G.act.clear();
+    for (int i : G.members)
+      if (!nm[i].done()) G.act.push_back(i);
+    if (G.act.empty()) return;
+    const int na = (int)G.act.size();
+    G.th.clear();
+    G.sub.clear();
+    std::vector<ChainParamsHost> cps(na);
+    std::vector<const double*> ys(na);
+    for (int a = 0; a < na; ++a) {
+      const int i = G.act[a];
+      const auto& x = nm[i].ask();
+      G.th.push_back({unpack(x[0]), unpack(x[1]), unpack(x[2]), unpack(x[3]), unpack(x[4])});
+      G.sub.push_back(P[i]);
+      const Theta& t = G.th.back();
+      cps[a] = {1.0 / t.l_t, t.l_t, t.sv_t * t.sv_t, t.sigma * t.sigma};
+      ys[a] = P[i].y;
+    }
+    c->stage[G.id].used = G.res_bytes;   // the previous round's uploads have been consumed
+    GainsOut gn;
+    {
+      OnStream on_(c, c->s_w);
+      StagingScope st_(c, G.id);
+      gn = run_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, G.id ? "fitB" : "fitA", &ys,
+                     G.alpha_all, G.asend_all);
+      HIPCHECK(hipMemcpyAsync(G.go.logs, gn.logs, (size_t)na * nch * sizeof(double),
+                              hipMemcpyDeviceToDevice, c->s_w));
+    }
+    {   // narrower outputs: their G / r slot padding must read as zero in the dense tail
+      OnStream on_(c, c->s_g);
+      for (int a = 0; a < na; ++a)
+        if (G.sub[a].mp != mpmax) {
+          HIPCHECK(hipMemsetAsync(G.go.G + a * sq, 0, sq * sizeof(double), c->s_g));
+          HIPCHECK(hipMemsetAsync(G.go.r + (size_t)a * mpmax, 0, mpmax * sizeof(double), c->s_g));
+        }
+    }
+    for (int a = 0; a < na; ++a) {
+      StageJob j;
+      j.p = &G.sub[a];
+      j.th = &G.th[a];
+      j.gi = gn;
+      j.gi.rec = gn.rec + (size_t)a * gn.recstride;
+      j.gi.g = gn.g + (size_t)a * gn.gstride;
+      j.gi.phi = gn.phi + (size_t)a * gn.phistride;
+      j.gi.logs = gn.logs + (size_t)a * nch;
+      j.alpha = G.alpha_all + (size_t)a * n;
+      j.asend = G.asend_all + (size_t)a * nch * kSStride;
+      j.G = G.go.G + a * sq;
+      j.r = G.go.r + (size_t)a * mpmax;
+      j.a2part = G.go.a2part + (size_t)a * npart;
+      j.ldg = mpmax;
+      j.group = G.id;
+      j.last = a == na - 1;
+      sp.push(j);
+    }
+    G.in_flight = true;
+  };
+  // wait for a group's values and hand them to its simplices (Gram copies of kept points go to
+  // the Gram stream, ahead of the group's next Grams)
+  auto finish_round = [&](OverlapGroup& G) {
+    if (sp.has_pending && sp.pending.group == G.id) sp.flush();   // its last Gram, then its tail
+    HIPCHECK(hipEventSynchronize(c->ev_grp[G.id]));
+    OnStream on_(c, c->s_g);
+    for (size_t a = 0; a < G.act.size(); ++a) {
+      double f = -G.hout[a];
+      if (G.hstat[2 * a] || G.hstat[2 * a + 1] || !std::isfinite(f)) f = INFINITY;
+      accept(G.act[a], f, G.go.G + a * sq, G.go.r + a * mpmax, mpmax);
+    }
+    G.in_flight = false;
+  };
+  sp.start();
+  begin_round(grp[0]);
+  begin_round(grp[1]);
+  for (int g = 0; grp[0].in_flight || grp[1].in_flight; g ^= 1) {
+    if (!grp[g].in_flight) continue;
+    finish_round(grp[g]);
+    begin_round(grp[g]);
+  }
+  sp.flush();
+  sp.join(c->main);
+}
+
 static void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* log_theta0,
                      const gpar_fit_options& o, double* theta_out, double* nlml_out,
                      int32_t* evals_out, FitKeep* keep, int64_t later_bytes = 0) {
@@ -1596,6 +1889,23 @@ static void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const dou
       kr[i] = ws<double>(ctx, "fitkeep_r" + std::to_string(i), mp);
     }
   }
+  // one evaluated point of output i: keep its Gram if it is the best so far (on c->stream, before
+  // the slot is reused), then tell the simplex
+  const AcceptFn accept = [&](int i, double f, const double* Gs, const double* rs, int64_t ldg) {
+    if (keep && f < best_f[i]) {
+      best_f[i] = f;
+      best_x[i] = nm[i].ask();
+      const size_t mp = (size_t)P[i].mp;
+      HIPCHECK(hipMemcpy2DAsync(kG[i], mp * sizeof(double), Gs, ldg * sizeof(double),
+                                mp * sizeof(double), mp, hipMemcpyDeviceToDevice, ctx->stream));
+      HIPCHECK(hipMemcpyAsync(kr[i], rs, mp * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    nm[i].tell(f);
+  };
+  int64_t mpmax = 0;
+  for (auto& p : P) mpmax = std::max(mpmax, p.mp);
+  if (ctx->overlap && nprob >= 4 && fit_pipelined(ctx, P) && split_active(ctx, P[0].n, mpmax))
+    fit_overlapped(ctx, P, nm, accept);
   std::vector<double> vals;
   while (true) {
     std::vector<int> act;
@@ -1611,23 +1921,13 @@ static void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const dou
     }
     vals.assign(act.size(), 0.0);
     std::vector<int> st;
-    GramOut go;
+    GramOut go{};
     eval_dtc(ctx, sub, th, vals.data(), st, keep ? &go : nullptr);
     for (size_t a = 0; a < act.size(); ++a) {
       double f = -vals[a];
       if (st[a] || !std::isfinite(f)) f = INFINITY;  // PosDefException -> reject the point
-      const int i = act[a];
-      if (keep && f < best_f[i]) {   // this round's G / r of output i, before the next round
-        best_f[i] = f;
-        best_x[i] = nm[i].ask();
-        const size_t mp = (size_t)P[i].mp;
-        HIPCHECK(hipMemcpy2DAsync(kG[i], mp * sizeof(double), go.G + a * go.ldg * go.ldg,
-                                  go.ldg * sizeof(double), mp * sizeof(double), mp,
-                                  hipMemcpyDeviceToDevice, ctx->stream));
-        HIPCHECK(hipMemcpyAsync(kr[i], go.r + a * go.ldg, mp * sizeof(double),
-                                hipMemcpyDeviceToDevice, ctx->stream));
-      }
-      nm[i].tell(f);
+      accept(act[a], f, keep ? go.G + a * go.ldg * go.ldg : nullptr,
+             keep ? go.r + a * go.ldg : nullptr, go.ldg);
     }
   }
   for (int i = 0; i < nprob; ++i) {

@@ -27,7 +27,7 @@ EXPORTED = (
     "gpar_fit", "gpar_fit_predict", "gpar_fit_predict_chain", "gpar_mc_normals", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
     "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_kernel_work", "gpar_ctx_reset_stats",
-    "gpar_ctx_set_lanes", "gpar_ctx_set_cu_split", "gpar_ctx_get_cu_split", "gpar_ctx_set_dist_cache", "gpar_ctx_set_dist_cache_keep", "gpar_ctx_dist_cache_stats",
+    "gpar_ctx_set_lanes", "gpar_ctx_set_cu_split", "gpar_ctx_set_fit_overlap", "gpar_ctx_get_cu_split", "gpar_ctx_set_dist_cache", "gpar_ctx_set_dist_cache_keep", "gpar_ctx_dist_cache_stats",
     "gpar_pairwise_distances", "gpar_ctx_set_input_stream", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
 )
 
@@ -99,6 +99,7 @@ def load(path: str | None = None):
             "gpar_ctx_set_lanes": (i32, [vp, i32]),
             "gpar_ctx_set_cu_split": (i32, [vp, i32]),
             "gpar_ctx_get_cu_split": (i32, [vp, C.POINTER(C.c_int32)]),
+            "gpar_ctx_set_fit_overlap": (i32, [vp, i32]),
             "gpar_ctx_set_dist_cache": (i32, [vp, i64]),
             "gpar_ctx_set_dist_cache_keep": (i32, [vp, i32]),
             "gpar_ctx_dist_cache_stats": (i32, [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i64)]),
@@ -250,6 +251,10 @@ class Context:
         """CUs per XCD for the batched fit's whitening beside the Gram (0: whole-chip kernels)."""
         self.check(load().gpar_ctx_set_cu_split(self.h, int(cus_per_xcd)))
         self._cu_split = int(cus_per_xcd)
+
+    def set_fit_overlap(self, on=True):
+        """Round-overlapping batched fit on the CU split (gpar_ctx_set_fit_overlap; default on)."""
+        self.check(load().gpar_ctx_set_fit_overlap(self.h, 1 if on else 0))
 
     def cu_split(self):
         """The CU split in effect (gpar_ctx_get_cu_split)."""

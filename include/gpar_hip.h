@@ -127,6 +127,13 @@ int32_t gpar_ctx_set_lanes(gpar_ctx* ctx, int32_t lanes);
  * explicit width at context creation.  Results agree with the whole-chip schedule up to the
  * Gram's split plan (last bits; deterministic for a given w). */
 int32_t gpar_ctx_set_cu_split(gpar_ctx* ctx, int32_t cus_per_xcd);
+/* Round-overlapping batched fit (on by default; the environment variable GPAR_OVERLAP=0 turns it
+ * off at context creation): on the CU-split schedule with >= 4 outputs, gpar_fit /
+ * gpar_fit_predict deal the outputs into two groups whose Nelder-Mead rounds take turns, so one
+ * group's dense tail, host step and next-round gains overlap the other group's whitenings and
+ * Grams instead of draining the chip after every round.  Each output evaluates the same points
+ * with the same arithmetic: results are bit-identical either way. */
+int32_t gpar_ctx_set_fit_overlap(gpar_ctx* ctx, int32_t on);
 /* The CU split in effect (0 when off or unsupported). */
 int32_t gpar_ctx_get_cu_split(const gpar_ctx* ctx, int32_t* cus_per_xcd);
 /* Distance cache of gpar_fit / gpar_fit_predict: the input distances |v_k - z_c| (squared for EQ)

@@ -10,6 +10,11 @@ positional arguments, keywords and return shapes as
   get_gpar_scaled_predictions   src/gp/gpar_scaled_inference.jl:20-136  -> (means, stds)
   get_sde_predictions           src/gp/temporal_gp_inference.jl:45-114  -> (lgssm, marginals)
 
+and adds the multi-output driver the reference writes as a loop in its examples
+(GPAR_scaled_examples.jl:132-175, eeg.jl:212-281):
+
+  get_gpar_scaled_predictions_batch  -> (means, stds), one vector per output, one library call
+
 with every number computed by the gfx950 kernels behind include/gpar_hip.h.  A caller switches
 `using GPARatScale` to `using GPARatScale, GPARatScaleHIP` and qualifies these five names (or
 imports them from GPARatScaleHIP).  The reference's helpers (to_ColVecs, unpack_gpar,
@@ -33,7 +38,7 @@ using GPARatScale: to_ColVecs, unpack_gpar, unpack_gp, parse_initial_gpar_params
                    parse_initial_gp_params
 
 export compute_gpar_dtc_objective, get_optim_scaled_gpar_params, compute_q_u,
-       get_gpar_scaled_predictions, get_sde_predictions
+       get_gpar_scaled_predictions, get_sde_predictions, get_gpar_scaled_predictions_batch
 
 const libgpar = get(ENV, "GPAR_HIP_LIB", "libgparhip.so")
 
@@ -302,6 +307,110 @@ function get_gpar_scaled_predictions(input_locations, pseudo_input_locations, ti
                             Ptr{Float64}, Int64, Int32, Int32, UInt64, Ptr{Float64}, Ptr{Float64}),
                            c.h, ppred, θ, ns, ts, Vs, Int64(size(Vs, 1)), md, Int32(samples), seed,
                            means, stds))
+        end
+    end
+    return means, stds
+end
+
+# ------------------------------------------------------------------ the GPAR per-output driver loop
+"""
+    get_gpar_scaled_predictions_batch(input_locations, pseudo_input_locations, time_loc, outputs,
+                                      inference_time_loc, inference_input_locations;
+                                      chained = true, kwargs...)
+
+The per-output driver loop of examples/GPAR_scaled_examples.jl:132-175 and examples/eeg.jl:212-281
+-- one `get_gpar_scaled_predictions` per output -- as ONE library call (gpar_fit_predict_chain /
+gpar_fit_predict): the P fits run as one batched Nelder-Mead on the GPU (pipelined, CU-split,
+distance-cached), then the predictions in output order.  Output i = 1..P has training inputs
+`input_locations[i]`, pseudo-inputs `pseudo_input_locations[i]` and targets `outputs[i]` on the shared
+`time_loc`, each as get_gpar_scaled_predictions takes them.
+
+Inference inputs:
+* `chained = true` (the reference's loops: y3 reads y2's predicted means,
+  GPAR_scaled_examples.jl:172; eeg.jl:249,274): `inference_input_locations` is the list of GIVEN
+  inference columns (e.g. `[test_y1]`, or eeg.jl's `[train_f3, train_f4, train_f5, train_f6]`), and
+  output i reads the first D_i columns of [given columns..., predicted means of outputs 1..i-1];
+* `chained = false`: `inference_input_locations[i]` are output i's own inference inputs.
+
+Initial log-parameters (`i_log_*`) are scalars shared by every output or `nothing` (a fresh
+U(0,1) draw per output, as each reference call makes).  Returns (means, stds): P vectors each,
+what get_gpar_scaled_predictions returns for that output.
+"""
+function get_gpar_scaled_predictions_batch(input_locations, pseudo_input_locations, time_loc,
+        outputs, inference_time_loc, inference_input_locations;
+        chained::Bool = true,
+        i_log_time_l = nothing, i_log_time_var = nothing, i_log_out_l = nothing,
+        i_log_out_var = nothing, i_log_noise_sigma = nothing,
+        optimization_time_limit = 1000.0, debug::Bool = false,
+        mode::Symbol = :mc, samples::Integer = 100, seed::UInt64 = rand(UInt64))
+    P = length(outputs)
+    length(input_locations) == length(pseudo_input_locations) == P ||
+        throw(DomainError(P, "one input / pseudo-input set per output"))
+    t = Vector{Float64}(time_loc)
+    ts = Vector{Float64}(inference_time_loc)
+    ns = length(ts)
+    Vs = [_colmat(x) for x in input_locations]
+    Zs = [_colmat(z) for z in pseudo_input_locations]
+    ys = [Vector{Float64}(y) for y in outputs]
+    # Matern52 for both kernels, as get_gpar_scaled_predictions hard-codes for its fit (:48-49)
+    probs = [problem(Vs[i], Zs[i], t, ys[i], Matern52(), Matern52()) for i in 1:P]
+    x0 = reduce(vcat, [Vector{Float64}(parse_initial_gpar_params(i_log_time_l, i_log_time_var,
+                       i_log_out_l, i_log_out_var, i_log_noise_sigma)) for _ in 1:P])
+    md = mode === :mc ? GPAR_PREDICT_MC : GPAR_PREDICT_ANALYTIC
+    θ = zeros(5 * P)
+    nlml = zeros(P)
+    ev = zeros(Int32, P)
+    means = [zeros(ns) for _ in 1:P]
+    stds = [zeros(ns) for _ in 1:P]
+    mptr = [pointer(m) for m in means]
+    sptr = [pointer(s) for s in stds]
+    opts = Ref(fit_options(optimization_time_limit))
+    debug && println("Starting the batched optimization of $P outputs")
+    c = ctx()
+    if chained
+        given = [Vector{Float64}(x) for x in inference_input_locations]
+        K = length(given) + P
+        all(length(g) == ns for g in given) || throw(DomainError(ns, "inference columns of length N*"))
+        # point-major chain: point k's K columns contiguous (chain[k*K + col])
+        chain = zeros(K, ns)
+        for (j, g) in enumerate(given)
+            chain[j, :] .= g
+        end
+        for i in 1:P
+            size(Vs[i], 1) <= length(given) + i - 1 ||
+                throw(DomainError(i, "output $i reads $(size(Vs[i], 1)) inference columns, only " *
+                                     "$(length(given)) given + $(i - 1) predicted exist before it"))
+        end
+        cols = Int32[length(given) + i - 1 for i in 1:P]
+        vptr = fill(pointer(chain), P)
+        lds = fill(Int64(K), P)
+        GC.@preserve Vs Zs ys t ts x0 θ nlml ev means stds chain cols probs begin
+            check(c, ccall((:gpar_fit_predict_chain, libgpar), Int32,
+                           (Ptr{Cvoid}, Ptr{GparProblem}, Int32, Ptr{Float64}, Ref{GparFitOptions},
+                            Int64, Ptr{Float64}, Ptr{Ptr{Float64}}, Ptr{Int64}, Int32, Int32, UInt64,
+                            Ptr{Float64}, Int64, Ptr{Int32}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32},
+                            Ptr{Ptr{Float64}}, Ptr{Ptr{Float64}}),
+                           c.h, probs, Int32(P), x0, opts, ns, ts, vptr, lds, md, Int32(samples),
+                           seed, chain, Int64(K), cols, θ, nlml, ev, mptr, sptr))
+        end
+    else
+        Vstar = [_colmat(x) for x in inference_input_locations]
+        length(Vstar) == P || throw(DomainError(P, "one inference input set per output"))
+        vptr = [pointer(v) for v in Vstar]
+        lds = Int64[size(v, 1) for v in Vstar]
+        GC.@preserve Vs Zs ys t ts x0 θ nlml ev means stds Vstar probs begin
+            check(c, ccall((:gpar_fit_predict, libgpar), Int32,
+                           (Ptr{Cvoid}, Ptr{GparProblem}, Int32, Ptr{Float64}, Ref{GparFitOptions},
+                            Int64, Ptr{Float64}, Ptr{Ptr{Float64}}, Ptr{Int64}, Int32, Int32, UInt64,
+                            Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Ptr{Float64}},
+                            Ptr{Ptr{Float64}}),
+                           c.h, probs, Int32(P), x0, opts, ns, ts, vptr, lds, md, Int32(samples),
+                           seed, θ, nlml, ev, mptr, sptr))
+        end
+    end
+    if debug
+        for i in 1:P
+            println("Output $i: optimum params $(Tuple(θ[5i-4:5i]))")
         end
     end
     return means, stds

@@ -85,3 +85,35 @@ def test_set_cu_split_rejects_bad_widths(ctx):
     assert ctx.cu_split() == 8
     ctx.set_cu_split(-1)
     assert ctx.cu_split() == 8    # the default width (applied to large enough Grams)
+
+
+def test_overlapped_rounds_equal_round_by_round(ctx):
+    """fit_overlapped (two groups of outputs taking turns, no drain between Nelder-Mead rounds)
+    evaluates the same points with the same per-problem arithmetic as the round-by-round fit:
+    bit-identical theta / -nlml, here with mixed Mp (padded Gram slots), an odd output count,
+    outputs converging at different rounds (g_tol on) and the kept Grams of fit_predict."""
+    outs, Ms = [2, 3, 5, 6, 4], [60, 200, 300, 130, 90]
+    probs, keep, ref = _batch(2500, outs, Ms, 61)
+    x0 = np.tile([0.0, 0.0, 0.0, 0.0, -2.0], (len(outs), 1))
+    ctx.set_cu_split(8)
+    res = {}
+    try:
+        for on in (False, True):
+            ctx.set_fit_overlap(on)
+            a = G.fit_batch(probs, x0, max_evals=20, g_tol=-1.0)
+            b = G.fit_batch(probs, x0, max_evals=400, g_tol=0.05)
+            t = ref[0][2]
+            ts = np.linspace(t[0], t[-1], 700) + 1e-3
+            Vs = [np.vstack([np.interp(ts, t, V[q]) for q in range(V.shape[0])]) for V, _, _, _ in ref]
+            c, cm, cs = G.fit_predict_batch(probs, x0, ts, Vs, max_evals=16, g_tol=-1.0)
+            res[on] = (a, b, c, cm, cs)
+    finally:
+        ctx.set_fit_overlap(True)
+    (a0, b0, c0, cm0, cs0), (a1, b1, c1, cm1, cs1) = res[False], res[True]
+    assert len(set(b0.evals)) > 1          # the groups shrink at different rounds
+    for x, y in ((a0, a1), (b0, b1), (c0, c1)):
+        np.testing.assert_array_equal(x.theta, y.theta)
+        np.testing.assert_array_equal(x.nlml, y.nlml)
+        np.testing.assert_array_equal(x.evals, y.evals)
+    for x, y in zip(cm0 + cs0, cm1 + cs1):
+        np.testing.assert_array_equal(x, y)

@@ -223,3 +223,23 @@ def test_returns_follow_the_reference():
     assert "return MvNormal(me, Symmetric(cov)), UpperTriangular(U)" in src   # :185,196
     assert "return opt_lgssm, [Marginal(" in src                   # temporal_gp_inference.jl:113
     assert "return means, stds" in src                             # gpar_scaled_inference.jl:135
+
+
+def test_multi_output_driver_binds_the_batched_entry_points():
+    """get_gpar_scaled_predictions_batch: the reference's per-output driver loop
+    (GPAR_scaled_examples.jl:132-175, eeg.jl:212-281) as one gpar_fit_predict_chain (chained
+    inference inputs) or gpar_fit_predict call, taking the reference call's positional arguments
+    per output and its fit keywords."""
+    src = _shim()
+    m = re.search(r"^function get_gpar_scaled_predictions_batch\(", src, re.M)
+    assert m
+    body = src[m.start():src.index("\nend\n", m.start())]
+    syms = [c[0] for c in _ccalls() if c[0] in body and f"(:{c[0]}, libgpar)" in body]
+    assert "gpar_fit_predict_chain" in syms and "gpar_fit_predict" in syms
+    pos, kw = _jl_function("get_gpar_scaled_predictions_batch")
+    assert pos == REFERENCE_SIGNATURES["get_gpar_scaled_predictions"][0]
+    for k in ("i_log_time_l", "i_log_time_var", "i_log_out_l", "i_log_out_var", "i_log_noise_sigma",
+              "optimization_time_limit", "debug", "chained"):
+        assert k in kw, k
+    assert "get_gpar_scaled_predictions_batch" in re.search(r"export ([\w,\s]+)\n", src).group(1)
+    assert "return means, stds" in body
