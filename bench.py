@@ -67,7 +67,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="north", choices=sorted(CONFIGS))
     ap.add_argument("--evals", type=int, default=None)
-    ap.add_argument("--predict", default="analytic", choices=["analytic", "mc"])
+    ap.add_argument("--predict", default="analytic", choices=["analytic", "mc", "path"],
+                    help="prediction estimator: analytic (S -> infinity limit), mc (the reference's "
+                         "100-sample estimator, gpar_scaled_inference.jl:110-130), path (tmp.jl:"
+                         "119-167: q(u) draws + posterior_rand paths of the time GP)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--separate-predict", action="store_true",
                     help="gpar_fit then one gpar_predict per output (q(u) recomputes the Gram at the "
@@ -352,6 +355,18 @@ def main():
         el = float(e[0])
     gram_n, gram_ms = ctx.kernel_stats("gram")
     wh_n, wh_ms = ctx.kernel_stats("whiten")
+    pred = {}
+    for fam, bound in (("pred_whiten", "hbm"), ("pred_adjoint", "hbm"), ("pred_rows", "hbm"),
+                       ("pred_gemm", "mfma")):
+        pn, pms = ctx.kernel_stats(fam)
+        if pn:
+            w = ctx.kernel_work(fam) / (pms * 1e-3)
+            pred[fam] = ({"bound": bound, "achieved": w / 1e9, "unit": "GB/s", "peak": HBM_PEAK_GBS,
+                          "frac": w / 1e9 / HBM_PEAK_GBS} if bound == "hbm" else
+                         {"bound": bound, "achieved": w / 1e12, "unit": "TFLOP/s",
+                          "peak": FP64_MFMA_PEAK_TFLOPS, "frac": w / 1e12 / FP64_MFMA_PEAK_TFLOPS})
+            pred[fam].update(launches=pn, avg_ms=pms / pn, ms_per_step=pms / args.steps,
+                             work_per_launch=ctx.kernel_work(fam) / pn)
     gram_work = ctx.kernel_work("gram")      # flops, N*M*(M+1) per launch
     wh_work = ctx.kernel_work("whiten")      # algorithmic HBM bytes (include/gpar_hip.h)
     try:   # telemetry only: never fails the line
@@ -494,6 +509,16 @@ def main():
             out["roofline_whiten"]["note"] = (
                 f"fit launches run on {8 * cu_split} of 256 CUs beside the Gram (HBM shared), "
                 "so per-launch time is not the whole-chip kernel's")
+        if pred:
+            pred["note"] = ("the analytic prediction's kernels (HIP events per launch, one per output "
+                            "per step): pred_whiten = merged-grid Cf*u assembly + whitening "
+                            "(whiten_kfu_mfma + whiten_vec; bytes 8 (N+N*) (D + M + 20)), pred_adjoint "
+                            "= adjoint_local_wide (bytes 8 ((N+N*)(Mp+1+21) + N* (Mp+1))), pred_rows = "
+                            "predict_rows (16 N* Mp), pred_gemm = the variance GEMM |Q V^T| with V "
+                            "triangular (N* M (M+1) flops)")
+            pred["ms_per_step_total"] = sum(v["ms_per_step"] for k, v in pred.items()
+                                            if isinstance(v, dict))
+            out["roofline_predict"] = pred
         out["memory"] = memory
         if self_check:
             out["self_check"] = self_check

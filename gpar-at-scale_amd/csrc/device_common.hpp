@@ -320,6 +320,24 @@ __device__ __forceinline__ void mat_inv(const double (&X)[D][D], double (&Z)[D][
   }
 }
 
+// Standard normal of the counter (seed, s, m), s < 2^32, m < 2^32: splitmix64 hashes + Box-Muller.
+// Reproducible for a given seed, independent of launch geometry (gpar_mc_normals /
+// gpar_path_normals export the same draws).
+__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__device__ __forceinline__ double counter_normal(uint64_t seed, uint64_t s, uint64_t m) {
+  const uint64_t key = (s << 32) | m;
+  const uint64_t a = splitmix64(seed ^ splitmix64(key * 2 + 1));
+  const uint64_t b = splitmix64(a ^ 0xD1B54A32D192ED03ull);
+  const double u1 = ((double)(a >> 11) + 0.5) * (1.0 / 9007199254740992.0);
+  const double u2 = ((double)(b >> 11)) * (1.0 / 9007199254740992.0);
+  return sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
+}
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);

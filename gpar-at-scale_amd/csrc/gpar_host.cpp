@@ -35,7 +35,8 @@ struct gpar_ctx {
   int split_w = 0, split_mask_w = 0;
   bool split_forced = false;      // set explicitly: no problem-size gate (split_active)
   bool split_dgw = true;          // a w/32 share of the DG items on the whitening CUs
-  hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr;
+  // s_d: the round-overlapping fit's dense tails, on the whitening CUs (fit_overlapped)
+  hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr, s_d = nullptr;
   hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
   // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
   // the caller's stream, e.g. the copies that produce its device inputs
@@ -62,7 +63,11 @@ struct gpar_ctx {
   Staging stage[2];
   Staging* staging = nullptr;
   bool overlap = true;            // gpar_ctx_set_fit_overlap (GPAR_OVERLAP=0 at creation): A/B
+  // gpar_fit_predict's predictions alternate over two streams (GPAR_PREDICT_LANES=1: one)
+  int predict_lanes = 2;
+  std::string ws_suffix;          // appended to workspace names (a prediction lane's own buffers)
   hipEvent_t ev_grp[2] = {nullptr, nullptr};   // fit_overlapped: a group's values are in
+  hipEvent_t ev_gn[2] = {nullptr, nullptr};    // fit_overlapped: a group's gains are done
   std::string err;
   struct Buf {
     void* p = nullptr;
@@ -151,7 +156,7 @@ static void flush_stats(gpar_ctx* c) {
 static bool is_cache_buf(const std::string& name) { return name.rfind("distcache", 0) == 0; }
 
 static void sync_all(gpar_ctx* c) {
-  for (hipStream_t st : {c->main, c->side, c->s_w, c->s_g, c->s_g2})
+  for (hipStream_t st : {c->main, c->side, c->s_w, c->s_g, c->s_g2, c->s_d})
     if (st) HIPCHECK(hipStreamSynchronize(st));
 }
 
@@ -181,7 +186,7 @@ static int64_t release_dist_cache(gpar_ctx* c, int64_t bytes = INT64_MAX) {
 static void* ws_bytes(gpar_ctx* c, const std::string& name, size_t bytes) {
   if (bytes == 0) bytes = 16;
   const bool evict = !is_cache_buf(name);   // eviction erases cache entries (b below)
-  auto& b = c->bufs[name];
+  auto& b = c->bufs[c->ws_suffix.empty() || !evict ? name : name + c->ws_suffix];
   if (b.bytes < bytes) {
     if (b.p) HIPCHECK(hipFree(b.p));
     b.p = nullptr;
@@ -1029,13 +1034,64 @@ static void chains_logpdf(gpar_ctx* c, int nchains, int64_t n, const double* t, 
 }
 
 
+// --------------------------------------------------------------------------- posterior paths
+// The path draws of a seed are decorrelated from its q(u) draws (gpar_path_normals exports them).
+constexpr uint64_t kPathSeedXor = 0x5851F42D4C957F2Dull;
+static uint64_t path_seed(uint64_t seed) { return seed ^ kPathSeedXor; }
+
+// S joint posterior samples of the latent f along one LGSSM chain (TemporalGPs posterior_rand,
+// tmp.jl:161-167) with the simulation smoother (k_path.hip): gains g of the chain over the n steps
+// of the grid t (params cp, observation noise `noise` per step or cp.r), data v_{k,s} = ym[k] - fx[k * ldfx + s]
+// (fx null: ym[k] for every sample).  Samples -> F[k * S + s].
+static void path_samples(gpar_ctx* c, int sdim, const GainsOut& g, const ChainParamsHost& cp,
+                         const double* t, const double* noise, int64_t n, const double* ym,
+                         const double* fx, int64_t ldfx, int S, uint64_t seed, double* F) {
+  const int64_t nch = (n + kChunk - 1) / kChunk;
+  const size_t cs = (size_t)nch * S * kSStride;
+  double* lq = ws<double>(c, "path_lq", (size_t)n * sdim * sdim);
+  double* phia = ws<double>(c, "path_phia", (size_t)nch * sdim * sdim);
+  double* z = ws<double>(c, "path_z", (size_t)S * n);
+  double* X = ws<double>(c, "path_X", (size_t)n * S);
+  double* h = ws<double>(c, "path_h", (size_t)n * 4);   // the adjoint fix-up rows (kGStride)
+  double* sp_ = ws<double>(c, "path_sp", cs);
+  double* cp_ = ws<double>(c, "path_cp", cs);
+  double* send = ws<double>(c, "path_send", cs);
+  double* cin = ws<double>(c, "path_cin", cs);
+  double* bend = ws<double>(c, "path_bend", cs);
+  double* chat = ws<double>(c, "path_chat", cs);
+  const uint64_t ps = path_seed(seed);
+  Timed tm_(c, "path");
+  // prior paths: local pass, carry with the chunk transfers prod A_k, final pass (x~[0] -> F,
+  // the data columns v - y~ -> z)
+  launch_dk_consts(c->stream, sdim, t, n, cp.inv_l, cp.s, lq);
+  launch_dk_phi(c->stream, sdim, g.rec, n, kChunk, nch, phia);
+  launch_dk_prior(c->stream, sdim, g.rec, lq, noise, cp.r, n, kChunk, nch, S, ps, ym, fx, ldfx,
+                  nullptr, sp_, nullptr, nullptr);
+  run_carry(c, sdim, phia, 0, sp_, cp_, 0, nch, S, S, 1, "pathp");
+  launch_dk_prior(c->stream, sdim, g.rec, lq, noise, cp.r, n, kChunk, nch, S, ps, ym, fx, ldfx,
+                  cp_, nullptr, F, z);
+  // smoother mean of the S columns (shared gains): whitening into X (column s), carry, adjoint,
+  // reverse carry -- the prediction's machinery -- then F += v - R Sigma^{-1} v
+  launch_whiten_vec(c->stream, sdim, g.rec, 0, z, n, n, kChunk, nch, S, X, 1, send, kSStride, S, 0,
+                    /*astride=*/S);
+  run_carry(c, sdim, g.phi, 0, send, cin, 0, nch, S, S, 1, "pathf");
+  launch_gains_adjoint(c->stream, sdim, g.rec, n, kChunk, nch, 1, h);
+  launch_adjoint_local_wide(c->stream, sdim, X, S, S, g.rec, g.g, cin, S, n, kChunk, nch, bend,
+                            nullptr);
+  run_carry(c, sdim, g.phi, 0, bend, chat, 0, nch, S, S, 1, "pathb", /*rev=*/true);
+  launch_dk_finish(c->stream, sdim, X, S, h, chat, z, noise, cp.r, n, kChunk, nch, S, F);
+  check_launch("path samples");
+}
+
 // --------------------------------------------------------------------------- prediction
 // Prediction half of get_gpar_scaled_predictions (gpar_scaled_inference.jl:63-135); see the
 // header of k_predict.hip for the algebra.
+// defer (device memory only): the outputs are queued on c->stream but not waited for -- the caller
+// synchronises (gpar_fit_predict's prediction lanes).
 static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
                          int64_t n_star, const double* t_star_in, const double* v_star_in,
                          int64_t ldvs, int mode, int samples, uint64_t seed, double* mean_out,
-                         double* std_out, const GramCache* gc = nullptr) {
+                         double* std_out, const GramCache* gc = nullptr, bool defer = false) {
   const int64_t n = P.n, m = P.m, d = P.d, mp = P.mp, mc = P.mc;
   // ---- test inputs on device, ascending (host inputs are stably sorted here, outputs
   //      un-permuted at the end; device inputs must already be ascending)
@@ -1100,50 +1156,14 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
   launch_merge_side(c->stream, P.t, n, ts, n_star, 0, P.y, s2, P.v, P.ldv, (int)d, tm, ym, rm, vm, d, nullptr);
   launch_merge_side(c->stream, ts, n_star, P.t, n, 1, nullptr, 1e10, vs, ldv_s, (int)d, tm, ym, rm, vm, d, pos);
   check_launch("predict: merge");
-  // ---- gains on the merged grid (noise sigma^2 train / 1e10 test)
-  std::vector<ChainParamsHost> cps{{1.0 / th.l_t, th.l_t, th.sv_t * th.sv_t, s2}};
-  GainsOut g = run_gains(c, P.sdim, tm, nt, cps, rm, false, "pred");
-  // ---- whiten Cf*u columns (on the fly) and y* into X, forward carry
-  const int64_t ldx = mp + 64;
-  double* X = ws<double>(c, "pr_X", (size_t)nt * ldx);
-  double* send = ws<double>(c, "pr_send", (size_t)nch * mc * 4);
-  double* cin = ws<double>(c, "pr_cin", (size_t)nch * mc * 4);
-  double* bend = ws<double>(c, "pr_bend", (size_t)nch * mc * 4);
-  double* chat = ws<double>(c, "pr_chat", (size_t)nch * mc * 4);
-  double* h = ws<double>(c, "pr_h", (size_t)nt * 4);
-  whiten_kfu_any(c, P, g.rec, vm, d, nt, nch, th, X, ldx, send, g.g, nullptr);
-  launch_whiten_vec(c->stream, P.sdim, g.rec, 0, ym, 0, nt, kChunk, nch, 1, X + mp, 0, send, 0,
-                    mc, mp, ldx);
-  check_launch("predict: whiten");
-  run_carry(c, P.sdim, g.phi, 0, send, cin, 0, nch, mc, mc, 1, "predf");
-  // ---- adjoint: Sigma^{-1} x = W^T (W x)
-  launch_gains_adjoint(c->stream, P.sdim, g.rec, nt, kChunk, nch, 1, h);
-  // u is read back only at the test rows (predict_rows), where rm = 1e10
-  launch_adjoint_local_wide(c->stream, P.sdim, X, ldx, mc, g.rec, g.g, cin, mc, nt, kChunk, nch,
-                            bend, rm);
-  check_launch("predict: adjoint");
-  run_carry(c, P.sdim, g.phi, 0, bend, chat, 0, nch, mc, mc, 1, "predb", /*rev=*/true);
-  // ---- per test row: Q = R Sigma^{-1} Cf*u, mean
-  double* Q = ws<double>(c, "pr_Q", (size_t)n_star * mp);
-  double* dmean = ws<double>(c, "pr_mean", n_star);
-  double* dstd = ws<double>(c, "pr_std", n_star);
-  launch_predict_rows(c->stream, P.sdim, X, ldx, h, chat, mc, mp, m, kChunk, pos, n_star, rm, ym, w,
-                      Q, mp, dmean);
-  check_launch("predict: rows");
-  // ---- Z = Q V^T;  ANALYTIC: std = |Z_i|;  MC: f_s = mean + Z xi_s, mean/std over samples
-  const int ncb = (int)((m + 127) / 128);
-  if (mode == GPAR_PREDICT_ANALYTIC) {
-    double* rowsq = ws<double>(c, "pr_rowsq", (size_t)ncb * n_star);
-    launch_gemm_nt(c->stream, Q, mp, Vm, ld, n_star, m, m, 0, nullptr, 0, rowsq, 0, nullptr,
-                   nullptr, nullptr, /*tri=*/1);
-    launch_rowsq_finish(c->stream, rowsq, n_star, ncb, dstd);
-  } else {
-    // Draws as Distributions samples q_u = MvNormal(m_e, Symmetric(inv(D)))
-    // (gpar_scaled_inference.jl:103,185): m_e + Lc xi with Lc = chol(inv(D)) lower, so a given
-    // xi (gpar_mc_normals) gives the reference's sample; f_s = mean + (I - S) K* U_u^{-1} Lc xi_s.
+  // q(u) draws as Distributions samples q_u = MvNormal(m_e, Symmetric(inv(D)))
+  // (gpar_scaled_inference.jl:103,185): m_e + Lc xi with Lc = chol(inv(D)) lower, so a given xi
+  // (gpar_mc_normals) gives the reference's sample; W = Lc^T L_u^{-1} carries it through U_u^{-1}.
+  int* stc = nullptr;
+  auto mc_factor = [&]() {
     double* Lc = ws<double>(c, "pr_Lc", (size_t)ld * ld);
     double* Tdc = ws<double>(c, "pr_Tdc", (size_t)q.nb * kDenseNB * kDenseNB);
-    int* stc = ws<int>(c, "pr_stc", 1);
+    stc = ws<int>(c, "pr_stc", 1);
     HIPCHECK(hipMemsetAsync(stc, 0, sizeof(int), c->stream));
     launch_pad_identity_copy(c->stream, q.cov, ld, (int)m, Lc);
     CholJob2Host cj{Lc, nullptr, Tdc, stc};
@@ -1153,35 +1173,119 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
     double* W = ws<double>(c, "pr_W", (size_t)ld * ld);
     launch_mc_factor(c->stream, Lc, X1, ld, (int)m, W);
     check_launch("predict: MC factor");
-    double* Z = ws<double>(c, "pr_Z", (size_t)n_star * mp);
-    double* rowsq = ws<double>(c, "pr_rowsq", (size_t)ncb * n_star);
-    double* xi = ws<double>(c, "pr_xi", (size_t)samples * mp);
-    double* mmc = ws<double>(c, "pr_mmc", n_star);
-    launch_gemm_nt(c->stream, Q, mp, W, ld, n_star, m, m, 0, Z, mp, rowsq, 0, nullptr, nullptr,
-                   nullptr, /*tri=*/0);
-    launch_normal(c->stream, xi, mp, samples, m, samples, seed);
-    if (samples <= 128) {   // one column tile: statistics in the GEMM epilogue
-      launch_gemm_nt(c->stream, Z, mp, xi, mp, n_star, samples, m, 1, nullptr, 0, nullptr, samples,
-                     dmean, mmc, dstd);
-    } else {
-      const int nsb = (int)((samples + 127) / 128);
-      double* part = ws<double>(c, "pr_mcpart", (size_t)nsb * n_star * 2);
-      launch_gemm_nt(c->stream, Z, mp, xi, mp, n_star, samples, m, 2, nullptr, 0, part, 0, nullptr,
-                     nullptr, nullptr);
-      launch_mc_stats_finish(c->stream, part, n_star, nsb, samples, dmean, mmc, dstd);
-    }
-    dmean = mmc;
+    return W;
+  };
+  auto check_mc_factor = [&]() {
     int st = 0;
     d2h(c, &st, stc, 1);
     sync(c);
     if (st) throw Error(GPAR_ERR_NOT_PD, "PosDefException: cholesky(Symmetric(inv(D))) failed (MvNormal, gpar_scaled_inference.jl:185)");
+  };
+  // ---- gains on the merged grid (noise sigma^2 train / 1e10 test)
+  std::vector<ChainParamsHost> cps{{1.0 / th.l_t, th.l_t, th.sv_t * th.sv_t, s2}};
+  const bool path = mode == GPAR_PREDICT_PATH;
+  GainsOut g = run_gains(c, P.sdim, tm, nt, cps, rm, false, "pred");
+  double* dmean = ws<double>(c, "pr_mean", n_star);
+  double* dstd = ws<double>(c, "pr_std", n_star);
+  if (path) {
+    // tmp.jl:119-167: per sample, fx_s = Cf*u U_u^{-1} e_s (e_s ~ q(u)) on the merged grid, then a
+    // posterior path of the time GP given y* - fx_s (FFBS), f*_s = fx_s + f_t,s
+    double* W = mc_factor();
+    double* xi = ws<double>(c, "pr_xi", (size_t)samples * mp);
+    launch_normal(c->stream, xi, mp, samples, m, samples, seed);
+    double* Bm = ws<double>(c, "pr_Bm", (size_t)samples * mp);
+    launch_path_bmat(c->stream, W, ld, w, xi, mp, samples, (int)m, mp, Bm, mp);
+    double* Ks = ws<double>(c, "pr_Ks", (size_t)nt * mp);   // Cf*u (gpar_scaled_inference.jl:89)
+    launch_dist2(c->stream, P.ok, vm, d, nt, P.z, P.ldz, m, mp, (int)d, P.zc, Ks, mp,
+                 /*take_sqrt=*/P.ok != GPAR_EQ);
+    launch_kfu_from_dist(c->stream, P.ok, Ks, nt, m, mp, 1.0 / th.l_o, th.sv_o * th.sv_o);
+    double* FX = ws<double>(c, "pr_FX", (size_t)nt * samples);
+    double* fxsq = ws<double>(c, "pr_fxsq", (size_t)nt);
+    launch_gemm_nt(c->stream, Ks, mp, Bm, mp, nt, samples, m, 0, FX, samples, fxsq, 0, nullptr,
+                   nullptr, nullptr, 0);
+    check_launch("predict: path fx");
+    double* F = ws<double>(c, "pr_F", (size_t)nt * samples);
+    path_samples(c, P.sdim, g, cps[0], tm, rm, nt, ym, FX, samples, samples, seed, F);
+    launch_path_stats(c->stream, FX, samples, F, samples, pos, n_star, dmean, dstd);
+    check_launch("predict: path stats");
+    check_mc_factor();
+  } else {
+    // ---- whiten Cf*u columns (on the fly) and y* into X, forward carry
+    const int64_t ldx = mp + 64;
+    double* X = ws<double>(c, "pr_X", (size_t)nt * ldx);
+    double* send = ws<double>(c, "pr_send", (size_t)nch * mc * 4);
+    double* cin = ws<double>(c, "pr_cin", (size_t)nch * mc * 4);
+    double* bend = ws<double>(c, "pr_bend", (size_t)nch * mc * 4);
+    double* chat = ws<double>(c, "pr_chat", (size_t)nch * mc * 4);
+    double* h = ws<double>(c, "pr_h", (size_t)nt * 4);
+    {   // algorithmic HBM bytes: merged inputs V* (d) read, gains records + fix-up rows (20), the
+        // m whitened Cf*u columns written, per merged row
+      Timed tm_(c, "pred_whiten", 8.0 * (double)nt * ((double)d + (double)m + 20.0));
+      whiten_kfu_any(c, P, g.rec, vm, d, nt, nch, th, X, ldx, send, g.g, nullptr);
+      launch_whiten_vec(c->stream, P.sdim, g.rec, 0, ym, 0, nt, kChunk, nch, 1, X + mp, 0, send, 0,
+                        mc, mp, ldx);
+    }
+    check_launch("predict: whiten");
+    run_carry(c, P.sdim, g.phi, 0, send, cin, 0, nch, mc, mc, 1, "predf");
+    // ---- adjoint: Sigma^{-1} x = W^T (W x)
+    launch_gains_adjoint(c->stream, P.sdim, g.rec, nt, kChunk, nch, 1, h);
+    // u is read back only at the test rows (predict_rows), where rm = 1e10
+    {   // bytes: the mc whitened columns read per merged row, records + fix-up rows + R (21), u
+        // written at the test rows
+      Timed tm_(c, "pred_adjoint", 8.0 * ((double)nt * ((double)mc + 21.0) + (double)n_star * (double)mc));
+      launch_adjoint_local_wide(c->stream, P.sdim, X, ldx, mc, g.rec, g.g, cin, mc, nt, kChunk, nch,
+                                bend, rm);
+    }
+    check_launch("predict: adjoint");
+    run_carry(c, P.sdim, g.phi, 0, bend, chat, 0, nch, mc, mc, 1, "predb", /*rev=*/true);
+    // ---- per test row: Q = R Sigma^{-1} Cf*u, mean
+    double* Q = ws<double>(c, "pr_Q", (size_t)n_star * mp);
+    {   // bytes: u rows at the test points read, Q rows written (mp each)
+      Timed tm_(c, "pred_rows", 16.0 * (double)n_star * (double)mp);
+      launch_predict_rows(c->stream, P.sdim, X, ldx, h, chat, mc, mp, m, kChunk, pos, n_star, rm, ym,
+                          w, Q, mp, dmean);
+    }
+    check_launch("predict: rows");
+    // ---- Z = Q V^T;  ANALYTIC: std = |Z_i|;  MC: f_s = mean + Z xi_s, mean/std over samples
+    const int ncb = (int)((m + 127) / 128);
+    if (mode == GPAR_PREDICT_ANALYTIC) {
+      double* rowsq = ws<double>(c, "pr_rowsq", (size_t)ncb * n_star);
+      {   // flops of |Q_i V^T|^2 with V lower triangular: 2 n* sum_c (c + 1) = n* m (m + 1)
+        Timed tm_(c, "pred_gemm", (double)n_star * (double)m * (double)(m + 1));
+        launch_gemm_nt(c->stream, Q, mp, Vm, ld, n_star, m, m, 0, nullptr, 0, rowsq, 0, nullptr,
+                       nullptr, nullptr, /*tri=*/1);
+      }
+      launch_rowsq_finish(c->stream, rowsq, n_star, ncb, dstd);
+    } else {
+      // MC: f_s = mean + (I - S) K* U_u^{-1} Lc xi_s
+      double* W = mc_factor();
+      double* Z = ws<double>(c, "pr_Z", (size_t)n_star * mp);
+      double* rowsq = ws<double>(c, "pr_rowsq", (size_t)ncb * n_star);
+      double* xi = ws<double>(c, "pr_xi", (size_t)samples * mp);
+      double* mmc = ws<double>(c, "pr_mmc", n_star);
+      launch_gemm_nt(c->stream, Q, mp, W, ld, n_star, m, m, 0, Z, mp, rowsq, 0, nullptr, nullptr,
+                     nullptr, /*tri=*/0);
+      launch_normal(c->stream, xi, mp, samples, m, samples, seed);
+      if (samples <= 128) {   // one column tile: statistics in the GEMM epilogue
+        launch_gemm_nt(c->stream, Z, mp, xi, mp, n_star, samples, m, 1, nullptr, 0, nullptr, samples,
+                       dmean, mmc, dstd);
+      } else {
+        const int nsb = (int)((samples + 127) / 128);
+        double* part = ws<double>(c, "pr_mcpart", (size_t)nsb * n_star * 2);
+        launch_gemm_nt(c->stream, Z, mp, xi, mp, n_star, samples, m, 2, nullptr, 0, part, 0, nullptr,
+                       nullptr, nullptr);
+        launch_mc_stats_finish(c->stream, part, n_star, nsb, samples, dmean, mmc, dstd);
+      }
+      dmean = mmc;
+      check_mc_factor();
+    }
+    check_launch("predict: gemm");
   }
-  check_launch("predict: gemm");
   // ---- outputs
   if (mem == GPAR_MEM_DEVICE) {
     HIPCHECK(hipMemcpyAsync(mean_out, dmean, n_star * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
     HIPCHECK(hipMemcpyAsync(std_out, dstd, n_star * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
-    sync(c);
+    if (!defer) sync(c);
   } else if (perm.empty()) {   // t* was ascending: straight into the caller's buffers
     d2h(c, mean_out, dmean, n_star);
     d2h(c, std_out, dstd, n_star);
@@ -1270,7 +1374,7 @@ static int fail(gpar_ctx* c, int code, const char* what) {
   c->stream = c->main;
   (void)hipStreamSynchronize(c->main);
   (void)hipStreamSynchronize(c->side);
-  for (hipStream_t st : {c->s_w, c->s_g, c->s_g2})
+  for (hipStream_t st : {c->s_w, c->s_g, c->s_g2, c->s_d})
     if (st) (void)hipStreamSynchronize(st);
   (void)hipGetLastError();
   return code;
@@ -1303,7 +1407,7 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
     if (hipGetDeviceProperties(&pr, c->device) != hipSuccess) return GPAR_ERR_HIP;
     if (pr.multiProcessorCount != 256) return GPAR_ERR_UNSUPPORTED;   // the MI355X layout only
     // a stream's CU mask is fixed at its creation: a new width gets new streams
-    for (hipStream_t* st : {&c->s_w, &c->s_g, &c->s_g2})
+    for (hipStream_t* st : {&c->s_w, &c->s_g, &c->s_g2, &c->s_d})
       if (*st) {
         (void)hipStreamSynchronize(*st);
         (void)hipStreamDestroy(*st);
@@ -1315,7 +1419,8 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
     for (int i = 0; i < 256; ++i) (i < 8 * w ? mw : mg)[i / 32] |= 1u << (i % 32);
     if (hipExtStreamCreateWithCUMask(&c->s_w, 8, mw) != hipSuccess ||
         hipExtStreamCreateWithCUMask(&c->s_g, 8, mg) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&c->s_g2, 8, mg) != hipSuccess)
+        hipExtStreamCreateWithCUMask(&c->s_g2, 8, mg) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&c->s_d, 8, mw) != hipSuccess)
       return GPAR_ERR_HIP;
     if (!c->ev_sp &&
         (hipEventCreateWithFlags(&c->ev_gd[0], hipEventDisableTiming) != hipSuccess ||
@@ -1356,6 +1461,7 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
   c->stream = c->main;
   if (const char* e = std::getenv("GPAR_PIPELINE")) c->pipeline = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_OVERLAP")) c->overlap = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GPAR_PREDICT_LANES")) c->predict_lanes = std::atoi(e) > 1 ? 2 : 1;
   // A/B knobs: GPAR_SPLIT_CUS overrides the default CU split, GPAR_SPLIT_DGW=0 keeps the DG
   // kernel off the whitening CUs
   if (const char* e = std::getenv("GPAR_SPLIT_DGW")) c->split_dgw = std::atoi(e) != 0;
@@ -1382,12 +1488,13 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev_pc[0]);
   (void)hipEventDestroy(ctx->ev_pc[1]);
   {
-    for (hipStream_t st : {ctx->s_w, ctx->s_g, ctx->s_g2})
+    for (hipStream_t st : {ctx->s_w, ctx->s_g, ctx->s_g2, ctx->s_d})
       if (st) {
         (void)hipStreamSynchronize(st);
         (void)hipStreamDestroy(st);
       }
-    for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_grp[0], ctx->ev_grp[1]})
+    for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_grp[0], ctx->ev_grp[1],
+                          ctx->ev_gn[0], ctx->ev_gn[1]})
       if (ev) (void)hipEventDestroy(ev);
     for (auto& s : ctx->stage)
       if (s.host) (void)hipHostFree(s.host);
@@ -1605,6 +1712,8 @@ static int64_t predict_ws_estimate(int64_t n, int64_t n_star, int64_t mp, int64_
                     + 4 * nch * (mp + 1) * 4       // carries
                     + 8 * mp * mp;                 // q(u) dense
   if (mode == GPAR_PREDICT_MC) doubles += n_star * mp + (int64_t)samples * mp + 2 * n_star * ((samples + 127) / 128);
+  if (mode == GPAR_PREDICT_PATH)   // Cf*u, fx, the data columns, their whitening and the samples
+    doubles += nt * mp + (int64_t)samples * (4 * nt + 2 * mp) + 6 * nch * samples * kSStride;
   return doubles * (int64_t)sizeof(double);
 }
 
@@ -1681,8 +1790,8 @@ static std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<
 // round (eval_dtc), every round drains the chip: its first whitening runs alone, its last Gram
 // runs alone, then the next round's gains, the dense tail and a host sync.  On the CU-split
 // schedule with >= 4 outputs, fit_overlapped deals the outputs into two groups that take turns:
-// while the host waits for group A's values (A's dense tail runs on the context stream beside the
-// split streams) and steps A's simplices, group B's whitenings and Grams keep both sides of the
+// while the host waits for group A's values (A's dense tail runs on the whitening CUs, which have
+// slack beside the Gram) and steps A's simplices, group B's whitenings and Grams keep both sides of the
 // split busy, and A's next round (gains on the whitening CUs, then its jobs) is queued behind
 // them -- one drain per fit instead of one per round.  Every output evaluates exactly the points
 // its own simplex asks for, in the same order, with the same kernels and per-problem arithmetic
@@ -1712,7 +1821,7 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
   int64_t mpmax = 0;
   for (auto& p : P) mpmax = std::max(mpmax, p.mp);
   const size_t sq = (size_t)mpmax * mpmax;
-  for (hipEvent_t* ev : {&c->ev_grp[0], &c->ev_grp[1]})
+  for (hipEvent_t* ev : {&c->ev_grp[0], &c->ev_grp[1], &c->ev_gn[0], &c->ev_gn[1]})
     if (!*ev) HIPCHECK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   OverlapGroup grp[2];
   for (int i = 0; i < np; ++i) grp[i & 1].members.push_back(i);
@@ -1754,21 +1863,22 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
   SplitPipe sp(c, n, mpmax);
   // a group's dense tail + finish on the context stream as soon as its round's last Gram is
   // issued; its values land in pinned memory, ev_grp[g] marks them
+  // (on the whitening CUs: beside the Gram on the whole chip it slowed every Gram by ~5 %)
   auto issue_dense = [&](OverlapGroup& G, int64_t job) {
-    OnStream on_(c, c->main);
+    OnStream on_(c, c->s_d);
     StagingScope st_(c, G.id);
-    HIPCHECK(hipStreamWaitEvent(c->main, c->ev_gd[job & 1], 0));
+    HIPCHECK(hipStreamWaitEvent(c->s_d, c->ev_gd[job & 1], 0));
     const int na = (int)G.act.size();
     DenseOut dn = run_dense(c, G.sub, G.th, G.go, false);
     std::vector<Finish2JobHost> fj(na);
     for (int a = 0; a < na; ++a) fj[a] = finish_job(dn, G.go, G.sub[a], a, nch, G.dout + a, nullptr);
     auto* dfj = ws<Finish2JobHost>(c, "finishjobs", np);
     h2d(c, dfj, fj.data(), na);
-    launch_finish2(c->main, dfj, na, dn.ld, dn.nb);
+    launch_finish2(c->s_d, dfj, na, dn.ld, dn.nb);
     check_launch("finish");
-    HIPCHECK(hipMemcpyAsync(G.hout, G.dout, na * sizeof(double), hipMemcpyDeviceToHost, c->main));
-    HIPCHECK(hipMemcpyAsync(G.hstat, dn.status, 2 * na * sizeof(int), hipMemcpyDeviceToHost, c->main));
-    HIPCHECK(hipEventRecord(c->ev_grp[G.id], c->main));
+    HIPCHECK(hipMemcpyAsync(G.hout, G.dout, na * sizeof(double), hipMemcpyDeviceToHost, c->s_d));
+    HIPCHECK(hipMemcpyAsync(G.hstat, dn.status, 2 * na * sizeof(int), hipMemcpyDeviceToHost, c->s_d));
+    HIPCHECK(hipEventRecord(c->ev_grp[G.id], c->s_d));
   };
   sp.on_gram = [&](const StageJob& j, int64_t job) {
     if (j.last) issue_dense(grp[j.group], job);
@@ -1794,14 +1904,19 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
       ys[a] = P[i].y;
     }
     c->stage[G.id].used = G.res_bytes;   // the previous round's uploads have been consumed
+    // the gains run on the whitening CUs beside the other group's whitenings (s_d), not in the
+    // whitening stream's order: queued there they delayed the next whitening, and with it the
+    // DG share that ends the previous Gram
     GainsOut gn;
     {
-      OnStream on_(c, c->s_w);
+      OnStream on_(c, c->s_d);
       StagingScope st_(c, G.id);
       gn = run_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, G.id ? "fitB" : "fitA", &ys,
                      G.alpha_all, G.asend_all);
       HIPCHECK(hipMemcpyAsync(G.go.logs, gn.logs, (size_t)na * nch * sizeof(double),
-                              hipMemcpyDeviceToDevice, c->s_w));
+                              hipMemcpyDeviceToDevice, c->s_d));
+      HIPCHECK(hipEventRecord(c->ev_gn[G.id], c->s_d));
+      HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gn[G.id], 0));
     }
     {   // narrower outputs: their G / r slot padding must read as zero in the dense tail
       OnStream on_(c, c->s_g);
@@ -1846,6 +1961,7 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
     G.in_flight = false;
   };
   sp.start();
+  HIPCHECK(hipStreamWaitEvent(c->s_d, c->ev_sp, 0));   // the inputs / distance cache on main
   begin_round(grp[0]);
   begin_round(grp[1]);
   for (int g = 0; grp[0].in_flight || grp[1].in_flight; g ^= 1) {
@@ -1974,9 +2090,10 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
   ARGCHECK(probs && nprob >= 1 && log_theta0 && theta_out && t_star && v_star && ldvs &&
                mean_out && std_out, "null argument");
   ARGCHECK(n_star >= 1, "n_star must be >= 1");
-  ARGCHECK(mode == GPAR_PREDICT_ANALYTIC || mode == GPAR_PREDICT_MC, "bad mode");
-  if (mode == GPAR_PREDICT_MC)
-    ARGCHECK(samples >= 2 && samples <= kMaxSamples, "MC mode takes 2..65536 samples");
+  ARGCHECK(mode == GPAR_PREDICT_ANALYTIC || mode == GPAR_PREDICT_MC || mode == GPAR_PREDICT_PATH,
+           "bad mode");
+  if (mode != GPAR_PREDICT_ANALYTIC)
+    ARGCHECK(samples >= 2 && samples <= kMaxSamples, "MC / path modes take 2..65536 samples");
   for (int i = 0; i < nprob; ++i) {
     ARGCHECK(v_star[i] && mean_out[i] && std_out[i], "null per-output pointer");
     ARGCHECK(ldvs[i] >= probs[i].d, "ldvs must be >= d");
@@ -1988,18 +2105,41 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
   std::vector<DevProblem> P;
   for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
   FitKeep keep;
+  const int mem = probs[0].mem;
+  // Prediction lanes: with device-memory outputs and no chain between the predictions, outputs
+  // alternate over the context's two streams, each lane with its own workspace (name suffix), so
+  // one output's memory-bound passes (merge, adjoint, rows) run beside the other's DP / MFMA work
+  // (whitening, variance GEMM).  A lane's host syncs (q(u)'s Cholesky status) wait for that lane
+  // only.
+  const bool lanes = mem == GPAR_MEM_DEVICE && !chain && nprob > 1 && ctx->predict_lanes > 1;
   // the predictions' workspace (named buffers, reused across the outputs: the largest counts)
   int64_t pred_bytes = 0;
   for (const auto& p : P)
     pred_bytes = std::max(pred_bytes, predict_ws_estimate(p.n, n_star, p.mp, p.d, mode, samples));
-  fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, &keep, pred_bytes);
-  const int mem = probs[0].mem;
+  fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, &keep, (lanes ? 2 : 1) * pred_bytes);
+  struct LaneScope {   // a lane's stream and workspace names; restored on any exit
+    gpar_ctx* c;
+    hipStream_t saved;
+    LaneScope(gpar_ctx* c_, int lane) : c(c_), saved(c_->stream) {
+      c->stream = lane ? c->side : c->main;
+      c->ws_suffix = lane ? "~1" : "";
+    }
+    ~LaneScope() {
+      c->stream = saved;
+      c->ws_suffix.clear();
+    }
+  };
+  if (lanes) {   // the side lane follows the fit (kept Grams, inputs) on the context stream
+    HIPCHECK(hipEventRecord(ctx->ev_fork, ctx->main));
+    HIPCHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+  }
   for (int i = 0; i < nprob; ++i) {
     const double* q = theta_out + 5 * i;
     const Theta th{q[0], q[1], q[2], q[3], q[4]};
+    LaneScope lane_(ctx, lanes ? (i & 1) : 0);
     predict_impl(ctx, P[i], th, mem, n_star, t_star, v_star[i], ldvs[i], mode, samples,
                  seed + (uint64_t)i, mean_out[i], std_out[i],
-                 keep.valid[i] ? &keep.gram[i] : nullptr);
+                 keep.valid[i] ? &keep.gram[i] : nullptr, /*defer=*/lanes);
     if (chain && chain_col[i] >= 0) {
       double* dst = chain + chain_col[i];
       if (mem == GPAR_MEM_DEVICE) {   // stream-ordered before the next output's merge reads it
@@ -2009,6 +2149,11 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
         for (int64_t k = 0; k < n_star; ++k) dst[k * ld_chain] = mean_out[i][k];
       }
     }
+  }
+  if (lanes) {
+    HIPCHECK(hipEventRecord(ctx->ev_join, ctx->side));
+    HIPCHECK(hipStreamWaitEvent(ctx->main, ctx->ev_join, 0));
+    sync(ctx);
   }
   if (chain && mem == GPAR_MEM_DEVICE) sync(ctx);
 }
@@ -2127,9 +2272,10 @@ int32_t gpar_predict(gpar_ctx* ctx, const gpar_problem* prob, const double* thet
   ARGCHECK(prob && theta && t_star && v_star && mean && std, "null argument");
   ARGCHECK(n_star >= 1, "n_star must be >= 1");
   ARGCHECK(ldvs >= prob->d, "ldvs must be >= d");
-  ARGCHECK(mode == GPAR_PREDICT_ANALYTIC || mode == GPAR_PREDICT_MC, "bad mode");
-  if (mode == GPAR_PREDICT_MC)
-    ARGCHECK(samples >= 2 && samples <= kMaxSamples, "MC mode takes 2..65536 samples");
+  ARGCHECK(mode == GPAR_PREDICT_ANALYTIC || mode == GPAR_PREDICT_MC || mode == GPAR_PREDICT_PATH,
+           "bad mode");
+  if (mode != GPAR_PREDICT_ANALYTIC)
+    ARGCHECK(samples >= 2 && samples <= kMaxSamples, "MC / path modes take 2..65536 samples");
   DevProblem P = prepare_problem(ctx, *prob, 0);
   std::vector<Theta> th = thetas_from(theta, 1);
   predict_impl(ctx, P, th[0], prob->mem, n_star, t_star, v_star, ldvs, mode, samples, seed, mean, std);
@@ -2145,6 +2291,56 @@ int32_t gpar_mc_normals(gpar_ctx* ctx, int32_t samples, int64_t m, uint64_t seed
   launch_normal(ctx->stream, xi, m, samples, m, samples, seed);
   check_launch("normal draws");
   d2h(ctx, xi_out, xi, (size_t)samples * m);
+  sync(ctx);
+  API_END(ctx)
+}
+
+int32_t gpar_path_normals(gpar_ctx* ctx, int32_t samples, int64_t n, int32_t d, uint64_t seed,
+                          double* xi_out) {
+  API_BEGIN(ctx)
+  ARGCHECK(xi_out, "null argument");
+  ARGCHECK(samples >= 1 && samples <= kMaxSamples, "samples must be in 1..65536");
+  ARGCHECK(d >= 1 && d <= 4 && n >= 1 && n * d <= ((int64_t)1 << 32) - 1, "n, d out of range");
+  double* xi = ws<double>(ctx, "path_xi_export", (size_t)samples * n * d);
+  launch_normal(ctx->stream, xi, n * d, samples, n * d, samples, path_seed(seed));
+  check_launch("path normal draws");
+  d2h(ctx, xi_out, xi, (size_t)samples * n * d);
+  sync(ctx);
+  API_END(ctx)
+}
+
+int32_t gpar_lgssm_posterior_rand(gpar_ctx* ctx, int64_t n, const double* t, const double* y,
+                                  const double* noise, int32_t kernel, const double* theta,
+                                  int32_t samples, uint64_t seed, int32_t mem, double* f_out) {
+  API_BEGIN(ctx)
+  ARGCHECK(n >= 1 && t && y && theta && f_out, "bad argument");
+  ARGCHECK(samples >= 1 && samples <= kMaxSamples, "samples must be in 1..65536");
+  ARGCHECK(mem == GPAR_MEM_HOST || mem == GPAR_MEM_DEVICE, "bad mem");
+  ARGCHECK(n <= ((int64_t)1 << 32) / 3, "n out of range");
+  const int sdim = sde_dim(kernel);
+  std::vector<ChainParamsHost> cps = chain_params(theta, 1);
+  const double *dt = t, *dy = y, *dn = noise;
+  if (mem == GPAR_MEM_HOST) {
+    check_sorted_host(t, n);
+    double* tt = ws<double>(ctx, "lpr_t", n);
+    double* yy = ws<double>(ctx, "lpr_y", n);
+    h2d(ctx, tt, t, n);
+    h2d(ctx, yy, y, n);
+    if (noise) {
+      double* nn = ws<double>(ctx, "lpr_noise", n);
+      h2d(ctx, nn, noise, n);
+      dn = nn;
+    }
+    dt = tt;
+    dy = yy;
+  }
+  GainsOut g = run_gains(ctx, sdim, dt, n, cps, dn, false, "lpr");
+  double* F = ws<double>(ctx, "lpr_F", (size_t)n * samples);
+  path_samples(ctx, sdim, g, cps[0], dt, dn, n, dy, nullptr, 0, samples, seed, F);
+  double* out = mem == GPAR_MEM_DEVICE ? f_out : ws<double>(ctx, "lpr_out", (size_t)n * samples);
+  launch_path_transpose(ctx->stream, F, n, samples, out);
+  check_launch("posterior_rand");
+  if (mem == GPAR_MEM_HOST) d2h(ctx, f_out, out, (size_t)n * samples);
   sync(ctx);
   API_END(ctx)
 }

@@ -34,7 +34,11 @@ __device__ __forceinline__ int64_t upper_bound(const double* a, int64_t n, doubl
   return lo;
 }
 
-// Scatter one side (train or test) into the merged arrays.  V rows are copied (d values).
+// Scatter one side (train or test) into the merged arrays.  A workgroup takes 256 consecutive
+// rows: each thread finds its row's merged position, then the group copies the rows' d inputs
+// cooperatively (consecutive threads -> consecutive elements: the reads are coalesced and the
+// writes nearly so, both sides being sorted), instead of one thread striding over its own row's
+// d values (measured 0.8 ms per side at 1e6 rows).
 __global__ __launch_bounds__(256) void merge_side(const double* __restrict__ ts, int64_t ns,
                                                   const double* __restrict__ other, int64_t no,
                                                   int is_test, const double* __restrict__ ys,
@@ -43,15 +47,26 @@ __global__ __launch_bounds__(256) void merge_side(const double* __restrict__ ts,
                                                   double* __restrict__ tm, double* __restrict__ ym,
                                                   double* __restrict__ rm, double* __restrict__ vm,
                                                   int64_t ldvm, int64_t* __restrict__ pos_out) {
-  const int64_t k = blockIdx.x * (int64_t)256 + threadIdx.x;
-  if (k >= ns) return;
-  const double tk = ts[k];
-  const int64_t pos = k + (is_test ? upper_bound(other, no, tk) : lower_bound(other, no, tk));
-  tm[pos] = tk;
-  ym[pos] = ys ? ys[k] : 0.0;
-  rm[pos] = rval;
-  for (int i = 0; i < d; ++i) vm[pos * ldvm + i] = vs[k * ldvs + i];
-  if (pos_out) pos_out[k] = pos;
+  __shared__ int64_t lpos[256];
+  const int64_t r0 = blockIdx.x * (int64_t)256;
+  const int64_t k = r0 + threadIdx.x;
+  if (k < ns) {
+    const double tk = ts[k];
+    const int64_t pos = k + (is_test ? upper_bound(other, no, tk) : lower_bound(other, no, tk));
+    tm[pos] = tk;
+    ym[pos] = ys ? ys[k] : 0.0;
+    rm[pos] = rval;
+    if (pos_out) pos_out[k] = pos;
+    lpos[threadIdx.x] = pos;
+  }
+  if (d <= 0) return;
+  __syncthreads();
+  const int rows = (int)((ns - r0) < 256 ? (ns - r0) : 256);
+  const int total = rows * d;   // <= 256 x 256
+  for (int e = threadIdx.x; e < total; e += 256) {
+    const int r = e / d, i = e - r * d;
+    vm[lpos[r] * ldvm + i] = vs[(r0 + r) * ldvs + i];
+  }
 }
 
 // ---------------------------------------------------------------------------- per test row
@@ -299,30 +314,15 @@ __global__ void pad_identity_copy(const double* __restrict__ src, int64_t ld, in
 }
 
 // ---------------------------------------------------------------------------- normal draws
-// xi[s * ld + m] ~ N(0, 1) for s < S, m < M (zero beyond), from a counter-based hash
-// (splitmix64) of (seed, s, m) + Box-Muller: reproducible for a given seed, independent of the
-// launch geometry and of the padding ld (gpar_mc_normals exports the same draws unpadded).
-__device__ __forceinline__ uint64_t splitmix64(uint64_t x) {
-  x += 0x9E3779B97F4A7C15ull;
-  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
-  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
-  return x ^ (x >> 31);
-}
+// xi[s * ld + m] ~ N(0, 1) for s < S, m < M (zero beyond): counter_normal(seed, s, m)
+// (device_common.hpp), independent of the launch geometry and of the padding ld (gpar_mc_normals
+// exports the same draws unpadded).
 __global__ void normal_kernel(double* __restrict__ xi, int64_t ld, int64_t S, int64_t M,
                               int64_t Sp, uint64_t seed) {
   const int64_t e = blockIdx.x * (int64_t)256 + threadIdx.x;
   if (e >= Sp * ld) return;
   const int64_t s = e / ld, m = e % ld;
-  double v = 0.0;
-  if (s < S && m < M) {
-    const uint64_t key = ((uint64_t)s << 32) | (uint64_t)m;
-    const uint64_t a = splitmix64(seed ^ splitmix64(key * 2 + 1));
-    const uint64_t b = splitmix64(a ^ 0xD1B54A32D192ED03ull);
-    const double u1 = ((double)(a >> 11) + 0.5) * (1.0 / 9007199254740992.0);
-    const double u2 = ((double)(b >> 11)) * (1.0 / 9007199254740992.0);
-    v = sqrt(-2.0 * log(u1)) * cospi(2.0 * u2);
-  }
-  xi[e] = v;
+  xi[e] = (s < S && m < M) ? counter_normal(seed, (uint64_t)s, (uint64_t)m) : 0.0;
 }
 
 // ---------------------------------------------------------------------------- chain scatter / gather

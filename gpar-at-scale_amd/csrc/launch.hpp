@@ -218,6 +218,27 @@ void launch_scatter_chains(hipStream_t st, const double* src, int64_t lds, int64
 void launch_gather_chains(hipStream_t st, const double* src, int64_t lds, int64_t ns,
                           const int64_t* pos, double* dst, int64_t ldd, int nchains);
 
+// k_path.hip (posterior path sampling: the simulation smoother batched over samples; layouts in
+// the file header)
+void launch_kfu_from_dist(hipStream_t st, int out_kind, double* K, int64_t n, int64_t m,
+                          int64_t mp, double inv_l, double s);
+void launch_path_bmat(hipStream_t st, const double* W, int64_t ld, const double* w, const double* xi,
+                      int64_t ldxi, int S, int m, int64_t mp, double* Bm, int64_t ldb);
+void launch_dk_consts(hipStream_t st, int sdim, const double* t, int64_t n, double inv_l, double s,
+                      double* lq);
+void launch_dk_phi(hipStream_t st, int sdim, const double* rec, int64_t n, int L, int64_t nch,
+                   double* phia);
+void launch_dk_prior(hipStream_t st, int sdim, const double* rec, const double* lq,
+                     const double* noise, double r, int64_t n, int L, int64_t nch, int S,
+                     uint64_t seed, const double* ym, const double* fx, int64_t ldfx,
+                     const double* cin, double* send, double* ft, double* z);
+void launch_dk_finish(hipStream_t st, int sdim, const double* X, int64_t ldx, const double* h,
+                      const double* chat, const double* z, const double* noise, double r,
+                      int64_t n, int L, int64_t nch, int S, double* f);
+void launch_path_stats(hipStream_t st, const double* fx, int64_t ldfx, const double* F, int S,
+                       const int64_t* pos, int64_t nstar, double* mean, double* std);
+void launch_path_transpose(hipStream_t st, const double* F, int64_t n, int S, double* out);
+
 // k_exact.hip
 void launch_exact_cov(hipStream_t st, const double* x, int64_t ldx, int64_t n, const double* x2,
                       int64_t ldx2, int64_t n2, int dx, int tk, int ok, double inv_lt, double s_t,

@@ -17,14 +17,14 @@ LIB_PATH = os.environ.get("GPAR_LIB_PATH", LIB_PATH)
 
 GPAR_OK, GPAR_ERR_ARG, GPAR_ERR_NOT_PD, GPAR_ERR_HIP, GPAR_ERR_OOM, GPAR_ERR_UNSUPPORTED, GPAR_ERR_STATE = range(7)
 GPAR_MEM_HOST, GPAR_MEM_DEVICE = 0, 1
-GPAR_PREDICT_ANALYTIC, GPAR_PREDICT_MC = 0, 1
+GPAR_PREDICT_ANALYTIC, GPAR_PREDICT_MC, GPAR_PREDICT_PATH = 0, 1, 2
 KERNEL_ID = {"matern12": 0, "matern32": 1, "matern52": 2, "eq": 3}
 
 # Every entry point include/gpar_hip.h declares (tests check the library exports them all).
 EXPORTED = (
     "gpar_abi_version", "gpar_ctx_create", "gpar_ctx_destroy", "gpar_last_error",
     "gpar_ctx_workspace_bytes", "gpar_ctx_trim", "gpar_dtc_objective", "gpar_dtc_objective_A",
-    "gpar_fit", "gpar_fit_predict", "gpar_fit_predict_chain", "gpar_mc_normals", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
+    "gpar_fit", "gpar_fit_predict", "gpar_fit_predict_chain", "gpar_mc_normals", "gpar_path_normals", "gpar_lgssm_posterior_rand", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
     "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_kernel_work", "gpar_ctx_reset_stats",
     "gpar_ctx_set_lanes", "gpar_ctx_set_cu_split", "gpar_ctx_set_fit_overlap", "gpar_ctx_get_cu_split", "gpar_ctx_set_dist_cache", "gpar_ctx_set_dist_cache_keep", "gpar_ctx_dist_cache_stats",
@@ -115,6 +115,8 @@ def load(path: str | None = None):
                                              C.POINTER(GparFitOptions), i64, vp, vp, vp, i32, i32,
                                              C.c_uint64, vp, i64, vp, dp, dp, dp, vp, vp]),
             "gpar_mc_normals": (i32, [vp, i32, i64, C.c_uint64, dp]),
+            "gpar_path_normals": (i32, [vp, i32, i64, i32, C.c_uint64, dp]),
+            "gpar_lgssm_posterior_rand": (i32, [vp, i64, dp, dp, dp, i32, dp, i32, C.c_uint64, i32, dp]),
             "gpar_q_u": (i32, [vp, C.POINTER(GparProblem), dp, dp, dp, dp]),
             "gpar_predict": (i32, [vp, C.POINTER(GparProblem), dp, i64, dp, dp, i64, i32, i32,
                                    C.c_uint64, dp, dp]),

@@ -148,6 +148,18 @@ def _after_torch(ctx, on=True):
         ctx.follow_stream(0, enable=False)
 
 
+_MODES = {"analytic": _lib.GPAR_PREDICT_ANALYTIC, "mc": _lib.GPAR_PREDICT_MC,
+          "path": _lib.GPAR_PREDICT_PATH}
+
+
+def _mode_id(mode):
+    """Prediction mode: "analytic" (the MC estimator's S -> infinity limit), "mc" (the reference's
+    estimator, gpar_scaled_inference.jl:110-130) or "path" (tmp.jl:119-167: posterior_rand paths)."""
+    if mode not in _MODES:
+        raise _arg_error(f"mode must be one of {sorted(_MODES)}")
+    return _MODES[mode]
+
+
 def _arg_error(msg):
     return _lib.DomainError(_lib.GPAR_ERR_ARG, msg)
 
@@ -354,7 +366,7 @@ def fit_predict_batch(problems, log_theta0, t_star, V_stars, max_evals=0, max_it
     LD = (C.c_int64 * P)(*ldvs)
     MP = (C.c_void_p * P)(*mp_)
     SP = (C.c_void_p * P)(*sp_)
-    md = _lib.GPAR_PREDICT_MC if mode == "mc" else _lib.GPAR_PREDICT_ANALYTIC
+    md = _mode_id(mode)
     if chain is not None and dev and chain.shape[0] != n_star:
         raise _arg_error("chain must have N* rows")
     with _after_torch(ctx, dev):
@@ -379,6 +391,46 @@ def mc_normals(samples, m, seed, device=0):
     xi = np.zeros((int(samples), int(m)))
     ctx.check(_lib.load().gpar_mc_normals(ctx.h, int(samples), int(m), int(seed), _ptr(xi)))
     return xi
+
+
+def path_normals(samples, n, d, seed, device=0):
+    """The backward-sampling draws of posterior_rand / mode="path" for (samples, n, d, seed):
+    samples x n x d (gpar_path_normals)."""
+    ctx = context(device)
+    xi = np.zeros((int(samples), int(n), int(d)))
+    ctx.check(_lib.load().gpar_path_normals(ctx.h, int(samples), int(n), int(d), int(seed), _ptr(xi)))
+    return xi
+
+
+def posterior_rand(t, y, theta, kernel="matern52", samples=1, seed=0, noise=None, device=0):
+    """TemporalGPs posterior_rand(rng, create_lgssm(t, l, pv, sigma, k; noise_vector), y, samples)
+    (called at src/gp/tmp.jl:161-167): joint draws of the latent f over t from its posterior given
+    y, by forward filtering and backward sampling (gpar_lgssm_posterior_rand).  theta = (l,
+    process_var, noise_sigma); noise: per-step observation variance (None: sigma^2).  Host arrays
+    -> samples x n numpy array; torch CUDA tensors -> samples x n device tensor."""
+    ctx, lib = context(device), _lib.load()
+    th = np.ascontiguousarray(np.asarray(theta, dtype=np.float64).reshape(3))
+    keep = _Keep()
+    if _is_torch(t):
+        import torch
+        n = t.numel()
+        out = torch.empty((int(samples), n), dtype=torch.float64, device=t.device)
+        tp, yp = _dev_vec(t, keep), _dev_vec(y, keep)
+        npp = _dev_vec(noise, keep) if noise is not None else None
+        with _after_torch(ctx):
+            ctx.check(lib.gpar_lgssm_posterior_rand(ctx.h, n, tp, yp, npp, _kernel_id(kernel),
+                                                    _ptr(th), int(samples), int(seed),
+                                                    _lib.GPAR_MEM_DEVICE, out.data_ptr()))
+        return out
+    n = len(np.asarray(t))
+    if len(np.asarray(y)) != n or (noise is not None and len(np.asarray(noise)) != n):
+        raise _arg_error("t, y (and noise) must have the same length")
+    out = np.zeros((int(samples), n))
+    ctx.check(lib.gpar_lgssm_posterior_rand(ctx.h, n, _host_vec(t, keep), _host_vec(y, keep),
+                                            _host_vec(noise, keep) if noise is not None else None,
+                                            _kernel_id(kernel), _ptr(th), int(samples), int(seed),
+                                            _lib.GPAR_MEM_HOST, _ptr(out)))
+    return out
 
 
 def get_optim_scaled_gpar_params(input_locations, pseudo_input_locations, time_loc, outputs,
@@ -466,7 +518,7 @@ def predict_scaled(input_locations, pseudo_input_locations, time_loc, outputs, t
     p, keep = make_problem(input_locations, pseudo_input_locations, time_loc, outputs,
                            out_kernel, time_kernel, qu_kuu_noise=qu_kuu_noise)
     th = np.ascontiguousarray(np.asarray(theta, dtype=np.float64).reshape(5))
-    md = _lib.GPAR_PREDICT_MC if mode == "mc" else _lib.GPAR_PREDICT_ANALYTIC
+    md = _mode_id(mode)
     if p.mem == _lib.GPAR_MEM_DEVICE:
         import torch
         vsp, ldvs, ns, ds = _dev_points(inference_input_locations, keep)

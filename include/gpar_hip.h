@@ -56,7 +56,9 @@ typedef enum gpar_mem { GPAR_MEM_HOST = 0, GPAR_MEM_DEVICE = 1 } gpar_mem;
 
 typedef enum gpar_predict_mode {
   GPAR_PREDICT_ANALYTIC = 0, /* exact S -> infinity limit of the reference's MC estimator */
-  GPAR_PREDICT_MC = 1        /* reference-faithful Monte Carlo (gpar_scaled_inference.jl:110-130) */
+  GPAR_PREDICT_MC = 1,       /* reference-faithful Monte Carlo (gpar_scaled_inference.jl:110-130) */
+  GPAR_PREDICT_PATH = 2      /* Monte Carlo over posterior paths (src/gp/tmp.jl:119-167): per sample
+                                a q(u) draw and a posterior_rand path of the time GP (FFBS) */
 } gpar_predict_mode;
 
 typedef struct gpar_ctx gpar_ctx;
@@ -213,7 +215,9 @@ int32_t gpar_q_u(gpar_ctx* ctx, const gpar_problem* prob, const double* theta,
  * mean/std [n_star] in prob->mem.  ANALYTIC: mean and std of the latent f (the MC
  * estimator's S -> infinity limit); MC: `samples` (2..65536; the reference takes 100) draws with
  * the given seed (gpar_mc_normals), mean and Bessel-corrected std over samples as the reference
- * does. */
+ * does; PATH: tmp.jl's variant, each sample's smoothed mean replaced by a posterior path draw
+ * (q(u) draws gpar_mc_normals, path draws gpar_path_normals), so the std also carries the time
+ * GP's posterior variance. */
 int32_t gpar_predict(gpar_ctx* ctx, const gpar_problem* prob, const double* theta,
                      int64_t n_star, const double* t_star, const double* v_star, int64_t ldvs,
                      int32_t mode, int32_t samples, uint64_t seed, double* mean, double* std);
@@ -224,6 +228,14 @@ int32_t gpar_predict(gpar_ctx* ctx, const gpar_problem* prob, const double* thet
  * (gpar_scaled_inference.jl:103,185), so a host-side restatement fed these draws reproduces the
  * device's MC estimate.  gpar_fit_predict draws output i with seed + i. */
 int32_t gpar_mc_normals(gpar_ctx* ctx, int32_t samples, int64_t m, uint64_t seed, double* xi_out);
+
+/* The posterior-path draws of GPAR_PREDICT_PATH / gpar_lgssm_posterior_rand for (samples, n, d,
+ * seed), host samples x n x d: with d = D + 1 (D = 1, 2, 3, the state dimension of Matern-1/2, 3/2,
+ * 5/2), xi_out[(s*n + k)*d + i] for i < D is the state noise of step k of sample s's prior path and
+ * i = D its observation noise (the simulation smoother, gpar_lgssm_posterior_rand).  Independent of
+ * the q(u) draws of the same seed (gpar_mc_normals). */
+int32_t gpar_path_normals(gpar_ctx* ctx, int32_t samples, int64_t n, int32_t d, uint64_t seed,
+                          double* xi_out);
 
 /* ---------------------------------------------------------------- fit + predict
  * Replaces get_gpar_scaled_predictions (src/gp/gpar_scaled_inference.jl:20-136) -- the fit of
@@ -275,6 +287,18 @@ int32_t gpar_lgssm_logpdf(gpar_ctx* ctx, int32_t nchains, int64_t n, const doubl
 int32_t gpar_lgssm_smooth(gpar_ctx* ctx, int32_t nchains, int64_t n, const double* t,
                           const double* y, int64_t ldy, const double* noise, int32_t kernel,
                           const double* theta, int32_t mem, double* mean, double* var);
+
+/* posterior_rand(rng, create_lgssm(t, l, pv, sigma, k; noise_vector), y, samples) (TemporalGPs,
+ * called at src/gp/tmp.jl:161-167): `samples` joint draws of the latent f over the grid t from
+ * its posterior given y, by the simulation smoother of Durbin & Koopman (2002): a prior path x~
+ * with its observations y~, then f = x~[0] + E[f | y - y~] (oracle/gpar_oracle.py
+ * lgssm_posterior_rand restates it; exact posterior draws, like forward-filter backward-sample,
+ * whose backward coefficients are numerically unstable on clustered grids), draws
+ * gpar_path_normals(samples, n, D + 1, seed).  theta: 3 natural (l, process_var, noise_sigma); noise:
+ * per-step observation variance or NULL (sigma^2).  f_out[s*n + k] (samples x n), in mem. */
+int32_t gpar_lgssm_posterior_rand(gpar_ctx* ctx, int64_t n, const double* t, const double* y,
+                                  const double* noise, int32_t kernel, const double* theta,
+                                  int32_t samples, uint64_t seed, int32_t mem, double* f_out);
 
 /* get_sde_predictions (temporal_gp_inference.jl:45-114): NM fit of (l, pv, sigma) per chain
  * on -logpdf, then smoothing over the merged train+test grid; marginals of f at t_star.

@@ -187,6 +187,58 @@ def sde_transition(kind, tau):
     return e * (np.eye(3) + tau * Nm + 0.5 * tau * tau * (Nm @ Nm))
 
 
+def _inc_gamma_p(m1, x):
+    """Regularized lower incomplete gamma P(m1, x) for an integer m1 >= 1: the series
+    e^{-x} sum_{k >= m1} x^k / k! for x < 4 (no cancellation for short steps), else
+    1 - e^{-x} sum_{k < m1} x^k / k!.  Same loop as the device's (k_path.hip)."""
+    if x < 4.0:
+        t = math.exp(-x)
+        for k in range(1, m1 + 1):
+            t *= x / k
+        acc, k = 0.0, m1
+        for _ in range(80):
+            acc += t
+            k += 1
+            t *= x / k
+            if t < 1e-18 * acc:
+                break
+        return acc
+    term, tot = 1.0, 1.0
+    for k in range(1, m1):
+        term *= x / k
+        tot += term
+    return 1.0 - math.exp(-x) * tot
+
+
+def sde_q_stable(kind, tau, s):
+    """Process-noise covariance Q(tau) = s Pinf - A s Pinf A^T of a step of scaled length tau in
+    closed form: the white noise drives the last state, so Q = q s int_0^tau a(u) a(u)^T du with
+    a(u) = exp(F u) e_d = e^{-lam u} (polynomial in u) and q the spectral density that makes
+    Q(inf) = s Pinf; the integrals are incomplete gamma functions.  Equal to the subtraction form
+    to rounding, but accurate (and positive definite) for short steps, where the subtraction loses
+    all digits of the small eigenvalues: the simulation smoother factors it (lgssm_posterior_rand)."""
+    lam = sde_lambda(kind)
+    if kind == "matern12":
+        al, q = [[1.0]], 2.0
+    elif kind == "matern32":
+        al, q = [[0.0, 1.0], [1.0, -lam]], 4.0 * lam ** 3
+    else:
+        al = [[0.0, 0.0, 0.5], [0.0, 1.0, -0.5 * lam], [1.0, -2.0 * lam, 0.5 * lam * lam]]
+        q = 16.0 * lam ** 5 / 3.0
+    d = len(al)
+    x = 2.0 * lam * tau
+    I = [math.factorial(m) / (2.0 * lam) ** (m + 1) * _inc_gamma_p(m + 1, x) for m in range(2 * d - 1)]
+    Q = np.zeros((d, d))
+    for i in range(d):
+        for j in range(d):
+            acc = 0.0
+            for pp in range(d):
+                for r in range(d):
+                    acc += al[i][pp] * al[j][r] * I[pp + r]
+            Q[i, j] = q * s * acc
+    return Q
+
+
 @dataclass
 class LGSSM:
     """Discretised time GP: per step k, x_k = A_k x_{k-1} + q_k, y_k = x_k[0] + eps_k.
@@ -198,6 +250,9 @@ class LGSSM:
     Q: np.ndarray   # N x d x d
     R: np.ndarray   # N
     P0: np.ndarray  # d x d  (prior at the prepended start point)
+    kind: str = ""
+    tau: np.ndarray = None   # N scaled step lengths (tau_0 = 1: the stationary start)
+    s: float = 1.0           # time-kernel variance
 
 
 def build_lgssm(t, kind, l, s, R):
@@ -222,7 +277,7 @@ def build_lgssm(t, kind, l, s, R):
         A[k] = a
         Q[k] = pinf - a @ pinf @ a.T
     R = np.broadcast_to(np.asarray(R, dtype=np.float64), (n,)).copy()
-    return LGSSM(A=A, Q=Q, R=R, P0=pinf)
+    return LGSSM(A=A, Q=Q, R=R, P0=pinf, kind=kind, tau=dt, s=s)
 
 
 def riccati(lg):
@@ -301,6 +356,104 @@ def rts_smooth(lg, X):
     if vec:
         ms = ms[:, :, 0]
     return ms, Ps
+
+
+def _chol_guarded(C):
+    """Lower Cholesky factor of a small symmetric PSD matrix, negative pivots clamped to zero
+    (the backward-sampling covariance C_k loses definiteness to rounding where it is nearly
+    singular); written out so the device kernel (k_path.hip) follows the same operation order."""
+    d = C.shape[0]
+    L = np.zeros((d, d))
+    for j in range(d):
+        t = C[j, j] - sum(L[j, q] * L[j, q] for q in range(j))
+        L[j, j] = math.sqrt(t) if t > 0.0 else 0.0
+        for i in range(j + 1, d):
+            v = C[i, j] - sum(L[i, q] * L[j, q] for q in range(j))
+            L[i, j] = v / L[j, j] if L[j, j] > 0.0 else 0.0
+    return L
+
+
+def ffbs_constants(lg):
+    """Data-independent coefficients of backward sampling from the LGSSM posterior (the
+    forward-filter backward-sample algorithm behind TemporalGPs ``posterior_rand``, called at
+    src/gp/tmp.jl:161-167; TemporalGPs itself is absent and unpinned, SURVEY §8c, so the algorithm
+    is restated from Carter & Kohn 1994 / Fruhwirth-Schnatter 1994):
+        x_{n-1} ~ N(m_{n-1}, P_{n-1}),
+        x_k | x_{k+1} ~ N(m_k + J_k (x_{k+1} - A_{k+1} m_k), C_k),
+        J_k = P_k A_{k+1}^T (A_{k+1} P_k A_{k+1}^T + Q_{k+1})^{-1},  C_k = P_k - J_k A_{k+1} P_k,
+    with (m_k, P_k) the filtered moments.  Returns J, B = I - J_k A_{k+1} and L = chol(C_k)
+    (n x d x d each; step n-1: J = 0, B = I, L = chol(P_{n-1})), so that a draw is
+    x_k = J_k x_{k+1} + B_k m_k + L_k xi_k."""
+    _, Pf, _, _ = riccati(lg)
+    n, d = lg.A.shape[0], lg.A.shape[1]
+    J = np.zeros((n, d, d))
+    B = np.zeros((n, d, d))
+    L = np.zeros((n, d, d))
+    for k in range(n):
+        P = Pf[k]
+        if k == n - 1:
+            B[k] = np.eye(d)
+            C = P
+        else:
+            A = lg.A[k + 1]
+            Pm = A @ P @ A.T + lg.Q[k + 1]
+            PAt = P @ A.T
+            J[k] = PAt @ np.linalg.inv(Pm)
+            C = P - J[k] @ PAt.T
+            B[k] = np.eye(d) - J[k] @ A
+        L[k] = _chol_guarded(0.5 * (C + C.T))
+    return J, B, L
+
+
+def lgssm_posterior_rand_ffbs(lg, Y, xi):
+    """Forward-filter backward-sample draws (ffbs_constants) of the latent f given Y (n, or n x S
+    one column per sample); xi: S x n x d.  Returns S x n.  The textbook algorithm, kept as a
+    cross-check of lgssm_posterior_rand's distribution: its backward coefficients amplify rounding
+    on clustered grids (see lgssm_posterior_rand)."""
+    xi = np.asarray(xi, dtype=np.float64)
+    S, n, d = xi.shape
+    Y = np.asarray(Y, dtype=np.float64)
+    Y2 = np.repeat(Y[:, None], S, axis=1) if Y.ndim == 1 else Y
+    _, _, _, mf = kalman_filter(lg, Y2)            # n x d x S
+    J, B, L = ffbs_constants(lg)
+    x = np.zeros((d, S))
+    f = np.empty((S, n))
+    for k in range(n - 1, -1, -1):
+        x = J[k] @ x + B[k] @ mf[k] + L[k] @ xi[:, k, :].T
+        f[:, k] = x[0]
+    return f
+
+
+def lgssm_posterior_rand(lg, Y, xi):
+    """TemporalGPs ``posterior_rand(rng, lgssm, y)`` (src/gp/tmp.jl:161-167) with the draws given:
+    joint samples of the latent f = x[0] from p(f | y).  TemporalGPs is absent and unpinned (SURVEY
+    §8c); the draws here come from the simulation smoother of Durbin & Koopman (2002), exact
+    posterior draws like forward-filter backward-sample (lgssm_posterior_rand_ffbs) but stable:
+      prior path   x~_0 = chol(s Pinf) eta_0,  x~_k = A_k x~_{k-1} + chol(Q_k) eta_k,
+                   y~_k = x~_k[0] + sqrt(R_k) eps_k   (Q_k in closed form: sde_q_stable),
+      draw         f = x~[0] + E[f | y - y~]    (rts_smooth's mean of the latent f).
+    (FFBS's J_k = P_k A^T (P^-_{k+1})^{-1} moves Matern-5/2 draws by 1.6e-2 under 1e-13 relative
+    perturbations of A / Q on a 700-point grid with steps down to 8e-5; this form by 4e-13.)
+    Y: n (one data vector for every sample) or n x S; xi: S x n x (d + 1), xi[s, k, :d] = eta,
+    xi[s, k, d] = eps (gpar_path_normals' layout).  Returns S x n samples."""
+    xi = np.asarray(xi, dtype=np.float64)
+    S, n, d1 = xi.shape
+    d = d1 - 1
+    Y = np.asarray(Y, dtype=np.float64)
+    Y2 = np.repeat(Y[:, None], S, axis=1) if Y.ndim == 1 else Y
+    x = np.zeros((d, S))
+    ft = np.empty((n, S))
+    yt = np.empty((n, S))
+    for k in range(n):
+        if k == 0:
+            x = _chol_guarded(lg.P0) @ xi[:, 0, :d].T
+        else:
+            Q = sde_q_stable(lg.kind, lg.tau[k], lg.s)
+            x = lg.A[k] @ x + _chol_guarded(Q) @ xi[:, k, :d].T
+        ft[k] = x[0]
+        yt[k] = x[0] + math.sqrt(lg.R[k]) * xi[:, k, d]
+    ms, _ = rts_smooth(lg, Y2 - yt)
+    return (ft + ms[:, 0, :]).T
 
 
 def dense_time_cov(t, kind, l, s):
@@ -620,6 +773,38 @@ def get_gpar_scaled_predictions_fixed(V, Z, t, y, t_star, V_star, theta, out_ker
         W = Y - msY[:, 0, :]
         std_s = np.sqrt(np.sum(W * W, axis=1))
     inv = np.argsort(perm, kind="stable")
+    return mean_s[inv][n:], std_s[inv][n:]
+
+
+def get_gpar_scaled_predictions_path_fixed(V, Z, t, y, t_star, V_star, theta, xi_u, xi_path,
+                                           out_kernel="matern52", time_kernel="matern52",
+                                           qu_kuu_noise=False):
+    """The Monte Carlo estimator of src/gp/tmp.jl:119-167 (the reference's scratch variant of
+    get_gpar_scaled_predictions) with the draws given: per sample s,
+      e_s = m_e + chol(inv(D)) xi_u[:, s]            (rand(q_u), :122-128 / gpar_scaled_inference.jl:103)
+      fx_s = Cf*u U_u^{-1} e_s                          (generate_fx_sample, :121-129)
+      f_t,s = posterior_rand(lgssm*, y* - fx_s)         (:161-167, FFBS: lgssm_posterior_rand)
+      f*_s = fx_s + f_t,s,
+    then the elementwise mean and Bessel std over the samples at the test points, as
+    gpar_scaled_inference.jl:130-135 reduces its samples.  xi_u: M x S; xi_path: S x (n + n*) x
+    (d + 1) (the merged grid in time order, lgssm_posterior_rand's layout).  Returns (mean, std) at the test points in input order."""
+    l_t, sv_t, l_o, sv_o, sigma = (float(v) for v in theta)
+    s_t, s_o, s2 = sv_t * sv_t, sv_o * sv_o, sigma * sigma
+    V, Z, V_star = to_colvecs(V), to_colvecs(Z), to_colvecs(V_star)
+    n, ns = len(t), len(t_star)
+    m_e, cov, U_u, D = compute_q_u(V, Z, t, y, theta, out_kernel, time_kernel, qu_kuu_noise)
+    tc, perm = merge_grid(t, t_star)
+    Vc = np.hstack([V, V_star])[:, perm]
+    yc = np.concatenate([np.asarray(y, float), np.zeros(ns)])[perm]
+    Rc = np.concatenate([np.full(n, s2), np.full(ns, 1e10)])[perm]
+    Kstar = pairwise(out_kernel, Vc, Z, l_o, s_o)
+    lg = build_lgssm(tc[perm], time_kernel, l_t, s_t, Rc)
+    E = m_e[:, None] + np.linalg.cholesky(cov) @ np.asarray(xi_u, dtype=np.float64)
+    FX = Kstar @ solve_triangular(U_u, E, lower=False)            # (n + n*) x S
+    Ft = lgssm_posterior_rand(lg, yc[:, None] - FX, xi_path)      # S x (n + n*)
+    F = FX + Ft.T
+    inv = np.argsort(perm, kind="stable")
+    mean_s, std_s = F.mean(axis=1), F.std(axis=1, ddof=1)
     return mean_s[inv][n:], std_s[inv][n:]
 
 

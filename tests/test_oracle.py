@@ -11,8 +11,10 @@ and the dense-linear-algebra identities behind every state-space shortcut are *a
 * RTS smoother marginals == dense GP posterior                       (TemporalGPs smooth)
 * analytic prediction == its dense (I - S) K* q(u) + S y closed form (gpar_scaled_inference.jl:20-136)
 * exact logpdf == scipy multivariate normal                          (optimized.jl:34,152)
+* posterior_rand draws (simulation smoother, and FFBS) follow the dense posterior (tmp.jl:161-167)
 plus the golden fixtures in tests/golden/ reproduce bit-for-bit-ish (regression guard).
 """
+import dataclasses
 import os
 
 import numpy as np
@@ -186,3 +188,50 @@ def test_oracle_reproduces_golden_nm():
     nm = O.nelder_mead(nlml, g["x0"], max_evals=int(g["max_evals"]))
     assert nm.evals == int(g["evals"])
     np.testing.assert_allclose(nm.x_min, g["x_min"], rtol=1e-10, atol=1e-12)
+
+
+@pytest.mark.parametrize("sampler", ["simulation_smoother", "ffbs"])
+def test_posterior_rand_samples_follow_the_dense_posterior(sampler):
+    """posterior_rand as restated (src/gp/tmp.jl:161-167): the simulation smoother the device
+    runs, and forward-filter backward-sample, both draw from the dense GP posterior
+    N(K Sigma^-1 y, K - K Sigma^-1 K): sample mean and joint covariance within sampling error
+    (S = 20000)."""
+    rng = np.random.default_rng(0)
+    t = np.sort(rng.uniform(0, 10, 60))
+    y = np.sin(t) + 0.1 * rng.standard_normal(60)
+    lg = O.build_lgssm(t, "matern52", 1.3, 0.8, 0.05)
+    S = 20000
+    if sampler == "ffbs":
+        f = O.lgssm_posterior_rand_ffbs(lg, y, rng.standard_normal((S, 60, 3)))
+    else:
+        f = O.lgssm_posterior_rand(lg, y, rng.standard_normal((S, 60, 4)))
+    K = O.dense_time_cov(t, "matern52", 1.3, 0.8)
+    Sig = K + 0.05 * np.eye(60)
+    mu = K @ np.linalg.solve(Sig, y)
+    post = K - K @ np.linalg.solve(Sig, K)
+    sd = np.sqrt(np.diag(post))
+    assert np.all(np.abs(f.mean(axis=0) - mu) <= 5 * sd / np.sqrt(S))
+    C = np.cov(f.T)
+    scale = np.sqrt(np.outer(np.diag(post), np.diag(post)))
+    assert np.abs(C - post).max() <= 6 * np.sqrt(2.0 / S) * scale.max()
+
+
+def test_simulation_smoother_is_stable_where_ffbs_is_not():
+    """Why the device samples with the simulation smoother: on a clustered grid (random times,
+    steps down to 1e-4) 1e-13 relative perturbations of the model move FFBS's Matern-5/2 draws by
+    far more than rounding, the simulation smoother's by ~1e-12."""
+    rng = np.random.default_rng(703)
+    t = np.sort(rng.uniform(0.0, 40.0, 700))
+    y = np.sin(0.7 * t) + 0.2 * rng.standard_normal(700)
+    noise = np.full(700, 0.04)
+    noise[rng.random(700) < 0.25] = 1e10
+    lg = O.create_lgssm(t, 1.7, 0.9, 0.2, kind="matern52", noise_vector=noise)
+    p = np.random.default_rng(9)
+    lg2 = dataclasses.replace(lg, A=lg.A * (1 + 1e-13 * p.standard_normal(lg.A.shape)),
+                              Q=lg.Q * (1 + 1e-13 * p.standard_normal(lg.Q.shape)),
+                              tau=lg.tau * (1 + 1e-13 * p.standard_normal(lg.tau.shape)))
+    xi = np.random.default_rng(5).standard_normal((4, 700, 4))
+    dk = np.abs(O.lgssm_posterior_rand(lg2, y, xi) - O.lgssm_posterior_rand(lg, y, xi)).max()
+    ff = np.abs(O.lgssm_posterior_rand_ffbs(lg2, y, xi[:, :, :3]) -
+                O.lgssm_posterior_rand_ffbs(lg, y, xi[:, :, :3])).max()
+    assert dk < 1e-10 and ff > 1e3 * dk, (dk, ff)

@@ -22,8 +22,9 @@ def main():
     ap.add_argument("--m", type=int, default=512)
     ap.add_argument("--outputs", type=int, default=3)
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--dmin", type=int, default=1, help="the first output's input dimension")
     a = ap.parse_args()
-    P = a.outputs + 1
+    P = a.dmin + a.outputs
     ds = D.gpar_dataset(a.n, P, seed=0)
     dev = torch.device("cuda", 0)
     t = torch.from_numpy(ds["t"]).to(dev)
@@ -31,7 +32,8 @@ def main():
     ts = torch.from_numpy(ds["t_star"]).to(dev)
     Fs = torch.from_numpy(ds["F_star"]).to(dev)
     problems, keep = [], []
-    for p in range(2, P + 1):
+    outs = list(range(a.dmin + 1, P + 1))
+    for p in outs:
         Z = torch.from_numpy(D.pseudo_inputs(ds["Y"][:, : p - 1], a.m, seed=p)).to(dev)
         pr, k = G.make_problem(Y[:, : p - 1], Z, t, Y[:, p - 1].contiguous(), qu_kuu_noise=True)
         problems.append(pr)
@@ -40,7 +42,7 @@ def main():
     for r in range(a.reps):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        G.fit_predict_batch(problems, x0, ts, [Fs[:, : p - 1] for p in range(2, P + 1)], max_evals=1,
+        G.fit_predict_batch(problems, x0, ts, [Fs[:, : p - 1] for p in outs], max_evals=1,
                             g_tol=-1.0)
         torch.cuda.synchronize()
         print(f"rep {r}: {time.perf_counter() - t0:.3f} s for {len(problems)} outputs", flush=True)
