@@ -516,8 +516,13 @@ def main():
                             "= adjoint_local_wide (bytes 8 ((N+N*)(Mp+1+21) + N* (Mp+1))), pred_rows = "
                             "predict_rows (16 N* Mp), pred_gemm = the variance GEMM |Q V^T| with V "
                             "triangular (N* M (M+1) flops)")
-            pred["ms_per_step_total"] = sum(v["ms_per_step"] for k, v in pred.items()
-                                            if isinstance(v, dict))
+            pred["ms_per_step_kernel_sum"] = sum(v["ms_per_step"] for k, v in pred.items()
+                                                 if isinstance(v, dict))
+            pw_n, pw_ms = ctx.kernel_stats("predictions")
+            if pw_n:   # the spans above overlap across the two prediction lanes; this does not
+                pred["wall_ms_per_step"] = pw_ms / args.steps
+                pred["wall_note"] = ("HIP events around all of one gpar_fit_predict call's "
+                                     "predictions (q(u), both lanes, to their join)")
             out["roofline_predict"] = pred
         out["memory"] = memory
         if self_check:

@@ -17,6 +17,7 @@
 #include <stdexcept>
 #include <string>
 #include <unordered_map>
+#include <optional>
 #include <vector>
 
 #include "launch.hpp"
@@ -630,7 +631,7 @@ struct SplitPipe {
     buf[1] = stage_bufs(c, 1, n, mpmax);
   }
   void start() {   // the split streams follow everything queued on the context stream so far
-    HIPCHECK(hipEventRecord(c->ev_sp, c->main));
+    HIPCHECK(hipEventRecord(c->ev_sp, c->stream));
     for (hipStream_t st : {c->s_w, c->s_g, c->s_g2}) HIPCHECK(hipStreamWaitEvent(st, c->ev_sp, 0));
   }
   void push(const StageJob& j) {
@@ -774,7 +775,7 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     sp.start();
     for (int i = 0; i < np; ++i) sp.push(job(i, sp.buf[i & 1]));
     sp.flush();
-    sp.join(c->main);
+    sp.join(c->stream);   // a prediction lane's q(u) runs this on the side stream
     return o;
   }
   StageBufs bufs[2];
@@ -808,15 +809,19 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     // every side-stream item has been waited for: P(np-1) by G(np-1), the corrections by their Gram
     return o;
   }
+  // one lane: the caller's stream (a prediction lane's q(u) may run on the side stream; its
+  // Gram's co-running correction then goes to main)
+  const hipStream_t base = c->stream;
+  const hipStream_t helper = base == c->side ? c->main : c->side;
   for (int i = 0; i < np; ++i) {
     const int lane = i % nlanes;
     const StageBufs& b = bufs[i % nbuf];
-    OnStream on_(c, lane ? c->side : c->main);
+    OnStream on_(c, lane ? c->side : base);
     const StageJob& j = job(i, b);
     stage_whiten(c, j, b);
     stage_post(c, j, b, fix_beta);
     stage_gram(c, j, b, fix_beta, nlanes > 1, (nlanes > 1 && lane) ? "_1" : "",
-               nlanes == 1 ? c->side : nullptr, 256);
+               nlanes == 1 ? helper : nullptr, 256);
   }
   if (nlanes > 1) {   // join: the dense tail on the context stream needs every G
     HIPCHECK(hipEventRecord(c->ev_join, c->side));
@@ -1812,6 +1817,13 @@ struct OverlapGroup {
   bool in_flight = false;
 };
 
+// Round overlap pays where the drain after each Nelder-Mead round is a large part of the round:
+// one 8-way shard of the north job (8 outputs per call) 2.70 -> 2.45 s per step; with all 63
+// north outputs in one call the round is long and the concurrent gains / dense tails on the
+// whitening CUs slow every Gram instead (5.13 -> 5.46 ms; 18.45 vs 18.75 s per job,
+// profiles/bench_r03d_*.json).
+constexpr int kOverlapMaxOutputs = 16;
+
 using AcceptFn = std::function<void(int, double, const double*, const double*, int64_t)>;
 
 static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
@@ -2020,7 +2032,8 @@ static void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const dou
   };
   int64_t mpmax = 0;
   for (auto& p : P) mpmax = std::max(mpmax, p.mp);
-  if (ctx->overlap && nprob >= 4 && fit_pipelined(ctx, P) && split_active(ctx, P[0].n, mpmax))
+  if (ctx->overlap && nprob >= 4 && nprob <= kOverlapMaxOutputs && fit_pipelined(ctx, P) &&
+      split_active(ctx, P[0].n, mpmax))
     fit_overlapped(ctx, P, nm, accept);
   std::vector<double> vals;
   while (true) {
@@ -2129,6 +2142,9 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
       c->ws_suffix.clear();
     }
   };
+  // wall time of the predictions (both lanes): from here on the context stream to the join
+  std::optional<Timed> tm_pred;
+  tm_pred.emplace(ctx, "predictions");
   if (lanes) {   // the side lane follows the fit (kept Grams, inputs) on the context stream
     HIPCHECK(hipEventRecord(ctx->ev_fork, ctx->main));
     HIPCHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
@@ -2153,9 +2169,9 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
   if (lanes) {
     HIPCHECK(hipEventRecord(ctx->ev_join, ctx->side));
     HIPCHECK(hipStreamWaitEvent(ctx->main, ctx->ev_join, 0));
-    sync(ctx);
   }
-  if (chain && mem == GPAR_MEM_DEVICE) sync(ctx);
+  tm_pred.reset();
+  if (lanes || (chain && mem == GPAR_MEM_DEVICE)) sync(ctx);
 }
 
 int32_t gpar_fit_predict(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,

@@ -130,7 +130,9 @@ int32_t gpar_ctx_set_lanes(gpar_ctx* ctx, int32_t lanes);
  * Gram's split plan (last bits; deterministic for a given w). */
 int32_t gpar_ctx_set_cu_split(gpar_ctx* ctx, int32_t cus_per_xcd);
 /* Round-overlapping batched fit (on by default; the environment variable GPAR_OVERLAP=0 turns it
- * off at context creation): on the CU-split schedule with >= 4 outputs, gpar_fit /
+ * off at context creation): on the CU-split schedule with 4..16 outputs per call (one rank's
+ * shard of the north job; a call with more outputs has long rounds and keeps the round-by-round
+ * schedule, which measured faster there), gpar_fit /
  * gpar_fit_predict deal the outputs into two groups whose Nelder-Mead rounds take turns, so one
  * group's dense tail, host step and next-round gains overlap the other group's whitenings and
  * Grams instead of draining the chip after every round.  Each output evaluates the same points

@@ -109,6 +109,7 @@ def test_overlapped_rounds_equal_round_by_round(ctx):
             res[on] = (a, b, c, cm, cs)
     finally:
         ctx.set_fit_overlap(True)
+        ctx.set_cu_split(-1)
     (a0, b0, c0, cm0, cs0), (a1, b1, c1, cm1, cs1) = res[False], res[True]
     assert len(set(b0.evals)) > 1          # the groups shrink at different rounds
     for x, y in ((a0, a1), (b0, b1), (c0, c1)):
