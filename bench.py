@@ -357,7 +357,7 @@ def main():
     wh_n, wh_ms = ctx.kernel_stats("whiten")
     pred = {}
     for fam, bound in (("pred_whiten", "hbm"), ("pred_adjoint", "hbm"), ("pred_rows", "hbm"),
-                       ("pred_gemm", "mfma")):
+                       ("pred_gemm", "mfma"), ("pred_var", "mfma")):
         pn, pms = ctx.kernel_stats(fam)
         if pn:
             w = ctx.kernel_work(fam) / (pms * 1e-3)
@@ -367,6 +367,7 @@ def main():
                           "peak": FP64_MFMA_PEAK_TFLOPS, "frac": w / 1e12 / FP64_MFMA_PEAK_TFLOPS})
             pred[fam].update(launches=pn, avg_ms=pms / pn, ms_per_step=pms / args.steps,
                              work_per_launch=ctx.kernel_work(fam) / pn)
+    pw_n, pw_ms = ctx.kernel_stats("predictions")   # wall span of each call's predictions
     gram_work = ctx.kernel_work("gram")      # flops, N*M*(M+1) per launch
     wh_work = ctx.kernel_work("whiten")      # algorithmic HBM bytes (include/gpar_hip.h)
     try:   # telemetry only: never fails the line
@@ -515,10 +516,11 @@ def main():
                             "(whiten_kfu_mfma + whiten_vec; bytes 8 (N+N*) (D + M + 20)), pred_adjoint "
                             "= adjoint_local_wide (bytes 8 ((N+N*)(Mp+1+21) + N* (Mp+1))), pred_rows = "
                             "predict_rows (16 N* Mp), pred_gemm = the variance GEMM |Q V^T| with V "
-                            "triangular (N* M (M+1) flops)")
+                            "triangular (N* M (M+1) flops); pred_var = predict_var, the rows, mean "
+                            "and variance fused (M <= 512, the default; replaces pred_rows + "
+                            "pred_gemm; flops as pred_gemm)")
             pred["ms_per_step_kernel_sum"] = sum(v["ms_per_step"] for k, v in pred.items()
                                                  if isinstance(v, dict))
-            pw_n, pw_ms = ctx.kernel_stats("predictions")
             if pw_n:   # the spans above overlap across the two prediction lanes; this does not
                 pred["wall_ms_per_step"] = pw_ms / args.steps
                 pred["wall_note"] = ("HIP events around all of one gpar_fit_predict call's "

@@ -66,6 +66,7 @@ struct gpar_ctx {
   bool overlap = true;            // gpar_ctx_set_fit_overlap (GPAR_OVERLAP=0 at creation): A/B
   // gpar_fit_predict's predictions alternate over two streams (GPAR_PREDICT_LANES=1: one)
   int predict_lanes = 2;
+  bool predict_fused = true;      // GPAR_PREDICT_FUSED=0: predict_rows + gemm_nt (A/B)
   std::string ws_suffix;          // appended to workspace names (a prediction lane's own buffers)
   hipEvent_t ev_grp[2] = {nullptr, nullptr};   // fit_overlapped: a group's values are in
   hipEvent_t ev_gn[2] = {nullptr, nullptr};    // fit_overlapped: a group's gains are done
@@ -1243,6 +1244,16 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
     }
     check_launch("predict: adjoint");
     run_carry(c, P.sdim, g.phi, 0, bend, chat, 0, nch, mc, mc, 1, "predb", /*rev=*/true);
+    // ---- ANALYTIC with m <= 512: rows, mean and |Q_i V^T| in one pass, Q never stored
+    if (mode == GPAR_PREDICT_ANALYTIC && c->predict_fused && predict_var_tiles(m) > 0) {
+      {   // flops of |Q_i V^T|^2 with V lower triangular, as pred_gemm
+        Timed tm_(c, "pred_var", (double)n_star * (double)m * (double)(m + 1));
+        launch_predict_var(c->stream, P.sdim, X, ldx, h, chat, mc, mp, m, kChunk, pos, n_star, rm,
+                           ym, w, Vm, ld, dmean, dstd);
+      }
+      check_launch("predict: rows + variance");
+      goto outputs;
+    }
     // ---- per test row: Q = R Sigma^{-1} Cf*u, mean
     double* Q = ws<double>(c, "pr_Q", (size_t)n_star * mp);
     {   // bytes: u rows at the test points read, Q rows written (mp each)
@@ -1286,6 +1297,7 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
     }
     check_launch("predict: gemm");
   }
+outputs:
   // ---- outputs
   if (mem == GPAR_MEM_DEVICE) {
     HIPCHECK(hipMemcpyAsync(mean_out, dmean, n_star * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
@@ -1466,6 +1478,7 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
   c->stream = c->main;
   if (const char* e = std::getenv("GPAR_PIPELINE")) c->pipeline = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_OVERLAP")) c->overlap = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GPAR_PREDICT_FUSED")) c->predict_fused = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_PREDICT_LANES")) c->predict_lanes = std::atoi(e) > 1 ? 2 : 1;
   // A/B knobs: GPAR_SPLIT_CUS overrides the default CU split, GPAR_SPLIT_DGW=0 keeps the DG
   // kernel off the whitening CUs
@@ -1582,6 +1595,12 @@ int32_t gpar_ctx_set_cu_split(gpar_ctx* ctx, int32_t cus_per_xcd) {
     ctx->err = "gpar_ctx_set_cu_split: cus_per_xcd must be -1 (default), 0 or a multiple of 4 "
                "below 32 (256-CU devices)";
   return rc;
+}
+
+int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on) {
+  if (!ctx) return GPAR_ERR_STATE;
+  ctx->predict_fused = on != 0;
+  return GPAR_OK;
 }
 
 int32_t gpar_ctx_set_fit_overlap(gpar_ctx* ctx, int32_t on) {

@@ -261,6 +261,181 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------- rows + variance, fused
+// predict_var<D, NT>: predict_rows and the ANALYTIC variance var_i = |Q_i V^T|^2 in one pass; Q is
+// never stored (predict_rows wrote N* x Mp doubles that gemm_nt then read once per 128-column
+// tile).  A workgroup takes 64 test rows: 4 waves, one per SIMD, whose 4 x NT accumulator tiles
+// (16 x 16) fill the AGPRs.  K-step s covers Q's columns [16 s, 16 s + 16): thread (wave, lane)
+// computes the 4 columns 4 wave .. 4 wave + 3 of row lane on the fly (Q[i][c] = R_k (X[k][c] +
+// h_k . chat[j][c]), as predict_rows) into LDS, k-major, and adds their dot with w for the mean.
+// Z's columns are cut into T = 4 NT tiles of 16; V is lower triangular, so tile t needs only the
+// k-steps s <= t.  Wave w owns the tile pairs (p, T - 1 - p), p = w, w + 4, ...: every pair needs
+// T + 1 k-steps, so the waves carry equal MFMA counts, and the whole launch executes sum_t (t + 1)
+// / T^2 of the dense MFMAs (51.6 % at M = 512; gemm_nt's 128-column skip: 62.5 %).  V's fragments
+// come straight from global memory (2 MB, L2-resident), one k-step ahead.
+constexpr int kVRows = 64, kVLds = 80;
+template <int V_> struct IntC { static constexpr int value = V_; };
+
+template <int D, int NT>
+__global__ __launch_bounds__(256, 1) void predict_var(
+    const double* __restrict__ X, int64_t ldx, const double* __restrict__ h,
+    const double* __restrict__ chat, int64_t mc, int64_t mp, int m, int L,
+    const int64_t* __restrict__ pos, int64_t nstar, const double* __restrict__ rm,
+    const double* __restrict__ ym, const double* __restrict__ w, const double* __restrict__ V,
+    int64_t ldv, double* __restrict__ mean, double* __restrict__ stdv) {
+  constexpr int T = 4 * NT;
+  __shared__ __attribute__((aligned(16))) double la[2][16 * kVLds];
+  __shared__ double red[4][kVRows];
+  __shared__ double dred[4][kVRows];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int frow = lane >> 4, fcol = lane & 15;
+  const int64_t r0 = (int64_t)blockIdx.x * kVRows;
+  // ---- staging role: row `lane` of the panel, Q columns sk .. sk + 3 of every k-step
+  const int64_t i = r0 + lane;
+  const bool rv = i < nstar;
+  const int64_t k = pos[rv ? i : nstar - 1];
+  const int64_t j = k >> __builtin_ctz(L);   // L is a power of two (kChunk)
+  const double R = rm[k];
+  double hk[D];
+#pragma unroll
+  for (int q = 0; q < D; ++q) hk[q] = h[k * kGStride + q];
+  const double* xr = X + k * ldx;
+  const double* cr = chat + j * mc * kSStride;
+  const int sk = wave * 4;
+  double xa[4], ca[4][D];
+  auto load = [&](int s) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = s * 16 + sk + e;   // < round_up(m, 16) <= mp: inside X's and chat's rows
+      xa[e] = xr[c];
+#pragma unroll
+      for (int q = 0; q < D; ++q) ca[e][q] = cr[c * kSStride + q];
+    }
+  };
+  double dot = 0.0;
+  auto store = [&](int s, int buf) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = s * 16 + sk + e;
+      double u = xa[e];
+#pragma unroll
+      for (int q = 0; q < D; ++q) u = fma(hk[q], ca[e][q], u);
+      const bool ok = rv && c < m;
+      const double qv = ok ? R * u : 0.0;
+      dot = fma(qv, w[c < m ? c : m - 1], dot);   // qv = 0 where masked
+      la[buf][(sk + e) * kVLds + lane] = qv;
+    }
+  };
+  // ---- this wave's tiles, in ascending order of the last k-step each needs: slots i < NT / 2
+  //      hold the low tiles p = w + 4 i, slots i >= NT / 2 the high tiles T - 1 - p.  The k-loop
+  //      runs in NT + 1 phases; phase q has slots q .. NT - 1 active, so no MFMA sits under a
+  //      branch (a branch around MFMAs made the register allocator copy the accumulators between
+  //      AGPRs and VGPRs at every join).  The waves' phase bounds differ, but every wave runs all S
+  //      k-steps, one barrier each.  V's fragments are buffer loads whose offset is pushed out of
+  //      range for a masked element (column >= m, k >= m): the hardware returns 0 without a
+  //      memory access, and no exec-mask branch splits the loop.
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  int lim[NT];
+  uint32_t vcol[NT];   // byte offset of this lane's V row (its Z column), ~0u when >= m
+#pragma unroll
+  for (int i = 0; i < NT; ++i) {
+    const int p = wv + 4 * (i < NT / 2 ? i : NT - 1 - i);
+    const int t = i < NT / 2 ? p : T - 1 - p;
+    lim[i] = 16 * t < m ? t : -1;
+    const int jj = 16 * t + fcol;
+    vcol[i] = jj < m ? (uint32_t)(jj * ldv) * 8u : ~0u;
+  }
+  const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<double*>(V), (short)0, __builtin_amdgcn_readfirstlane((int)(m * ldv * 8)), 0x00020000);
+  // fb[i]: slot i's fragments of the current k-step; reloaded with the next step's right after the
+  // slot's MFMAs, so the loads have the rest of the step to land
+  double fb[NT][4];
+  auto loadB = [&](int s, int i) {
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int kk = s * 16 + ks * 4 + frow;
+      const uint32_t off = (kk < m && vcol[i] != ~0u) ? vcol[i] + 8u * (uint32_t)kk : ~0u;
+      fb[i][ks] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(vr, off, 0, 0));
+    }
+  };
+  d4 acc[4][NT];
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int i = 0; i < NT; ++i) acc[a][i] = d4{0.0, 0.0, 0.0, 0.0};
+  const int S = (m + 15) / 16;
+  load(0);
+  store(0, 0);
+#pragma unroll
+  for (int i = 0; i < NT; ++i) loadB(0, i);
+  __syncthreads();
+  int s = 0;
+  // one k-step with slots Q .. NT - 1 active
+  auto step = [&](auto qc) {
+    constexpr int Q = decltype(qc)::value;
+    const int buf = s & 1;
+    const bool more = s + 1 < S;
+    if (more) load(s + 1);
+    const double* A = la[buf];
+    double fa[4][4];
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int a = 0; a < 4; ++a) fa[ks][a] = A[(ks * 4 + frow) * kVLds + a * 16 + fcol];
+#pragma unroll
+    for (int i = Q; i < NT; ++i) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int a = 0; a < 4; ++a)
+          acc[a][i] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[ks][a], fb[i][ks], acc[a][i], 0, 0, 0);
+      loadB(s + 1, i);   // out of range (zeros, no access) past k = m
+    }
+    if (more) store(s + 1, buf ^ 1);
+    __syncthreads();
+    ++s;
+  };
+  auto phase = [&](auto qc) {
+    constexpr int Q = decltype(qc)::value;
+    int end = S;   // phase Q ends after slot Q - 1's last step ... phase NT runs to S
+    if constexpr (Q < NT) end = lim[Q] + 1 < S ? lim[Q] + 1 : S;
+    while (s < end) step(qc);
+  };
+  static_assert(NT <= 8, "phases below cover NT <= 8");
+  phase(IntC<0>{});
+  if constexpr (NT > 1) phase(IntC<1>{});
+  if constexpr (NT > 2) phase(IntC<2>{});
+  if constexpr (NT > 3) phase(IntC<3>{});
+  if constexpr (NT > 4) phase(IntC<4>{});
+  if constexpr (NT > 5) phase(IntC<5>{});
+  if constexpr (NT > 6) phase(IntC<6>{});
+  if constexpr (NT > 7) phase(IntC<7>{});
+  phase(IntC<NT>{});
+  // ---- epilogue: row sums of squares over this wave's tiles, then over the 16 lanes of a row and
+  //      the 4 waves; the mean's dot over the 4 waves
+#pragma unroll
+  for (int a = 0; a < 4; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      double s2 = 0.0;
+#pragma unroll
+      for (int tt = 0; tt < NT; ++tt) s2 = fma(acc[a][tt][r], acc[a][tt][r], s2);
+#pragma unroll
+      for (int off = 1; off < 16; off <<= 1) s2 += __shfl_xor(s2, off, 64);
+      if (fcol == 0) red[wave][a * 16 + frow + 4 * r] = s2;
+    }
+  dred[wave][lane] = dot;
+  __syncthreads();
+  if (wave == 0 && rv) {
+    const double var = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+    stdv[i] = sqrt(var);
+    double u = xr[mp];
+#pragma unroll
+    for (int q = 0; q < D; ++q) u = fma(hk[q], cr[mp * kSStride + q], u);
+    mean[i] = ym[k] - R * u + ((dred[0][lane] + dred[1][lane]) + (dred[2][lane] + dred[3][lane]));
+  }
+}
+
 // var_i = sum over column blocks of rowsq; std = sqrt(var)
 __global__ void rowsq_finish(const double* __restrict__ rowsq, int64_t rows, int nblk,
                              double* __restrict__ std_out) {
@@ -372,6 +547,37 @@ void launch_predict_rows(hipStream_t st, int sdim, const double* X, int64_t ldx,
     case 2: predict_rows<2><<<nb, 256, 0, st>>>(X, ldx, h, chat, mc, mp, m, L, pos, nstar, rm, ym, w, Q, ldq, mean); break;
     default: predict_rows<3><<<nb, 256, 0, st>>>(X, ldx, h, chat, mc, mp, m, L, pos, nstar, rm, ym, w, Q, ldq, mean); break;
   }
+}
+
+int predict_var_tiles(int64_t m) {   // NT of predict_var for m inducing points; 0: unsupported
+  if (m < 1 || m > 512) return 0;
+  const int64_t t16 = (m + 15) / 16;
+  return (int)(((t16 + 7) / 8) * 8 / 4);
+}
+
+void launch_predict_var(hipStream_t st, int sdim, const double* X, int64_t ldx, const double* h,
+                        const double* chat, int64_t mc, int64_t mp, int64_t m, int L,
+                        const int64_t* pos, int64_t nstar, const double* rm, const double* ym,
+                        const double* w, const double* V, int64_t ldv, double* mean, double* stdv) {
+  if (nstar <= 0) return;
+  const unsigned nb = (unsigned)((nstar + kVRows - 1) / kVRows);
+#define GPAR_PV(DD, NN)                                                                          \
+  predict_var<DD, NN><<<nb, 256, 0, st>>>(X, ldx, h, chat, mc, mp, (int)m, L, pos, nstar, rm, ym, \
+                                          w, V, ldv, mean, stdv)
+#define GPAR_PV_NT(DD)                  \
+  switch (predict_var_tiles(m)) {       \
+    case 2: GPAR_PV(DD, 2); break;      \
+    case 4: GPAR_PV(DD, 4); break;      \
+    case 6: GPAR_PV(DD, 6); break;      \
+    default: GPAR_PV(DD, 8); break;     \
+  }
+  switch (sdim) {
+    case 1: GPAR_PV_NT(1); break;
+    case 2: GPAR_PV_NT(2); break;
+    default: GPAR_PV_NT(3); break;
+  }
+#undef GPAR_PV_NT
+#undef GPAR_PV
 }
 
 void launch_gemm_nt(hipStream_t st, const double* A, int64_t lda, const double* B, int64_t ldb,

@@ -200,6 +200,12 @@ void launch_predict_rows(hipStream_t st, int sdim, const double* X, int64_t ldx,
                          const double* chat, int64_t mc, int64_t mp, int64_t m, int L,
                          const int64_t* pos, int64_t nstar, const double* rm, const double* ym,
                          const double* w, double* Q, int64_t ldq, double* mean);
+// fused predict_rows + ANALYTIC variance (m <= 512; predict_var_tiles(m) == 0 otherwise)
+int predict_var_tiles(int64_t m);
+void launch_predict_var(hipStream_t st, int sdim, const double* X, int64_t ldx, const double* h,
+                        const double* chat, int64_t mc, int64_t mp, int64_t m, int L,
+                        const int64_t* pos, int64_t nstar, const double* rm, const double* ym,
+                        const double* w, const double* V, int64_t ldv, double* mean, double* stdv);
 void launch_gemm_nt(hipStream_t st, const double* A, int64_t lda, const double* B, int64_t ldb,
                     int64_t rows, int64_t cols, int64_t K, int mode, double* C, int64_t ldc,
                     double* rowsq, int64_t valid_cols, const double* base, double* out0,

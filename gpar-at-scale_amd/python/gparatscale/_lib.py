@@ -28,7 +28,7 @@ EXPORTED = (
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
     "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_kernel_work", "gpar_ctx_reset_stats",
     "gpar_ctx_set_lanes", "gpar_ctx_set_cu_split", "gpar_ctx_set_fit_overlap", "gpar_ctx_get_cu_split", "gpar_ctx_set_dist_cache", "gpar_ctx_set_dist_cache_keep", "gpar_ctx_dist_cache_stats",
-    "gpar_pairwise_distances", "gpar_ctx_set_input_stream", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
+    "gpar_pairwise_distances", "gpar_ctx_set_predict_fused", "gpar_ctx_set_input_stream", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
 )
 
 
@@ -89,6 +89,7 @@ def load(path: str | None = None):
             "gpar_abi_version": (i32, []),
             "gpar_ctx_create": (i32, [i32, C.POINTER(vp)]),
             "gpar_ctx_destroy": (i32, [vp]),
+            "gpar_ctx_set_predict_fused": (i32, [vp, i32]),
             "gpar_last_error": (C.c_char_p, [vp]),
             "gpar_ctx_workspace_bytes": (i64, [vp]),
             "gpar_ctx_trim": (i32, [vp]),
@@ -257,6 +258,11 @@ class Context:
     def set_fit_overlap(self, on=True):
         """Round-overlapping batched fit on the CU split (gpar_ctx_set_fit_overlap; default on)."""
         self.check(load().gpar_ctx_set_fit_overlap(self.h, 1 if on else 0))
+
+    def set_predict_fused(self, on=True):
+        """Fused rows + variance kernel of the ANALYTIC prediction (gpar_ctx_set_predict_fused;
+        default on, m <= 512)."""
+        self.check(load().gpar_ctx_set_predict_fused(self.h, 1 if on else 0))
 
     def cu_split(self):
         """The CU split in effect (gpar_ctx_get_cu_split)."""

@@ -138,6 +138,11 @@ int32_t gpar_ctx_set_cu_split(gpar_ctx* ctx, int32_t cus_per_xcd);
  * Grams instead of draining the chip after every round.  Each output evaluates the same points
  * with the same arithmetic: results are bit-identical either way. */
 int32_t gpar_ctx_set_fit_overlap(gpar_ctx* ctx, int32_t on);
+/* ANALYTIC prediction with m <= 512 (on by default; GPAR_PREDICT_FUSED=0 turns it off at context
+ * creation): the test rows' Q_i = R Sigma^{-1} Cf*u rows, the mean and the variance |Q_i V^T|^2
+ * in one fused kernel (predict_var), Q never stored; off: predict_rows writes Q and gemm_nt reads
+ * it.  Same quantities, summed in a different order (last bits). */
+int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
 /* The CU split in effect (0 when off or unsupported). */
 int32_t gpar_ctx_get_cu_split(const gpar_ctx* ctx, int32_t* cus_per_xcd);
 /* Distance cache of gpar_fit / gpar_fit_predict: the input distances |v_k - z_c| (squared for EQ)

@@ -4,8 +4,6 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-bash tools/pmc_predict.sh > gpurun_out/r03e_pmc.log 2>&1 || { tail -20 gpurun_out/r03e_pmc.log; exit 1; }
-tail -3 gpurun_out/r03e_pmc.log
 for v in 1 2; do
   GPAR_PREDICT_LANES=$v timeout -k 10 200 python -u tools/predict_probe.py --outputs 8 --dmin 30 --reps 3 \
     > gpurun_out/r03e_probe_l$v.log 2>&1 || { tail -20 gpurun_out/r03e_probe_l$v.log; exit 1; }
@@ -27,3 +25,5 @@ for f in ("north_l2", "north_l1", "shard"):
     print(f, round(d["ms_per_step"], 1), d["value"], d["roofline"]["avg_ms"], rp.get("wall_ms_per_step"),
           {k: round(v["ms_per_step"], 1) for k, v in rp.items() if isinstance(v, dict)})
 PY
+bash tools/pmc_predict.sh > gpurun_out/r03e_pmc.log 2>&1 || { tail -20 gpurun_out/r03e_pmc.log; exit 1; }
+tail -3 gpurun_out/r03e_pmc.log

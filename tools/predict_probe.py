@@ -46,6 +46,13 @@ def main():
                             g_tol=-1.0)
         torch.cuda.synchronize()
         print(f"rep {r}: {time.perf_counter() - t0:.3f} s for {len(problems)} outputs", flush=True)
+    # release the library's context and the device tensors while the runtime (and a profiler's
+    # tool library) is still up: under rocprofv3 --pmc the process otherwise faulted in a static
+    # destructor after the profiler had finalised
+    del problems, keep, t, Y, ts, Fs
+    G.context().close()
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
 
 
 if __name__ == "__main__":
