@@ -332,6 +332,27 @@ def main():
                              seed=p, device=local, qu_kuu_noise=qn)
         return S.gather_thetas(res, P, dev)   # fitted hyperparameters, P x 5 (tiny)
 
+    if args.qu_noise_free:
+        # the reference's noise-free Cuu (gpar_scaled_inference.jl:157-159) can be numerically
+        # singular for M = 512 pseudo-inputs drawn from the data: the reference then throws
+        # PosDefException, and so does the library -- report that instead of a throughput
+        step0 = step
+
+        def step():
+            t_fail = time.perf_counter()
+            try:
+                return step0()
+            except G.PosDefException as e:
+                torch.cuda.synchronize()
+                if rank == 0:
+                    print(json.dumps({"metric": "GPAR fit+predict wall-clock (ms) and pts\u00b7outputs/sec, "
+                                                f"N={D.fmt_count(N)} M={M} P={P}",
+                                      "value": None, "unit": "pts\u00b7outputs/s", "n_gpus": world,
+                                      "error": str(e), "qu_convention": "noise-free Cuu (reference)",
+                                      "seconds_until_error": time.perf_counter() - t_fail,
+                                      "config": {"workload": args.config, "qu_kuu_noise": False}}),
+                          flush=True)
+                sys.exit(3)
     for _ in range(args.warmup):
         step()
     cpu_res = None
@@ -367,7 +388,7 @@ def main():
                           "peak": FP64_MFMA_PEAK_TFLOPS, "frac": w / 1e12 / FP64_MFMA_PEAK_TFLOPS})
             pred[fam].update(launches=pn, avg_ms=pms / pn, ms_per_step=pms / args.steps,
                              work_per_launch=ctx.kernel_work(fam) / pn)
-    pw_n, pw_ms = ctx.kernel_stats("predictions")   # wall span of each call's predictions
+    pwall_n, pwall_ms = ctx.kernel_stats("predictions")   # wall span of each call's predictions
     gram_work = ctx.kernel_work("gram")      # flops, N*M*(M+1) per launch
     wh_work = ctx.kernel_work("whiten")      # algorithmic HBM bytes (include/gpar_hip.h)
     try:   # telemetry only: never fails the line
@@ -521,8 +542,8 @@ def main():
                             "pred_gemm; flops as pred_gemm)")
             pred["ms_per_step_kernel_sum"] = sum(v["ms_per_step"] for k, v in pred.items()
                                                  if isinstance(v, dict))
-            if pw_n:   # the spans above overlap across the two prediction lanes; this does not
-                pred["wall_ms_per_step"] = pw_ms / args.steps
+            if pwall_n:   # the spans above overlap across the two prediction lanes; this does not
+                pred["wall_ms_per_step"] = pwall_ms / args.steps
                 pred["wall_note"] = ("HIP events around all of one gpar_fit_predict call's "
                                      "predictions (q(u), both lanes, to their join)")
             out["roofline_predict"] = pred

@@ -1144,6 +1144,8 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
   double* X1 = ws<double>(c, "pr_X1", (size_t)ld * ld);
   double* Vm = ws<double>(c, "pr_V", (size_t)ld * ld);
   launch_eye(c->stream, I, ld, (int)m);
+  // V = 0 outside its m x m block (predict_var reads the whole ld x ld buffer)
+  HIPCHECK(hipMemsetAsync(Vm, 0, (size_t)ld * ld * sizeof(double), c->stream));
   TrsmJobHost tj[2] = {{Lu, ld, I, ld, X1, ld, (int)m, m, 0, 0}, {LD, ld, X1, ld, Vm, ld, (int)m, m, 0, 0}};
   auto* dtj = ws<TrsmJobHost>(c, "pr_trsm", 2);
   h2d(c, dtj, tj, 2);
@@ -1245,7 +1247,7 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
     check_launch("predict: adjoint");
     run_carry(c, P.sdim, g.phi, 0, bend, chat, 0, nch, mc, mc, 1, "predb", /*rev=*/true);
     // ---- ANALYTIC with m <= 512: rows, mean and |Q_i V^T| in one pass, Q never stored
-    if (mode == GPAR_PREDICT_ANALYTIC && c->predict_fused && predict_var_tiles(m) > 0) {
+    if (mode == GPAR_PREDICT_ANALYTIC && c->predict_fused && ld == mp && predict_var_tiles(mp) > 0) {
       {   // flops of |Q_i V^T|^2 with V lower triangular, as pred_gemm
         Timed tm_(c, "pred_var", (double)n_star * (double)m * (double)(m + 1));
         launch_predict_var(c->stream, P.sdim, X, ldx, h, chat, mc, mp, m, kChunk, pos, n_star, rm,

@@ -1284,7 +1284,13 @@ __global__ __launch_bounds__(64) void adjoint_local(double* __restrict__ X, int6
 // Wide form for the prediction's many columns: a 256-column workgroup per chunk stages the
 // chunk's gains records and fix-up rows in LDS once (read back as broadcasts; from memory they
 // were scalar loads waited on step by step), and with `wmask` writes u only at the rows the
-// caller reads (test points: wmask[k] >= 1e10, gpar_scaled_inference.jl:100-107).
+// caller reads (test points: wmask[k] >= 1e10, gpar_scaled_inference.jl:100-107).  A wave whose
+// 64 columns are all past ncols leaves after the staging (the prediction's ncols = Mp + 1 left a
+// third of the workgroups carrying one column through the whole chunk), and each thread keeps
+// kAdjPF rows of X in flight ahead of the recursion (the loads do not depend on it; at 4
+// workgroups per CU the unrolled loop's 4 were too few: 77 % of wave time waiting on memory).
+constexpr int kAdjPF = 12;
+
 template <int D>
 __global__ __launch_bounds__(256) void adjoint_local_wide(double* __restrict__ X, int64_t ldx,
                                                          int64_t ncols, const double* __restrict__ rec,
@@ -1309,35 +1315,44 @@ __global__ __launch_bounds__(256) void adjoint_local_wide(double* __restrict__ X
   for (int e = tid; e < nk * D; e += 256) lg[e] = g[(k0 + e / D) * kGStride + e % D];
   if (tid < nk) lw[tid] = wmask ? (wmask[k0 + tid] >= 1e10) : 1;
   __syncthreads();
+  if ((int64_t)blockIdx.y * 256 + (tid & ~63) >= ncols) return;   // the whole wave is idle
   double cf[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) cf[i] = cin[(j * mc + cc) * kSStride + i];
   double lam[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) lam[i] = 0.0;
-#pragma unroll 4
-  for (int s = nk - 1; s >= 0; --s) {
-    const int64_t k = k0 + s;
-    const double* r = lrec + s * RU;
-    const double* gk = lg + s * D;
-    double w = X[k * ldx + cc];
+  const double* xc = X + k0 * ldx + cc;
+  double xb[kAdjPF];   // xb[p]: row s of the current group s = top - p
 #pragma unroll
-    for (int i = 0; i < D; ++i) w = fma(gk[i], cf[i], w);
-    double u = w * r[D * D + D];
+  for (int p = 0; p < kAdjPF; ++p) xb[p] = nk - 1 - p >= 0 ? xc[(int64_t)(nk - 1 - p) * ldx] : 0.0;
+  for (int top = nk - 1; top >= 0; top -= kAdjPF) {
 #pragma unroll
-    for (int i = 0; i < D; ++i) u = fma(r[D * D + i], lam[i], u);
-    lam[0] -= u;
-    double nl[D];
+    for (int p = 0; p < kAdjPF; ++p) {
+      const int s = top - p;
+      if (s < 0) break;   // uniform: nk is the workgroup's
+      double w = xb[p];
+      if (s - kAdjPF >= 0) xb[p] = xc[(int64_t)(s - kAdjPF) * ldx];
+      const double* r = lrec + s * RU;
+      const double* gk = lg + s * D;
 #pragma unroll
-    for (int q = 0; q < D; ++q) {
-      double acc = 0.0;
+      for (int i = 0; i < D; ++i) w = fma(gk[i], cf[i], w);
+      double u = w * r[D * D + D];
 #pragma unroll
-      for (int i = 0; i < D; ++i) acc = fma(r[i * D + q], lam[i], acc);
-      nl[q] = acc;
+      for (int i = 0; i < D; ++i) u = fma(r[D * D + i], lam[i], u);
+      lam[0] -= u;
+      double nl[D];
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < D; ++i) acc = fma(r[i * D + q], lam[i], acc);
+        nl[q] = acc;
+      }
+#pragma unroll
+      for (int i = 0; i < D; ++i) lam[i] = nl[i];
+      if (act && lw[s]) X[(k0 + s) * ldx + c] = u;
     }
-#pragma unroll
-    for (int i = 0; i < D; ++i) lam[i] = nl[i];
-    if (act && lw[s]) X[k * ldx + c] = u;
   }
   if (act) {
 #pragma unroll

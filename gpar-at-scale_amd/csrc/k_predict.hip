@@ -262,36 +262,45 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
 }
 
 // ---------------------------------------------------------------------------- rows + variance, fused
-// predict_var<D, NT>: predict_rows and the ANALYTIC variance var_i = |Q_i V^T|^2 in one pass; Q is
+// predict_var<D, NG>: predict_rows and the ANALYTIC variance var_i = |Q_i V^T|^2 in one pass; Q is
 // never stored (predict_rows wrote N* x Mp doubles that gemm_nt then read once per 128-column
-// tile).  A workgroup takes 64 test rows: 4 waves, one per SIMD, whose 4 x NT accumulator tiles
-// (16 x 16) fill the AGPRs.  K-step s covers Q's columns [16 s, 16 s + 16): thread (wave, lane)
-// computes the 4 columns 4 wave .. 4 wave + 3 of row lane on the fly (Q[i][c] = R_k (X[k][c] +
-// h_k . chat[j][c]), as predict_rows) into LDS, k-major, and adds their dot with w for the mean.
-// Z's columns are cut into T = 4 NT tiles of 16; V is lower triangular, so tile t needs only the
-// k-steps s <= t.  Wave w owns the tile pairs (p, T - 1 - p), p = w, w + 4, ...: every pair needs
-// T + 1 k-steps, so the waves carry equal MFMA counts, and the whole launch executes sum_t (t + 1)
-// / T^2 of the dense MFMAs (51.6 % at M = 512; gemm_nt's 128-column skip: 62.5 %).  V's fragments
-// come straight from global memory (2 MB, L2-resident), one k-step ahead.
-constexpr int kVRows = 64, kVLds = 80;
+// tile, 10.3 GB per launch at N* = 1e6 by the counters).  A workgroup takes 64 test rows, wave w
+// the 16 rows 16 w .. 16 w + 15 against all T = 4 NG column tiles of Z (16 wide; NG = Mp / 64;
+// the accumulators fill the AGPRs).  Each lane computes its own A fragments on the fly: row fcol
+// of its wave, Q[i][c] = R_k (X[k][c] + h_k . chat[j][c]) at the 4 columns of every k-step it
+// feeds to the MFMA (loaded two k-steps ahead), and its share of the mean's dot with w.
+// V's k-slab of each step (16 k of every column still needed) goes global -> LDS by DMA
+// (global_load_lds_dwordx4, 8 columns x 128 B per wave-instruction), column-major with the
+// 16-byte k-pairs of column c XOR-swizzled by (c >> 1) & 7 on the source side, so the MFMA
+// fragment reads (16 columns x one k) hit 16 distinct bank pairs.  V is lower triangular, so tile
+// t needs only k-steps s <= t; the k-loop runs in NG phases of 4 steps, phase G with the tiles
+// 4 G .. T - 1: every wave has the same work at every step (one barrier per step), no MFMA sits
+// under a branch (a branch around MFMAs made the register allocator copy the accumulators at
+// every join), and the tiles of group G already past their diagonal multiply V's exact zeros in
+// phase G's later steps (56 % of the dense MFMAs at M = 512; gemm_nt's 128-column skip: 62.5 %).
+// V must be zero outside its m x m block (the caller clears the Mp x Mp buffer).
+constexpr int kVRows = 64;
 template <int V_> struct IntC { static constexpr int value = V_; };
+// 16 bytes global -> LDS by DMA (wave-uniform LDS base + lane * 16).  A plain __device__ function:
+// the builtin inside the kernel template's lambdas made the host pass drop the launch stubs.
+__device__ __forceinline__ void dma16(const double* src, double* lds) {
+  __builtin_amdgcn_global_load_lds(src, lds, 16, 0, 0);
+}
 
-template <int D, int NT>
+template <int D, int NG>
 __global__ __launch_bounds__(256, 1) void predict_var(
     const double* __restrict__ X, int64_t ldx, const double* __restrict__ h,
     const double* __restrict__ chat, int64_t mc, int64_t mp, int m, int L,
     const int64_t* __restrict__ pos, int64_t nstar, const double* __restrict__ rm,
     const double* __restrict__ ym, const double* __restrict__ w, const double* __restrict__ V,
     int64_t ldv, double* __restrict__ mean, double* __restrict__ stdv) {
-  constexpr int T = 4 * NT;
-  __shared__ __attribute__((aligned(16))) double la[2][16 * kVLds];
-  __shared__ double red[4][kVRows];
-  __shared__ double dred[4][kVRows];
+  constexpr int T = 4 * NG, NC = 64 * NG, NS = 4 * NG;   // tiles, columns, k-steps
+  __shared__ __attribute__((aligned(16))) double lb[2][NC * 16];
+  __shared__ double lw[NC];   // w, zero past m
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int frow = lane >> 4, fcol = lane & 15;
-  const int64_t r0 = (int64_t)blockIdx.x * kVRows;
-  // ---- staging role: row `lane` of the panel, Q columns sk .. sk + 3 of every k-step
-  const int64_t i = r0 + lane;
+  // ---- this lane's Q row (the MFMA A operand's row fcol)
+  const int64_t i = (int64_t)blockIdx.x * kVRows + wave * 16 + fcol;
   const bool rv = i < nstar;
   const int64_t k = pos[rv ? i : nstar - 1];
   const int64_t j = k >> __builtin_ctz(L);   // L is a power of two (kChunk)
@@ -301,138 +310,126 @@ __global__ __launch_bounds__(256, 1) void predict_var(
   for (int q = 0; q < D; ++q) hk[q] = h[k * kGStride + q];
   const double* xr = X + k * ldx;
   const double* cr = chat + j * mc * kSStride;
-  const int sk = wave * 4;
-  double xa[4], ca[4][D];
-  auto load = [&](int s) {
+  // raw inputs of the A fragments of the next k-step: X's and chat's columns at this lane's row
+  double xa[1][4], ca[1][4][D];
+  auto loadA = [&](int s, int st) __attribute__((always_inline)) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = s * 16 + sk + e;   // < round_up(m, 16) <= mp: inside X's and chat's rows
-      xa[e] = xr[c];
+    for (int ks = 0; ks < 4; ++ks) {
+      const int c = s * 16 + ks * 4 + frow;   // < Mp: inside X's and chat's rows
+      xa[st][ks] = xr[c];
 #pragma unroll
-      for (int q = 0; q < D; ++q) ca[e][q] = cr[c * kSStride + q];
+      for (int q = 0; q < D; ++q) ca[st][ks][q] = cr[c * kSStride + q];
     }
   };
   double dot = 0.0;
-  auto store = [&](int s, int buf) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int c = s * 16 + sk + e;
-      double u = xa[e];
-#pragma unroll
-      for (int q = 0; q < D; ++q) u = fma(hk[q], ca[e][q], u);
-      const bool ok = rv && c < m;
-      const double qv = ok ? R * u : 0.0;
-      dot = fma(qv, w[c < m ? c : m - 1], dot);   // qv = 0 where masked
-      la[buf][(sk + e) * kVLds + lane] = qv;
-    }
-  };
-  // ---- this wave's tiles, in ascending order of the last k-step each needs: slots i < NT / 2
-  //      hold the low tiles p = w + 4 i, slots i >= NT / 2 the high tiles T - 1 - p.  The k-loop
-  //      runs in NT + 1 phases; phase q has slots q .. NT - 1 active, so no MFMA sits under a
-  //      branch (a branch around MFMAs made the register allocator copy the accumulators between
-  //      AGPRs and VGPRs at every join).  The waves' phase bounds differ, but every wave runs all S
-  //      k-steps, one barrier each.  V's fragments are buffer loads whose offset is pushed out of
-  //      range for a masked element (column >= m, k >= m): the hardware returns 0 without a
-  //      memory access, and no exec-mask branch splits the loop.
-  const int wv = __builtin_amdgcn_readfirstlane(wave);
-  int lim[NT];
-  uint32_t vcol[NT];   // byte offset of this lane's V row (its Z column), ~0u when >= m
-#pragma unroll
-  for (int i = 0; i < NT; ++i) {
-    const int p = wv + 4 * (i < NT / 2 ? i : NT - 1 - i);
-    const int t = i < NT / 2 ? p : T - 1 - p;
-    lim[i] = 16 * t < m ? t : -1;
-    const int jj = 16 * t + fcol;
-    vcol[i] = jj < m ? (uint32_t)(jj * ldv) * 8u : ~0u;
-  }
-  const __amdgpu_buffer_rsrc_t vr = __builtin_amdgcn_make_buffer_rsrc(
-      const_cast<double*>(V), (short)0, __builtin_amdgcn_readfirstlane((int)(m * ldv * 8)), 0x00020000);
-  // fb[i]: slot i's fragments of the current k-step; reloaded with the next step's right after the
-  // slot's MFMAs, so the loads have the rest of the step to land
-  double fb[NT][4];
-  auto loadB = [&](int s, int i) {
+  double fa[4];
+  auto makeA = [&](int s, int st) __attribute__((always_inline)) {
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
-      const int kk = s * 16 + ks * 4 + frow;
-      const uint32_t off = (kk < m && vcol[i] != ~0u) ? vcol[i] + 8u * (uint32_t)kk : ~0u;
-      fb[i][ks] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(vr, off, 0, 0));
+      const int c = s * 16 + ks * 4 + frow;
+      double u = xa[st][ks];
+#pragma unroll
+      for (int q = 0; q < D; ++q) u = fma(hk[q], ca[st][ks][q], u);
+      const bool ok = rv && c < m;
+      fa[ks] = ok ? R * u : 0.0;
+      dot = fma(fa[ks], lw[c], dot);
     }
   };
-  d4 acc[4][NT];
+  // ---- V's k-slab of step s into lb[buf]: wave-instruction q moves columns 8 q .. 8 q + 7 (lane
+  //      -> column 8 q + lane / 8, physical pair lane % 8 = logical pair ^ ((column >> 1) & 7));
+  //      columns of groups already finished (< 64 (s / 4)) are not moved again
+  //      (instruction q = wave + 4 r: column 8 q + lane / 8, whose (c >> 1) & 7 depends on the
+  //      lane and the wave's parity only, so the source is one lane base + r * 32 rows of V)
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int dc = lane >> 3, dp = lane & 7;
+  const int kp = dp ^ ((4 * (wv & 1) + (dc >> 1)) & 7);
+  const double* vsrc = V + (int64_t)(8 * wv + dc) * ldv + 2 * kp;
+  auto dmaB = [&](int s, int buf) __attribute__((always_inline)) {
+    const int q0 = 8 * (s >> 2);   // first instruction still needed (8 per 64-column group)
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+    for (int r = 0; r < NC / 32; ++r) {
+      const int q = wv + 4 * r;
+      if (q < q0) continue;   // wave-uniform
+      dma16(vsrc + (int64_t)r * 32 * ldv + s * 16, &lb[0][0] + buf * (NC * 16) + q * 128);
+    }
+  };
+  d4 acc[T];
 #pragma unroll
-    for (int i = 0; i < NT; ++i) acc[a][i] = d4{0.0, 0.0, 0.0, 0.0};
-  const int S = (m + 15) / 16;
-  load(0);
-  store(0, 0);
-#pragma unroll
-  for (int i = 0; i < NT; ++i) loadB(0, i);
+  for (int t = 0; t < T; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+  for (int c = tid; c < NC; c += 256) lw[c] = c < m ? w[c] : 0.0;
+  loadA(0, 0);
+  dmaB(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  int s = 0;
-  // one k-step with slots Q .. NT - 1 active
-  auto step = [&](auto qc) {
-    constexpr int Q = decltype(qc)::value;
-    const int buf = s & 1;
-    const bool more = s + 1 < S;
-    if (more) load(s + 1);
-    const double* A = la[buf];
-    double fa[4][4];
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-      for (int a = 0; a < 4; ++a) fa[ks][a] = A[(ks * 4 + frow) * kVLds + a * 16 + fcol];
-#pragma unroll
-    for (int i = Q; i < NT; ++i) {
-#pragma unroll
-      for (int ks = 0; ks < 4; ++ks)
-#pragma unroll
-        for (int a = 0; a < 4; ++a)
-          acc[a][i] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[ks][a], fb[i][ks], acc[a][i], 0, 0, 0);
-      loadB(s + 1, i);   // out of range (zeros, no access) past k = m
+  // one k-step s with tiles T0 .. T - 1: fa from the inputs loaded during step s - 1; then the
+  // loads of step s + 1 (A inputs; slab s + 1 -> lb[(s + 1) & 1] by DMA) under this step's
+  // MFMAs; wait for them, barrier
+  auto step = [&](auto t0c, int s) __attribute__((always_inline)) {
+    constexpr int T0 = decltype(t0c)::value;
+    makeA(s, 0);
+    if (s + 1 < NS) {
+      loadA(s + 1, 0);
+      dmaB(s + 1, (s + 1) & 1);
     }
-    if (more) store(s + 1, buf ^ 1);
-    __syncthreads();
-    ++s;
-  };
-  auto phase = [&](auto qc) {
-    constexpr int Q = decltype(qc)::value;
-    int end = S;   // phase Q ends after slot Q - 1's last step ... phase NT runs to S
-    if constexpr (Q < NT) end = lim[Q] + 1 < S ? lim[Q] + 1 : S;
-    while (s < end) step(qc);
-  };
-  static_assert(NT <= 8, "phases below cover NT <= 8");
-  phase(IntC<0>{});
-  if constexpr (NT > 1) phase(IntC<1>{});
-  if constexpr (NT > 2) phase(IntC<2>{});
-  if constexpr (NT > 3) phase(IntC<3>{});
-  if constexpr (NT > 4) phase(IntC<4>{});
-  if constexpr (NT > 5) phase(IntC<5>{});
-  if constexpr (NT > 6) phase(IntC<6>{});
-  if constexpr (NT > 7) phase(IntC<7>{});
-  phase(IntC<NT>{});
-  // ---- epilogue: row sums of squares over this wave's tiles, then over the 16 lanes of a row and
-  //      the 4 waves; the mean's dot over the 4 waves
+    const double* B = &lb[0][0] + (s & 1) * (NC * 16);
 #pragma unroll
-  for (int a = 0; a < 4; ++a)
+    for (int t = T0; t < T; ++t)
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int c = t * 16 + fcol, kk = ks * 4 + frow;
+        const double bf = B[c * 16 + (((kk >> 1) ^ ((c >> 1) & 7)) << 1) + (kk & 1)];
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[ks], bf, acc[t], 0, 0, 0);
+        // keep the scheduler's window to a few tiles: hoisting every fragment read of a
+        // 32-tile step ran out of VGPRs and spilled the accumulators
+        if (ks == 3 && (t & 1)) __builtin_amdgcn_sched_barrier(0);
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  };
+  // phase G: k-steps 4 G .. 4 G + 3 with tiles 4 G .. T - 1.  Phase 0's first step is peeled (a
+  // loop whose accumulators enter as the zero constant copied them every step)
+  auto phase = [&](auto gc) __attribute__((always_inline)) {
+    constexpr int G = decltype(gc)::value;
+    int s = 4 * G;
+    if constexpr (G == 0) step(IntC<0>{}, s++);
+#pragma unroll 1
+    for (; s < 4 * G + 4; ++s) step(IntC<4 * G>{}, s);
+  };
+  static_assert(NG >= 1 && NG <= 8, "NG in 1..8");
+  phase(IntC<0>{});
+  if constexpr (NG > 1) phase(IntC<1>{});
+  if constexpr (NG > 2) phase(IntC<2>{});
+  if constexpr (NG > 3) phase(IntC<3>{});
+  if constexpr (NG > 4) phase(IntC<4>{});
+  if constexpr (NG > 5) phase(IntC<5>{});
+  if constexpr (NG > 6) phase(IntC<6>{});
+  if constexpr (NG > 7) phase(IntC<7>{});
+  // ---- epilogue: row sums of squares (rows frow + 4 r of the wave's 16) over the tiles and the
+  //      16 lanes of a row; the mean's dot over the 4 lanes (frow) sharing a row
+  double s2[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    double v = 0.0;
+#pragma unroll
+    for (int t = 0; t < T; ++t) v = fma(acc[t][r], acc[t][r], v);
+#pragma unroll
+    for (int off = 1; off < 16; off <<= 1) v += __shfl_xor(v, off, 64);
+    s2[r] = v;
+  }
+  dot += __shfl_xor(dot, 16, 64);
+  dot += __shfl_xor(dot, 32, 64);
+  if (fcol == 0) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
-      double s2 = 0.0;
-#pragma unroll
-      for (int tt = 0; tt < NT; ++tt) s2 = fma(acc[a][tt][r], acc[a][tt][r], s2);
-#pragma unroll
-      for (int off = 1; off < 16; off <<= 1) s2 += __shfl_xor(s2, off, 64);
-      if (fcol == 0) red[wave][a * 16 + frow + 4 * r] = s2;
+      const int64_t ir = (int64_t)blockIdx.x * kVRows + wave * 16 + frow + 4 * r;
+      if (ir < nstar) stdv[ir] = sqrt(s2[r]);
     }
-  dred[wave][lane] = dot;
-  __syncthreads();
-  if (wave == 0 && rv) {
-    const double var = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
-    stdv[i] = sqrt(var);
+  }
+  if (frow == 0 && rv) {
     double u = xr[mp];
 #pragma unroll
     for (int q = 0; q < D; ++q) u = fma(hk[q], cr[mp * kSStride + q], u);
-    mean[i] = ym[k] - R * u + ((dred[0][lane] + dred[1][lane]) + (dred[2][lane] + dred[3][lane]));
+    mean[i] = ym[k] - R * u + dot;
   }
 }
 
@@ -549,10 +546,8 @@ void launch_predict_rows(hipStream_t st, int sdim, const double* X, int64_t ldx,
   }
 }
 
-int predict_var_tiles(int64_t m) {   // NT of predict_var for m inducing points; 0: unsupported
-  if (m < 1 || m > 512) return 0;
-  const int64_t t16 = (m + 15) / 16;
-  return (int)(((t16 + 7) / 8) * 8 / 4);
+int predict_var_tiles(int64_t mp) {   // NG (64-column groups) of predict_var; 0: unsupported
+  return (mp >= 64 && mp <= 512 && mp % 64 == 0) ? (int)(mp / 64) : 0;
 }
 
 void launch_predict_var(hipStream_t st, int sdim, const double* X, int64_t ldx, const double* h,
@@ -564,19 +559,19 @@ void launch_predict_var(hipStream_t st, int sdim, const double* X, int64_t ldx, 
 #define GPAR_PV(DD, NN)                                                                          \
   predict_var<DD, NN><<<nb, 256, 0, st>>>(X, ldx, h, chat, mc, mp, (int)m, L, pos, nstar, rm, ym, \
                                           w, V, ldv, mean, stdv)
-#define GPAR_PV_NT(DD)                  \
-  switch (predict_var_tiles(m)) {       \
+#define GPAR_PV_NG(DD)                  \
+  switch (predict_var_tiles(mp)) {     \
     case 2: GPAR_PV(DD, 2); break;      \
     case 4: GPAR_PV(DD, 4); break;      \
     case 6: GPAR_PV(DD, 6); break;      \
     default: GPAR_PV(DD, 8); break;     \
   }
   switch (sdim) {
-    case 1: GPAR_PV_NT(1); break;
-    case 2: GPAR_PV_NT(2); break;
-    default: GPAR_PV_NT(3); break;
+    case 1: GPAR_PV_NG(1); break;
+    case 2: GPAR_PV_NG(2); break;
+    default: GPAR_PV_NG(3); break;
   }
-#undef GPAR_PV_NT
+#undef GPAR_PV_NG
 #undef GPAR_PV
 }
 

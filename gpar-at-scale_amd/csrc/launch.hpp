@@ -200,8 +200,9 @@ void launch_predict_rows(hipStream_t st, int sdim, const double* X, int64_t ldx,
                          const double* chat, int64_t mc, int64_t mp, int64_t m, int L,
                          const int64_t* pos, int64_t nstar, const double* rm, const double* ym,
                          const double* w, double* Q, int64_t ldq, double* mean);
-// fused predict_rows + ANALYTIC variance (m <= 512; predict_var_tiles(m) == 0 otherwise)
-int predict_var_tiles(int64_t m);
+// fused predict_rows + ANALYTIC variance (Mp in {128, 256, 384, 512}: predict_var_tiles(Mp) > 0;
+// V zero outside its m x m block, ld = Mp)
+int predict_var_tiles(int64_t mp);
 void launch_predict_var(hipStream_t st, int sdim, const double* X, int64_t ldx, const double* h,
                         const double* chat, int64_t mc, int64_t mp, int64_t m, int L,
                         const int64_t* pos, int64_t nstar, const double* rm, const double* ym,
