@@ -213,11 +213,11 @@ def main():
     if temporal:   # every owned output is a temporal-only chain (rows of one contiguous block)
         y1 = Y_d[:, [p - 1 for p in mine]].T.contiguous() if mine else None
     host = args.inputs == "host"
+    if args.api == "per-output" and (args.inference != "given" or temporal or args.separate_predict):
+        sys.exit("--api per-output: given inference inputs, the GPAR configs only")
     if host:
         if world > 1 or args.inference != "given" or temporal or args.separate_predict:
             sys.exit("--inputs host: one rank, given inference inputs, the GPAR configs only")
-    if args.api == "per-output" and (args.inference != "given" or temporal or args.separate_predict):
-        sys.exit("--api per-output: given inference inputs, the GPAR configs only")
         # the same problems from host (numpy) buffers: D x N ColVecs, as the Julia shim passes them
         Yh_all = Y_d.cpu().numpy()
         t_hh, ts_hh, Fs_hh = t_d.cpu().numpy(), ts_d.cpu().numpy(), Fs_d.cpu().numpy()
@@ -715,6 +715,37 @@ def _cpu_sample(CR, O, n, ns, M, d, out_kernel, theta, qu_kuu_noise=True):
     return t_eval, time.perf_counter() - t0
 
 
+def _reference_literal_cost(O, N, P, EV, t_eval, sizes=(2000, 4000, 8000)):
+    """The reference as written evaluates logdet(noise_matrix) with a dense N x N LU of the time
+    covariance plus noise (src/gp/dtc.jl:96-99,123), O(N^3) on top of the O(N) filter the port
+    times.  Timed here (scipy lu_factor, this process's BLAS threads) at N <= 8000, fitted as
+    c N^3 on the largest size and extrapolated to the job's N -- where the dense matrix alone would
+    take 8 N^2 bytes (8 TB at N = 1e6), so the reference cannot run the job at all."""
+    try:
+        from scipy.linalg import lu_factor
+        times = {}
+        for n in sizes:
+            t = np.sort(np.random.default_rng(5).uniform(0.0, n / 10.0, n))
+            Sig = O.dense_time_cov(t, "matern52", 2.0, 4.0) + 0.02 * np.eye(n)
+            lu_factor(Sig[:200, :200], check_finite=False)   # warm the BLAS threads
+            t0 = time.perf_counter()
+            lu_factor(Sig, overwrite_a=True, check_finite=False)
+            times[n] = time.perf_counter() - t0
+            del Sig
+        nmax = max(sizes)
+        c = times[nmax] / float(nmax) ** 3
+        t_lu = c * float(N) ** 3
+        t_job = (P - 1) * EV * (t_eval + t_lu)
+        return {"lu_seconds": {str(k): round(v, 3) for k, v in times.items()},
+                "lu_seconds_at_N_extrapolated": t_lu, "job_seconds_extrapolated": t_job,
+                "value": N * P / t_job, "unit": "pts·outputs/s", "dense_bytes_at_N": 8.0 * N * N,
+                "note": "dense LU of the N x N noise matrix per evaluation (dtc.jl:96-99,123), c N^3 "
+                        f"from N = {nmax}, plus the port's O(N) evaluation; the predictions are left "
+                        "out (they would add more)"}
+    except Exception as exc:   # telemetry only
+        return {"error": repr(exc)}
+
+
 def cpu_baseline(N, NS, M, P, EV, out_kernel, d_sample=32, n_ratio=100_000, qu_kuu_noise=True):
     """Time the C/OpenMP CPU restatement of the reference path (oracle/cpu_ref.{c,py}, SURVEY §8d
     "cpu_ref": kernel assembly, Kalman gains and per-column decorrelate sweeps, RTS smoother in C;
@@ -756,8 +787,9 @@ def cpu_baseline(N, NS, M, P, EV, out_kernel, d_sample=32, n_ratio=100_000, qu_k
                             f"threaded job scaled by these ratios: est {tj1:.0f}s per job"}
     except Exception as exc:   # threadpoolctl missing: report the threaded figure only
         single = {"value": None, "error": repr(exc)}
+    literal = _reference_literal_cost(O, N, P, EV, t_eval)
     return {"value": N * P / t_job, "unit": "pts·outputs/s", "cores": int(cores), "kind": "port",
-            "host_cpu": _cpu_model(), "single_thread": single,
+            "host_cpu": _cpu_model(), "single_thread": single, "reference_literal": literal,
             "ran": "in a child process beside the GPU warm-up (joined before the timed region)",
             "sample": f"C/OpenMP + OpenBLAS restatement (oracle/cpu_ref), {int(cores)} threads, at the job's "
                       f"own sizes: 1 DTC objective eval (N={N}, M={M}, D={d_sample}) = {t_eval:.2f}s + "

@@ -1,6 +1,6 @@
 #!/bin/bash
-# r03g: fused rows + variance (predict_var) -- parity subset, probe A/B fused vs unfused under
-# rocprofv3 --stats, north bench with the predictions' wall-time span.
+# r03g: predict_var v3 (row-split waves, LDS-DMA V slabs) + adjoint prefetch -- parity subset,
+# probe A/B fused vs unfused under rocprofv3 --stats, north bench.
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -6,10 +6,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-timeout -k 10 500 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --qu-noise-free \
-  > gpurun_out/r03i_qunf.json 2> gpurun_out/r03i_qunf.err
-rc=$?; echo "qu-noise-free rc=$rc"; tail -c 600 gpurun_out/r03i_qunf.json
-if [ $rc -ne 0 ] && [ $rc -ne 3 ]; then tail -20 gpurun_out/r03i_qunf.err; exit 1; fi
+# (the --qu-noise-free run: profiles/bench_r03i_north_qu_noise_free.json, NOT_PD at q(u))
 timeout -k 10 600 python -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --api per-output --inputs host \
   > gpurun_out/r03i_perout_host.json 2> gpurun_out/r03i_perout_host.err || { tail -20 gpurun_out/r03i_perout_host.err; exit 1; }
 python3 -c "import json; d=json.load(open('gpurun_out/r03i_perout_host.json')); print('per-output host', round(d['ms_per_step'],1), d['value'])"
