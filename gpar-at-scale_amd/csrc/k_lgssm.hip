@@ -1286,10 +1286,12 @@ __global__ __launch_bounds__(64) void adjoint_local(double* __restrict__ X, int6
 // were scalar loads waited on step by step), and with `wmask` writes u only at the rows the
 // caller reads (test points: wmask[k] >= 1e10, gpar_scaled_inference.jl:100-107).  A wave whose
 // 64 columns are all past ncols leaves after the staging (the prediction's ncols = Mp + 1 left a
-// third of the workgroups carrying one column through the whole chunk), and each thread keeps
-// kAdjPF rows of X in flight ahead of the recursion (the loads do not depend on it; at 4
-// workgroups per CU the unrolled loop's 4 were too few: 77 % of wave time waiting on memory).
-constexpr int kAdjPF = 12;
+// third of the workgroups carrying one column through the whole chunk).  X goes through a buffer
+// descriptor over the chunk's rows: each thread keeps kAdjPF rows in flight ahead of the
+// recursion, and the store of u at a train row gets an out-of-range offset and is dropped by the
+// hardware.  With plain loads / a predicated store the branches made the compiler wait for every
+// load at every step (vmcnt(0)): one row in flight per thread, 77 % of wave time waiting.
+constexpr int kAdjPF = 8;
 
 template <int D>
 __global__ __launch_bounds__(256) void adjoint_local_wide(double* __restrict__ X, int64_t ldx,
@@ -1322,36 +1324,53 @@ __global__ __launch_bounds__(256) void adjoint_local_wide(double* __restrict__ X
   double lam[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) lam[i] = 0.0;
-  const double* xc = X + k0 * ldx + cc;
-  double xb[kAdjPF];   // xb[p]: row s of the current group s = top - p
+  // the chunk's rows of X: [k0, k1) x ldx doubles (< 4 GiB for any L x ldx the library uses)
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      X + k0 * ldx, (short)0, __builtin_amdgcn_readfirstlane((int)((int64_t)nk * ldx * 8)),
+      0x00020000);
+  const uint32_t col = (uint32_t)cc * 8u, rowb = (uint32_t)ldx * 8u;
+  auto ld = [&](int s) {   // X[k0 + s][cc], s clamped to row 0 (a spare reload at the end)
+    const uint32_t off = (uint32_t)(s > 0 ? s : 0) * rowb + col;
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
+  };
+  auto stepfn = [&](int s, double w) {
+    const double* r = lrec + s * RU;
+    const double* gk = lg + s * D;
 #pragma unroll
-  for (int p = 0; p < kAdjPF; ++p) xb[p] = nk - 1 - p >= 0 ? xc[(int64_t)(nk - 1 - p) * ldx] : 0.0;
-  for (int top = nk - 1; top >= 0; top -= kAdjPF) {
+    for (int i = 0; i < D; ++i) w = fma(gk[i], cf[i], w);
+    double u = w * r[D * D + D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) u = fma(r[D * D + i], lam[i], u);
+    lam[0] -= u;
+    double nl[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) acc = fma(r[i * D + q], lam[i], acc);
+      nl[q] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) lam[i] = nl[i];
+    // u only where the caller reads it; elsewhere an out-of-range offset (dropped)
+    const uint32_t off = (act && lw[s]) ? (uint32_t)s * rowb + col : ~0u;
+    typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, u), xr, off, 0, 0);
+  };
+  // a short last chunk's top nk % kAdjPF rows one by one, then whole groups with the ring
+  const int rem = nk % kAdjPF;
+  for (int s = nk - 1; s >= nk - rem; --s) stepfn(s, ld(s));
+  const int top0 = nk - rem - 1;
+  double xb[kAdjPF];   // xb[p]: row top - p of the current group
+#pragma unroll
+  for (int p = 0; p < kAdjPF; ++p) xb[p] = ld(top0 - p);
+  for (int top = top0; top >= 0; top -= kAdjPF) {
 #pragma unroll
     for (int p = 0; p < kAdjPF; ++p) {
       const int s = top - p;
-      if (s < 0) break;   // uniform: nk is the workgroup's
-      double w = xb[p];
-      if (s - kAdjPF >= 0) xb[p] = xc[(int64_t)(s - kAdjPF) * ldx];
-      const double* r = lrec + s * RU;
-      const double* gk = lg + s * D;
-#pragma unroll
-      for (int i = 0; i < D; ++i) w = fma(gk[i], cf[i], w);
-      double u = w * r[D * D + D];
-#pragma unroll
-      for (int i = 0; i < D; ++i) u = fma(r[D * D + i], lam[i], u);
-      lam[0] -= u;
-      double nl[D];
-#pragma unroll
-      for (int q = 0; q < D; ++q) {
-        double acc = 0.0;
-#pragma unroll
-        for (int i = 0; i < D; ++i) acc = fma(r[i * D + q], lam[i], acc);
-        nl[q] = acc;
-      }
-#pragma unroll
-      for (int i = 0; i < D; ++i) lam[i] = nl[i];
-      if (act && lw[s]) X[(k0 + s) * ldx + c] = u;
+      const double w = xb[p];
+      xb[p] = ld(s - kAdjPF);
+      stepfn(s, w);
     }
   }
   if (act) {
