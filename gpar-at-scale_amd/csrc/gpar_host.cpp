@@ -67,6 +67,7 @@ struct gpar_ctx {
   // gpar_fit_predict's predictions alternate over two streams (GPAR_PREDICT_LANES=1: one)
   int predict_lanes = 2;
   bool predict_fused = true;      // GPAR_PREDICT_FUSED=0: predict_rows + gemm_nt (A/B)
+  bool qu_batch = true;           // GPAR_QU_BATCH=0: gpar_fit_predict's q(u) per output (A/B)
   std::string ws_suffix;          // appended to workspace names (a prediction lane's own buffers)
   hipEvent_t ev_grp[2] = {nullptr, nullptr};   // fit_overlapped: a group's values are in
   hipEvent_t ev_gn[2] = {nullptr, nullptr};    // fit_overlapped: a group's gains are done
@@ -956,6 +957,12 @@ struct GramCache {
   const double* r = nullptr;
 };
 
+// the fit's kept Grams (fit_impl, for gpar_fit_predict): output i's at its returned minimiser
+struct FitKeep {
+  std::vector<GramCache> gram;
+  std::vector<char> valid;
+};
+
 static QuOut run_q_u(gpar_ctx* c, const DevProblem& p, const Theta& th,
                      const GramCache* gc = nullptr) {
   std::vector<DevProblem> P{p};
@@ -1010,6 +1017,113 @@ static QuOut run_q_u(gpar_ctx* c, const DevProblem& p, const Theta& th,
   if (st[0]) throw Error(GPAR_ERR_NOT_PD, "PosDefException: cholesky(Symmetric(Cuu)) failed (gpar_scaled_inference.jl:159)");
   if (st[1]) throw Error(GPAR_ERR_NOT_PD, "PosDefException: cholesky(Symmetric(D)) failed (gpar_scaled_inference.jl:188)");
   return q;
+}
+
+// q(u) and the substitutions every prediction mode needs, for all outputs of a gpar_fit_predict
+// call at once (a batched prediction used to run them per output: the blocked Cholesky, the
+// finish, three trsm and a trsv, each a latency-bound launch of one small job, ~4 ms per output
+// and a host sync each).  Per output i: Lu, LD (chol(Cuu), chol(D)), me = m_e, w = U_u^{-1} m_e
+// = L_u^{-T} m_e, X1 = L_u^{-1}, Vm = L_D^{-1} L_u^{-1} (zero outside m x m), and for the MC / path
+// modes cov = inv(D) = X^T X, X = L_D^{-1} (the same substitutions as run_q_u + predict_impl).
+struct QuPre {
+  const double *Lu, *LD, *me, *w, *X1, *Vm, *cov;
+  int64_t ld;
+  int nb;
+};
+
+static std::vector<QuPre> run_q_u_batch(gpar_ctx* c, const std::vector<DevProblem>& P,
+                                        const std::vector<Theta>& T, const FitKeep& keep,
+                                        bool want_cov) {
+  const int np = (int)P.size();
+  int64_t mpmax = 0, mmax = 0;
+  for (const auto& p : P) { mpmax = std::max(mpmax, p.mp); mmax = std::max(mmax, p.m); }
+  const bool qn = P[0].qu_noise;
+  bool kept = qn;
+  for (int i = 0; i < np; ++i)
+    kept = kept && i < (int)keep.valid.size() && keep.valid[i] && keep.gram[i].G;
+  GramOut go;
+  const size_t sq = (size_t)mpmax * mpmax;
+  if (kept) {   // the fit's Grams at the fitted theta, packed at the batch's ld
+    go.ldg = mpmax;
+    go.npart = 1;
+    go.G = ws<double>(c, "qub_G", (size_t)np * sq);
+    go.r = ws<double>(c, "qub_r", (size_t)np * mpmax);
+    go.a2part = ws<double>(c, "qub_zero_a2", (size_t)np);   // dtc terms: unused in q(u) mode
+    go.logs = ws<double>(c, "qub_zero_logs", (size_t)np * P[0].nch);
+    HIPCHECK(hipMemsetAsync(go.a2part, 0, (size_t)np * sizeof(double), c->stream));
+    HIPCHECK(hipMemsetAsync(go.logs, 0, (size_t)np * P[0].nch * sizeof(double), c->stream));
+    HIPCHECK(hipMemsetAsync(go.G, 0, (size_t)np * sq * sizeof(double), c->stream));
+    HIPCHECK(hipMemsetAsync(go.r, 0, (size_t)np * mpmax * sizeof(double), c->stream));
+    for (int i = 0; i < np; ++i) {
+      const GramCache& g = keep.gram[i];
+      HIPCHECK(hipMemcpy2DAsync(go.G + i * sq, mpmax * sizeof(double), g.G, P[i].mp * sizeof(double),
+                                P[i].mp * sizeof(double), P[i].mp, hipMemcpyDeviceToDevice, c->stream));
+      HIPCHECK(hipMemcpyAsync(go.r + (size_t)i * mpmax, g.r, P[i].mp * sizeof(double),
+                              hipMemcpyDeviceToDevice, c->stream));
+    }
+  } else {
+    go = run_gram_stage(c, P, T, /*fix_beta=*/!qn);
+  }
+  DenseOut dn = run_dense(c, P, T, go, /*qu_mode=*/true);
+  const int64_t ld = dn.ld;
+  double* me = ws<double>(c, "qub_me", (size_t)np * ld);
+  double* dout = ws<double>(c, "qub_out", (size_t)np);
+  std::vector<Finish2JobHost> fj(np);
+  for (int i = 0; i < np; ++i) fj[i] = finish_job(dn, go, P[i], i, P[0].nch, dout + i, me + i * ld);
+  auto* dfj = ws<Finish2JobHost>(c, "qub_finish", np);
+  h2d(c, dfj, fj.data(), np);
+  launch_finish2(c->stream, dfj, np, ld, dn.nb);
+  check_launch("finish(q_u batch)");
+  std::vector<int> st(2 * np);
+  d2h(c, st.data(), dn.status, 2 * np);
+  sync(c);
+  for (int i = 0; i < np; ++i) {
+    if (st[2 * i]) throw Error(GPAR_ERR_NOT_PD, "PosDefException: cholesky(Symmetric(Cuu)) failed (gpar_scaled_inference.jl:159), output " + std::to_string(i));
+    if (st[2 * i + 1]) throw Error(GPAR_ERR_NOT_PD, "PosDefException: cholesky(Symmetric(D)) failed (gpar_scaled_inference.jl:188), output " + std::to_string(i));
+  }
+  // w, X1, Vm (and X, cov) by substitution, one launch each for all outputs
+  double* I = ws<double>(c, "qub_eye", (size_t)ld * ld);
+  double* w = ws<double>(c, "qub_w", (size_t)np * ld);
+  double* X1 = ws<double>(c, "qub_X1", (size_t)np * ld * ld);
+  double* Vm = ws<double>(c, "qub_V", (size_t)np * ld * ld);
+  HIPCHECK(hipMemsetAsync(Vm, 0, (size_t)np * ld * ld * sizeof(double), c->stream));
+  launch_eye(c->stream, I, ld, (int)mmax);
+  std::vector<TrsvJobHost> tv(np);
+  std::vector<TrsmJobHost> t1(np), t2(np), t3(np);
+  double* Xc = want_cov ? ws<double>(c, "qub_Xc", (size_t)np * ld * ld) : nullptr;
+  double* cov = want_cov ? ws<double>(c, "qub_cov", (size_t)np * ld * ld) : nullptr;
+  for (int i = 0; i < np; ++i) {
+    const double* Lu = dn.Lu + i * (size_t)ld * ld;
+    const double* LD = dn.Llam + i * (size_t)ld * ld;
+    const int m = (int)P[i].m;
+    tv[i] = {Lu, ld, m, me + i * ld, w + i * ld, 1};
+    t1[i] = {Lu, ld, I, ld, X1 + i * (size_t)ld * ld, ld, m, P[i].m, 0, 0};
+    t2[i] = {LD, ld, X1 + i * (size_t)ld * ld, ld, Vm + i * (size_t)ld * ld, ld, m, P[i].m, 0, 0};
+    if (want_cov) t3[i] = {LD, ld, I, ld, Xc + i * (size_t)ld * ld, ld, m, P[i].m, 0, 0};
+  }
+  auto* dtv = ws<TrsvJobHost>(c, "qub_trsv", np);
+  auto* dt1 = ws<TrsmJobHost>(c, "qub_trsm1", np);
+  auto* dt2 = ws<TrsmJobHost>(c, "qub_trsm2", np);
+  h2d(c, dtv, tv.data(), np);
+  h2d(c, dt1, t1.data(), np);
+  h2d(c, dt2, t2.data(), np);
+  launch_trsv(c->stream, dtv, np);
+  launch_trsm(c->stream, dt1, np, mmax);
+  launch_trsm(c->stream, dt2, np, mmax);
+  if (want_cov) {
+    auto* dt3 = ws<TrsmJobHost>(c, "qub_trsm3", np);
+    h2d(c, dt3, t3.data(), np);
+    launch_trsm(c->stream, dt3, np, mmax);
+    for (int i = 0; i < np; ++i)
+      launch_gram_small(c->stream, Xc + i * (size_t)ld * ld, ld, (int)P[i].m, cov + i * (size_t)ld * ld, ld);
+  }
+  check_launch("q_u batch substitutions");
+  std::vector<QuPre> out(np);
+  for (int i = 0; i < np; ++i)
+    out[i] = {dn.Lu + i * (size_t)ld * ld, dn.Llam + i * (size_t)ld * ld, me + i * ld, w + i * ld,
+              X1 + i * (size_t)ld * ld, Vm + i * (size_t)ld * ld,
+              want_cov ? cov + i * (size_t)ld * ld : nullptr, ld, dn.nb};
+  return out;
 }
 
 // logpdf of independent LGSSM chains sharing t (device pointers).
@@ -1097,7 +1211,8 @@ static void path_samples(gpar_ctx* c, int sdim, const GainsOut& g, const ChainPa
 static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
                          int64_t n_star, const double* t_star_in, const double* v_star_in,
                          int64_t ldvs, int mode, int samples, uint64_t seed, double* mean_out,
-                         double* std_out, const GramCache* gc = nullptr, bool defer = false) {
+                         double* std_out, const GramCache* gc = nullptr, bool defer = false,
+                         const QuPre* pre = nullptr) {
   const int64_t n = P.n, m = P.m, d = P.d, mp = P.mp, mc = P.mc;
   // ---- test inputs on device, ascending (host inputs are stably sorted here, outputs
   //      un-permuted at the end; device inputs must already be ascending)
@@ -1129,28 +1244,48 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
     vs = dvs;
     ldv_s = d;
   }
-  // ---- q(u): m_e, L_u = chol(Cuu), L_D = chol(D)
-  QuOut q = run_q_u(c, P, th, gc);
-  const double* Lu = ws<double>(c, "Kuu", 1);
-  const double* LD = ws<double>(c, "Lam", 1);
-  const int64_t ld = q.ld;
-  // w = L_u^{-T} m_e and V = L_D^{-1} L_u^{-1} by substitution (noise-free Cuu: see run_q_u)
-  double* w = ws<double>(c, "pr_w", ld);
-  TrsvJobHost tv{Lu, ld, (int)m, q.me, w, 1};
-  auto* dtv = ws<TrsvJobHost>(c, "pr_trsv", 1);
-  h2d(c, dtv, &tv, 1);
-  launch_trsv(c->stream, dtv, 1);
-  double* I = ws<double>(c, "qu_eye", (size_t)ld * ld);
-  double* X1 = ws<double>(c, "pr_X1", (size_t)ld * ld);
-  double* Vm = ws<double>(c, "pr_V", (size_t)ld * ld);
-  launch_eye(c->stream, I, ld, (int)m);
-  // V = 0 outside its m x m block (predict_var reads the whole ld x ld buffer)
-  HIPCHECK(hipMemsetAsync(Vm, 0, (size_t)ld * ld * sizeof(double), c->stream));
-  TrsmJobHost tj[2] = {{Lu, ld, I, ld, X1, ld, (int)m, m, 0, 0}, {LD, ld, X1, ld, Vm, ld, (int)m, m, 0, 0}};
-  auto* dtj = ws<TrsmJobHost>(c, "pr_trsm", 2);
-  h2d(c, dtj, tj, 2);
-  launch_trsm(c->stream, dtj, 1, m);
-  launch_trsm(c->stream, dtj + 1, 1, m);
+  // ---- q(u): m_e, L_u = chol(Cuu), L_D = chol(D); w = L_u^{-T} m_e, X1 = L_u^{-1} and
+  //      V = L_D^{-1} L_u^{-1} by substitution (noise-free Cuu: see run_q_u) -- or all of it
+  //      precomputed for a batch of outputs (run_q_u_batch)
+  QuOut q{};
+  const double *Lu, *LD, *w, *X1, *Vm;
+  int64_t ld;
+  if (pre) {
+    ld = pre->ld;
+    Lu = pre->Lu;
+    LD = pre->LD;
+    w = pre->w;
+    X1 = pre->X1;
+    Vm = pre->Vm;
+    q.ld = ld;
+    q.nb = pre->nb;
+    q.me = const_cast<double*>(pre->me);
+    q.cov = const_cast<double*>(pre->cov);
+  } else {
+    q = run_q_u(c, P, th, gc);
+    Lu = ws<double>(c, "Kuu", 1);
+    LD = ws<double>(c, "Lam", 1);
+    ld = q.ld;
+    double* wv = ws<double>(c, "pr_w", ld);
+    TrsvJobHost tv{Lu, ld, (int)m, q.me, wv, 1};
+    auto* dtv = ws<TrsvJobHost>(c, "pr_trsv", 1);
+    h2d(c, dtv, &tv, 1);
+    launch_trsv(c->stream, dtv, 1);
+    double* I = ws<double>(c, "qu_eye", (size_t)ld * ld);
+    double* X1v = ws<double>(c, "pr_X1", (size_t)ld * ld);
+    double* Vmv = ws<double>(c, "pr_V", (size_t)ld * ld);
+    launch_eye(c->stream, I, ld, (int)m);
+    // V = 0 outside its m x m block (predict_var reads the whole ld x ld buffer)
+    HIPCHECK(hipMemsetAsync(Vmv, 0, (size_t)ld * ld * sizeof(double), c->stream));
+    TrsmJobHost tj[2] = {{Lu, ld, I, ld, X1v, ld, (int)m, m, 0, 0}, {LD, ld, X1v, ld, Vmv, ld, (int)m, m, 0, 0}};
+    auto* dtj = ws<TrsmJobHost>(c, "pr_trsm", 2);
+    h2d(c, dtj, tj, 2);
+    launch_trsm(c->stream, dtj, 1, m);
+    launch_trsm(c->stream, dtj + 1, 1, m);
+    w = wv;
+    X1 = X1v;
+    Vm = Vmv;
+  }
   check_launch("predict: q(u) tail");
   // ---- merged grid
   const int64_t nt = n + n_star;
@@ -1481,6 +1616,7 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
   if (const char* e = std::getenv("GPAR_PIPELINE")) c->pipeline = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_OVERLAP")) c->overlap = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_PREDICT_FUSED")) c->predict_fused = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GPAR_QU_BATCH")) c->qu_batch = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_PREDICT_LANES")) c->predict_lanes = std::atoi(e) > 1 ? 2 : 1;
   // A/B knobs: GPAR_SPLIT_CUS overrides the default CU split, GPAR_SPLIT_DGW=0 keeps the DG
   // kernel off the whitening CUs
@@ -1687,10 +1823,6 @@ int32_t gpar_dtc_objective(gpar_ctx* ctx, const gpar_problem* probs, int32_t npr
 // Batched Nelder-Mead over the outputs: one objective round serves every pending point.
 // keep (optional): per output, the Gram of its lowest-value evaluation (ld = mp) in context
 // workspace, and whether that evaluation is the returned minimiser (bitwise).
-struct FitKeep {
-  std::vector<GramCache> gram;
-  std::vector<char> valid;
-};
 
 // Distance cache: the squared distances |v_k - z_c|^2 do not depend on theta, so for the
 // outputs it holds they are computed once per fit (dist2, k_dist.hip) and every evaluation's
@@ -2166,6 +2298,19 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
   // wall time of the predictions (both lanes): from here on the context stream to the join
   std::optional<Timed> tm_pred;
   tm_pred.emplace(ctx, "predictions");
+  // q(u) and its substitutions for every output at once (one sync), when the outputs share the
+  // q(u) convention
+  bool same_qu = true;
+  for (const auto& p : P) same_qu = same_qu && p.qu_noise == P[0].qu_noise;
+  std::vector<QuPre> pre;
+  if (ctx->qu_batch && nprob > 1 && same_qu) {
+    std::vector<Theta> T;
+    for (int i = 0; i < nprob; ++i) {
+      const double* q = theta_out + 5 * i;
+      T.push_back(Theta{q[0], q[1], q[2], q[3], q[4]});
+    }
+    pre = run_q_u_batch(ctx, P, T, keep, mode != GPAR_PREDICT_ANALYTIC);
+  }
   if (lanes) {   // the side lane follows the fit (kept Grams, inputs) on the context stream
     HIPCHECK(hipEventRecord(ctx->ev_fork, ctx->main));
     HIPCHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
@@ -2176,7 +2321,8 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
     LaneScope lane_(ctx, lanes ? (i & 1) : 0);
     predict_impl(ctx, P[i], th, mem, n_star, t_star, v_star[i], ldvs[i], mode, samples,
                  seed + (uint64_t)i, mean_out[i], std_out[i],
-                 keep.valid[i] ? &keep.gram[i] : nullptr, /*defer=*/lanes);
+                 keep.valid[i] ? &keep.gram[i] : nullptr, /*defer=*/lanes,
+                 pre.empty() ? nullptr : &pre[i]);
     if (chain && chain_col[i] >= 0) {
       double* dst = chain + chain_col[i];
       if (mem == GPAR_MEM_DEVICE) {   // stream-ordered before the next output's merge reads it
