@@ -425,6 +425,31 @@ def main():
                      "whiten": {"avg_ms": pw_ms / pw_n, "achieved_gbs": pw, "frac": pw / HBM_PEAK_GBS},
                      "note": "untimed, after the timed steps: a batched fit of these outputs with "
                              "the CU split off (whole-chip kernels), HIP events as above"}
+    pred_probe = None
+    if rank == 0 and problems and not host and "fit" in last and args.predict == "analytic":
+        # after the timed region: two outputs' predictions one at a time (gpar_predict: one lane,
+        # whole chip), so each prediction kernel's HIP-event time is its own duration, not a span
+        # shared with the other lane's kernels as in the timed calls
+        fr = last["fit"]
+        idx = sorted({len(problems) // 2, len(problems) - 1})
+        ctx.reset_stats()
+        for i in idx:
+            p = gpar_out[i]
+            G.predict_scaled(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], fr.theta[i], ts_d,
+                             Fs_d[:, : p - 1], cfg["out_kernel"], "matern52", mode="analytic",
+                             device=local, qu_kuu_noise=qn)
+        pred_probe = {"outputs": [gpar_out[i] for i in idx]}
+        for fam, bound in (("pred_whiten", "hbm"), ("pred_adjoint", "hbm"), ("pred_var", "mfma")):
+            pn, pms = ctx.kernel_stats(fam)
+            if pn:
+                w = ctx.kernel_work(fam) / (pms * 1e-3)
+                pred_probe[fam] = ({"avg_ms": pms / pn, "achieved": w / 1e9, "unit": "GB/s",
+                                    "frac": w / 1e9 / HBM_PEAK_GBS} if bound == "hbm" else
+                                   {"avg_ms": pms / pn, "achieved": w / 1e12, "unit": "TFLOP/s",
+                                    "frac": w / 1e12 / FP64_MFMA_PEAK_TFLOPS})
+        pred_probe["note"] = ("untimed, after the timed steps: single-output gpar_predict calls at "
+                              "the fitted theta (one stream, whole chip), HIP events per kernel family "
+                              "as roofline_predict")
     self_check = None
     if rank == 0 and problems and "fit" in last:
         # the timed steps' own outputs: each checked output's -nlml (the objective value the
@@ -546,6 +571,8 @@ def main():
                 pred["wall_ms_per_step"] = pwall_ms / args.steps
                 pred["wall_note"] = ("HIP events around all of one gpar_fit_predict call's "
                                      "predictions (q(u), both lanes, to their join)")
+            if pred_probe:
+                pred["one_lane_probe"] = pred_probe
             out["roofline_predict"] = pred
         out["memory"] = memory
         if self_check:

@@ -39,6 +39,7 @@ struct gpar_ctx {
   // s_d: the round-overlapping fit's dense tails, on the whitening CUs (fit_overlapped)
   hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr, s_d = nullptr;
   hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
+  hipEvent_t ev_g0 = nullptr, ev_gr = nullptr;   // split round start: gains uploaded / the rest's gains done
   // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
   // the caller's stream, e.g. the copies that produce its device inputs
   bool has_input_stream = false;
@@ -68,6 +69,8 @@ struct gpar_ctx {
   int predict_lanes = 2;
   bool predict_fused = true;      // GPAR_PREDICT_FUSED=0: predict_rows + gemm_nt (A/B)
   bool qu_batch = true;           // GPAR_QU_BATCH=0: gpar_fit_predict's q(u) per output (A/B)
+  bool dense_early = true;        // GPAR_DENSE_EARLY=0: the whole dense tail after the round's Grams (A/B)
+  bool split_head = true;         // GPAR_SPLIT_HEAD=0: the split round's first job on the whitening CUs, gains in one launch (A/B)
   std::string ws_suffix;          // appended to workspace names (a prediction lane's own buffers)
   hipEvent_t ev_grp[2] = {nullptr, nullptr};   // fit_overlapped: a group's values are in
   hipEvent_t ev_gn[2] = {nullptr, nullptr};    // fit_overlapped: a group's gains are done
@@ -430,7 +433,8 @@ static GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                           const std::vector<ChainParamsHost>& cps, const double* noise,
                           bool want_pf, const std::string& tag,
                           const std::vector<const double*>* ys = nullptr,
-                          double* alpha_loc = nullptr, double* asend = nullptr) {
+                          double* alpha_loc = nullptr, double* asend = nullptr,
+                          hipStream_t st_rest = nullptr) {
   const int nchains = (int)cps.size();
   const int64_t nch = (n + kChunk - 1) / kChunk;
   const int rs = rec_size(sdim);
@@ -453,10 +457,25 @@ static GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
     dys = ws<const double*>(c, tag + "_ys", nchains);
     h2d(c, dys, ys->data(), nchains);
   }
+  // st_rest: chain 0 on c->stream, chains 1.. on st_rest (after the uploads above), which then
+  // records c->ev_gr; the chains' arrays are strided per chain, so a range is a pointer offset
+  const int n0 = (st_rest && nchains > 1) ? 1 : nchains;
+  if (n0 < nchains) HIPCHECK(hipEventRecord(c->ev_g0, c->stream));
   {
     Timed tm_(c, "gains");
-    launch_gains(c->stream, sdim, t, n, kChunk, nch, nchains, dcps, noise, agg, pst, o.rec, o.g,
+    launch_gains(c->stream, sdim, t, n, kChunk, nch, n0, dcps, noise, agg, pst, o.rec, o.g,
                  o.phi, o.logs, o.pf, dys, alpha_loc, asend);
+  }
+  if (n0 < nchains) {
+    HIPCHECK(hipStreamWaitEvent(st_rest, c->ev_g0, 0));
+    launch_gains(st_rest, sdim, t, n, kChunk, nch, nchains - n0, dcps + n0, noise,
+                 agg + (size_t)n0 * nch * 3 * d2, pst + (size_t)n0 * nch * d2,
+                 o.rec + (size_t)n0 * o.recstride, o.g + (size_t)n0 * o.gstride,
+                 o.phi + (size_t)n0 * o.phistride, o.logs + (size_t)n0 * nch,
+                 o.pf ? o.pf + (size_t)n0 * n * d2 : nullptr, dys ? dys + n0 : nullptr,
+                 alpha_loc ? alpha_loc + (size_t)n0 * n : nullptr,
+                 asend ? asend + (size_t)n0 * nch * kSStride : nullptr);
+    HIPCHECK(hipEventRecord(c->ev_gr, st_rest));
   }
   check_launch("gains");
   return o;
@@ -636,8 +655,17 @@ struct SplitPipe {
     HIPCHECK(hipEventRecord(c->ev_sp, c->stream));
     for (hipStream_t st : {c->s_w, c->s_g, c->s_g2}) HIPCHECK(hipStreamWaitEvent(st, c->ev_sp, 0));
   }
+  bool head = false;           // job 0 runs whole-chip on the caller's stream (split_head)
   void push(const StageJob& j) {
-    {
+    if (k == 0 && head) {
+      // nothing runs on the Gram CUs before the first Gram: the first whitening and its short
+      // chain take the whole chip (the caller's unmasked stream, which the split streams follow
+      // since start()); the whitening side continues after them
+      stage_whiten(c, j, buf[0]);
+      stage_post(c, j, buf[0], false);
+      HIPCHECK(hipEventRecord(c->ev_pc[0], c->stream));
+      HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[0], 0));
+    } else {
       OnStream on_(c, c->s_w);
       if (k >= 2) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[k & 1], 0));
       stage_whiten(c, j, buf[k & 1]);
@@ -709,6 +737,10 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
 
   // group problems sharing (t, n, time kernel) into one batched gains launch
   const bool shared = shares_grid(P);
+  const bool pipe = fit_pipelined(c, P, fix_beta);
+  const bool split_pipe = pipe && split_active(c, n, mpmax);
+  const bool split_head = split_pipe && c->split_head && shared && np > 1;
+  const double* logs_src = nullptr;
   std::vector<GainsOut> gains(np);
   // shared gains: every output's alpha_loc (y filtered from zero per chunk) comes out of the
   // gains pass itself; only its chunk end states are copied into the carry's alpha column
@@ -723,8 +755,10 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     }
     alpha_all = ws<double>(c, "alpha_all", (size_t)np * n);
     asend_all = ws<double>(c, "asend_all", (size_t)np * nch * kSStride);
+    // split pipeline: the first output's gains alone on the context stream, so its whitening can
+    // start, the others' on s_g2 (Gram CUs, idle until the first Gram's correction)
     GainsOut g = run_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fit", &ys, alpha_all,
-                           asend_all);
+                           asend_all, split_head ? c->s_g2 : nullptr);
     for (int i = 0; i < np; ++i) {
       gains[i] = g;
       gains[i].rec = g.rec + (size_t)i * g.recstride;
@@ -732,8 +766,10 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
       gains[i].phi = g.phi + (size_t)i * g.phistride;
       gains[i].logs = g.logs + (size_t)i * nch;
     }
-    HIPCHECK(hipMemcpyAsync(o.logs, g.logs, (size_t)np * nch * sizeof(double),
-                            hipMemcpyDeviceToDevice, c->stream));
+    if (!split_head)   // else after the pipeline (the other outputs' gains run on s_g2)
+      HIPCHECK(hipMemcpyAsync(o.logs, g.logs, (size_t)np * nch * sizeof(double),
+                              hipMemcpyDeviceToDevice, c->stream));
+    logs_src = g.logs;
   }
 
   // Outputs alternate between the context stream and a side stream, each with its own
@@ -744,7 +780,6 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   // whitening(i + 1) issued ahead of Gram(i), and output i's short chain between them (alpha's end
   // states, the chunk carry, vec_fix, the beta tail) runs on the side stream beside a whitening
   // instead of on the critical path.  Two beta / carry buffers (fit_pipelined).
-  const bool pipe = fit_pipelined(c, P, fix_beta);
   reserve_gram_parts(c, P, nlanes);
   // the stage job of output i, its gains (per output unless shared) run on c->stream
   std::vector<StageJob> jobs(np);
@@ -772,12 +807,20 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     j.ldg = mpmax;
     return j;
   };
-  if (pipe && split_active(c, n, mpmax)) {
+  if (split_pipe) {
     SplitPipe sp(c, n, mpmax);
+    sp.head = split_head;
     sp.start();
+    // the whitening side needs every output's gains from job 1 on
+    if (split_head) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr, 0));
     for (int i = 0; i < np; ++i) sp.push(job(i, sp.buf[i & 1]));
     sp.flush();
     sp.join(c->stream);   // a prediction lane's q(u) runs this on the side stream
+    if (split_head) {     // s_g2's gains precede the last Gram's correction, which join covers
+      HIPCHECK(hipStreamWaitEvent(c->stream, c->ev_gr, 0));
+      HIPCHECK(hipMemcpyAsync(o.logs, logs_src, (size_t)np * nch * sizeof(double),
+                              hipMemcpyDeviceToDevice, c->stream));
+    }
     return o;
   }
   StageBufs bufs[2];
@@ -845,11 +888,11 @@ struct DenseOut {
 
 // L_u = chol(Kuu [+ s2 I]), T_u = L_u^-1, Lambda = T_u G T_u^T + I, L_lam = chol(Lambda) for
 // every problem: blocked 64 x 64 MFMA kernels (k_chol.hip), matrices padded with identity to
-// ld = Mp (padding contributes log 1 = 0 and zero right-hand sides).
-static DenseOut run_dense(gpar_ctx* c, const std::vector<DevProblem>& P,
-                          const std::vector<Theta>& th, const GramOut& go, bool qu_mode) {
+// ld = Mp (padding contributes log 1 = 0 and zero right-hand sides).  run_dense_pre is the part
+// that does not read G (Kuu, its Cholesky factor and inverse), run_dense_post the rest.
+static DenseOut run_dense_pre(gpar_ctx* c, const std::vector<DevProblem>& P,
+                              const std::vector<Theta>& th, int64_t ld, bool qu_mode) {
   const int np = (int)P.size();
-  const int64_t ld = go.ldg;
   const int nb = (int)(ld / kDenseNB);
   DenseOut o;
   o.ld = ld;
@@ -858,42 +901,61 @@ static DenseOut run_dense(gpar_ctx* c, const std::vector<DevProblem>& P,
   o.Lu = ws<double>(c, "Kuu", (size_t)np * sq);
   o.Llam = ws<double>(c, "Lam", (size_t)np * sq);
   o.Tu = ws<double>(c, "Tu", (size_t)np * sq);
-  double* X = ws<double>(c, "TG", (size_t)np * sq);
   double* Tdu = ws<double>(c, "Tdu", (size_t)np * nb * kDenseNB * kDenseNB);
   o.Tdl = ws<double>(c, "Tdl", (size_t)np * nb * kDenseNB * kDenseNB);
   o.Tl = nullptr;
   o.status = ws<int>(c, "status", (size_t)np * 2);
   HIPCHECK(hipMemsetAsync(o.status, 0, np * 2 * sizeof(int), c->stream));
   std::vector<KuuJobHost> kj(np);
-  std::vector<CholJob2Host> cu(np), cl(np);
-  std::vector<TgtJobHost> tj(np);
+  std::vector<CholJob2Host> cu(np);
   for (int i = 0; i < np; ++i) {
     const DevProblem& p = P[i];
     const double s2 = th[i].sigma * th[i].sigma;
     kj[i] = {p.z, p.ldz, (int)p.d, p.ok, 1.0 / th[i].l_o, th[i].sv_o * th[i].sv_o,
              (qu_mode ? p.qu_noise : p.kuu_noise) ? s2 : 0.0, o.Lu + i * sq, ld, (int)p.m, (int)ld};
     cu[i] = {o.Lu + i * sq, o.Tu + i * sq, Tdu + (size_t)i * nb * kDenseNB * kDenseNB, o.status + 2 * i};
-    cl[i] = {o.Llam + i * sq, o.Tl ? o.Tl + i * sq : nullptr,
-             o.Tdl + (size_t)i * nb * kDenseNB * kDenseNB, o.status + 2 * i + 1};
-    tj[i] = {o.Tu + i * sq, go.G + i * sq, X + i * sq, o.Llam + i * sq};
   }
   auto* dkj = ws<KuuJobHost>(c, "kuujobs", np);
   auto* dcu = ws<CholJob2Host>(c, "chol2u", np);
-  auto* dcl = ws<CholJob2Host>(c, "chol2l", np);
-  auto* dtj = ws<TgtJobHost>(c, "tgtjobs", np);
   h2d(c, dkj, kj.data(), np);
   h2d(c, dcu, cu.data(), np);
-  h2d(c, dcl, cl.data(), np);
-  h2d(c, dtj, tj.data(), np);
   Timed tm_(c, "dense");
   launch_kuu(c->stream, dkj, np, (int)ld);
   check_launch("kuu");
   launch_chol_blocked(c->stream, dcu, np, ld, nb, /*want_t=*/true);
   check_launch("chol(Kuu)");
+  return o;
+}
+
+static void run_dense_post(gpar_ctx* c, const std::vector<DevProblem>& P, const GramOut& go,
+                           const DenseOut& o) {
+  const int np = (int)P.size();
+  const int64_t ld = o.ld;
+  const int nb = o.nb;
+  const size_t sq = (size_t)ld * ld;
+  double* X = ws<double>(c, "TG", (size_t)np * sq);
+  std::vector<CholJob2Host> cl(np);
+  std::vector<TgtJobHost> tj(np);
+  for (int i = 0; i < np; ++i) {
+    cl[i] = {o.Llam + i * sq, o.Tl ? o.Tl + i * sq : nullptr,
+             o.Tdl + (size_t)i * nb * kDenseNB * kDenseNB, o.status + 2 * i + 1};
+    tj[i] = {o.Tu + i * sq, go.G + i * sq, X + i * sq, o.Llam + i * sq};
+  }
+  auto* dcl = ws<CholJob2Host>(c, "chol2l", np);
+  auto* dtj = ws<TgtJobHost>(c, "tgtjobs", np);
+  h2d(c, dcl, cl.data(), np);
+  h2d(c, dtj, tj.data(), np);
+  Timed tm_(c, "dense");
   launch_tgt(c->stream, dtj, np, ld, nb);
   check_launch("Lambda = T G T^T + I");
   launch_chol_blocked(c->stream, dcl, np, ld, nb, /*want_t=*/false);
   check_launch("chol(Lambda)");
+}
+
+static DenseOut run_dense(gpar_ctx* c, const std::vector<DevProblem>& P,
+                          const std::vector<Theta>& th, const GramOut& go, bool qu_mode) {
+  DenseOut o = run_dense_pre(c, P, th, go.ldg, qu_mode);
+  run_dense_post(c, P, go, o);
   return o;
 }
 
@@ -921,9 +983,21 @@ static std::vector<Theta> thetas_from(const double* theta, int np) {
 static void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<Theta>& th,
                      double* out, std::vector<int>& status_out, GramOut* gram_out = nullptr) {
   const int np = (int)P.size();
+  // On the CU-split pipeline the G-independent half of the dense tail (Kuu, its factor and
+  // inverse) goes first on the Gram stream: it runs beside the gains and the first whitening,
+  // while the Gram CUs would otherwise wait, instead of after the round's last Gram.
+  int64_t mpmax = 0;
+  for (const auto& p : P) mpmax = std::max(mpmax, p.mp);
+  const bool early = c->dense_early && fit_pipelined(c, P) && split_active(c, P[0].n, mpmax);
+  DenseOut dn{};
+  if (early) {
+    OnStream on_(c, c->s_g);
+    dn = run_dense_pre(c, P, th, mpmax, false);
+  }
   GramOut go = run_gram_stage(c, P, th);
   if (gram_out) *gram_out = go;
-  DenseOut dn = run_dense(c, P, th, go, false);
+  if (!early) dn = run_dense_pre(c, P, th, go.ldg, false);
+  run_dense_post(c, P, go, dn);
   const int64_t nch = P[0].nch;
   std::vector<Finish2JobHost> fj(np);
   double* dout = ws<double>(c, "dtc_out", np);
@@ -1332,7 +1406,7 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
   double* dstd = ws<double>(c, "pr_std", n_star);
   if (path) {
     // tmp.jl:119-167: per sample, fx_s = Cf*u U_u^{-1} e_s (e_s ~ q(u)) on the merged grid, then a
-    // posterior path of the time GP given y* - fx_s (FFBS), f*_s = fx_s + f_t,s
+    // posterior path of the time GP given y* - fx_s (simulation smoother, path_samples), f*_s = fx_s + f_t,s
     double* W = mc_factor();
     double* xi = ws<double>(c, "pr_xi", (size_t)samples * mp);
     launch_normal(c->stream, xi, mp, samples, m, samples, seed);
@@ -1376,8 +1450,18 @@ static void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int 
     {   // bytes: the mc whitened columns read per merged row, records + fix-up rows + R (21), u
         // written at the test rows
       Timed tm_(c, "pred_adjoint", 8.0 * ((double)nt * ((double)mc + 21.0) + (double)n_star * (double)mc));
-      launch_adjoint_local_wide(c->stream, P.sdim, X, ldx, mc, g.rec, g.g, cin, mc, nt, kChunk, nch,
-                                bend, rm);
+      if (mp % 256 == 0) {
+        // the Cf*u columns in whole 256-column workgroups, and y* (column mp) by the narrow
+        // kernel: as column 512 of the wide one it was a third workgroup per chunk carrying one
+        // live column through the whole chunk
+        launch_adjoint_local_wide(c->stream, P.sdim, X, ldx, mp, g.rec, g.g, cin, mc, nt, kChunk,
+                                  nch, bend, rm);
+        launch_adjoint_local(c->stream, P.sdim, X + mp, ldx, 1, g.rec, g.g, cin + mp * kSStride,
+                             mc, nt, kChunk, nch, bend + mp * kSStride, 1, 0, 0);
+      } else {
+        launch_adjoint_local_wide(c->stream, P.sdim, X, ldx, mc, g.rec, g.g, cin, mc, nt, kChunk,
+                                  nch, bend, rm);
+      }
     }
     check_launch("predict: adjoint");
     run_carry(c, P.sdim, g.phi, 0, bend, chat, 0, nch, mc, mc, 1, "predb", /*rev=*/true);
@@ -1579,7 +1663,9 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
     if (!c->ev_sp &&
         (hipEventCreateWithFlags(&c->ev_gd[0], hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_gd[1], hipEventDisableTiming) != hipSuccess ||
-         hipEventCreateWithFlags(&c->ev_sp, hipEventDisableTiming) != hipSuccess))
+         hipEventCreateWithFlags(&c->ev_sp, hipEventDisableTiming) != hipSuccess ||
+         hipEventCreateWithFlags(&c->ev_g0, hipEventDisableTiming) != hipSuccess ||
+         hipEventCreateWithFlags(&c->ev_gr, hipEventDisableTiming) != hipSuccess))
       return GPAR_ERR_HIP;
     c->split_mask_w = w;
   }
@@ -1617,6 +1703,8 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
   if (const char* e = std::getenv("GPAR_OVERLAP")) c->overlap = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_PREDICT_FUSED")) c->predict_fused = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_QU_BATCH")) c->qu_batch = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GPAR_DENSE_EARLY")) c->dense_early = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GPAR_SPLIT_HEAD")) c->split_head = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_PREDICT_LANES")) c->predict_lanes = std::atoi(e) > 1 ? 2 : 1;
   // A/B knobs: GPAR_SPLIT_CUS overrides the default CU split, GPAR_SPLIT_DGW=0 keeps the DG
   // kernel off the whitening CUs
@@ -1650,7 +1738,7 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
         (void)hipStreamDestroy(st);
       }
     for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_grp[0], ctx->ev_grp[1],
-                          ctx->ev_gn[0], ctx->ev_gn[1]})
+                          ctx->ev_gn[0], ctx->ev_gn[1], ctx->ev_g0, ctx->ev_gr})
       if (ev) (void)hipEventDestroy(ev);
     for (auto& s : ctx->stage)
       if (s.host) (void)hipHostFree(s.host);

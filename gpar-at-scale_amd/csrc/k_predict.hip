@@ -280,6 +280,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
 // phase G's later steps (56 % of the dense MFMAs at M = 512; gemm_nt's 128-column skip: 62.5 %).
 // V must be zero outside its m x m block (the caller clears the Mp x Mp buffer).
 constexpr int kVRows = 64;
+#ifndef PV_ABL
+#define PV_ABL 0   // timing ablations only: 1 no A-operand loads, 2 no V slab DMA, 3 no per-step wait + barrier, 4 no MFMA
+#endif
 template <int V_> struct IntC { static constexpr int value = V_; };
 // 16 bytes global -> LDS by DMA (wave-uniform LDS base + lane * 16).  A plain __device__ function:
 // the builtin inside the kernel template's lambdas made the host pass drop the launch stubs.
@@ -368,8 +371,12 @@ __global__ __launch_bounds__(256, 1) void predict_var(
     constexpr int T0 = decltype(t0c)::value;
     makeA(s, 0);
     if (s + 1 < NS) {
+#if PV_ABL != 1
       loadA(s + 1, 0);
+#endif
+#if PV_ABL != 2
       dmaB(s + 1, (s + 1) & 1);
+#endif
     }
     const double* B = &lb[0][0] + (s & 1) * (NC * 16);
 #pragma unroll
@@ -378,13 +385,19 @@ __global__ __launch_bounds__(256, 1) void predict_var(
       for (int ks = 0; ks < 4; ++ks) {
         const int c = t * 16 + fcol, kk = ks * 4 + frow;
         const double bf = B[c * 16 + (((kk >> 1) ^ ((c >> 1) & 7)) << 1) + (kk & 1)];
+#if PV_ABL != 4
         acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[ks], bf, acc[t], 0, 0, 0);
+#else
+        acc[t][0] += fa[ks] * bf;
+#endif
         // keep the scheduler's window to a few tiles: hoisting every fragment read of a
         // 32-tile step ran out of VGPRs and spilled the accumulators
         if (ks == 3 && (t & 1)) __builtin_amdgcn_sched_barrier(0);
       }
+#if PV_ABL != 3
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+#endif
   };
   // phase G: k-steps 4 G .. 4 G + 3 with tiles 4 G .. T - 1.  Phase 0's first step is peeled (a
   // loop whose accumulators enter as the zero constant copied them every step)

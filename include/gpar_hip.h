@@ -58,7 +58,8 @@ typedef enum gpar_predict_mode {
   GPAR_PREDICT_ANALYTIC = 0, /* exact S -> infinity limit of the reference's MC estimator */
   GPAR_PREDICT_MC = 1,       /* reference-faithful Monte Carlo (gpar_scaled_inference.jl:110-130) */
   GPAR_PREDICT_PATH = 2      /* Monte Carlo over posterior paths (src/gp/tmp.jl:119-167): per sample
-                                a q(u) draw and a posterior_rand path of the time GP (FFBS) */
+                                a q(u) draw and a posterior_rand path of the time GP (simulation
+                                smoother, gpar_lgssm_posterior_rand) */
 } gpar_predict_mode;
 
 typedef struct gpar_ctx gpar_ctx;
