@@ -19,6 +19,8 @@
 //    consumer: vec_fix_kernel here, the Gram loader in k_gram.hip).
 #include "device_common.hpp"
 
+#include <cstdlib>
+
 namespace gpar {
 
 struct ChainParams {
@@ -1293,8 +1295,8 @@ __global__ __launch_bounds__(64) void adjoint_local(double* __restrict__ X, int6
 // load at every step (vmcnt(0)): one row in flight per thread, 77 % of wave time waiting.
 constexpr int kAdjPF = 8;
 
-template <int D>
-__global__ __launch_bounds__(256) void adjoint_local_wide(double* __restrict__ X, int64_t ldx,
+template <int D, int CW>
+__global__ __launch_bounds__(CW) void adjoint_local_wide(double* __restrict__ X, int64_t ldx,
                                                          int64_t ncols, const double* __restrict__ rec,
                                                          const double* __restrict__ g,
                                                          const double* __restrict__ cin, int64_t mc,
@@ -1307,17 +1309,17 @@ __global__ __launch_bounds__(256) void adjoint_local_wide(double* __restrict__ X
   __shared__ unsigned char lw[256];
   const int64_t j = blockIdx.x;
   const int tid = threadIdx.x;
-  const int64_t c = (int64_t)blockIdx.y * 256 + tid;
+  const int64_t c = (int64_t)blockIdx.y * CW + tid;
   const bool act = c < ncols;
   const int64_t cc = act ? c : 0;
   const int64_t k0 = j * L;
   const int64_t k1 = (k0 + L < n) ? k0 + L : n;
   const int nk = (int)(k1 - k0);
-  for (int e = tid; e < nk * RU; e += 256) lrec[e] = rec[(k0 + e / RU) * RS + e % RU];
-  for (int e = tid; e < nk * D; e += 256) lg[e] = g[(k0 + e / D) * kGStride + e % D];
+  for (int e = tid; e < nk * RU; e += CW) lrec[e] = rec[(k0 + e / RU) * RS + e % RU];
+  for (int e = tid; e < nk * D; e += CW) lg[e] = g[(k0 + e / D) * kGStride + e % D];
   if (tid < nk) lw[tid] = wmask ? (wmask[k0 + tid] >= 1e10) : 1;
   __syncthreads();
-  if ((int64_t)blockIdx.y * 256 + (tid & ~63) >= ncols) return;   // the whole wave is idle
+  if ((int64_t)blockIdx.y * CW + (tid & ~63) >= ncols) return;   // the whole wave is idle
   double cf[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) cf[i] = cin[(j * mc + cc) * kSStride + i];
@@ -1845,8 +1847,19 @@ void launch_adjoint_local(hipStream_t st, int sdim, double* X, int64_t ldx, int6
 void launch_adjoint_local_wide(hipStream_t st, int sdim, double* X, int64_t ldx, int64_t ncols,
                                const double* rec, const double* g, const double* cin, int64_t mc,
                                int64_t n, int L, int64_t nch, double* bend, const double* wmask) {
+  // a prediction's Mp + 1 <= 576 columns in one workgroup per chunk: the whole row of X is read
+  // by one workgroup at a time (GPAR_ADJ_CW=256: 256-column workgroups, A/B)
+  static const int cw_env = [] {
+    const char* e = std::getenv("GPAR_ADJ_CW");
+    return e ? std::atoi(e) : 576;
+  }();
+  if (cw_env == 576 && ncols <= 576 && ncols > 256) {
+    dim3 grid((unsigned)nch, 1u);
+    GPAR_DISPATCH_D(sdim, (adjoint_local_wide<DD, 576><<<grid, 576, 0, st>>>(X, ldx, ncols, rec, g, cin, mc, n, L, bend, wmask)));
+    return;
+  }
   dim3 grid((unsigned)nch, (unsigned)((ncols + 255) / 256));
-  GPAR_DISPATCH_D(sdim, adjoint_local_wide<DD><<<grid, 256, 0, st>>>(X, ldx, ncols, rec, g, cin, mc, n, L, bend, wmask));
+  GPAR_DISPATCH_D(sdim, (adjoint_local_wide<DD, 256><<<grid, 256, 0, st>>>(X, ldx, ncols, rec, g, cin, mc, n, L, bend, wmask)));
 }
 
 void launch_smooth_mean(hipStream_t st, int sdim, const double* u, const double* h,

@@ -14,6 +14,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("trace")
     ap.add_argument("--top", type=int, default=20)
+    ap.add_argument("--hip", default=None, help="rocprofv3 --hip-trace CSV (run_hip_api_trace.csv): "
+                    "the host's HIP calls inside the median boundary")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.trace)))
     name_key = "Kernel_Name" if "Kernel_Name" in rows[0] else "Name"
@@ -65,6 +67,24 @@ def main():
         for e in ev:
             if start - 2_000_000 <= e[0] < y[0] + 200_000:
                 print(f"  {(e[0] - start) / 1e6:8.3f} {(e[1] - start) / 1e6:8.3f}  {e[2][:70]}")
+        if a.hip:
+            hrows = list(csv.DictReader(open(a.hip)))
+            fn = "Function" if "Function" in hrows[0] else "Name"
+            calls = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r[fn]) for r in hrows)
+            inside = [c_ for c_ in calls if start <= c_[0] < y[0]]
+            print(f"HIP API calls inside the median boundary: {len(inside)}, "
+                  f"{sum(c_[1] - c_[0] for c_ in inside) / 1e6:.3f} ms in calls; per function "
+                  "(count, total ms):")
+            agg = collections.defaultdict(lambda: [0, 0])
+            for c_ in inside:
+                agg[c_[2]][0] += 1
+                agg[c_[2]][1] += c_[1] - c_[0]
+            for k, (n_, t_) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:25]:
+                print(f"  {k:40s} {n_:5d} {t_ / 1e6:8.3f}")
+            print("timeline of the calls (start, duration in ms from the last reduction's end):")
+            for c_ in inside:
+                if c_[1] - c_[0] > 20_000:   # calls longer than 20 us
+                    print(f"  {(c_[0] - start) / 1e6:8.3f} {(c_[1] - c_[0]) / 1e6:8.3f}  {c_[2]}")
     span = ev[-1][1] - t0
     print(f"trace span {span / 1e9:.3f} s")
 
