@@ -69,7 +69,7 @@ struct gpar_ctx {
   int predict_lanes = 2;
   bool predict_fused = true;      // GPAR_PREDICT_FUSED=0: predict_rows + gemm_nt (A/B)
   bool qu_batch = true;           // GPAR_QU_BATCH=0: gpar_fit_predict's q(u) per output (A/B)
-  int dense_early = 1;            // GPAR_DENSE_EARLY=0: the whole dense tail after the round's Grams; 2: its prefix queued before the gains (A/B)
+  bool dense_early = true;        // GPAR_DENSE_EARLY=0: the whole dense tail after the round's Grams (A/B)
   bool split_head = true;         // GPAR_SPLIT_HEAD=0: the split round's first job on the whitening CUs, gains in one launch (A/B)
   std::string ws_suffix;          // appended to workspace names (a prediction lane's own buffers)
   hipEvent_t ev_grp[2] = {nullptr, nullptr};   // fit_overlapped: a group's values are in
@@ -714,10 +714,7 @@ struct SplitPipe {
 //   true beta only: q(u) factors the noise-free Cuu (cond >= 1e7), which amplifies the ~10x
 //   larger rounding of the correction form (emulated: 7e-15 vs 7e-16 of max |G|).
 static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
-                              const std::vector<Theta>& th, bool fix_beta = false,
-                              const std::function<void()>& after_head = nullptr) {
-  // after_head: work the caller queues on the Gram stream ahead of the first Gram (split path;
-  // elsewhere it runs first)
+                              const std::vector<Theta>& th, bool fix_beta = false) {
   const int np = (int)P.size();
   int64_t mpmax = 0, n = P[0].n;
   for (auto& p : P) mpmax = std::max(mpmax, p.mp);
@@ -742,7 +739,6 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   const bool shared = shares_grid(P);
   const bool pipe = fit_pipelined(c, P, fix_beta);
   const bool split_pipe = pipe && split_active(c, n, mpmax);
-  if (!split_pipe && after_head) after_head();
   const bool split_head = split_pipe && c->split_head && shared && np > 1;
   const double* logs_src = nullptr;
   std::vector<GainsOut> gains(np);
@@ -812,9 +808,6 @@ static GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     return j;
   };
   if (split_pipe) {
-    // the caller's Gram-stream work (the dense prefix) goes in after the gains launches, which
-    // start the round's critical path, and ahead of the split streams' wait on them
-    if (after_head) after_head();
     SplitPipe sp(c, n, mpmax);
     sp.head = split_head;
     sp.start();
@@ -997,13 +990,11 @@ static void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::v
   for (const auto& p : P) mpmax = std::max(mpmax, p.mp);
   const bool early = c->dense_early && fit_pipelined(c, P) && split_active(c, P[0].n, mpmax);
   DenseOut dn{};
-  auto pre = [&]() {
+  if (early) {
     OnStream on_(c, c->s_g);
     dn = run_dense_pre(c, P, th, mpmax, false);
-  };
-  if (early && c->dense_early == 2) pre();
-  GramOut go = run_gram_stage(c, P, th, false,
-                              early && c->dense_early == 1 ? std::function<void()>(pre) : nullptr);
+  }
+  GramOut go = run_gram_stage(c, P, th);
   if (gram_out) *gram_out = go;
   if (!early) dn = run_dense_pre(c, P, th, go.ldg, false);
   run_dense_post(c, P, go, dn);
@@ -1702,7 +1693,7 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
   if (const char* e = std::getenv("GPAR_OVERLAP")) c->overlap = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_PREDICT_FUSED")) c->predict_fused = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_QU_BATCH")) c->qu_batch = std::atoi(e) != 0;
-  if (const char* e = std::getenv("GPAR_DENSE_EARLY")) c->dense_early = std::atoi(e);
+  if (const char* e = std::getenv("GPAR_DENSE_EARLY")) c->dense_early = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_SPLIT_HEAD")) c->split_head = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_PREDICT_LANES")) c->predict_lanes = std::atoi(e) > 1 ? 2 : 1;
   // A/B knobs: GPAR_SPLIT_CUS overrides the default CU split, GPAR_SPLIT_DGW=0 keeps the DG

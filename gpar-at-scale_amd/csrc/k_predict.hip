@@ -280,6 +280,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
 // phase G's later steps (56 % of the dense MFMAs at M = 512; gemm_nt's 128-column skip: 62.5 %).
 // V must be zero outside its m x m block (the caller clears the Mp x Mp buffer).
 constexpr int kVRows = 64;
+#ifndef PV_PF2
+#define PV_PF2 1   // A operands staged by LDS-DMA two k-steps ahead (workgroups whose rows span <= 2 chunks)
+#endif
 #ifndef PV_ABL
 #define PV_ABL 0   // timing ablations only: 1 no A-operand loads, 2 no V slab DMA, 3 no per-step wait + barrier, 4 no MFMA
 #endif
@@ -288,6 +291,17 @@ template <int V_> struct IntC { static constexpr int value = V_; };
 // the builtin inside the kernel template's lambdas made the host pass drop the launch stubs.
 __device__ __forceinline__ void dma16(const double* src, double* lds) {
   __builtin_amdgcn_global_load_lds(src, lds, 16, 0, 0);
+}
+
+// The same by inline asm, for the prefetching path of predict_var: an LDS-DMA the compiler sees
+// makes it wait for every outstanding load (vmcnt(0)) before any later LDS read it cannot prove
+// disjoint, the prefetches included; these are invisible to it, and the kernel waits for them
+// itself.  lds: the wave-uniform LDS byte address of lane 0's 16 bytes.
+__device__ __forceinline__ void dma16a(const double* src, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
+               : "memory", "m0");
 }
 
 template <int D, int NG>
@@ -300,6 +314,13 @@ __global__ __launch_bounds__(256, 1) void predict_var(
   constexpr int T = 4 * NG, NC = 64 * NG, NS = 4 * NG;   // tiles, columns, k-steps
   __shared__ __attribute__((aligned(16))) double lb[2][NC * 16];
   __shared__ double lw[NC];   // w, zero past m
+#if PV_PF2
+  // two-step-ahead operand rings (slot s % 3): X's 16 columns of k-step s for the 64 rows (row r's
+  // 16-byte pieces at slot p ^ (r & 7)), and the chunk carries chat of the <= 2 chunks the rows
+  // lie in (chunk slot, 16 columns, kSStride)
+  __shared__ __attribute__((aligned(16))) double lx[3][kVRows * 16];
+  __shared__ __attribute__((aligned(16))) double lc[3][2 * 16 * kSStride];
+#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int frow = lane >> 4, fcol = lane & 15;
   // ---- this lane's Q row (the MFMA A operand's row fcol)
@@ -356,27 +377,155 @@ __global__ __launch_bounds__(256, 1) void predict_var(
       dma16(vsrc + (int64_t)r * 32 * ldv + s * 16, &lb[0][0] + buf * (NC * 16) + q * 128);
     }
   };
+#if PV_PF2
+  // ---- workgroups whose 64 rows lie in <= 2 chunks take the prefetching path: every operand of
+  //      step s is in LDS, moved by DMA during step s - 2, and read by inline asm (a compiler-visible
+  //      LDS read behind an outstanding LDS-DMA makes the compiler wait for every load, the
+  //      prefetch included); the loop then has no compiler-tracked loads and the only waits are the
+  //      per-step vmcnt + s_barrier below
+  const int sh = __builtin_ctz(L);
+  const int64_t i0 = (int64_t)blockIdx.x * kVRows;
+  const int64_t i1 = (i0 + kVRows < nstar ? i0 + kVRows : nstar) - 1;
+  const int64_t jlo = pos[i0] >> sh, jhi = pos[i1] >> sh;
+  const bool pf = jhi - jlo <= 1;   // workgroup-uniform
+  const double* xsrc[2];
+#pragma unroll
+  for (int q = 0; q < 2; ++q) {
+    const int rl = wave * 16 + (lane >> 3) + 8 * q;
+    const int64_t ir = i0 + rl;
+    const int64_t kr = pos[ir < nstar ? ir : nstar - 1];
+    xsrc[q] = X + kr * ldx + 2 * ((lane & 7) ^ (rl & 7));
+  }
+  // wave 0 moves the carries: lane -> chunk slot lane / 32, 16-byte piece lane % 32
+  const double* csrc = chat + ((jlo + ((lane >> 5) ? (jhi - jlo) : 0)) * mc) * kSStride + 2 * (lane & 31);
+  const uint32_t lbb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)(&lb[0][0]);
+  const uint32_t lxb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)(&lx[0][0]);
+  const uint32_t lcb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)(&lc[0][0]);
+  auto dmaXC = [&](int s) __attribute__((always_inline)) {
+    const uint32_t dx = lxb + 8u * (uint32_t)((s % 3) * (kVRows * 16) + (wv * 16) * 16);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) dma16a(xsrc[q] + s * 16, dx + 8u * (uint32_t)(q * 128));
+    if (wv == 0) dma16a(csrc + s * 16 * kSStride, lcb + 8u * (uint32_t)((s % 3) * (2 * 16 * kSStride)));
+  };
+  auto dmaBa = [&](int s, int buf) __attribute__((always_inline)) {   // dmaB by dma16a
+    const int q0 = 8 * (s >> 2);
+#pragma unroll
+    for (int r = 0; r < NC / 32; ++r) {
+      const int q = wv + 4 * r;
+      if (q < q0) continue;   // wave-uniform
+      dma16a(vsrc + (int64_t)r * 32 * ldv + s * 16, lbb + 8u * (uint32_t)(buf * (NC * 16) + q * 128));
+    }
+  };
+  // this lane's LDS byte offsets in slot 0: its 4 X operands (row 16 wave + fcol), its chunk
+  // slot's carries of columns frow + 4 ks, and w
+  const int xrl = wave * 16 + fcol;
+  const uint32_t lwb = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)(&lw[0]);
+  uint32_t xo[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int cl = ks * 4 + frow;
+    xo[ks] = lxb + 8u * (uint32_t)(xrl * 16 + ((((cl >> 1) ^ (xrl & 7)) << 1) + (cl & 1)));
+  }
+  const int cslot = (int)(j - jlo) & 1;
+  const uint32_t co = lcb + 8u * (uint32_t)(cslot * 16 * kSStride + frow * kSStride);
+  double wa[4];
+  // operands of step s into xa / ca / wa (columns s 16 + 4 ks + frow); q = 0..2 of the carries are
+  // read whatever D (kSStride = 4 keeps them in bounds)
+  auto readA = [&](int s) __attribute__((always_inline)) {
+    const uint32_t sx = (uint32_t)(s % 3) * (uint32_t)(kVRows * 16 * 8);
+    const uint32_t sc = co + (uint32_t)(s % 3) * (uint32_t)(2 * 16 * kSStride * 8);
+    const uint32_t sw = lwb + 8u * (uint32_t)(s * 16 + frow);
+    double c3[4][3];
+    asm volatile(
+        "ds_read_b64 %0, %20\n\t"
+        "ds_read_b64 %1, %21\n\t"
+        "ds_read_b64 %2, %22\n\t"
+        "ds_read_b64 %3, %23\n\t"
+        "ds_read_b64 %4, %24\n\t"
+        "ds_read_b64 %5, %24 offset:8\n\t"
+        "ds_read_b64 %6, %24 offset:16\n\t"
+        "ds_read_b64 %7, %24 offset:128\n\t"
+        "ds_read_b64 %8, %24 offset:136\n\t"
+        "ds_read_b64 %9, %24 offset:144\n\t"
+        "ds_read_b64 %10, %24 offset:256\n\t"
+        "ds_read_b64 %11, %24 offset:264\n\t"
+        "ds_read_b64 %12, %24 offset:272\n\t"
+        "ds_read_b64 %13, %24 offset:384\n\t"
+        "ds_read_b64 %14, %24 offset:392\n\t"
+        "ds_read_b64 %15, %24 offset:400\n\t"
+        "ds_read_b64 %16, %25\n\t"
+        "ds_read_b64 %17, %25 offset:32\n\t"
+        "ds_read_b64 %18, %25 offset:64\n\t"
+        "ds_read_b64 %19, %25 offset:96\n\t"
+        "s_waitcnt lgkmcnt(0)"
+        : "=v"(xa[0][0]), "=v"(xa[0][1]), "=v"(xa[0][2]), "=v"(xa[0][3]),
+          "=v"(c3[0][0]), "=v"(c3[0][1]), "=v"(c3[0][2]), "=v"(c3[1][0]), "=v"(c3[1][1]),
+          "=v"(c3[1][2]), "=v"(c3[2][0]), "=v"(c3[2][1]), "=v"(c3[2][2]), "=v"(c3[3][0]),
+          "=v"(c3[3][1]), "=v"(c3[3][2]), "=v"(wa[0]), "=v"(wa[1]), "=v"(wa[2]), "=v"(wa[3])
+        : "v"(xo[0] + sx), "v"(xo[1] + sx), "v"(xo[2] + sx), "v"(xo[3] + sx), "v"(sc), "v"(sw));
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+      for (int q = 0; q < D; ++q) ca[0][ks][q] = c3[ks][q];
+  };
+#endif
   d4 acc[T];
 #pragma unroll
   for (int t = 0; t < T; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
   for (int c = tid; c < NC; c += 256) lw[c] = c < m ? w[c] : 0.0;
+#if PV_PF2
+  if (pf) {
+    dmaBa(0, 0);
+    dmaXC(0);
+    if (NS > 1) dmaXC(1);
+  } else {
+    loadA(0, 0);
+    dmaB(0, 0);
+  }
+#else
   loadA(0, 0);
   dmaB(0, 0);
+#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // one k-step s with tiles T0 .. T - 1: fa from the inputs loaded during step s - 1; then the
   // loads of step s + 1 (A inputs; slab s + 1 -> lb[(s + 1) & 1] by DMA) under this step's
   // MFMAs; wait for them, barrier
-  auto step = [&](auto t0c, int s) __attribute__((always_inline)) {
+  auto step = [&](auto t0c, auto pfc, int s) __attribute__((always_inline)) {
     constexpr int T0 = decltype(t0c)::value;
-    makeA(s, 0);
-    if (s + 1 < NS) {
+    constexpr bool PF = decltype(pfc)::value;
+#if PV_PF2
+    bool x2 = false;
+    if constexpr (PF) {
+      // step s's operands from the rings (landed before the previous step's barrier), then the
+      // V slab of s + 1 and the operands of s + 2
+      readA(s);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) {
+        const int c = s * 16 + ks * 4 + frow;
+        double u = xa[0][ks];
+#pragma unroll
+        for (int q = 0; q < D; ++q) u = fma(hk[q], ca[0][ks][q], u);
+        const bool ok = rv && c < m;
+        fa[ks] = ok ? R * u : 0.0;
+        dot = fma(fa[ks], wa[ks], dot);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (s + 1 < NS) dmaBa(s + 1, (s + 1) & 1);
+      x2 = s + 2 < NS;
+      if (x2) dmaXC(s + 2);
+    } else
+#endif
+    {
+      makeA(s, 0);
+      if (s + 1 < NS) {
 #if PV_ABL != 1
-      loadA(s + 1, 0);
+        loadA(s + 1, 0);
 #endif
 #if PV_ABL != 2
-      dmaB(s + 1, (s + 1) & 1);
+        dmaB(s + 1, (s + 1) & 1);
 #endif
+      }
     }
     const double* B = &lb[0][0] + (s & 1) * (NC * 16);
 #pragma unroll
@@ -395,28 +544,53 @@ __global__ __launch_bounds__(256, 1) void predict_var(
         if (ks == 3 && (t & 1)) __builtin_amdgcn_sched_barrier(0);
       }
 #if PV_ABL != 3
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+#if PV_PF2
+    if constexpr (PF) {
+      // all but step s + 2's DMAs (issued last: X 2 per wave, the carries 1 more on wave 0) have
+      // landed; a bare s_barrier (__syncthreads would first wait for every load, the prefetch
+      // included); this step's LDS reads were consumed before it
+      if (x2) {
+        if (wv == 0)
+          asm volatile("s_waitcnt vmcnt(3)\n\ts_barrier" ::: "memory");
+        else
+          asm volatile("s_waitcnt vmcnt(2)\n\ts_barrier" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+    } else
+#endif
+    {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
 #endif
   };
   // phase G: k-steps 4 G .. 4 G + 3 with tiles 4 G .. T - 1.  Phase 0's first step is peeled (a
   // loop whose accumulators enter as the zero constant copied them every step)
-  auto phase = [&](auto gc) __attribute__((always_inline)) {
+  auto phase = [&](auto gc, auto pfc) __attribute__((always_inline)) {
     constexpr int G = decltype(gc)::value;
     int s = 4 * G;
-    if constexpr (G == 0) step(IntC<0>{}, s++);
+    if constexpr (G == 0) step(IntC<0>{}, pfc, s++);
 #pragma unroll 1
-    for (; s < 4 * G + 4; ++s) step(IntC<4 * G>{}, s);
+    for (; s < 4 * G + 4; ++s) step(IntC<4 * G>{}, pfc, s);
   };
   static_assert(NG >= 1 && NG <= 8, "NG in 1..8");
-  phase(IntC<0>{});
-  if constexpr (NG > 1) phase(IntC<1>{});
-  if constexpr (NG > 2) phase(IntC<2>{});
-  if constexpr (NG > 3) phase(IntC<3>{});
-  if constexpr (NG > 4) phase(IntC<4>{});
-  if constexpr (NG > 5) phase(IntC<5>{});
-  if constexpr (NG > 6) phase(IntC<6>{});
-  if constexpr (NG > 7) phase(IntC<7>{});
+  auto phases = [&](auto pfc) __attribute__((always_inline)) {
+    phase(IntC<0>{}, pfc);
+    if constexpr (NG > 1) phase(IntC<1>{}, pfc);
+    if constexpr (NG > 2) phase(IntC<2>{}, pfc);
+    if constexpr (NG > 3) phase(IntC<3>{}, pfc);
+    if constexpr (NG > 4) phase(IntC<4>{}, pfc);
+    if constexpr (NG > 5) phase(IntC<5>{}, pfc);
+    if constexpr (NG > 6) phase(IntC<6>{}, pfc);
+    if constexpr (NG > 7) phase(IntC<7>{}, pfc);
+  };
+#if PV_PF2
+  if (pf)
+    phases(std::true_type{});
+  else
+#endif
+    phases(std::false_type{});
   // ---- epilogue: row sums of squares (rows frow + 4 r of the wave's 16) over the tiles and the
   //      16 lanes of a row; the mean's dot over the 4 lanes (frow) sharing a row
   double s2[4];

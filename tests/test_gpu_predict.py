@@ -137,12 +137,16 @@ def test_fit_predict_equals_fit_then_predict(qu_noise):
         np.testing.assert_array_equal(stds[i].cpu().numpy(), s2.cpu().numpy())
 
 
-@pytest.mark.parametrize("M", [30, 140, 300, 512, 520])
-def test_predict_fused_rows_variance_equals_unfused(M):
+@pytest.mark.parametrize("M,n,n_star", [(30, 3000, 333), (140, 3000, 333), (300, 3000, 333),
+                                         (512, 3000, 333), (520, 3000, 333), (512, 2000, 6000),
+                                         (140, 2000, 6000), (300, 1500, 5000)])
+def test_predict_fused_rows_variance_equals_unfused(M, n, n_star):
     """predict_var (rows, mean and |Q_i V^T|^2 fused, m <= 512: NT = 2, 4, 6, 8 tile slots per
     wave; 520 takes the unfused path both ways) against predict_rows + gemm_nt on the same q(u):
-    the same sums in another order.  N* = 333 leaves a ragged last 64-row panel."""
-    t, V, Z, y, ts, Vs = _data(3000, 4, M, 21, 333)
+    the same sums in another order.  N* = 333 leaves a ragged last 64-row panel and spreads a
+    64-row panel over more than two chunks of the merged grid (the kernel's direct-load path);
+    N* > N keeps most panels within two chunks (its LDS-DMA prefetching path)."""
+    t, V, Z, y, ts, Vs = _data(n, 4, M, 21, n_star)
     theta = (1.3, 0.9, 0.9, 1.2, 0.3)
     ctx = G.context()
     try:
@@ -157,7 +161,7 @@ def test_predict_fused_rows_variance_equals_unfused(M):
     assert np.all(np.isfinite(m1)) and np.all(s1 > 0)
     np.testing.assert_allclose(m1, m0, rtol=1e-11, atol=1e-13 * np.abs(m0).max())
     np.testing.assert_allclose(s1, s0, rtol=1e-11, atol=1e-13 * np.abs(s0).max())
-    if M == 300:   # and the oracle directly, at an NT = 6 shape with masked high tiles
+    if M == 300 and n == 3000:   # and the oracle directly, at an NT = 6 shape with masked high tiles
         m_ref, s_ref = O.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, "matern52",
                                                            "matern32", "analytic", qu_kuu_noise=True)
         np.testing.assert_allclose(m1, m_ref, rtol=1e-7, atol=1e-9 * np.abs(m_ref).max())
