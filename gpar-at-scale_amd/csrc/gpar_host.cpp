@@ -70,6 +70,8 @@ struct gpar_ctx {
   bool predict_fused = true;      // GPAR_PREDICT_FUSED=0: predict_rows + gemm_nt (A/B)
   bool qu_batch = true;           // GPAR_QU_BATCH=0: gpar_fit_predict's q(u) per output (A/B)
   bool dense_early = true;        // GPAR_DENSE_EARLY=0: the whole dense tail after the round's Grams (A/B)
+  int overlap_max = 16;           // GPAR_OVERLAP_MAX: largest call that takes the round overlap (kOverlapMaxOutputs; A/B)
+  int overlap_b = 0;              // GPAR_OVERLAP_B: size of the overlap's second group (0: halves; A/B)
   bool split_head = true;         // GPAR_SPLIT_HEAD=0: the split round's first job on the whitening CUs, gains in one launch (A/B)
   std::string ws_suffix;          // appended to workspace names (a prediction lane's own buffers)
   hipEvent_t ev_grp[2] = {nullptr, nullptr};   // fit_overlapped: a group's values are in
@@ -1694,6 +1696,8 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
   if (const char* e = std::getenv("GPAR_PREDICT_FUSED")) c->predict_fused = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_QU_BATCH")) c->qu_batch = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_DENSE_EARLY")) c->dense_early = std::atoi(e) != 0;
+  if (const char* e = std::getenv("GPAR_OVERLAP_MAX")) c->overlap_max = std::atoi(e);
+  if (const char* e = std::getenv("GPAR_OVERLAP_B")) c->overlap_b = std::atoi(e);
   if (const char* e = std::getenv("GPAR_SPLIT_HEAD")) c->split_head = std::atoi(e) != 0;
   if (const char* e = std::getenv("GPAR_PREDICT_LANES")) c->predict_lanes = std::atoi(e) > 1 ? 2 : 1;
   // A/B knobs: GPAR_SPLIT_CUS overrides the default CU split, GPAR_SPLIT_DGW=0 keeps the DG
@@ -2067,7 +2071,14 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
   for (hipEvent_t* ev : {&c->ev_grp[0], &c->ev_grp[1], &c->ev_gn[0], &c->ev_gn[1]})
     if (!*ev) HIPCHECK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   OverlapGroup grp[2];
-  for (int i = 0; i < np; ++i) grp[i & 1].members.push_back(i);
+  // outputs dealt alternately; with c->overlap_b > 0 (A/B) group B is every k-th output instead
+  // (about overlap_b of them), group A the rest
+  if (c->overlap_b > 0 && c->overlap_b < np) {
+    const int k = std::max(2, np / c->overlap_b);
+    for (int i = 0; i < np; ++i) grp[(i % k == k - 1) ? 1 : 0].members.push_back(i);
+  } else {
+    for (int i = 0; i < np; ++i) grp[i & 1].members.push_back(i);
+  }
   for (int g = 0; g < 2; ++g) {
     OverlapGroup& G = grp[g];
     G.id = g;
@@ -2263,7 +2274,7 @@ static void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const dou
   };
   int64_t mpmax = 0;
   for (auto& p : P) mpmax = std::max(mpmax, p.mp);
-  if (ctx->overlap && nprob >= 4 && nprob <= kOverlapMaxOutputs && fit_pipelined(ctx, P) &&
+  if (ctx->overlap && nprob >= 4 && nprob <= ctx->overlap_max && fit_pipelined(ctx, P) &&
       split_active(ctx, P[0].n, mpmax))
     fit_overlapped(ctx, P, nm, accept);
   std::vector<double> vals;

@@ -137,10 +137,11 @@ def test_fit_predict_equals_fit_then_predict(qu_noise):
         np.testing.assert_array_equal(stds[i].cpu().numpy(), s2.cpu().numpy())
 
 
-@pytest.mark.parametrize("M,n,n_star", [(30, 3000, 333), (140, 3000, 333), (300, 3000, 333),
-                                         (512, 3000, 333), (520, 3000, 333), (512, 2000, 6000),
-                                         (140, 2000, 6000), (300, 1500, 5000)])
-def test_predict_fused_rows_variance_equals_unfused(M, n, n_star):
+@pytest.mark.parametrize("M,n,n_star,tk", [(30, 3000, 333, "matern32"), (140, 3000, 333, "matern32"),
+                                            (300, 3000, 333, "matern32"), (512, 3000, 333, "matern32"),
+                                            (520, 3000, 333, "matern32"), (512, 2000, 6000, "matern32"),
+                                            (140, 2000, 6000, "matern12"), (300, 1500, 5000, "matern52")])
+def test_predict_fused_rows_variance_equals_unfused(M, n, n_star, tk):
     """predict_var (rows, mean and |Q_i V^T|^2 fused, m <= 512: NT = 2, 4, 6, 8 tile slots per
     wave; 520 takes the unfused path both ways) against predict_rows + gemm_nt on the same q(u):
     the same sums in another order.  N* = 333 leaves a ragged last 64-row panel and spreads a
@@ -151,10 +152,10 @@ def test_predict_fused_rows_variance_equals_unfused(M, n, n_star):
     ctx = G.context()
     try:
         ctx.set_predict_fused(False)
-        m0, s0 = G.predict_scaled(V, Z, t, y, theta, ts, Vs, "matern52", "matern32", mode="analytic",
+        m0, s0 = G.predict_scaled(V, Z, t, y, theta, ts, Vs, "matern52", tk, mode="analytic",
                                   qu_kuu_noise=True)
         ctx.set_predict_fused(True)
-        m1, s1 = G.predict_scaled(V, Z, t, y, theta, ts, Vs, "matern52", "matern32", mode="analytic",
+        m1, s1 = G.predict_scaled(V, Z, t, y, theta, ts, Vs, "matern52", tk, mode="analytic",
                                   qu_kuu_noise=True)
     finally:
         ctx.set_predict_fused(True)
@@ -163,6 +164,6 @@ def test_predict_fused_rows_variance_equals_unfused(M, n, n_star):
     np.testing.assert_allclose(s1, s0, rtol=1e-11, atol=1e-13 * np.abs(s0).max())
     if M == 300 and n == 3000:   # and the oracle directly, at an NT = 6 shape with masked high tiles
         m_ref, s_ref = O.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, "matern52",
-                                                           "matern32", "analytic", qu_kuu_noise=True)
+                                                           tk, "analytic", qu_kuu_noise=True)
         np.testing.assert_allclose(m1, m_ref, rtol=1e-7, atol=1e-9 * np.abs(m_ref).max())
         np.testing.assert_allclose(s1, s_ref, rtol=1e-7, atol=1e-9 * np.abs(s_ref).max())
