@@ -40,6 +40,7 @@ struct gpar_ctx {
   hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr, s_d = nullptr;
   hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
   hipEvent_t ev_g0 = nullptr, ev_gr = nullptr;   // split round start: gains uploaded / the rest's gains done
+  hipEvent_t ev_dn = nullptr;                    // split round start: the dense prefix follows the context stream
   // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
   // the caller's stream, e.g. the copies that produce its device inputs
   bool has_input_stream = false;
@@ -993,6 +994,10 @@ static void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::v
   const bool early = c->dense_early && fit_pipelined(c, P) && split_active(c, P[0].n, mpmax);
   DenseOut dn{};
   if (early) {
+    // the Gram stream first follows everything queued on the context stream (host inputs' uploads,
+    // the pseudo-input centres, the distance cache), then factors Kuu beside the round's gains
+    HIPCHECK(hipEventRecord(c->ev_dn, c->stream));
+    HIPCHECK(hipStreamWaitEvent(c->s_g, c->ev_dn, 0));
     OnStream on_(c, c->s_g);
     dn = run_dense_pre(c, P, th, mpmax, false);
   }
@@ -1657,7 +1662,8 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
          hipEventCreateWithFlags(&c->ev_gd[1], hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_sp, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_g0, hipEventDisableTiming) != hipSuccess ||
-         hipEventCreateWithFlags(&c->ev_gr, hipEventDisableTiming) != hipSuccess))
+         hipEventCreateWithFlags(&c->ev_gr, hipEventDisableTiming) != hipSuccess ||
+         hipEventCreateWithFlags(&c->ev_dn, hipEventDisableTiming) != hipSuccess))
       return GPAR_ERR_HIP;
     c->split_mask_w = w;
   }
@@ -1732,7 +1738,7 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
         (void)hipStreamDestroy(st);
       }
     for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_grp[0], ctx->ev_grp[1],
-                          ctx->ev_gn[0], ctx->ev_gn[1], ctx->ev_g0, ctx->ev_gr})
+                          ctx->ev_gn[0], ctx->ev_gn[1], ctx->ev_g0, ctx->ev_gr, ctx->ev_dn})
       if (ev) (void)hipEventDestroy(ev);
     for (auto& s : ctx->stage)
       if (s.host) (void)hipHostFree(s.host);
