@@ -1950,10 +1950,10 @@ static int64_t fit_ws_estimate(const gpar_ctx* c, const std::vector<DevProblem>&
 
 // The same for the prediction of a gpar_fit_predict call (predict_impl, merged grid of n + n_star).
 static int64_t predict_ws_estimate(int64_t n, int64_t n_star, int64_t mp, int64_t d, int mode,
-                                   int samples) {
+                                   int samples, bool fused) {
   const int64_t nt = n + n_star, nch = (nt + kChunk - 1) / kChunk;
   int64_t doubles = nt * (mp + 64)                 // whitened Cf*u + y*
-                    + n_star * (mp + 8 + d)        // Q rows, mean / std, sorted test inputs
+                    + n_star * ((fused ? 0 : mp) + 8 + d)   // Q rows (not with predict_var), mean / std, sorted test inputs
                     + nt * (20 + 8 + d)            // gains records, grid, merged inputs
                     + 4 * nch * (mp + 1) * 4       // carries
                     + 8 * mp * mp;                 // q(u) dense
@@ -2376,7 +2376,10 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
   // the predictions' workspace (named buffers, reused across the outputs: the largest counts)
   int64_t pred_bytes = 0;
   for (const auto& p : P)
-    pred_bytes = std::max(pred_bytes, predict_ws_estimate(p.n, n_star, p.mp, p.d, mode, samples));
+    pred_bytes = std::max(pred_bytes, predict_ws_estimate(p.n, n_star, p.mp, p.d, mode, samples,
+                                                          mode == GPAR_PREDICT_ANALYTIC &&
+                                                              ctx->predict_fused &&
+                                                              predict_var_tiles(p.mp) > 0));
   fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, &keep, (lanes ? 2 : 1) * pred_bytes);
   struct LaneScope {   // a lane's stream and workspace names; restored on any exit
     gpar_ctx* c;
