@@ -1,0 +1,483 @@
+// host_fit.cpp -- the batched Nelder-Mead fit: distance cache, round-overlapping schedule,
+// gpar_fit, and the host-only ask/tell optimiser.
+#include "host.hpp"
+
+namespace gpar {
+
+// Batched Nelder-Mead over the outputs: one objective round serves every pending point.
+// keep (optional): per output, the Gram of its lowest-value evaluation (ld = mp) in context
+// workspace, and whether that evaluation is the returned minimiser (bitwise).
+
+// Distance cache: the squared distances |v_k - z_c|^2 do not depend on theta, so for the
+// outputs it holds they are computed once per fit (dist2, k_dist.hip) and every evaluation's
+// whitening reads them (whiten_kfu_d2, memory-bound) instead of rebuilding the distance
+// contraction on MFMA inside the fused kernel, whose cost grows with D.  Measured at N = 1e6,
+// M = 512: fused 1.62 / 2.13 / 2.6 / 3.2 ms at D = 16 / 32 / 48 / 63, cached 1.75 ms at any D;
+// so outputs with D >= kDistCacheMinD are cached, widest first, while the budget lasts
+// (gpar_ctx_set_dist_cache; default: the free HBM less a reserve).  n x mp doubles each.
+constexpr int64_t kDistCacheMinD = 17;
+// With the CU split the whitening runs on a quarter of the chip, where the fused kernel is
+// compute-bound (D <= 16: 5.05 ms per launch on 64 CUs against 3.62 ms for the cached one), so a
+// batched fit over long series caches every output the budget holds (the narrowest fit last; at
+// the north config all 63: 258 GB, 10 GB of the 309 GB left free after the predictions).  Short
+// series (N < 2^16) keep the D >= 17 rule: there the fused kernel is latency-bound either way, and
+// the small-D fits then stay on the arithmetic a single-output q(u) recomputes (gpar_fit_predict's
+// reused Gram stays bit-identical to gpar_predict's).
+constexpr int64_t kDistCacheMinDSplit = 1;
+constexpr int64_t kDistCacheSplitMinN = (int64_t)1 << 16;
+
+// Device bytes a batched fit's evaluations allocate besides the cache (run_gram_stage, run_dense,
+// the kept Grams): the cache's auto budget leaves room for them.
+int64_t fit_ws_estimate(const gpar_ctx* c, const std::vector<DevProblem>& P) {
+  const int64_t np = (int64_t)P.size(), n = P[0].n, nch = (n + kChunk - 1) / kChunk;
+  int64_t mpmax = 0, rs = 4;
+  for (auto& p : P) {
+    mpmax = std::max(mpmax, p.mp);
+    rs = std::max<int64_t>(rs, rec_size(p.sdim));
+  }
+  const int64_t nbuf = (fit_pipelined(c, P) || c->lanes > 1) ? 2 : 1;
+  const GramPlan pl = gram_plan(n, mpmax, false, 256, 256);
+  const int64_t doubles = nbuf * ((n + 16) * mpmax + n + 3 * nch * (mpmax + 1) * 4)   // beta, carries
+                          + np * n * (rs + 5)                 // gains records, fix-up rows, alpha
+                          + 7 * np * mpmax * mpmax            // G, dense tail, kept Grams
+                          + 2 * (pl.part_doubles + pl.rpart_doubles);
+  return doubles * (int64_t)sizeof(double);
+}
+
+// The same for the prediction of a gpar_fit_predict call (predict_impl, merged grid of n + n_star).
+int64_t predict_ws_estimate(int64_t n, int64_t n_star, int64_t mp, int64_t d, int mode,
+                                   int samples, bool fused) {
+  const int64_t nt = n + n_star, nch = (nt + kChunk - 1) / kChunk;
+  int64_t doubles = nt * (mp + 64)                 // whitened Cf*u + y*
+                    + n_star * ((fused ? 0 : mp) + 8 + d)   // Q rows (not with predict_var), mean / std, sorted test inputs
+                    + nt * (20 + 8 + d)            // gains records, grid, merged inputs
+                    + 4 * nch * (mp + 1) * 4       // carries
+                    + 8 * mp * mp;                 // q(u) dense
+  if (mode == GPAR_PREDICT_MC) doubles += n_star * mp + (int64_t)samples * mp + 2 * n_star * ((samples + 127) / 128);
+  if (mode == GPAR_PREDICT_PATH)   // Cf*u, fx, the data columns, their whitening and the samples
+    doubles += nt * mp + (int64_t)samples * (4 * nt + 2 * mp) + 6 * nch * samples * kSStride;
+  return doubles * (int64_t)sizeof(double);
+}
+
+// later_bytes: what the call allocates after the cache (fit_ws_estimate + predict_ws_estimate).
+std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<DevProblem>& P,
+                                                 int64_t later_bytes) {
+  std::vector<DevProblem> Q = P;
+  c->cache_outputs = 0;
+  if (c->dist_cache_bytes == 0) return Q;
+  // explicit budget: total cache bytes.  auto: new allocations take at most the free HBM less a
+  // reserve -- 1 % of the part plus the workspace the call still has to allocate (what the
+  // context already holds under other names is reused) -- and cache buffers the context already
+  // holds (gpar_ctx_set_dist_cache_keep) are reused at no cost.  Either way an allocation that
+  // fails stops the cache there, and a later workspace allocation that finds no memory evicts
+  // cache slots (ws_bytes), so the cache never turns into an out-of-memory failure.
+  int64_t budget = c->dist_cache_bytes;
+  int64_t fresh = INT64_MAX;
+  if (budget < 0) {
+    size_t fr = 0, tot = 0;
+    HIPCHECK(hipMemGetInfo(&fr, &tot));
+    int64_t held_other = 0;
+    for (auto& kv : c->bufs)
+      if (!is_cache_buf(kv.first)) held_other += (int64_t)kv.second.bytes;
+    const int64_t need = std::max<int64_t>(0, later_bytes - held_other);
+    const int64_t reserve = std::max<int64_t>((int64_t)1 << 30, (int64_t)(tot / 100)) + need;
+    fresh = std::max<int64_t>(0, (int64_t)fr - reserve);
+    budget = INT64_MAX;
+  }
+  std::vector<int> order(P.size());
+  for (size_t i = 0; i < P.size(); ++i) order[i] = (int)i;
+  std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return P[a].d > P[b].d; });
+  int64_t mpmax = 0;
+  for (auto& p : P) mpmax = std::max(mpmax, p.mp);
+  // every output (D >= 1) only where the whitening runs on the CU split's quarter of the chip,
+  // i.e. the pipelined split schedule actually runs (fit_pipelined && split_active)
+  const int64_t min_d = (fit_pipelined(c, P) && split_active(c, P[0].n, mpmax) &&
+                         P[0].n >= kDistCacheSplitMinN) ? kDistCacheMinDSplit : kDistCacheMinD;
+  int slot = 0;
+  for (int i : order) {
+    const DevProblem& p = P[i];
+    if (p.d < min_d) continue;
+    const int64_t bytes = p.n * p.mp * (int64_t)sizeof(double);
+    const std::string name = "distcache" + std::to_string(slot);
+    const auto it = c->bufs.find(name);
+    const int64_t held = it != c->bufs.end() ? (int64_t)it->second.bytes : 0;
+    const int64_t need = held >= bytes ? 0 : bytes - held;   // ws() frees the smaller one first
+    if (bytes > budget || need > fresh) continue;
+    double* d2 = nullptr;
+    try {
+      d2 = reinterpret_cast<double*>(ws_bytes(c, name, (size_t)bytes));
+    } catch (const Error& e) {
+      if (e.code != GPAR_ERR_OOM) throw;
+      c->bufs.erase(name);   // another tenant took the memory: cache what fits so far
+      break;
+    }
+    budget -= bytes;
+    fresh -= need;
+    if ((int)c->cache_valid.size() <= slot) c->cache_valid.resize(slot + 1, 0);
+    c->cache_valid[slot] = 1;
+    launch_dist2(c->stream, p.ok, p.v, p.ldv, p.n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, d2, p.mp,
+                 /*take_sqrt=*/p.ok != GPAR_EQ);
+    check_launch("dist2 (cache)");
+    Q[i].d2 = d2;
+    Q[i].d2_is_r = p.ok != GPAR_EQ;
+    Q[i].cache_slot = slot;
+    ++slot;
+  }
+  c->cache_outputs = slot;
+  return Q;
+}
+
+// ---------------------------------------------------------------- round-overlapping batched fit
+// fit_impl's batched Nelder-Mead evaluates one simplex point per output per round.  Round by
+// round (eval_dtc), every round drains the chip: its first whitening runs alone, its last Gram
+// runs alone, then the next round's gains, the dense tail and a host sync.  On the CU-split
+// schedule with >= 4 outputs, fit_overlapped deals the outputs into two groups that take turns:
+// while the host waits for group A's values (A's dense tail runs on the whitening CUs, which have
+// slack beside the Gram) and steps A's simplices, group B's whitenings and Grams keep both sides of the
+// split busy, and A's next round (gains on the whitening CUs, then its jobs) is queued behind
+// them -- one drain per fit instead of one per round.  Every output evaluates exactly the points
+// its own simplex asks for, in the same order, with the same kernels and per-problem arithmetic
+// (batched gains and dense-tail launches compute each problem independently), so the fit equals
+// the round-by-round one bit for bit.  Uploads go through pinned arenas (gpar_ctx::staging): a
+// pageable copy queued behind running work could block the host and stall the pipeline.
+struct OverlapGroup {
+  int id = 0;
+  std::vector<int> members;        // output indices dealt to this group
+  std::vector<int> act;            // this round's active members
+  std::vector<Theta> th;           // their hyperparameters this round
+  std::vector<DevProblem> sub;     // their problems (stable while their jobs are queued)
+  GramOut go{};                    // one G / r / alpha^2 / log S slot per member
+  double *alpha_all = nullptr, *asend_all = nullptr, *dout = nullptr;
+  double* hout = nullptr;          // pinned: -dtc values of the round
+  int* hstat = nullptr;            // pinned: Cholesky status flags (2 per output)
+  size_t res_bytes = 0;            // the arena's result prefix
+  bool in_flight = false;
+};
+
+// Round overlap pays where the drain after each Nelder-Mead round is a large part of the round:
+// one 8-way shard of the north job (8 outputs per call) 2.70 -> 2.45 s per step; with all 63
+// north outputs in one call the round is long and the concurrent gains / dense tails on the
+// whitening CUs slow every Gram instead (5.13 -> 5.46 ms; 18.45 vs 18.75 s per job,
+// profiles/bench_r03d_*.json).
+constexpr int kOverlapMaxOutputs = 16;
+
+using AcceptFn = std::function<void(int, double, const double*, const double*, int64_t)>;
+
+static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
+                           std::vector<NelderMead>& nm, const AcceptFn& accept) {
+  const int np = (int)P.size();
+  const int64_t n = P[0].n, nch = P[0].nch, npart = vec_fix_blocks(n);
+  int64_t mpmax = 0;
+  for (auto& p : P) mpmax = std::max(mpmax, p.mp);
+  const size_t sq = (size_t)mpmax * mpmax;
+  for (hipEvent_t* ev : {&c->ev_grp[0], &c->ev_grp[1], &c->ev_gn[0], &c->ev_gn[1]})
+    if (!*ev) HIPCHECK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+  OverlapGroup grp[2];
+  // outputs dealt alternately; with c->overlap_b > 0 (A/B) group B is every k-th output instead
+  // (about overlap_b of them), group A the rest
+  if (c->overlap_b > 0 && c->overlap_b < np) {
+    const int k = std::max(2, np / c->overlap_b);
+    for (int i = 0; i < np; ++i) grp[(i % k == k - 1) ? 1 : 0].members.push_back(i);
+  } else {
+    for (int i = 0; i < np; ++i) grp[i & 1].members.push_back(i);
+  }
+  for (int g = 0; g < 2; ++g) {
+    OverlapGroup& G = grp[g];
+    G.id = g;
+    const size_t cap = G.members.size();
+    const std::string sfx = g ? "B" : "A";
+    G.go.ldg = mpmax;
+    G.go.npart = npart;
+    G.go.G = ws<double>(c, "ovG" + sfx, cap * sq);
+    G.go.r = ws<double>(c, "ovr" + sfx, cap * mpmax);
+    G.go.a2part = ws<double>(c, "ova2" + sfx, cap * npart);
+    G.go.logs = ws<double>(c, "ovlogs" + sfx, cap * nch);
+    G.alpha_all = ws<double>(c, "ovalpha" + sfx, cap * n);
+    G.asend_all = ws<double>(c, "ovasend" + sfx, cap * nch * kSStride);
+    G.dout = ws<double>(c, "ovout" + sfx, cap);
+    gpar_ctx::Staging& s = c->stage[g];
+    const size_t vbytes = (cap * sizeof(double) + 255) & ~(size_t)255;
+    G.res_bytes = vbytes + ((2 * cap * sizeof(int) + 255) & ~(size_t)255);
+    const size_t need = G.res_bytes + ((size_t)1 << 20) + cap * 4096;
+    if (s.cap < need) {
+      if (s.host) HIPCHECK(hipHostFree(s.host));
+      s.host = nullptr;
+      s.cap = 0;
+      HIPCHECK(hipHostMalloc((void**)&s.host, need, hipHostMallocDefault));
+      s.cap = need;
+    }
+    G.hout = reinterpret_cast<double*>(s.host);
+    G.hstat = reinterpret_cast<int*>(s.host + vbytes);
+  }
+  reserve_gram_parts(c, P, 1);
+  struct StagingScope {   // h2d through group g's pinned arena inside the scope
+    gpar_ctx* c;
+    StagingScope(gpar_ctx* c_, int g) : c(c_) { c->staging = &c->stage[g]; }
+    ~StagingScope() { c->staging = nullptr; }
+  };
+
+  SplitPipe sp(c, n, mpmax);
+  // a group's dense tail + finish on the context stream as soon as its round's last Gram is
+  // issued; its values land in pinned memory, ev_grp[g] marks them
+  // (on the whitening CUs: beside the Gram on the whole chip it slowed every Gram by ~5 %)
+  auto issue_dense = [&](OverlapGroup& G, int64_t job) {
+    OnStream on_(c, c->s_d);
+    StagingScope st_(c, G.id);
+    HIPCHECK(hipStreamWaitEvent(c->s_d, c->ev_gd[job & 1], 0));
+    const int na = (int)G.act.size();
+    DenseOut dn = run_dense(c, G.sub, G.th, G.go, false);
+    std::vector<Finish2JobHost> fj(na);
+    for (int a = 0; a < na; ++a) fj[a] = finish_job(dn, G.go, G.sub[a], a, nch, G.dout + a, nullptr);
+    auto* dfj = ws<Finish2JobHost>(c, "finishjobs", np);
+    h2d(c, dfj, fj.data(), na);
+    launch_finish2(c->s_d, dfj, na, dn.ld, dn.nb);
+    check_launch("finish");
+    HIPCHECK(hipMemcpyAsync(G.hout, G.dout, na * sizeof(double), hipMemcpyDeviceToHost, c->s_d));
+    HIPCHECK(hipMemcpyAsync(G.hstat, dn.status, 2 * na * sizeof(int), hipMemcpyDeviceToHost, c->s_d));
+    HIPCHECK(hipEventRecord(c->ev_grp[G.id], c->s_d));
+  };
+  sp.on_gram = [&](const StageJob& j, int64_t job) {
+    if (j.last) issue_dense(grp[j.group], job);
+  };
+  // ask every active member for its next point; queue the group's gains and its jobs
+  auto begin_round = [&](OverlapGroup& G) {
+    G.act.clear();
+    for (int i : G.members)
+      if (!nm[i].done()) G.act.push_back(i);
+    if (G.act.empty()) return;
+    const int na = (int)G.act.size();
+    G.th.clear();
+    G.sub.clear();
+    std::vector<ChainParamsHost> cps(na);
+    std::vector<const double*> ys(na);
+    for (int a = 0; a < na; ++a) {
+      const int i = G.act[a];
+      const auto& x = nm[i].ask();
+      G.th.push_back({unpack(x[0]), unpack(x[1]), unpack(x[2]), unpack(x[3]), unpack(x[4])});
+      G.sub.push_back(P[i]);
+      const Theta& t = G.th.back();
+      cps[a] = {1.0 / t.l_t, t.l_t, t.sv_t * t.sv_t, t.sigma * t.sigma};
+      ys[a] = P[i].y;
+    }
+    c->stage[G.id].used = G.res_bytes;   // the previous round's uploads have been consumed
+    // the gains run on the whitening CUs beside the other group's whitenings (s_d), not in the
+    // whitening stream's order: queued there they delayed the next whitening, and with it the
+    // DG share that ends the previous Gram
+    GainsOut gn;
+    {
+      OnStream on_(c, c->s_d);
+      StagingScope st_(c, G.id);
+      gn = run_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, G.id ? "fitB" : "fitA", &ys,
+                     G.alpha_all, G.asend_all);
+      HIPCHECK(hipMemcpyAsync(G.go.logs, gn.logs, (size_t)na * nch * sizeof(double),
+                              hipMemcpyDeviceToDevice, c->s_d));
+      HIPCHECK(hipEventRecord(c->ev_gn[G.id], c->s_d));
+      HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gn[G.id], 0));
+    }
+    {   // narrower outputs: their G / r slot padding must read as zero in the dense tail
+      OnStream on_(c, c->s_g);
+      for (int a = 0; a < na; ++a)
+        if (G.sub[a].mp != mpmax) {
+          HIPCHECK(hipMemsetAsync(G.go.G + a * sq, 0, sq * sizeof(double), c->s_g));
+          HIPCHECK(hipMemsetAsync(G.go.r + (size_t)a * mpmax, 0, mpmax * sizeof(double), c->s_g));
+        }
+    }
+    for (int a = 0; a < na; ++a) {
+      StageJob j;
+      j.p = &G.sub[a];
+      j.th = &G.th[a];
+      j.gi = gn;
+      j.gi.rec = gn.rec + (size_t)a * gn.recstride;
+      j.gi.g = gn.g + (size_t)a * gn.gstride;
+      j.gi.phi = gn.phi + (size_t)a * gn.phistride;
+      j.gi.logs = gn.logs + (size_t)a * nch;
+      j.alpha = G.alpha_all + (size_t)a * n;
+      j.asend = G.asend_all + (size_t)a * nch * kSStride;
+      j.G = G.go.G + a * sq;
+      j.r = G.go.r + (size_t)a * mpmax;
+      j.a2part = G.go.a2part + (size_t)a * npart;
+      j.ldg = mpmax;
+      j.group = G.id;
+      j.last = a == na - 1;
+      sp.push(j);
+    }
+    G.in_flight = true;
+  };
+  // wait for a group's values and hand them to its simplices (Gram copies of kept points go to
+  // the Gram stream, ahead of the group's next Grams)
+  auto finish_round = [&](OverlapGroup& G) {
+    if (sp.has_pending && sp.pending.group == G.id) sp.flush();   // its last Gram, then its tail
+    HIPCHECK(hipEventSynchronize(c->ev_grp[G.id]));
+    OnStream on_(c, c->s_g);
+    for (size_t a = 0; a < G.act.size(); ++a) {
+      double f = -G.hout[a];
+      if (G.hstat[2 * a] || G.hstat[2 * a + 1] || !std::isfinite(f)) f = INFINITY;
+      accept(G.act[a], f, G.go.G + a * sq, G.go.r + a * mpmax, mpmax);
+    }
+    G.in_flight = false;
+  };
+  sp.start();
+  HIPCHECK(hipStreamWaitEvent(c->s_d, c->ev_sp, 0));   // the inputs / distance cache on main
+  begin_round(grp[0]);
+  begin_round(grp[1]);
+  for (int g = 0; grp[0].in_flight || grp[1].in_flight; g ^= 1) {
+    if (!grp[g].in_flight) continue;
+    finish_round(grp[g]);
+    begin_round(grp[g]);
+  }
+  sp.flush();
+  sp.join(c->main);
+}
+
+void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* log_theta0,
+                     const gpar_fit_options& o, double* theta_out, double* nlml_out,
+                     int32_t* evals_out, FitKeep* keep, int64_t later_bytes) {
+  // the cache lives for this fit call only, unless the caller keeps it (gpar_ctx_set_dist_cache_keep)
+  struct CacheRelease {
+    gpar_ctx* c;
+    ~CacheRelease() {
+      if (c->dist_cache_keep) return;
+      try {
+        release_dist_cache(c);
+      } catch (...) {
+      }
+    }
+  } release_{ctx};
+  const std::vector<DevProblem> P =
+      attach_dist_cache(ctx, P0, fit_ws_estimate(ctx, P0) + later_bytes);
+  const int nprob = (int)P.size();
+  std::vector<NelderMead> nm;
+  nm.reserve(nprob);
+  for (int i = 0; i < nprob; ++i)
+    nm.emplace_back(std::vector<double>(log_theta0 + 5 * i, log_theta0 + 5 * i + 5), o.max_evals,
+                    o.max_iterations, o.g_tol, o.time_limit);
+  std::vector<double> best_f(nprob, INFINITY);
+  std::vector<std::vector<double>> best_x(nprob);
+  std::vector<double*> kG(nprob, nullptr), kr(nprob, nullptr);
+  if (keep) {
+    for (int i = 0; i < nprob; ++i) {
+      const size_t mp = (size_t)P[i].mp;
+      kG[i] = ws<double>(ctx, "fitkeep_G" + std::to_string(i), mp * mp);
+      kr[i] = ws<double>(ctx, "fitkeep_r" + std::to_string(i), mp);
+    }
+  }
+  // one evaluated point of output i: keep its Gram if it is the best so far (on c->stream, before
+  // the slot is reused), then tell the simplex
+  const AcceptFn accept = [&](int i, double f, const double* Gs, const double* rs, int64_t ldg) {
+    if (keep && f < best_f[i]) {
+      best_f[i] = f;
+      best_x[i] = nm[i].ask();
+      const size_t mp = (size_t)P[i].mp;
+      HIPCHECK(hipMemcpy2DAsync(kG[i], mp * sizeof(double), Gs, ldg * sizeof(double),
+                                mp * sizeof(double), mp, hipMemcpyDeviceToDevice, ctx->stream));
+      HIPCHECK(hipMemcpyAsync(kr[i], rs, mp * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+    }
+    nm[i].tell(f);
+  };
+  int64_t mpmax = 0;
+  for (auto& p : P) mpmax = std::max(mpmax, p.mp);
+  if (ctx->overlap && nprob >= 4 && nprob <= ctx->overlap_max && fit_pipelined(ctx, P) &&
+      split_active(ctx, P[0].n, mpmax))
+    fit_overlapped(ctx, P, nm, accept);
+  std::vector<double> vals;
+  while (true) {
+    std::vector<int> act;
+    for (int i = 0; i < nprob; ++i)
+      if (!nm[i].done()) act.push_back(i);
+    if (act.empty()) break;
+    std::vector<DevProblem> sub;
+    std::vector<Theta> th;
+    for (int i : act) {
+      sub.push_back(P[i]);
+      const auto& x = nm[i].ask();
+      th.push_back({unpack(x[0]), unpack(x[1]), unpack(x[2]), unpack(x[3]), unpack(x[4])});
+    }
+    vals.assign(act.size(), 0.0);
+    std::vector<int> st;
+    GramOut go{};
+    eval_dtc(ctx, sub, th, vals.data(), st, keep ? &go : nullptr);
+    for (size_t a = 0; a < act.size(); ++a) {
+      double f = -vals[a];
+      if (st[a] || !std::isfinite(f)) f = INFINITY;  // PosDefException -> reject the point
+      accept(act[a], f, keep ? go.G + a * go.ldg * go.ldg : nullptr,
+             keep ? go.r + a * go.ldg : nullptr, go.ldg);
+    }
+  }
+  for (int i = 0; i < nprob; ++i) {
+    const auto& x = nm[i].x_min();
+    for (int j = 0; j < 5; ++j) theta_out[5 * i + j] = unpack(x[j]);
+    if (nlml_out) nlml_out[i] = nm[i].f_min();
+    if (evals_out) evals_out[i] = nm[i].evals();
+  }
+  if (keep) {
+    keep->gram.assign(nprob, GramCache{});
+    keep->valid.assign(nprob, 0);
+    for (int i = 0; i < nprob; ++i) {
+      keep->valid[i] = !best_x[i].empty() && best_x[i] == nm[i].x_min();
+      if (keep->valid[i]) keep->gram[i] = GramCache{kG[i], kr[i]};
+    }
+  }
+}
+}  // namespace gpar
+using namespace gpar;
+extern "C" {
+
+int32_t gpar_fit(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                 const double* log_theta0, const gpar_fit_options* opts, double* theta_out,
+                 double* nlml_out, int32_t* evals_out) {
+  API_BEGIN(ctx)
+  ARGCHECK(probs && nprob >= 1 && log_theta0 && theta_out, "null argument");
+  check_batch(probs, nprob);
+  gpar_fit_options o{0, 1000, 1e-8, 0.0};
+  if (opts) o = *opts;
+  std::vector<DevProblem> P;
+  for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
+  fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, nullptr);
+  API_END(ctx)
+}
+
+// ---------------------------------------------------------------- host-only Nelder-Mead
+struct gpar_nm {
+  gpar::NelderMead nm;
+};
+
+int32_t gpar_nm_create(int32_t n, const double* x0, const gpar_fit_options* opts, gpar_nm** out) {
+  if (!out || !x0 || n < 1) return GPAR_ERR_ARG;
+  gpar_fit_options o{0, 1000, 1e-8, 0.0};
+  if (opts) o = *opts;
+  *out = new gpar_nm{gpar::NelderMead(std::vector<double>(x0, x0 + n), o.max_evals,
+                                      o.max_iterations, o.g_tol, o.time_limit)};
+  return GPAR_OK;
+}
+
+int32_t gpar_nm_destroy(gpar_nm* nm) {
+  delete nm;
+  return GPAR_OK;
+}
+
+int32_t gpar_nm_ask(gpar_nm* nm, double* x) {
+  if (!nm || !x) return -1;
+  if (nm->nm.done()) return 0;
+  const auto& p = nm->nm.ask();
+  std::copy(p.begin(), p.end(), x);
+  return 1;
+}
+
+int32_t gpar_nm_tell(gpar_nm* nm, double f) {
+  if (!nm || nm->nm.done()) return GPAR_ERR_STATE;
+  nm->nm.tell(f);
+  return GPAR_OK;
+}
+
+int32_t gpar_nm_result(const gpar_nm* nm, double* x_min, double* f_min, int32_t* evals,
+                       int32_t* iterations) {
+  if (!nm) return GPAR_ERR_STATE;
+  const auto& x = nm->nm.x_min();
+  if (x_min) std::copy(x.begin(), x.end(), x_min);
+  if (f_min) *f_min = nm->nm.f_min();
+  if (evals) *evals = nm->nm.evals();
+  if (iterations) *iterations = nm->nm.iterations();
+  return GPAR_OK;
+}
+
+}  // extern "C"

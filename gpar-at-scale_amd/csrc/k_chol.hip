@@ -108,10 +108,7 @@ __global__ __launch_bounds__(256) void potrf_diag(const CholJob2* __restrict__ j
   if (cls == 0) S[i * kSD] = rv[0];   // column 0 is final from the start
   __syncthreads();
   bool bad = false;
-#ifndef POTRF_ABL
-#define POTRF_ABL 0   // timing ablations only: 1 no elimination loop, 2 no inverse loop
-#endif
-  for (int k = 0; k < (POTRF_ABL == 1 ? 0 : kNB - 1); ++k) {
+  for (int k = 0; k < kNB - 1; ++k) {
     double piv = S[k * kSD + k];
     if (!(piv > 0.0)) { bad = true; piv = 1.0; }
     const double c = (i > k) ? S[i * kSD + k] * rcp_pos(piv) : 0.0;
@@ -160,7 +157,7 @@ __global__ __launch_bounds__(256) void potrf_diag(const CholJob2* __restrict__ j
     if (q == 0) Ti[j * kSD + j] = dinv[j];
     __builtin_amdgcn_s_waitcnt(0xc07f);
     __builtin_amdgcn_wave_barrier();
-    for (int r = 1; r < (POTRF_ABL == 2 ? 0 : kNB); ++r) {
+    for (int r = 1; r < kNB; ++r) {
       double acc = 0.0;
       if (r > j)
         for (int k = j + q; k < r; k += 4) acc = fma(S[r * kSD + k], Ti[k * kSD + j], acc);

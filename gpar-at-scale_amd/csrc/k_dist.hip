@@ -207,15 +207,9 @@ __global__ __launch_bounds__(256) void dist2_direct_kernel(
 // (4-row tiles) and inline exp constants measured the same.  Requires L <= kW2MaxL, even lds /
 // ldb, 16-byte aligned src / beta (mp is a multiple of 128).
 constexpr int kW2MaxL = 256;
-#ifndef D2_NT
-#define D2_NT 1   // non-temporal d2 loads and beta stores (streamed once): 1.656 -> 1.575 ms at D = 32
-#endif
 
-#ifndef W2V
-#define W2V 0   // A/B: 1 = 4-row prefetch at three workgroups per CU
-#endif
-constexpr int kW2T = W2V ? 4 : 8;
-constexpr int kW2Occ = W2V ? 3 : 2;
+constexpr int kW2T = 8;     // rows of d2 prefetched per thread
+constexpr int kW2Occ = 2;   // workgroups per CU
 
 // RIN: src holds the distances r = sqrt_pos(d2) (the fit's cache, Matern kernels) instead of d2.
 template <int TK, int OK, bool RIN>
@@ -250,16 +244,12 @@ __global__ __launch_bounds__(256, kW2Occ) void whiten_kfu_d2x2(
 #pragma unroll
     for (int r = 0; r < kW2T; ++r) {
       const int rr = (r0 + r < nk) ? r0 + r : nk - 1;
-#if D2_NT
       {
         typedef double v2d __attribute__((ext_vector_type(2)));
         const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(sp + (int64_t)rr * lds));
         px[r].x = t.x;
         px[r].y = t.y;
       }
-#else
-      px[r] = *reinterpret_cast<const double2*>(sp + (int64_t)rr * lds);
-#endif
     }
   };
   if (nk > 0) prefetch(0);
@@ -315,15 +305,11 @@ __global__ __launch_bounds__(256, kW2Occ) void whiten_kfu_d2x2(
         double2 o;
         o.x = aa;
         o.y = ab;
-#if D2_NT
         typedef double v2d __attribute__((ext_vector_type(2)));
         v2d t;
         t.x = o.x;
         t.y = o.y;
         __builtin_nontemporal_store(t, reinterpret_cast<v2d*>(bp + (int64_t)(r0 + r) * ldb));
-#else
-        *reinterpret_cast<double2*>(bp + (int64_t)(r0 + r) * ldb) = o;
-#endif
       }
     };
     if (r0 + kW2T <= nk) {

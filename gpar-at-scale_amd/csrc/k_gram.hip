@@ -12,286 +12,16 @@
 // (A = L_u^{-1} beta^T; Lambda = A A^T + I), which the build reassociates as
 // Lambda = L_u^{-1} (beta^T beta) L_u^{-T} + I.
 //
-// Tiling: split-K over the time axis; one 256-thread workgroup = 4 waves, each owning one
-// 64 x 64 lower-triangle sub-tile of G = 4 x 4 MFMA tiles of v_mfma_f64_16x16x4_f64
-// (C/D: col = lane & 15, row = (lane >> 4) + 4 * reg).  K-step = 16 time rows staged
-// global -> LDS by LDS-DMA (no VGPRs), double buffered; each wave stages one 64-column panel.
+// Tiling: split-K over the time axis on v_mfma_f64_16x16x4_f64 (C/D: col = lane & 15, row =
+// (lane >> 4) + 4 * reg).  K-step = 16 time rows staged global -> LDS by LDS-DMA (no VGPRs),
+// double buffered.  v3 (gram3_*, the default): fat two-wave workgroups, one wave per SIMD with 32
+// accumulator tiles; v2 (gram2_kernel, the two-lane mode's one-workgroup-per-CU plan): 4 waves of
+// 16 / 18 tiles.
 #include <type_traits>
 
 #include "gram_common.hpp"
 
 namespace gpar {
-#ifndef GRAM_ABL
-#define GRAM_ABL 0   // timing ablations only: 2 no LDS-DMA, 3 no MFMA, 5 no chunk-correction tail
-#endif
-
-// Work decomposition.  G's lower triangle is cut into 64 x 64 sub-tiles (p_i >= p_j over
-// npan = Mp / 64 panels).  A workgroup = 4 waves = up to 4 sub-tiles whose operands come from
-// at most 4 distinct panels, staged once per K-step and shared through LDS:
-//   * "off" groups: the 2 x 2 sub-tiles of an off-diagonal 128 x 128 block (panels 2a, 2a+1 |
-//     2b, 2b+1), nb (nb - 1) / 2 of them (nb = npan / 2);
-//   * "diag" groups: the 3 sub-tiles (2a,2a), (2a+1,2a), (2a+1,2a+1) of every diagonal block,
-//     chained in order and cut into groups of 4 -- a group spans <= 4 consecutive panels.
-// No sub-tile is computed twice (the old 128-tile design recomputed the upper half of the
-// diagonal tiles: 20 % of the MFMA work at M = 512).  Diag groups also own r = beta^T alpha for
-// the panels they stage first.
-struct WaveInfo {
-  int nsub;     // sub-tiles in the group (waves >= nsub have no MFMA work)
-  int sa, sb;   // LDS panel slots of this wave's row (A) / column (B) operand
-  int pa, pb;   // panel indices of this wave's sub-tile (pa >= pb)
-  int stage;    // panel this wave stages into slot `wave` (-1: slot unused)
-  int rown;     // 1 if this group accumulates r for that panel
-};
-
-__device__ __forceinline__ void diag_sub(int qd, int& pi, int& pj) {
-  const int a = qd / 3, w = qd - 3 * a;
-  pi = 2 * a + (w >= 1);
-  pj = 2 * a + (w == 2);
-}
-
-// Pure scalar arithmetic (no per-wave arrays: dynamically indexed arrays go to scratch).
-__device__ __forceinline__ WaveInfo decode_wave(int gid, int npan, int w) {
-  WaveInfo g;
-  const int nb = npan >> 1;
-  const int noff = nb * (nb - 1) / 2;
-  if (gid < noff) {
-    int a = 1;
-    while (a * (a + 1) / 2 <= gid) ++a;
-    const int b = gid - a * (a - 1) / 2;
-    g.nsub = 4;
-    g.sa = w >> 1;
-    g.sb = 2 + (w & 1);
-    g.pa = 2 * a + (w >> 1);
-    g.pb = 2 * b + (w & 1);
-    g.stage = (w < 2) ? 2 * a + w : 2 * b + (w - 2);
-    g.rown = 0;
-    return g;
-  }
-  const int h = gid - noff;
-  const int nq = 3 * nb;
-  const int last = (4 * h + 3 < nq) ? 4 * h + 3 : nq - 1;
-  int t, pmin, pmax, prev = -1;
-  diag_sub(4 * h, t, pmin);
-  diag_sub(last, pmax, t);
-  if (h > 0) diag_sub(4 * h - 1, prev, t);
-  g.nsub = last - 4 * h + 1;
-  const int qd = 4 * h + w;
-  if (qd <= last) {
-    diag_sub(qd, g.pa, g.pb);
-  } else {
-    g.pa = g.pb = pmin;
-  }
-  g.sa = g.pa - pmin;
-  g.sb = g.pb - pmin;
-  const int p = pmin + w;
-  g.stage = (p <= pmax) ? p : -1;
-  g.rown = (p <= pmax && p > prev) ? 1 : 0;
-  return g;
-}
-
-template <int D>
-__global__ __launch_bounds__(256, 2) void gram_kernel(
-    const double* __restrict__ beta, int64_t ldb, int64_t n, const double* __restrict__ ecor,
-    const double* __restrict__ cin, const double* __restrict__ qv, int64_t mc, int L,
-    const double* __restrict__ alpha, int npan, int ngroups, int nsplit, int64_t rows_per_split,
-    double* __restrict__ part, double* __restrict__ rpart, int xcd) {
-  // LDS: img [2 slot][4 panel][kBK rows][64], XOR-swizzled (odd rows swap their 16-column
-  //      halves: conflict-free MFMA operand reads) by the LDS-DMA source addresses;
-  //      ar [2 slot][4 wave][kBK] alpha_k (wave-private)
-  __shared__ __attribute__((aligned(16))) double smem[8 * kPanelD + 2 * 4 * kBK];
-  double* ringa = smem + 8 * kPanelD;
-
-  // XCD-aware decode: blocks b and b+8 share an XCD; each XCD group takes whole splits, so
-  // the groups of one split (which read the same beta rows) share that XCD's L2.
-  // (xcd == 0, more than 64 groups: a split no longer fits one XCD's 64 slots; linear decode)
-  const int b = blockIdx.x;
-  int split, gid;
-  if (xcd) {
-    const int q = b >> 3;
-    split = (q / ngroups) * 8 + (b & 7);
-    gid = q % ngroups;
-  } else {
-    split = b / ngroups;
-    gid = b % ngroups;
-  }
-  if (split >= nsplit) return;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const WaveInfo gi = decode_wave(gid, npan, wave);
-  // A wave without a sub-tile runs dummy MFMAs (never stored); an unused slot stages a
-  // duplicate panel (never read): no divergent per-wave branches inside the K-step.
-  const int spanel = gi.stage < 0 ? gi.pa : gi.stage;
-  const bool owns_r = gi.rown != 0;
-  const bool mf = wave < gi.nsub;
-
-  const int64_t kb = (int64_t)split * rows_per_split;
-  int64_t ke = kb + rows_per_split;
-  if (ke > n) ke = n;
-  const int nsteps = (int)((ke - kb + kBK - 1) / kBK);
-
-  d4 acc[4][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[a][c] = d4{0.0, 0.0, 0.0, 0.0};
-  // r = beta^T alpha for the staged panel's column tiles c (C layout: lanes lq = lane >> 4 hold
-  // rows lq + 4 i); reduced over lq at the end
-  double racc4[4] = {0.0, 0.0, 0.0, 0.0};
-  const int lq = lane >> 4, lc = lane & 15;
-
-  // ---- staging of K-step `s` into LDS slot s & 1 (this wave: its panel + its alpha copy)
-  // beta: 8 x global_load_lds_dwordx4, each 2 rows x 64 doubles; lane l lands at LDS row
-  // 2i + l/32, columns 2(l%32), +1 and fetches the source columns XORed with 16 on the odd row,
-  // which writes the swizzled image directly.  The beta workspace carries kBK zero rows past n,
-  // so no row is clamped: scalar row base + a constant per-lane byte offset.
-  const int hl = lane >> 5, cl2 = (lane & 31) * 2;
-  const uint32_t boff =
-      (uint32_t)(((int64_t)hl * ldb + (int64_t)spanel * kPW + (cl2 ^ (hl << 4))) * 8);
-  const char* bbase = reinterpret_cast<const char*>(beta);
-  const double* zrow = beta + n * ldb;   // first of the kBK zero pad rows
-  auto issue = [&](int s) __attribute__((always_inline)) {
-    const int64_t k0 = kb + (int64_t)s * kBK;
-    double* img = smem + ((s & 1) * 4 + wave) * kPanelD;
-#pragma unroll
-    for (int i = 0; i < kBK / 2; ++i) {
-      const char* rowp = bbase + (k0 + 2 * i) * ldb * 8;
-#if GRAM_ABL != 2
-      __builtin_amdgcn_global_load_lds(rowp + boff, img + 2 * i * kPW, 16, 0, 0);
-#else
-      (void)rowp;
-#endif
-    }
-    if (lane < 32) {
-      // rows >= n read zeros (beta's pad rows)
-      const int64_t kr = k0 + (lane >> 1);
-      const unsigned* as = kr < n ? reinterpret_cast<const unsigned*>(alpha + kr) + (lane & 1)
-                                  : reinterpret_cast<const unsigned*>(zrow);
-      __builtin_amdgcn_global_load_lds(as, ringa + ((s & 1) * 4 + wave) * kBK, 4, 0, 0);
-    }
-  };
-
-  const int frow = lane >> 4, fcol = lane & 15;
-  const int par = frow & 1;
-  int offa[4], offb[4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a) {
-    offa[a] = gi.sa * kPanelD + frow * kPW + ((a ^ par) << 4) + fcol;
-    offb[a] = gi.sb * kPanelD + frow * kPW + ((a ^ par) << 4) + fcol;
-  }
-  // r operand: this wave's own staged panel, rows lq + 4 i, column c * 16 + lc (swizzled)
-  const int roff = wave * kPanelD + lq * kPW + lc;
-
-  if (nsteps > 0) issue(0);
-  // hipcc does not order LDS-DMA writes before later ds_reads: wait explicitly (the memory
-  // clobber keeps the reads below the wait), then the barrier publishes every wave's panel.
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int s = 0; s < nsteps; ++s) {
-    if (s + 1 < nsteps) issue(s + 1);
-    const double* base = smem + (s & 1) * 4 * kPanelD;
-#pragma unroll
-    for (int ks = 0; ks < kBK / 4; ++ks) {
-      double fa[4], fb[4];
-#pragma unroll
-      for (int a = 0; a < 4; ++a) fa[a] = base[offa[a] + ks * 4 * kPW];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) fb[c] = base[offb[c] + ks * 4 * kPW];
-#if GRAM_ABL == 3
-      acc[0][0][0] += fa[0] * fb[0] + fa[1] * fb[1] + fa[2] * fb[2] + fa[3] * fb[3];
-#else
-      __builtin_amdgcn_s_setprio(1);   // favour the MFMA-issuing wave of the SIMD pair
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[a], fb[c], acc[a][c], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-#endif
-    }
-    {
-      const double* ar = ringa + ((s & 1) * 4 + wave) * kBK;
-      const double* im = base + roff;
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const double av = ar[lq + 4 * i];
-        const int rsw = (i * 4 + lq) & 1;   // row parity = lq parity
-#pragma unroll
-        for (int c = 0; c < 4; ++c)
-          racc4[c] = fma(av, im[4 * i * kPW + ((c ^ rsw) << 4)], racc4[c]);
-      }
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-  }
-
-#if GRAM_ABL != 5
-  // ---- chunk-correction tail (ecor null: beta was fixed up beforehand, nothing to add): chunks [j0, j1) of this split.  MFMA operands straight from
-  // global memory: E_j / C_j are stored [col][4] per chunk, which is exactly the 16 x 4 (A) and
-  // 4 x 16 (B) fragment layout (lane: column lane & 15, component lane >> 4); component 3 and
-  // components >= d are zero in E, and the C fragments are masked.
-  if (ecor) {
-    const int64_t nch = (n + L - 1) / L;
-    const int64_t j0 = (int64_t)split * nch / nsplit, j1 = (int64_t)(split + 1) * nch / nsplit;
-    const bool cv = lq < D;
-    const int64_t oa = ((int64_t)gi.pa * kPW + lc) * kSStride + lq;
-    const int64_t ob = ((int64_t)gi.pb * kPW + lc) * kSStride + lq;
-    const int64_t os = ((int64_t)spanel * kPW + lc) * kSStride + lq;
-    const int64_t cstride = mc * kSStride;
-    double ea[4], ca[4], eb[4], cb[4], cs[4], qq;
-    auto load = [&](int64_t j) __attribute__((always_inline)) {
-      const double* ej = ecor + j * cstride;
-      const double* cj = cin + j * cstride;
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        ea[t] = ej[oa + t * 16 * kSStride];
-        eb[t] = ej[ob + t * 16 * kSStride];
-        ca[t] = cj[oa + t * 16 * kSStride];
-        cb[t] = cj[ob + t * 16 * kSStride];
-        cs[t] = cj[os + t * 16 * kSStride];
-      }
-      qq = qv[j * 4 + lq];
-    };
-    for (int64_t j = j0; j < j1; ++j) {
-      load(j);
-#pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        ca[t] = cv ? ca[t] : 0.0;
-        cb[t] = cv ? cb[t] : 0.0;
-        cs[t] = cv ? cs[t] : 0.0;
-      }
-#pragma unroll
-      for (int a = 0; a < 4; ++a)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ea[a], cb[c], acc[a][c], 0, 0, 0);
-          acc[a][c] = __builtin_amdgcn_mfma_f64_16x16x4f64(ca[a], eb[c], acc[a][c], 0, 0, 0);
-        }
-      // r: column c * 16 + lc of the staged panel gets C_j[col, lq] q_j[lq] (summed over lq below)
-#pragma unroll
-      for (int c = 0; c < 4; ++c) racc4[c] = fma(cs[c], cv ? qq : 0.0, racc4[c]);
-    }
-  }
-#endif
-
-  if (mf) {
-    double* pt = part + (((int64_t)split * ngroups + gid) * 4 + wave) * (kPW * kPW);
-#pragma unroll
-    for (int a = 0; a < 4; ++a)
-#pragma unroll
-      for (int c = 0; c < 4; ++c)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) pt[(a * 16 + frow + 4 * r) * kPW + c * 16 + fcol] = acc[a][c][r];
-  }
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    double v = racc4[c];
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    if (owns_r && lq == 0) rpart[(int64_t)split * npan * kPW + (int64_t)spanel * kPW + c * 16 + lc] = v;
-  }
-}
 
 // ============================================================================ v2 decomposition
 // The v1 groups compute every diagonal 64 x 64 sub-tile whole although 6 of its 16 tiles lie
@@ -897,35 +627,6 @@ __global__ __launch_bounds__(256) void gram2_reduce(const double* __restrict__ p
   G[gc * ldg + gr] = s;
 }
 
-// Sum split partials in split order (deterministic) into the full symmetric G (ldg); the
-// last grid row sums r.
-__global__ __launch_bounds__(256) void gram_reduce(const double* __restrict__ part,
-                                                   const double* __restrict__ rpart, int npan,
-                                                   int ngroups, int nsplit, double* __restrict__ G,
-                                                   int64_t ldg, double* __restrict__ r) {
-  const int e = blockIdx.x * 256 + threadIdx.x;   // element within the sub-tile
-  if ((int)blockIdx.y == ngroups * 4) {
-    const int mp = npan * kPW;
-    for (int c = e; c < mp; c += gridDim.x * 256) {
-      double s = 0.0;
-      for (int sp = 0; sp < nsplit; ++sp) s += rpart[(int64_t)sp * mp + c];
-      r[c] = s;
-    }
-    return;
-  }
-  const int gid = blockIdx.y >> 2, w = blockIdx.y & 3;
-  const WaveInfo gi = decode_wave(gid, npan, w);
-  if (w >= gi.nsub) return;
-  const int row = e / kPW, cl = e % kPW;
-  if (gi.pa == gi.pb && row < cl) return;
-  double s = 0.0;
-  for (int sp = 0; sp < nsplit; ++sp)
-    s += part[(((int64_t)sp * ngroups + gid) * 4 + w) * (kPW * kPW) + e];
-  const int64_t gr = (int64_t)gi.pa * kPW + row, gc = (int64_t)gi.pb * kPW + cl;
-  G[gr * ldg + gc] = s;
-  G[gc * ldg + gr] = s;
-}
-
 // Materialise the corrected beta (only for the (dtc, A) parity entry point).
 template <int D>
 __global__ __launch_bounds__(256) void beta_fix_kernel(double* __restrict__ beta, int64_t ldb,
@@ -949,9 +650,6 @@ __global__ __launch_bounds__(256) void beta_fix_kernel(double* __restrict__ beta
 
 namespace gpar {
 
-#ifndef GRAM_V1
-#define GRAM_V1 0   // 1: the v1 decomposition (whole diagonal sub-tiles), for A/B only
-#endif
 
 // v2: split counts for the OFF and DG workgroups minimising the per-CU work
 // ceil(workgroups / 256) x max(16 x rows_off, 18 x rows_dg), at most 512 workgroups (2 per CU);
@@ -997,16 +695,10 @@ static void gram2_plan(int64_t n, int64_t mp, GramPlan& p, bool one_per_cu) {
   p.rpart_doubles = (int64_t)p.sdg * mp;
 }
 
-#ifndef GRAM_V3
-#define GRAM_V3 1   // 0: the v2 kernel at two workgroups per CU as well (A/B)
-#endif
-#ifndef GRAM3_CORUN
-#define GRAM3_CORUN 1   // 1: the chunk correction runs beside the OFF kernel on a second stream
-#endif
 #define HIPCHECK_G(x) do { if ((x) != hipSuccess) throw std::runtime_error("launch_gram: " #x); } while (0)
-#ifndef GRAM3_DG_SLOTS
-#define GRAM3_DG_SLOTS 1024
-#endif
+// DG workgroup slots of the whole chip: 238 VGPRs, so two waves per SIMD (512 slots: 2.18 ms per
+// launch, 1024: 1.16 ms, 2048: 1.27 ms at the north config)
+constexpr int kGram3DgSlots = 1024;
 
 // v3: split counts for OFF (32 tiles per wave) and DG (18 tiles per wave, one diagonal block per
 // workgroup), two launches of up to 512 workgroups each (two per CU, one wave per SIMD).
@@ -1029,7 +721,7 @@ static void gram3_plan(int64_t n, int64_t mp, GramPlan& p, int cus, int dg_cus) 
   };
   p.soff = p.noff ? splits(p.noff, 2 * cus) : 0;
   // DG (238 VGPRs, 33 KB LDS) runs two waves per SIMD: 1024 slots
-  p.sdg = splits(p.ndg, GRAM3_DG_SLOTS * dg_cus / 256);
+  p.sdg = splits(p.ndg, kGram3DgSlots * dg_cus / 256);
   p.rows_off = p.noff ? rows_of(p.soff) : 0;
   p.rows_dg = rows_of(p.sdg);
   p.nsplit = p.sdg;
@@ -1051,42 +743,10 @@ static void gram3_plan(int64_t n, int64_t mp, GramPlan& p, int cus, int dg_cus) 
 
 GramPlan gram_plan(int64_t n, int64_t mp, bool one_per_cu, int cus, int dg_cus) {
   GramPlan p;
-  if (!GRAM_V1) {
-    if (GRAM_V3 && !one_per_cu)
-      gram3_plan(n, mp, p, cus, dg_cus > 0 ? dg_cus : cus);
-    else
-      gram2_plan(n, mp, p, one_per_cu);
-    return p;
-  }
-  p.npan = (int)(mp / kPW);
-  const int nb = p.npan / 2;
-  const int noff = nb * (nb - 1) / 2;
-  p.ngroups = noff + (3 * nb + 3) / 4;
-  int64_t maxs = (n + 255) / 256;          // keep >= 256 rows per split
-  int ns;
-  // XCD-aware decode (whole splits per XCD, so a split's groups share one L2) while it still
-  // fills the 8 x 64 co-resident slots; otherwise a linear decode over ~512 blocks.
-  const int spx0 = 64 / p.ngroups;
-  const double occ_xcd = spx0 > 0 ? 8.0 * p.ngroups * spx0 / 512.0 : 0.0;
-  const double occ_lin = (double)p.ngroups * (512 / p.ngroups > 0 ? 512 / p.ngroups : 1) / 512.0;
-  if (spx0 > 0 && (occ_xcd >= 0.9 || occ_xcd >= occ_lin - 0.02)) {
-    p.xcd = 1;
-    ns = 8 * (64 / p.ngroups);
-    if (maxs < 8) maxs = 8;
-    if (ns > maxs) ns = (int)((maxs / 8) * 8);
-    if (ns < 8) ns = 8;
-  } else {                                 // wide G (M > 768): fill the 512 slots linearly
-    p.xcd = 0;
-    ns = 512 / p.ngroups;
-    if (ns < 1) ns = 1;
-    if (ns > maxs) ns = (int)(maxs < 1 ? 1 : maxs);
-  }
-  p.nsplit = ns;
-  int64_t rps = (n + ns - 1) / ns;
-  rps = ((rps + kBK - 1) / kBK) * kBK;
-  p.rows_per_split = rps;
-  p.part_doubles = (int64_t)ns * p.ngroups * 4 * kPW * kPW;
-  p.rpart_doubles = (int64_t)ns * mp;
+  if (!one_per_cu)
+    gram3_plan(n, mp, p, cus, dg_cus > 0 ? dg_cus : cus);
+  else
+    gram2_plan(n, mp, p, one_per_cu);
   return p;
 }
 
@@ -1096,7 +756,7 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
                  int64_t ldg, double* r, hipStream_t side, hipEvent_t ev_a, hipEvent_t ev_b,
                  hipStream_t st_w, hipEvent_t ev_w, int w_items) {
   if (plan.v3) {
-    const bool corun = GRAM3_CORUN && ecor && side && plan.noff > 0;
+    const bool corun = ecor && side && plan.noff > 0;
     const int ncs = ecor ? (corun ? plan.ncs_slim : plan.ncs) : 0;
     const int noffw = ((plan.noff * plan.soff + 7) / 8) * 8;   // XCD deal
     const int ndgw = ((plan.ndg * plan.sdg + 7) / 8) * 8;
@@ -1157,16 +817,7 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
 #undef GRAM2_ARGS
     const int nrows = plan.noff * 4 * 16 + plan.ndg * 4 * kD2T + 1;
     gram2_reduce<<<nrows, 256, 0, st>>>(part, rpart, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, G, ldg, r);
-    return;
   }
-  const int nblk = plan.xcd ? plan.ngroups * ((plan.nsplit + 7) / 8) * 8 : plan.ngroups * plan.nsplit;
-  switch (sdim) {
-    case 1: gram_kernel<1><<<nblk, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart, plan.xcd); break;
-    case 2: gram_kernel<2><<<nblk, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart, plan.xcd); break;
-    default: gram_kernel<3><<<nblk, 256, 0, st>>>(beta, ldb, n, ecor, cin, qv, mc, L, alpha, plan.npan, plan.ngroups, plan.nsplit, plan.rows_per_split, part, rpart, plan.xcd); break;
-  }
-  dim3 rgrid((kPW * kPW + 255) / 256, plan.ngroups * 4 + 1);
-  gram_reduce<<<rgrid, 256, 0, st>>>(part, rpart, plan.npan, plan.ngroups, plan.nsplit, G, ldg, r);
 }
 
 void launch_beta_fix(hipStream_t st, int sdim, double* beta, int64_t ldb, int64_t n,

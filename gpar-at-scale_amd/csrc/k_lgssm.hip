@@ -595,9 +595,6 @@ __global__ __launch_bounds__(256) void whiten_kfu(
 // Matern-5/2, EQ: a d^2 error of eps |v - c| |z - c| is harmless); Matern-1/2 keeps the direct
 // form (its kappa is not smooth in d^2 at 0).
 constexpr int kMT = 16;   // steps per sub-tile
-#ifndef WHITEN_ABL
-#define WHITEN_ABL 0   // timing ablations only: 1 no kernel evaluation, 2 no MFMA, 3 no recursion, 4 no beta store
-#endif
 
 template <int TK, int OK, int DP>
 __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
@@ -725,9 +722,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     __syncthreads();
     commit(nt);
     __syncthreads();
-#if WHITEN_ABL != 4
     flush();
-#endif
     if (kt + kMT < k1) prefetch(kt + kMT);
     // cross products (v - c).(z - c) and the step norms |v - c|^2
     d4 acc[4];
@@ -747,13 +742,9 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
 #pragma unroll
       for (int ks = 0; ks < NKS; ++ks) {
         if (ks < nks) {
-#if WHITEN_ABL != 2
 #pragma unroll
           for (int ct = 0; ct < 4; ++ct)
             acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(af[ks], bf[ct][ks], acc[ct], 0, 0, 0);
-#else
-          acc[0][0] += af[ks] * bf[0][ks];
-#endif
         }
       }
     } else {
@@ -762,13 +753,9 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
         if (ks < nks) {
           const double a = vs[fr * VS + 4 * ks + fq];
           vnp = fma(a, a, vnp);
-#if WHITEN_ABL != 2
 #pragma unroll
           for (int ct = 0; ct < 4; ++ct)
             acc[ct] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, bf[ct][ks], acc[ct], 0, 0, 0);
-#else
-          acc[0][0] += a * bf[0][ks];
-#endif
         }
       }
     }
@@ -782,21 +769,13 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
       for (int ct = 0; ct < 4; ++ct) {
         double d2 = vn + zn[ct] - 2.0 * acc[ct][r];
         if constexpr (OK == KEQ) d2 = d2 > 0.0 ? d2 : 0.0;   // the Matern forms clamp in sqrt_pos
-#if WHITEN_ABL != 1
         xt[wave][fq + 4 * r][ct * 16 + fr] = skappa_sq<OK>(d2, inv_lo, s_o);
-#else
-        xt[wave][fq + 4 * r][ct * 16 + fr] = d2;
-#endif
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
     auto step = [&](int kk) __attribute__((always_inline)) {
       const double x = colv ? xt[wave][kk][lane] : 0.0;
-#if WHITEN_ABL == 3
-      xt[wave][kk][lane] = x;
-      return;
-#endif
       const double* rr = rl + kk * RS;
       double mm[SD];
 #pragma unroll
@@ -823,9 +802,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     ntp = nt;
     ktp = kt;
   }
-#if WHITEN_ABL != 4
   flush();
-#endif
   if (cola) {
 #pragma unroll
     for (int i = 0; i < SD; ++i) {

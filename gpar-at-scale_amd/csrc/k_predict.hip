@@ -280,12 +280,6 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
 // phase G's later steps (56 % of the dense MFMAs at M = 512; gemm_nt's 128-column skip: 62.5 %).
 // V must be zero outside its m x m block (the caller clears the Mp x Mp buffer).
 constexpr int kVRows = 64;
-#ifndef PV_PF2
-#define PV_PF2 1   // A operands staged by LDS-DMA two k-steps ahead (workgroups whose rows span <= 2 chunks)
-#endif
-#ifndef PV_ABL
-#define PV_ABL 0   // timing ablations only: 1 no A-operand loads, 2 no V slab DMA, 3 no per-step wait + barrier, 4 no MFMA
-#endif
 template <int V_> struct IntC { static constexpr int value = V_; };
 // 16 bytes global -> LDS by DMA (wave-uniform LDS base + lane * 16).  A plain __device__ function:
 // the builtin inside the kernel template's lambdas made the host pass drop the launch stubs.
@@ -314,13 +308,11 @@ __global__ __launch_bounds__(256, 1) void predict_var(
   constexpr int T = 4 * NG, NC = 64 * NG, NS = 4 * NG;   // tiles, columns, k-steps
   __shared__ __attribute__((aligned(16))) double lb[2][NC * 16];
   __shared__ double lw[NC];   // w, zero past m
-#if PV_PF2
   // two-step-ahead operand rings (slot s % 3): X's 16 columns of k-step s for the 64 rows (row r's
   // 16-byte pieces at slot p ^ (r & 7)), and the chunk carries chat of the <= 2 chunks the rows
   // lie in (chunk slot, 16 columns, kSStride)
   __shared__ __attribute__((aligned(16))) double lx[3][kVRows * 16];
   __shared__ __attribute__((aligned(16))) double lc[3][2 * 16 * kSStride];
-#endif
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int frow = lane >> 4, fcol = lane & 15;
   // ---- this lane's Q row (the MFMA A operand's row fcol)
@@ -377,7 +369,6 @@ __global__ __launch_bounds__(256, 1) void predict_var(
       dma16(vsrc + (int64_t)r * 32 * ldv + s * 16, &lb[0][0] + buf * (NC * 16) + q * 128);
     }
   };
-#if PV_PF2
   // ---- workgroups whose 64 rows lie in <= 2 chunks take the prefetching path: every operand of
   //      step s is in LDS, moved by DMA during step s - 2, and read by inline asm (a compiler-visible
   //      LDS read behind an outstanding LDS-DMA makes the compiler wait for every load, the
@@ -468,12 +459,10 @@ __global__ __launch_bounds__(256, 1) void predict_var(
 #pragma unroll
       for (int q = 0; q < D; ++q) ca[0][ks][q] = c3[ks][q];
   };
-#endif
   d4 acc[T];
 #pragma unroll
   for (int t = 0; t < T; ++t) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
   for (int c = tid; c < NC; c += 256) lw[c] = c < m ? w[c] : 0.0;
-#if PV_PF2
   if (pf) {
     dmaBa(0, 0);
     dmaXC(0);
@@ -482,10 +471,6 @@ __global__ __launch_bounds__(256, 1) void predict_var(
     loadA(0, 0);
     dmaB(0, 0);
   }
-#else
-  loadA(0, 0);
-  dmaB(0, 0);
-#endif
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // one k-step s with tiles T0 .. T - 1: fa from the inputs loaded during step s - 1; then the
@@ -494,7 +479,6 @@ __global__ __launch_bounds__(256, 1) void predict_var(
   auto step = [&](auto t0c, auto pfc, int s) __attribute__((always_inline)) {
     constexpr int T0 = decltype(t0c)::value;
     constexpr bool PF = decltype(pfc)::value;
-#if PV_PF2
     bool x2 = false;
     if constexpr (PF) {
       // step s's operands from the rings (landed before the previous step's barrier), then the
@@ -515,16 +499,11 @@ __global__ __launch_bounds__(256, 1) void predict_var(
       x2 = s + 2 < NS;
       if (x2) dmaXC(s + 2);
     } else
-#endif
     {
       makeA(s, 0);
       if (s + 1 < NS) {
-#if PV_ABL != 1
         loadA(s + 1, 0);
-#endif
-#if PV_ABL != 2
         dmaB(s + 1, (s + 1) & 1);
-#endif
       }
     }
     const double* B = &lb[0][0] + (s & 1) * (NC * 16);
@@ -534,17 +513,11 @@ __global__ __launch_bounds__(256, 1) void predict_var(
       for (int ks = 0; ks < 4; ++ks) {
         const int c = t * 16 + fcol, kk = ks * 4 + frow;
         const double bf = B[c * 16 + (((kk >> 1) ^ ((c >> 1) & 7)) << 1) + (kk & 1)];
-#if PV_ABL != 4
         acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[ks], bf, acc[t], 0, 0, 0);
-#else
-        acc[t][0] += fa[ks] * bf;
-#endif
         // keep the scheduler's window to a few tiles: hoisting every fragment read of a
         // 32-tile step ran out of VGPRs and spilled the accumulators
         if (ks == 3 && (t & 1)) __builtin_amdgcn_sched_barrier(0);
       }
-#if PV_ABL != 3
-#if PV_PF2
     if constexpr (PF) {
       // all but step s + 2's DMAs (issued last: X 2 per wave, the carries 1 more on wave 0) have
       // landed; a bare s_barrier (__syncthreads would first wait for every load, the prefetch
@@ -558,12 +531,10 @@ __global__ __launch_bounds__(256, 1) void predict_var(
         asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
       }
     } else
-#endif
     {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
-#endif
   };
   // phase G: k-steps 4 G .. 4 G + 3 with tiles 4 G .. T - 1.  Phase 0's first step is peeled (a
   // loop whose accumulators enter as the zero constant copied them every step)
@@ -585,11 +556,9 @@ __global__ __launch_bounds__(256, 1) void predict_var(
     if constexpr (NG > 6) phase(IntC<6>{}, pfc);
     if constexpr (NG > 7) phase(IntC<7>{}, pfc);
   };
-#if PV_PF2
   if (pf)
     phases(std::true_type{});
   else
-#endif
     phases(std::false_type{});
   // ---- epilogue: row sums of squares (rows frow + 4 r of the wave's 16) over the tiles and the
   //      16 lanes of a row; the mean's dot over the 4 lanes (frow) sharing a row

@@ -65,9 +65,7 @@ struct TrsvJobHost {
 };
 
 struct GramPlan {
-  int npan = 0, ngroups = 0, nsplit = 0;   // 64-column panels, 4-sub-tile groups, time splits
-  int xcd = 1;                              // XCD-aware block decode (ngroups <= 64)
-  int64_t rows_per_split = 0;
+  int npan = 0, nsplit = 0;   // 64-column panels, time splits of r (the DG kernel's)
   int64_t part_doubles = 0, rpart_doubles = 0;
   // v2 decomposition (k_gram.hip): OFF / DG workgroup counts, their time splits and rows
   int v2 = 0, noff = 0, ndg = 0, soff = 0, sdg = 0;
