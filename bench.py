@@ -16,10 +16,10 @@ all-gathered.  value = N * P / wall-clock per step (pts*outputs/s, whole job).
 Usage: python bench.py [--gpus N] [--steps K] [--warmup W] [--config north|eeg|dtc|small|ssm]
 
 Launch: under torchrun (WORLD_SIZE set) every process is one rank.  Started directly with
---gpus N > 1, the parent checks that N devices are visible (torch.cuda.device_count(), which does
-not initialise HIP) and starts N rank processes itself (RANK / LOCAL_RANK / WORLD_SIZE /
-MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment) before anything touches the GPU; it
-forwards rank 0's JSON line and exits with the first non-zero rank status.
+--gpus N > 1, the parent checks that N devices are visible (KFD topology in sysfs: it never
+initialises HIP, nor imports torch) and starts N rank processes itself (RANK / LOCAL_RANK /
+WORLD_SIZE / MASTER_ADDR=127.0.0.1 / MASTER_PORT in their environment); it forwards rank 0's JSON
+line and exits with the first non-zero rank status.
 """
 from __future__ import annotations
 
@@ -116,6 +116,7 @@ def main():
                          "258 GB per step costs ~5.8 s on MI355X (fresh VRAM is cleared); 'release': "
                          "the library default, freed when each fit call returns")
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
+    ap.add_argument("--cpu-check-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--stub", action="store_true",
                     help="launcher check without a GPU: ranks join a gloo group, take their output "
                          "shards and report them; no compute (tests/test_bench_launch.py)")
@@ -162,6 +163,23 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=dev)
+
+    # every rank's view of the job: the next SCALE record shows the backend (nccl = RCCL) and N
+    # distinct devices
+    me = {"rank": rank, "local_rank": local, "device": torch.cuda.current_device(),
+          "world_size": dist.get_world_size() if world > 1 else 1,
+          "backend": dist.get_backend() if world > 1 else None, "host": socket.gethostname()}
+    try:
+        props = torch.cuda.get_device_properties(dev)
+        me["device_name"] = props.name
+        me["device_uuid"] = str(getattr(props, "uuid", "")) or None
+        me["pci_bus_id"] = getattr(props, "pci_bus_id", None)
+    except Exception:   # noqa: BLE001  telemetry only
+        pass
+    rank_info = [me]
+    if world > 1:
+        rank_info = [None] * world
+        dist.all_gather_object(rank_info, me)
 
     # ---------------------------------------------------------------- inputs (untimed)
     t0 = time.perf_counter()
@@ -468,6 +486,41 @@ def main():
                       "ok": bool(max(rels) <= 1e-9),
                       "what": "-nlml of the timed run's last step at its fitted theta vs a fresh "
                               "whole-chip single-output gpar_dtc_objective there (rel <= 1e-9)"}
+    p_chk = check_output(P)
+    if (rank == 0 and cpu_child is not None and p_chk in gpar_out and not host
+            and os.path.getsize(cpu_child.check_path) > 0):
+        # the C port's objective and analytic prediction of output p_chk at CHECK_THETA, computed
+        # by the CPU baseline child on this run's own data, against the GPU's (gpar_dtc_objective,
+        # gpar_predict: the prediction at N* = N takes predict_var's prefetching path, as the
+        # timed predictions do)
+        ref = np.load(cpu_child.check_path)
+        i = gpar_out.index(p_chk)
+        v = G.dtc_objective_batch([problems[i]], [CHECK_THETA], device=local)[0]
+        gm, gs = G.predict_scaled(Y_d[:, : p_chk - 1], Zs[p_chk], t_d, ycols[p_chk], CHECK_THETA,
+                                  ts_d, Fs_d[:, : p_chk - 1], cfg["out_kernel"], "matern52",
+                                  mode="analytic", device=local, qu_kuu_noise=qn)
+        gm, gs = gm.cpu().numpy(), gs.cpu().numpy()
+        rm, rs = ref["mean"], ref["std"]
+
+        def excess(a, b):   # max |a - b| / (rtol |b| + atol): <= 1 passes rtol 1e-7, atol 1e-8 max|b|
+            return float(np.max(np.abs(a - b) / (1e-7 * np.abs(b) + 1e-8 * np.abs(b).max())))
+        port = {"reference": "C port (oracle/cpu_ref, pinned to the numpy oracle by "
+                             "tests/test_cpu_ref.py), run by the cpu_baseline child on this data",
+                "output": p_chk, "theta": list(CHECK_THETA), "dtc_gpu": v, "dtc_port": float(ref["dtc"][0]),
+                "dtc_rel": abs(v - float(ref["dtc"][0])) / abs(float(ref["dtc"][0])),
+                "mean_max_abs": float(np.max(np.abs(gm - rm))), "std_max_abs": float(np.max(np.abs(gs - rs))),
+                "mean_excess": excess(gm, rm), "std_excess": excess(gs, rs)}
+        port["ok"] = bool(port["dtc_rel"] <= 1e-9 and port["mean_excess"] <= 1.0
+                          and port["std_excess"] <= 1.0)
+        port["what"] = ("gpar_dtc_objective (rel <= 1e-9) and gpar_predict's mean / std (rtol 1e-7, "
+                        "atol 1e-8 max|ref|; *_excess <= 1 passes) at N = N*, against the port")
+        self_check = dict(self_check or {}, cpu_port=port)
+        self_check["ok"] = bool(self_check.get("ok", True) and port["ok"])
+    if cpu_child is not None:
+        try:
+            os.unlink(cpu_child.check_path)
+        except OSError:
+            pass
     out = None
     if rank == 0:
         P_work = len(mine) if shard_of else P
@@ -522,6 +575,7 @@ def main():
                                  "cu_split, part of gram3_dg_kernel on the whitening CUs)",
                          "launches": gram_n, "avg_ms": avg, "flops_per_launch": flops,
                          "lanes": args.lanes},
+            "ranks": rank_info,
             "kernels": {"gram_ms_per_step": gram_ms / args.steps, "whiten_ms_per_step": wh_ms / args.steps,
                         "whiten_launches": wh_n},
         }
@@ -603,18 +657,41 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def visible_gpu_count(root="/sys/class/kfd/kfd/topology/nodes", env=None):
+    """GPUs this process could use, counted WITHOUT initialising HIP (the launcher parent must stay
+    HIP-free: torch.cuda.device_count() may fall back to hipGetDeviceCount when amdsmi discovery
+    fails).  KFD topology nodes with a non-zero gpu_id are GPUs (CPU nodes have 0); a
+    ROCR_VISIBLE_DEVICES / HIP_VISIBLE_DEVICES / CUDA_VISIBLE_DEVICES list narrows the count."""
+    env = os.environ if env is None else env
+    n = 0
+    try:
+        for node in os.listdir(root):
+            try:
+                with open(os.path.join(root, node, "gpu_id")) as f:
+                    if int(f.read().strip() or "0") != 0:
+                        n += 1
+            except (OSError, ValueError):
+                continue
+    except OSError:
+        return 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = env.get(var)
+        if v is not None:
+            n = min(n, len([x for x in v.split(",") if x.strip() != ""]))
+    return n
+
+
 def launch_ranks(n, argv, stub=False):
     """Start one bench process per GPU (rank r on device r) and forward rank 0's JSON line.
 
-    Called before the parent touches the GPU: torch.cuda.device_count() only counts devices.
-    Returns the exit status: 2 when fewer than n devices are visible, else the first non-zero
-    rank status (0 when every rank succeeded)."""
-    if not stub:
-        import torch
-        have = torch.cuda.device_count()
-        if have < n:
-            log(f"bench: --gpus {n} but only {have} device(s) visible")
-            return 2
+    The parent never initialises HIP (it does not even import torch): the devices are counted from
+    the KFD topology in sysfs (visible_gpu_count), and only the rank processes touch the GPU.
+    Returns the exit status: 2 when fewer than n devices are visible (not checked with stub, the
+    CPU-only launcher check), else the first non-zero rank status (0 when every rank succeeded)."""
+    have = visible_gpu_count()
+    if not stub and have < n:
+        log(f"bench: --gpus {n} but only {have} device(s) visible")
+        return 2
     env0 = dict(os.environ, MASTER_ADDR="127.0.0.1", MASTER_PORT=str(_free_port()),
                 WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n))
     procs = []
@@ -690,16 +767,23 @@ def _cpu_threads():
 def start_cpu_baseline(args):
     """Start the CPU baseline (cpu_baseline below) in a child process, before this process touches
     the GPU: it then runs beside the inputs and the warm-up steps instead of after the timed region.
-    Returns the Popen (joined by join_cpu_baseline before the timed region)."""
+    Returns the Popen (joined by join_cpu_baseline before the timed region); its check_path is the
+    .npz the child leaves its objective value and predictions in (the self-check's reference)."""
+    import tempfile
     th = _cpu_threads()
     env = dict(os.environ, OMP_NUM_THREADS=str(th), OPENBLAS_NUM_THREADS=str(th))
-    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--config", args.config]
+    fd, path = tempfile.mkstemp(prefix="gpar_cpu_check_", suffix=".npz")
+    os.close(fd)
+    cmd = [sys.executable, os.path.abspath(__file__), "--cpu-baseline-child", "--config", args.config,
+           "--cpu-check-file", path]
     if args.evals:
         cmd += ["--evals", str(args.evals)]
     if args.qu_noise_free:
         cmd += ["--qu-noise-free"]
     log(f"cpu_baseline: child process with {th} threads beside the warm-up")
-    return subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    child = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True)
+    child.check_path = path
+    return child
 
 
 def join_cpu_baseline(child, timeout=900):
@@ -720,26 +804,53 @@ def cpu_baseline_child(args):
     if args.evals:
         cfg["evals"] = args.evals
     res = cpu_baseline(cfg["N"], cfg["N"], cfg["M"], cfg["P"], cfg["evals"], cfg["out_kernel"],
-                       qu_kuu_noise=not args.qu_noise_free)
+                       qu_kuu_noise=not args.qu_noise_free, check_path=args.cpu_check_file)
     print(json.dumps(res), flush=True)
 
 
-def _cpu_sample(CR, O, n, ns, M, d, out_kernel, theta, qu_kuu_noise=True):
+def _cpu_sample(CR, O, n, ns, M, d, out_kernel, theta, qu_kuu_noise=True, data=None):
     """One DTC objective evaluation and one analytic prediction of the C port at n training /
-    ns test points (D = d inputs), seconds each."""
-    t, Y = O.synthetic_gpar(n, d + 1, seed=1, noise=0.8)
-    V = Y[:, :d].T
-    y = Y[:, d]
-    Z = O.pick_pseudo_inputs(V, M, 3)
+    ns test points (D = d inputs): (seconds, seconds, objective value, (mean, std)).  data: the
+    bench's own (V, Z, t, y, t_star, V_star) of one output, else a seeded synthetic problem."""
+    if data is None:
+        t, Y = O.synthetic_gpar(n, d + 1, seed=1, noise=0.8)
+        V = Y[:, :d].T
+        y = Y[:, d]
+        Z = O.pick_pseudo_inputs(V, M, 3)
+        ts = np.sort(np.random.default_rng(2).uniform(t[0], t[-1], ns))
+        Vs = np.vstack([np.interp(ts, t, V[q]) for q in range(d)])
+    else:
+        V, Z, t, y, ts, Vs = data
     t0 = time.perf_counter()
-    CR.compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel, "matern52")
+    val, _ = CR.compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel, "matern52")
     t_eval = time.perf_counter() - t0
-    ts = np.sort(np.random.default_rng(2).uniform(t[0], t[-1], ns))
-    Vs = np.vstack([np.interp(ts, t, V[q]) for q in range(d)])
     t0 = time.perf_counter()
-    CR.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, out_kernel, "matern52",
-                                         qu_kuu_noise=qu_kuu_noise)
-    return t_eval, time.perf_counter() - t0
+    pred = CR.get_gpar_scaled_predictions_fixed(V, Z, t, y, ts, Vs, theta, out_kernel, "matern52",
+                                                qu_kuu_noise=qu_kuu_noise)
+    return t_eval, time.perf_counter() - t0, float(val), pred
+
+
+# The output whose data the CPU baseline times and the bench's self-check compares the GPU with
+# (D = 32 at the north config: the job's median width).
+CHECK_OUTPUT = 33
+# the fixed hyperparameters of that comparison (natural units; log theta = (log 2, ..., -2))
+CHECK_THETA = (2.0, 2.0, 2.0, 2.0, float(np.exp(-2.0) + 1e-3))
+
+
+def check_output(P):
+    return min(CHECK_OUTPUT, P)
+
+
+def bench_output_data(N, P, M, p):
+    """Output p's problem exactly as the bench builds it (gparatscale.data, seed 0): host
+    (V D x N, Z D x M, t, y, t_star, V_star D x N*)."""
+    from gparatscale import data as D
+    ds = D.gpar_dataset(N, P, seed=0, observation_noise=0.8)
+    Y = ds["Y"]
+    V = np.ascontiguousarray(Y[:, : p - 1].T)
+    Z = np.ascontiguousarray(D.pseudo_inputs(Y[:, : p - 1], M, seed=p).T)
+    Vs = np.ascontiguousarray(ds["F_star"][:, : p - 1].T)
+    return V, Z, ds["t"], np.ascontiguousarray(Y[:, p - 1]), ds["t_star"], Vs
 
 
 def _reference_literal_cost(O, N, P, EV, t_eval, sizes=(2000, 4000, 8000)):
@@ -773,15 +884,17 @@ def _reference_literal_cost(O, N, P, EV, t_eval, sizes=(2000, 4000, 8000)):
         return {"error": repr(exc)}
 
 
-def cpu_baseline(N, NS, M, P, EV, out_kernel, d_sample=32, n_ratio=100_000, qu_kuu_noise=True):
+def cpu_baseline(N, NS, M, P, EV, out_kernel, n_ratio=100_000, qu_kuu_noise=True,
+                 check_path=None):
     """Time the C/OpenMP CPU restatement of the reference path (oracle/cpu_ref.{c,py}, SURVEY §8d
     "cpu_ref": kernel assembly, Kalman gains and per-column decorrelate sweeps, RTS smoother in C;
     cholesky / trsm / gemm in OpenBLAS, as the reference leaves them to Julia's OpenBLAS; "port").
 
     Threaded leg (the OpenMP / OpenBLAS threads this process was given): one DTC objective
-    evaluation and one analytic prediction at the job's own sizes (N training points, N* = NS test
-    points, M, D = d_sample), so nothing is extrapolated in N: job = (P - 1) outputs x (EV
-    evaluations + 1 prediction).
+    evaluation and one analytic prediction on the bench's own data of output CHECK_OUTPUT (N
+    training points, N* = NS test points, D = p - 1) at CHECK_THETA, so nothing is extrapolated in
+    N: job = (P - 1) outputs x (EV evaluations + 1 prediction).  The objective value and the
+    predicted mean / std go to check_path (.npz) for the bench's self-check against the GPU.
     One-thread figure (the reference's sequential column loop, dtc.jl:110-117): the same two
     pieces at N = N* = n_ratio with all threads and with one (threadpoolctl's limit of 1); the
     one-thread job is the threaded job scaled by those measured ratios (assumption: the thread
@@ -795,17 +908,26 @@ def cpu_baseline(N, NS, M, P, EV, out_kernel, d_sample=32, n_ratio=100_000, qu_k
     except Exception:
         blas = 1
     cores = max(CR.threads(), blas)
-    theta = (2.0, 2.0, 2.0, 2.0, float(np.exp(-2.0) + 1e-3))
+    theta = CHECK_THETA
+    p_chk = check_output(P)
+    d_sample = p_chk - 1
+    data = bench_output_data(N, P, M, p_chk)
     _cpu_sample(CR, O, 4096, 1024, M, d_sample, out_kernel, theta, qu_kuu_noise)   # warm-up, untimed
-    t_eval, t_pred = _cpu_sample(CR, O, N, NS, M, d_sample, out_kernel, theta, qu_kuu_noise)
+    t_eval, t_pred, val, (pm_, ps_) = _cpu_sample(CR, O, N, NS, M, d_sample, out_kernel, theta,
+                                                  qu_kuu_noise, data=data)
+    if check_path:
+        np.savez(check_path, dtc=np.array([val]), mean=pm_, std=ps_, theta=np.array(theta),
+                 output=np.array([p_chk]))
     t_job = (P - 1) * (EV * t_eval + t_pred)
     single = None
     try:
         from threadpoolctl import threadpool_limits
         n_ratio = min(n_ratio, N)
-        em, pm = _cpu_sample(CR, O, n_ratio, n_ratio, M, d_sample, out_kernel, theta, qu_kuu_noise)
+        em, pm, _, _ = _cpu_sample(CR, O, n_ratio, n_ratio, M, d_sample, out_kernel, theta,
+                                   qu_kuu_noise)
         with threadpool_limits(limits=1):
-            e1, p1 = _cpu_sample(CR, O, n_ratio, n_ratio, M, d_sample, out_kernel, theta, qu_kuu_noise)
+            e1, p1, _, _ = _cpu_sample(CR, O, n_ratio, n_ratio, M, d_sample, out_kernel, theta,
+                                       qu_kuu_noise)
         re_, rp_ = e1 / em, p1 / pm
         tj1 = (P - 1) * (EV * t_eval * re_ + t_pred * rp_)
         single = {"value": N * P / tj1, "cores": 1,
@@ -818,10 +940,11 @@ def cpu_baseline(N, NS, M, P, EV, out_kernel, d_sample=32, n_ratio=100_000, qu_k
     return {"value": N * P / t_job, "unit": "pts·outputs/s", "cores": int(cores), "kind": "port",
             "host_cpu": _cpu_model(), "single_thread": single, "reference_literal": literal,
             "ran": "in a child process beside the GPU warm-up (joined before the timed region)",
-            "sample": f"C/OpenMP + OpenBLAS restatement (oracle/cpu_ref), {int(cores)} threads, at the job's "
-                      f"own sizes: 1 DTC objective eval (N={N}, M={M}, D={d_sample}) = {t_eval:.2f}s + "
-                      f"1 analytic predict (N={N}, N*={NS}) = {t_pred:.2f}s; job = {P - 1} outputs x "
-                      f"({EV} evals + 1 predict) = {t_job:.0f}s (no extrapolation in N)"}
+            "sample": f"C/OpenMP + OpenBLAS restatement (oracle/cpu_ref), {int(cores)} threads, on the "
+                      f"bench's own output {p_chk} (D = {d_sample}) at fixed theta: 1 DTC objective eval "
+                      f"(N={N}, M={M}) = {t_eval:.2f}s + 1 analytic predict (N={N}, N*={NS}) = "
+                      f"{t_pred:.2f}s; job = {P - 1} outputs x ({EV} evals + 1 predict) = {t_job:.0f}s "
+                      "(no extrapolation in N)"}
 
 
 if __name__ == "__main__":

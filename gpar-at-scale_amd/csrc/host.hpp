@@ -30,12 +30,13 @@ struct gpar_ctx {
   hipStream_t side = nullptr;     // second stream: alternate outputs of a batch run here
   hipEvent_t ev_fork = nullptr, ev_join = nullptr;
   hipEvent_t ev_pw = nullptr, ev_pc[2] = {nullptr, nullptr};   // the fit's pipelined Gram stage
-  bool pipeline = true;           // GPAR_PIPELINE=0 turns the pipelined Gram stage off (A/B)
+  // Schedule knobs (gpar_ctx_set_schedule; GPAR_<KNOB> in the environment at creation).  Every
+  // one selects an order or a placement of the same launches, never different arithmetic:
+  // results are bit-identical with any setting (tests/test_gpu_schedule.py).
   // gpar_ctx_set_cu_split(w): the pipelined fit's whitening runs on w CUs of every XCD and the
   // Gram (its co-running correction too) on the other 32 - w, concurrently (CU-masked streams)
   int split_w = 0, split_mask_w = 0;
   bool split_forced = false;      // set explicitly: no problem-size gate (split_active)
-  bool split_dgw = true;          // a w/32 share of the DG items on the whitening CUs
   // s_d: the round-overlapping fit's dense tails, on the whitening CUs (fit_overlapped)
   hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr, s_d = nullptr;
   hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
@@ -65,15 +66,17 @@ struct gpar_ctx {
   };
   Staging stage[2];
   Staging* staging = nullptr;
-  bool overlap = true;            // gpar_ctx_set_fit_overlap (GPAR_OVERLAP=0 at creation): A/B
-  // gpar_fit_predict's predictions alternate over two streams (GPAR_PREDICT_LANES=1: one)
-  int predict_lanes = 2;
-  bool predict_fused = true;      // GPAR_PREDICT_FUSED=0: predict_rows + gemm_nt (A/B)
-  bool qu_batch = true;           // GPAR_QU_BATCH=0: gpar_fit_predict's q(u) per output (A/B)
-  bool dense_early = true;        // GPAR_DENSE_EARLY=0: the whole dense tail after the round's Grams (A/B)
-  int overlap_max = 16;           // GPAR_OVERLAP_MAX: largest call that takes the round overlap (kOverlapMaxOutputs; A/B)
-  int overlap_b = 0;              // GPAR_OVERLAP_B: size of the overlap's second group (0: halves; A/B)
-  bool split_head = true;         // GPAR_SPLIT_HEAD=0: the split round's first job on the whitening CUs, gains in one launch (A/B)
+  bool overlap = true;            // "overlap": round-overlapping batched fit (gpar_ctx_set_fit_overlap)
+  int predict_lanes = 2;          // "predict_lanes": gpar_fit_predict's predictions over 1 or 2 streams
+  bool predict_fused = true;      // "predict_fused": predict_var (off: predict_rows + gemm_nt; last bits differ)
+  bool qu_batch = true;           // "qu_batch": gpar_fit_predict's q(u) batched over the outputs
+  bool dense_early = true;        // "dense_early": the G-independent dense tail ahead of the round's Grams
+  bool split_head = true;         // "split_head": the split round's first whitening whole-chip, gains on two streams
+  // "serialize": side, s_w, s_g, s_g2 and s_d all alias `main`, so every launch runs in issue order
+  // on one stream (the created streams stay in own_*): the order-free reference the concurrent
+  // schedule must equal bit for bit.  Plans, CU shares of work items and workspaces are unchanged.
+  bool serialize = false;
+  hipStream_t own_side = nullptr, own_s[4] = {nullptr, nullptr, nullptr, nullptr};
   std::string ws_suffix;          // appended to workspace names (a prediction lane's own buffers)
   hipEvent_t ev_grp[2] = {nullptr, nullptr};   // fit_overlapped: a group's values are in
   hipEvent_t ev_gn[2] = {nullptr, nullptr};    // fit_overlapped: a group's gains are done
@@ -351,13 +354,9 @@ struct SplitPipe {
     {
       OnStream on_(c, c->s_g);
       HIPCHECK(hipStreamWaitEvent(c->s_g, c->ev_pc[i & 1], 0));
-      if (c->split_dgw) {
-        if (i >= 1) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[(i - 1) & 1], 0));
-        stage_gram(c, pending, buf[i & 1], false, false, "", c->s_g2, gcus, c->s_w, c->ev_pw,
-                   c->split_w);
-      } else {
-        stage_gram(c, pending, buf[i & 1], false, false, "", c->s_g2, gcus);
-      }
+      if (i >= 1) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[(i - 1) & 1], 0));
+      stage_gram(c, pending, buf[i & 1], false, false, "", c->s_g2, gcus, c->s_w, c->ev_pw,
+                 c->split_w);
       HIPCHECK(hipEventRecord(c->ev_gd[i & 1], c->s_g));
     }
     has_pending = false;

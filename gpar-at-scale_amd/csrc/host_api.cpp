@@ -1,6 +1,8 @@
 // host_api.cpp -- context lifetime, options, telemetry and gpar_dtc_objective.
 #include "host.hpp"
 
+#include <cctype>
+
 namespace gpar {
 
 // Entry: order the context's streams after the caller's input stream (if one was set).
@@ -21,11 +23,17 @@ int fail(gpar_ctx* c, int code, const char* what) {
   c->err = what;
   c->stream = c->main;
   (void)hipStreamSynchronize(c->main);
-  (void)hipStreamSynchronize(c->side);
-  for (hipStream_t st : {c->s_w, c->s_g, c->s_g2, c->s_d})
+  for (hipStream_t st : {c->own_side, c->own_s[0], c->own_s[1], c->own_s[2], c->own_s[3]})
     if (st) (void)hipStreamSynchronize(st);
   (void)hipGetLastError();
   return code;
+}
+
+// The stream handles launches use: the created streams, or all `main` when serialized.
+static void route_streams(gpar_ctx* c) {
+  c->side = c->serialize ? c->main : c->own_side;
+  hipStream_t* act[4] = {&c->s_w, &c->s_g, &c->s_g2, &c->s_d};
+  for (int i = 0; i < 4; ++i) *act[i] = (c->serialize && c->own_s[i]) ? c->main : c->own_s[i];
 }
 
 // CU split of the pipelined fit (gpar_ctx_set_cu_split): CU-masked streams for the whitening
@@ -40,21 +48,24 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
     if (hipGetDeviceProperties(&pr, c->device) != hipSuccess) return GPAR_ERR_HIP;
     if (pr.multiProcessorCount != 256) return GPAR_ERR_UNSUPPORTED;   // the MI355X layout only
     // a stream's CU mask is fixed at its creation: a new width gets new streams
-    for (hipStream_t* st : {&c->s_w, &c->s_g, &c->s_g2, &c->s_d})
-      if (*st) {
-        (void)hipStreamSynchronize(*st);
-        (void)hipStreamDestroy(*st);
-        *st = nullptr;
+    for (hipStream_t& st : c->own_s)
+      if (st) {
+        (void)hipStreamSynchronize(st);
+        (void)hipStreamDestroy(st);
+        st = nullptr;
       }
+    route_streams(c);
     c->split_mask_w = 0;
     c->split_w = 0;
+    // own_s: s_w (whitening), s_g (Gram), s_g2 (its co-running correction), s_d (dense tails)
     uint32_t mw[8] = {0}, mg[8] = {0};
     for (int i = 0; i < 256; ++i) (i < 8 * w ? mw : mg)[i / 32] |= 1u << (i % 32);
-    if (hipExtStreamCreateWithCUMask(&c->s_w, 8, mw) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&c->s_g, 8, mg) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&c->s_g2, 8, mg) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&c->s_d, 8, mw) != hipSuccess)
+    if (hipExtStreamCreateWithCUMask(&c->own_s[0], 8, mw) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&c->own_s[1], 8, mg) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&c->own_s[2], 8, mg) != hipSuccess ||
+        hipExtStreamCreateWithCUMask(&c->own_s[3], 8, mw) != hipSuccess)
       return GPAR_ERR_HIP;
+    route_streams(c);
     if (!c->ev_sp &&
         (hipEventCreateWithFlags(&c->ev_gd[0], hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_gd[1], hipEventDisableTiming) != hipSuccess ||
@@ -67,6 +78,45 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
   }
   c->split_w = w;
   c->split_forced = forced;
+  return GPAR_OK;
+}
+
+static constexpr const char* kScheduleKnobs[] = {"overlap", "predict_fused", "qu_batch",
+                                                  "dense_early", "split_head", "predict_lanes",
+                                                  "serialize"};
+
+// gpar_ctx_set_schedule / gpar_ctx_get_schedule (GPAR_ERR_ARG: unknown knob or value).
+static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
+  if (k == "overlap") c->overlap = v != 0;
+  else if (k == "predict_fused") c->predict_fused = v != 0;
+  else if (k == "qu_batch") c->qu_batch = v != 0;
+  else if (k == "dense_early") c->dense_early = v != 0;
+  else if (k == "split_head") c->split_head = v != 0;
+  else if (k == "predict_lanes") {
+    if (v != 1 && v != 2) return GPAR_ERR_ARG;
+    c->predict_lanes = v;
+  } else if (k == "serialize") {
+    // the streams about to be re-routed must not hold queued work
+    (void)hipStreamSynchronize(c->main);
+    for (hipStream_t st : {c->own_side, c->own_s[0], c->own_s[1], c->own_s[2], c->own_s[3]})
+      if (st) (void)hipStreamSynchronize(st);
+    c->serialize = v != 0;
+    route_streams(c);
+  } else {
+    return GPAR_ERR_ARG;
+  }
+  return GPAR_OK;
+}
+
+static int get_schedule(const gpar_ctx* c, const std::string& k, int32_t* v) {
+  if (k == "overlap") *v = c->overlap;
+  else if (k == "predict_fused") *v = c->predict_fused;
+  else if (k == "qu_batch") *v = c->qu_batch;
+  else if (k == "dense_early") *v = c->dense_early;
+  else if (k == "split_head") *v = c->split_head;
+  else if (k == "predict_lanes") *v = c->predict_lanes;
+  else if (k == "serialize") *v = c->serialize;
+  else return GPAR_ERR_ARG;
   return GPAR_OK;
 }
 }  // namespace gpar
@@ -84,7 +134,7 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
   auto* c = new gpar_ctx();
   c->device = device;
   if (hipStreamCreateWithFlags(&c->main, hipStreamNonBlocking) != hipSuccess ||
-      hipStreamCreateWithFlags(&c->side, hipStreamNonBlocking) != hipSuccess ||
+      hipStreamCreateWithFlags(&c->own_side, hipStreamNonBlocking) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
       hipEventCreateWithFlags(&c->ev_input, hipEventDisableTiming) != hipSuccess ||
@@ -95,18 +145,14 @@ int32_t gpar_ctx_create(int32_t device, gpar_ctx** out) {
     return GPAR_ERR_HIP;
   }
   c->stream = c->main;
-  if (const char* e = std::getenv("GPAR_PIPELINE")) c->pipeline = std::atoi(e) != 0;
-  if (const char* e = std::getenv("GPAR_OVERLAP")) c->overlap = std::atoi(e) != 0;
-  if (const char* e = std::getenv("GPAR_PREDICT_FUSED")) c->predict_fused = std::atoi(e) != 0;
-  if (const char* e = std::getenv("GPAR_QU_BATCH")) c->qu_batch = std::atoi(e) != 0;
-  if (const char* e = std::getenv("GPAR_DENSE_EARLY")) c->dense_early = std::atoi(e) != 0;
-  if (const char* e = std::getenv("GPAR_OVERLAP_MAX")) c->overlap_max = std::atoi(e);
-  if (const char* e = std::getenv("GPAR_OVERLAP_B")) c->overlap_b = std::atoi(e);
-  if (const char* e = std::getenv("GPAR_SPLIT_HEAD")) c->split_head = std::atoi(e) != 0;
-  if (const char* e = std::getenv("GPAR_PREDICT_LANES")) c->predict_lanes = std::atoi(e) > 1 ? 2 : 1;
-  // A/B knobs: GPAR_SPLIT_CUS overrides the default CU split, GPAR_SPLIT_DGW=0 keeps the DG
-  // kernel off the whitening CUs
-  if (const char* e = std::getenv("GPAR_SPLIT_DGW")) c->split_dgw = std::atoi(e) != 0;
+  route_streams(c);
+  // schedule knobs from the environment (GPAR_OVERLAP=0, GPAR_SERIALIZE=1, ...)
+  for (const char* k : kScheduleKnobs) {
+    std::string env = "GPAR_";
+    for (const char* q = k; *q; ++q) env += (char)std::toupper((unsigned char)*q);
+    if (const char* e = std::getenv(env.c_str())) (void)set_schedule(c, k, std::atoi(e));
+  }
+  // GPAR_SPLIT_CUS overrides the default CU split
   const char* e_split = std::getenv("GPAR_SPLIT_CUS");
   if (e_split)
     (void)set_cu_split(c, std::atoi(e_split), true);
@@ -120,7 +166,7 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
   if (!ctx) return GPAR_ERR_STATE;
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->main);
-  (void)hipStreamSynchronize(ctx->side);
+  (void)hipStreamSynchronize(ctx->own_side);
   for (auto& kv : ctx->bufs)
     if (kv.second.p) (void)hipFree(kv.second.p);
   (void)hipEventDestroy(ctx->ev_fork);
@@ -130,7 +176,7 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
   (void)hipEventDestroy(ctx->ev_pc[0]);
   (void)hipEventDestroy(ctx->ev_pc[1]);
   {
-    for (hipStream_t st : {ctx->s_w, ctx->s_g, ctx->s_g2, ctx->s_d})
+    for (hipStream_t st : ctx->own_s)
       if (st) {
         (void)hipStreamSynchronize(st);
         (void)hipStreamDestroy(st);
@@ -141,7 +187,7 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
     for (auto& s : ctx->stage)
       if (s.host) (void)hipHostFree(s.host);
   }
-  (void)hipStreamDestroy(ctx->side);
+  (void)hipStreamDestroy(ctx->own_side);
   (void)hipStreamDestroy(ctx->main);
   delete ctx;
   return GPAR_OK;
@@ -231,6 +277,20 @@ int32_t gpar_ctx_set_fit_overlap(gpar_ctx* ctx, int32_t on) {
   if (!ctx) return GPAR_ERR_STATE;
   ctx->overlap = on != 0;
   return GPAR_OK;
+}
+
+int32_t gpar_ctx_set_schedule(gpar_ctx* ctx, const char* knob, int32_t value) {
+  if (!ctx) return GPAR_ERR_STATE;
+  const int rc = knob ? set_schedule(ctx, knob, value) : GPAR_ERR_ARG;
+  if (rc != GPAR_OK)
+    ctx->err = std::string("gpar_ctx_set_schedule: unknown knob or bad value: ") + (knob ? knob : "(null)");
+  return rc;
+}
+
+int32_t gpar_ctx_get_schedule(const gpar_ctx* ctx, const char* knob, int32_t* value) {
+  if (!ctx) return GPAR_ERR_STATE;
+  if (!knob || !value) return GPAR_ERR_ARG;
+  return get_schedule(ctx, knob, value);
 }
 
 int32_t gpar_ctx_get_cu_split(const gpar_ctx* ctx, int32_t* cus_per_xcd) {

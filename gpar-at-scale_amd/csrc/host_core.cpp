@@ -114,7 +114,7 @@ bool fit_pipelined(const gpar_ctx* c, const std::vector<DevProblem>& P, bool fix
   int64_t mpmax = 0;
   for (auto& p : P) mpmax = std::max(mpmax, p.mp);
   const int64_t beta_bytes = (P[0].n + 16) * mpmax * (int64_t)sizeof(double);
-  return P.size() > 1 && !fix_beta && c->lanes == 1 && shares_grid(P) && c->pipeline &&
+  return P.size() > 1 && !fix_beta && c->lanes == 1 && shares_grid(P) &&
          beta_bytes <= kPipeMaxBetaBytes;
 }
 

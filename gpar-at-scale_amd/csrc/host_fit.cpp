@@ -173,14 +173,8 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
   for (hipEvent_t* ev : {&c->ev_grp[0], &c->ev_grp[1], &c->ev_gn[0], &c->ev_gn[1]})
     if (!*ev) HIPCHECK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
   OverlapGroup grp[2];
-  // outputs dealt alternately; with c->overlap_b > 0 (A/B) group B is every k-th output instead
-  // (about overlap_b of them), group A the rest
-  if (c->overlap_b > 0 && c->overlap_b < np) {
-    const int k = std::max(2, np / c->overlap_b);
-    for (int i = 0; i < np; ++i) grp[(i % k == k - 1) ? 1 : 0].members.push_back(i);
-  } else {
-    for (int i = 0; i < np; ++i) grp[i & 1].members.push_back(i);
-  }
+  // outputs dealt alternately (unequal groups measured slower at 63 outputs, r03w)
+  for (int i = 0; i < np; ++i) grp[i & 1].members.push_back(i);
   for (int g = 0; g < 2; ++g) {
     OverlapGroup& G = grp[g];
     G.id = g;
@@ -376,7 +370,7 @@ void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* lo
   };
   int64_t mpmax = 0;
   for (auto& p : P) mpmax = std::max(mpmax, p.mp);
-  if (ctx->overlap && nprob >= 4 && nprob <= ctx->overlap_max && fit_pipelined(ctx, P) &&
+  if (ctx->overlap && nprob >= 4 && nprob <= kOverlapMaxOutputs && fit_pipelined(ctx, P) &&
       split_active(ctx, P[0].n, mpmax))
     fit_overlapped(ctx, P, nm, accept);
   std::vector<double> vals;

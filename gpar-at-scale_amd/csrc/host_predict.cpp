@@ -210,6 +210,9 @@ void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
                          double* std_out, const GramCache* gc, bool defer,
                          const QuPre* pre) {
   const int64_t n = P.n, m = P.m, d = P.d, mp = P.mp, mc = P.mc;
+  if (mode == GPAR_PREDICT_PATH)   // path draw (s, k, i): counter index k (sdim + 1) + i, 32 bits
+    ARGCHECK((n + n_star) * (P.sdim + 1) <= ((int64_t)1 << 32),
+             "path mode: (n + n_star) * (state dimension + 1) must be <= 2^32");
   // ---- test inputs on device, ascending (host inputs are stably sorted here, outputs
   //      un-permuted at the end; device inputs must already be ascending)
   std::vector<int64_t> perm;
@@ -339,8 +342,8 @@ void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
                  /*take_sqrt=*/P.ok != GPAR_EQ);
     launch_kfu_from_dist(c->stream, P.ok, Ks, nt, m, mp, 1.0 / th.l_o, th.sv_o * th.sv_o);
     double* FX = ws<double>(c, "pr_FX", (size_t)nt * samples);
-    double* fxsq = ws<double>(c, "pr_fxsq", (size_t)nt);
-    launch_gemm_nt(c->stream, Ks, mp, Bm, mp, nt, samples, m, 0, FX, samples, fxsq, 0, nullptr,
+    // FX only: no row sums (mode 0 writes them per 128-column block when asked)
+    launch_gemm_nt(c->stream, Ks, mp, Bm, mp, nt, samples, m, 0, FX, samples, nullptr, 0, nullptr,
                    nullptr, nullptr, 0);
     check_launch("predict: path fx");
     double* F = ws<double>(c, "pr_F", (size_t)nt * samples);
@@ -656,8 +659,9 @@ int32_t gpar_lgssm_posterior_rand(gpar_ctx* ctx, int64_t n, const double* t, con
   ARGCHECK(n >= 1 && t && y && theta && f_out, "bad argument");
   ARGCHECK(samples >= 1 && samples <= kMaxSamples, "samples must be in 1..65536");
   ARGCHECK(mem == GPAR_MEM_HOST || mem == GPAR_MEM_DEVICE, "bad mem");
-  ARGCHECK(n <= ((int64_t)1 << 32) / 3, "n out of range");
   const int sdim = sde_dim(kernel);
+  // draw (s, k, i) is counter_normal(seed, s, k (sdim + 1) + i): the index must fit 32 bits
+  ARGCHECK(n * (sdim + 1) <= ((int64_t)1 << 32), "n * (state dimension + 1) must be <= 2^32");
   std::vector<ChainParamsHost> cps = chain_params(theta, 1);
   const double *dt = t, *dy = y, *dn = noise;
   if (mem == GPAR_MEM_HOST) {

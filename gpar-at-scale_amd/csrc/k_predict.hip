@@ -117,7 +117,8 @@ __global__ __launch_bounds__(256) void predict_rows(const double* __restrict__ X
 // A: rows x K (row-major, lda), B: cols x K (row-major, ldb); 128 x 128 tile per 256-thread
 // block (2 x 2 waves of 4 x 4 v_mfma_f64_16x16x4_f64), K-step 16 through LDS (k-major,
 // padded rows: conflict-free fragment reads, see k_gram.hip).
-// Epilogues: mode 0: C written (ldc) + rowsq[colblock][row] = sum_c C^2 over the tile;
+// Epilogues: mode 0: C written (ldc) + rowsq[colblock][row] = sum_c C^2 over the tile (rowsq
+//            null: C only);
 //            mode 1: MC statistics over the tile's first `valid_cols` columns:
 //                    out0[row] = base[row] + mean_c C, out1[row] = Bessel std_c C;
 //            mode 2: rowsq[colblock][row][2] = (sum_c C, sum_c C^2) over the tile's columns
@@ -244,7 +245,7 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(
       const double t1 = red[(0 * 128 + tid) * 2 + 0] + red[(1 * 128 + tid) * 2 + 0];
       const double t2 = red[(0 * 128 + tid) * 2 + 1] + red[(1 * 128 + tid) * 2 + 1];
       if (mode == 0) {
-        rowsq[(int64_t)blockIdx.y * rows + row] = t2;
+        if (rowsq) rowsq[(int64_t)blockIdx.y * rows + row] = t2;
       } else if (mode == 2) {
         // MC over more than one 128-column tile: partial sum / sum of squares of this tile
         rowsq[((int64_t)blockIdx.y * rows + row) * 2 + 0] = t1;

@@ -12,8 +12,6 @@ import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "..", "libgparhip.so"))
-# timing ablations only (tools/build_abl.sh builds variants next to the library)
-LIB_PATH = os.environ.get("GPAR_LIB_PATH", LIB_PATH)
 
 GPAR_OK, GPAR_ERR_ARG, GPAR_ERR_NOT_PD, GPAR_ERR_HIP, GPAR_ERR_OOM, GPAR_ERR_UNSUPPORTED, GPAR_ERR_STATE = range(7)
 GPAR_MEM_HOST, GPAR_MEM_DEVICE = 0, 1
@@ -28,7 +26,8 @@ EXPORTED = (
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
     "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_kernel_work", "gpar_ctx_reset_stats",
     "gpar_ctx_set_lanes", "gpar_ctx_set_cu_split", "gpar_ctx_set_fit_overlap", "gpar_ctx_get_cu_split", "gpar_ctx_set_dist_cache", "gpar_ctx_set_dist_cache_keep", "gpar_ctx_dist_cache_stats",
-    "gpar_pairwise_distances", "gpar_ctx_set_predict_fused", "gpar_ctx_set_input_stream", "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
+    "gpar_pairwise_distances", "gpar_ctx_set_predict_fused", "gpar_ctx_set_input_stream", "gpar_ctx_set_schedule", "gpar_ctx_get_schedule",
+    "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
 )
 
 
@@ -101,6 +100,8 @@ def load(path: str | None = None):
             "gpar_ctx_set_cu_split": (i32, [vp, i32]),
             "gpar_ctx_get_cu_split": (i32, [vp, C.POINTER(C.c_int32)]),
             "gpar_ctx_set_fit_overlap": (i32, [vp, i32]),
+            "gpar_ctx_set_schedule": (i32, [vp, C.c_char_p, i32]),
+            "gpar_ctx_get_schedule": (i32, [vp, C.c_char_p, C.POINTER(i32)]),
             "gpar_ctx_set_dist_cache": (i32, [vp, i64]),
             "gpar_ctx_set_dist_cache_keep": (i32, [vp, i32]),
             "gpar_ctx_dist_cache_stats": (i32, [vp, C.POINTER(i32), C.POINTER(i32), C.POINTER(i64)]),
@@ -263,6 +264,17 @@ class Context:
         """Fused rows + variance kernel of the ANALYTIC prediction (gpar_ctx_set_predict_fused;
         default on, m <= 512)."""
         self.check(load().gpar_ctx_set_predict_fused(self.h, 1 if on else 0))
+
+    def set_schedule(self, knob, value):
+        """A schedule knob (gpar_ctx_set_schedule: pipeline, overlap, qu_batch, dense_early,
+        split_head, predict_lanes, serialize, predict_fused); results are bit-identical with any
+        setting except predict_fused."""
+        self.check(load().gpar_ctx_set_schedule(self.h, knob.encode(), int(value)))
+
+    def schedule(self, knob):
+        v = C.c_int32(0)
+        self.check(load().gpar_ctx_get_schedule(self.h, knob.encode(), C.byref(v)))
+        return int(v.value)
 
     def cu_split(self):
         """The CU split in effect (gpar_ctx_get_cu_split)."""

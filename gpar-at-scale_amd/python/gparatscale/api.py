@@ -405,7 +405,7 @@ def path_normals(samples, n, d, seed, device=0):
 def posterior_rand(t, y, theta, kernel="matern52", samples=1, seed=0, noise=None, device=0):
     """TemporalGPs posterior_rand(rng, create_lgssm(t, l, pv, sigma, k; noise_vector), y, samples)
     (called at src/gp/tmp.jl:161-167): joint draws of the latent f over t from its posterior given
-    y, by forward filtering and backward sampling (gpar_lgssm_posterior_rand).  theta = (l,
+    y, by the Durbin-Koopman simulation smoother (gpar_lgssm_posterior_rand).  theta = (l,
     process_var, noise_sigma); noise: per-step observation variance (None: sigma^2).  Host arrays
     -> samples x n numpy array; torch CUDA tensors -> samples x n device tensor."""
     ctx, lib = context(device), _lib.load()
@@ -414,6 +414,9 @@ def posterior_rand(t, y, theta, kernel="matern52", samples=1, seed=0, noise=None
     if _is_torch(t):
         import torch
         n = t.numel()
+        # the C side cannot see device buffer lengths (as make_problem checks for the GPAR inputs)
+        if y.numel() != n or (noise is not None and noise.numel() != n):
+            raise _arg_error("t, y (and noise) must have the same length")
         out = torch.empty((int(samples), n), dtype=torch.float64, device=t.device)
         tp, yp = _dev_vec(t, keep), _dev_vec(y, keep)
         npp = _dev_vec(noise, keep) if noise is not None else None

@@ -144,6 +144,21 @@ int32_t gpar_ctx_set_fit_overlap(gpar_ctx* ctx, int32_t on);
  * in one fused kernel (predict_var), Q never stored; off: predict_rows writes Q and gemm_nt reads
  * it.  Same quantities, summed in a different order (last bits). */
 int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
+/* Schedule knobs: each selects an order or a placement of the same launches, never different
+ * arithmetic, so results are bit-identical with any setting (tests/test_gpu_schedule.py):
+ *   "overlap"       1: round-overlapping batched fit, as gpar_ctx_set_fit_overlap (default 1)
+ *   "qu_batch"      1: gpar_fit_predict runs q(u) batched over the outputs (default 1)
+ *   "dense_early"   1: the G-independent half of the dense tail ahead of a split round's Grams (1)
+ *   "split_head"    1: a split round's first whitening on the whole chip (default 1)
+ *   "predict_lanes" 1 or 2: streams gpar_fit_predict's predictions alternate over (default 2)
+ *   "serialize"     1: every launch of every schedule on the context's one stream, in issue order,
+ *                   with the same plans, CU shares of work items and workspaces: the order-free
+ *                   reference the concurrent schedule equals bit for bit (default 0)
+ *   "predict_fused" as gpar_ctx_set_predict_fused (changes the summation order: last bits)
+ * The environment variable GPAR_<KNOB> (upper case) sets a knob at context creation.
+ * GPAR_ERR_ARG for an unknown knob or value. */
+int32_t gpar_ctx_set_schedule(gpar_ctx* ctx, const char* knob, int32_t value);
+int32_t gpar_ctx_get_schedule(const gpar_ctx* ctx, const char* knob, int32_t* value);
 /* The CU split in effect (0 when off or unsupported). */
 int32_t gpar_ctx_get_cu_split(const gpar_ctx* ctx, int32_t* cus_per_xcd);
 /* Distance cache of gpar_fit / gpar_fit_predict: the input distances |v_k - z_c| (squared for EQ)

@@ -46,7 +46,16 @@ const libgpar = get(ENV, "GPAR_HIP_LIB", "libgparhip.so")
 const GPAR_ABI_VERSION = Int32(1)
 const GPAR_OK, GPAR_ERR_ARG, GPAR_ERR_NOT_PD = Int32(0), Int32(1), Int32(2)
 const GPAR_MEM_HOST = Int32(0)
-const GPAR_PREDICT_ANALYTIC, GPAR_PREDICT_MC = Int32(0), Int32(1)
+const GPAR_PREDICT_ANALYTIC, GPAR_PREDICT_MC, GPAR_PREDICT_PATH = Int32(0), Int32(1), Int32(2)
+
+# prediction estimator: :mc (the reference's, gpar_scaled_inference.jl:110-130), :analytic (its
+# S -> infinity limit) or :path (tmp.jl:119-167, posterior_rand paths); anything else is an error
+function predict_mode(mode::Symbol)
+    mode === :mc && return GPAR_PREDICT_MC
+    mode === :analytic && return GPAR_PREDICT_ANALYTIC
+    mode === :path && return GPAR_PREDICT_PATH
+    throw(DomainError(mode, "mode must be :mc, :analytic or :path"))
+end
 
 kernel_id(::Matern12) = Int32(0)
 kernel_id(::Matern32) = Int32(1)
@@ -269,7 +278,7 @@ function get_gpar_scaled_predictions(input_locations, pseudo_input_locations, ti
     t = Vector{Float64}(time_loc)
     y = Vector{Float64}(outputs)
     ts = Vector{Float64}(inference_time_loc)
-    md = mode === :mc ? GPAR_PREDICT_MC : GPAR_PREDICT_ANALYTIC
+    md = predict_mode(mode)
     x0 = Vector{Float64}(parse_initial_gpar_params(i_log_time_l, i_log_time_var, i_log_out_l,
                                                    i_log_out_var, i_log_noise_sigma))
     debug && println("Starting optimization")
@@ -356,7 +365,7 @@ function get_gpar_scaled_predictions_batch(input_locations, pseudo_input_locatio
     probs = [problem(Vs[i], Zs[i], t, ys[i], Matern52(), Matern52()) for i in 1:P]
     x0 = reduce(vcat, [Vector{Float64}(parse_initial_gpar_params(i_log_time_l, i_log_time_var,
                        i_log_out_l, i_log_out_var, i_log_noise_sigma)) for _ in 1:P])
-    md = mode === :mc ? GPAR_PREDICT_MC : GPAR_PREDICT_ANALYTIC
+    md = predict_mode(mode)
     θ = zeros(5 * P)
     nlml = zeros(P)
     ev = zeros(Int32, P)

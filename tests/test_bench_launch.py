@@ -44,3 +44,42 @@ def test_launcher_refuses_missing_devices():
     r = _bench("--gpus", "2")
     assert r.returncode == 2
     assert "device(s) visible" in r.stderr
+
+
+def test_launcher_parent_never_initialises_hip(monkeypatch, capfd):
+    """the launcher parent must stay HIP-free.  Every torch entry point that
+    could initialise HIP raises here; the parent still counts devices, spawns the ranks and
+    forwards rank 0's line (the stub ranks are separate processes)."""
+    import importlib.util
+    import torch
+
+    def boom(*a, **k):
+        raise AssertionError("the launcher parent initialised HIP")
+
+    monkeypatch.setattr(torch._C, "_cuda_getDeviceCount", boom, raising=False)
+    monkeypatch.setattr(torch.cuda, "device_count", boom)
+    monkeypatch.setattr(torch.cuda, "is_available", boom)
+    monkeypatch.setattr(torch.cuda, "init", boom)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        monkeypatch.delenv(k, raising=False)
+    spec = importlib.util.spec_from_file_location("bench_launch_check", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    assert bench.launch_ranks(2, ["--gpus", "2", "--stub"], stub=True) == 0
+    line = json.loads(capfd.readouterr().out.strip().splitlines()[-1])
+    assert line["n_gpus"] == 2
+
+
+def test_visible_gpu_count_reads_kfd_topology(tmp_path):
+    import importlib.util
+    spec = importlib.util.spec_from_file_location("bench_count_check", os.path.join(ROOT, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    for i, gid in enumerate([0, 0, 51234, 7781, 9123]):   # two CPU nodes, three GPUs
+        (tmp_path / str(i)).mkdir()
+        (tmp_path / str(i) / "gpu_id").write_text(f"{gid}\n")
+    (tmp_path / "junk").mkdir()                           # no gpu_id file: ignored
+    assert bench.visible_gpu_count(str(tmp_path), env={}) == 3
+    assert bench.visible_gpu_count(str(tmp_path), env={"HIP_VISIBLE_DEVICES": "0,1"}) == 2
+    assert bench.visible_gpu_count(str(tmp_path), env={"ROCR_VISIBLE_DEVICES": ""}) == 0
+    assert bench.visible_gpu_count(str(tmp_path / "absent"), env={}) == 0

@@ -13,6 +13,12 @@ the N x P output matrix), and is compared with
     prediction (gpar_scaled_inference.jl:20-136, q(u) with Cuu + sigma^2 I as the bench) rtol 1e-7.
 The cached distances themselves (dist2 at D = 1..16, the range the all-D cache added) are checked
 against direct differences in test_gpu_dist_cache.py.
+
+The bench predicts at N* = N test times interleaved with the training times, where predict_var's
+64-row panels lie within two chunks of the merged grid and take its LDS-DMA prefetching path, and
+the predictions alternate over two lanes.  That layout runs here too: N = N* =
+4e5, two outputs (D = 8, 32) through fit_predict_batch on the headline schedule, each output's
+objective and prediction against the C port.
 """
 import os
 import subprocess
@@ -110,3 +116,51 @@ def test_headline_output_matches_cpu_port(runs, CR, i):
                                                   qu_kuu_noise=True)
     np.testing.assert_allclose(means[i], rm, rtol=1e-7, atol=1e-8 * np.abs(rm).max())
     np.testing.assert_allclose(stds[i], rs, rtol=1e-7, atol=1e-8 * np.abs(rs).max())
+
+
+NN_OUTS = [9, 33]                   # D = 8, 32
+
+
+@pytest.fixture(scope="module")
+def runs_nn():
+    import torch
+    dev = torch.device("cuda", 0)
+    ds = D.gpar_dataset(N, max(NN_OUTS), seed=0, observation_noise=0.8)   # N* = N, interleaved
+    assert len(ds["t_star"]) == N
+    Y_d = torch.from_numpy(ds["Y"]).to(dev)
+    t_d = torch.from_numpy(ds["t"]).to(dev)
+    ts_d = torch.from_numpy(ds["t_star"]).to(dev)
+    Fs_d = torch.from_numpy(ds["F_star"]).to(dev)
+    probs, keep, Zs = [], [], {}
+    for p in NN_OUTS:
+        Zs[p] = D.pseudo_inputs(ds["Y"][:, : p - 1], M, seed=p)
+        pr, k = G.make_problem(Y_d[:, : p - 1], torch.from_numpy(Zs[p]).to(dev), t_d,
+                               Y_d[:, p - 1].contiguous(), "matern52", "matern52", qu_kuu_noise=True)
+        probs.append(pr)
+        keep.append(k)
+    x0 = np.tile([0.0, 0.0, 0.0, 0.0, -2.0], (len(NN_OUTS), 1))
+    ctx = G.context(0)
+    ctx.set_cu_split(-1)
+    ctx.set_dist_cache(-1)
+    fr, means, stds = G.fit_predict_batch(probs, x0, ts_d, [Fs_d[:, : p - 1] for p in NN_OUTS],
+                                          max_evals=EV, g_tol=-1.0)
+    return dict(ds=ds, Zs=Zs, fr=fr, means=[m.cpu().numpy() for m in means],
+                stds=[s.cpu().numpy() for s in stds])
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("i", range(len(NN_OUTS)))
+def test_headline_n_star_equals_n_matches_cpu_port(runs_nn, CR, i):
+    p = NN_OUTS[i]
+    ds, fr = runs_nn["ds"], runs_nn["fr"]
+    V = np.ascontiguousarray(ds["Y"][:, : p - 1].T)
+    Z = np.ascontiguousarray(runs_nn["Zs"][p].T)
+    y = np.ascontiguousarray(ds["Y"][:, p - 1])
+    theta = fr.theta[i]
+    ref, _ = CR.compute_gpar_dtc_objective(V, Z, ds["t"], y, theta)
+    assert abs(-fr.nlml[i] - ref) <= 1e-9 * abs(ref), (p, -fr.nlml[i], ref)
+    Vs = np.ascontiguousarray(ds["F_star"][:, : p - 1].T)
+    rm, rs = CR.get_gpar_scaled_predictions_fixed(V, Z, ds["t"], y, ds["t_star"], Vs, theta,
+                                                  qu_kuu_noise=True)
+    np.testing.assert_allclose(runs_nn["means"][i], rm, rtol=1e-7, atol=1e-8 * np.abs(rm).max())
+    np.testing.assert_allclose(runs_nn["stds"][i], rs, rtol=1e-7, atol=1e-8 * np.abs(rs).max())

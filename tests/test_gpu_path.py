@@ -72,11 +72,13 @@ def _gpar_case(kernel="matern52"):
     return V, Z, t, y, ts, Vs
 
 
-@pytest.mark.parametrize("qu_noise", [False, True])
-def test_path_prediction_replays_through_the_oracle(qu_noise):
+@pytest.mark.parametrize("qu_noise,S", [(False, 8), (True, 8), (True, 200)])
+def test_path_prediction_replays_through_the_oracle(qu_noise, S):
+    """S = 200: more than one 128-column block of the f_x GEMM (its row-sum epilogue
+    wrote past a buffer sized for one block)."""
     V, Z, t, y, ts, Vs = _gpar_case()
     theta = (1.3, 0.9, 0.8, 1.1, 0.2)
-    S, seed = 8, 77
+    seed = 77
     mean, std = G.predict_scaled(V, Z, t, y, theta, ts, Vs, mode="path", samples=S, seed=seed,
                                  qu_kuu_noise=qu_noise)
     xi_u = G.mc_normals(S, Z.shape[1], seed).T
@@ -117,3 +119,10 @@ def test_path_arguments():
         G.posterior_rand(t[::-1].copy(), y, (1.0, 1.0, 0.1), samples=2)
     with pytest.raises(G.Unsupported):
         G.posterior_rand(t, y, (1.0, 1.0, 0.1), kernel="eq", samples=2)
+    # device inputs: lengths checked on the host (the C side cannot see them)
+    import torch
+    td, yd = torch.from_numpy(t).cuda(), torch.from_numpy(y).cuda()
+    with pytest.raises(G.DomainError):
+        G.posterior_rand(td, yd[:-1], (1.0, 1.0, 0.1), samples=2)
+    with pytest.raises(G.DomainError):
+        G.posterior_rand(td, yd, (1.0, 1.0, 0.1), samples=2, noise=yd[:10])

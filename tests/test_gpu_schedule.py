@@ -1,0 +1,103 @@
+"""The concurrent schedules against their serialized twin.
+
+The headline schedule runs a batched fit on several CU-masked streams with hand-placed events: the
+whitening of output i + 1 beside the Gram of output i, the Gram's chunk correction on a third
+stream, a share of its diagonal-block items on the whitening CUs, the round-overlapping groups'
+dense tails and gains on a fourth, and the predictions over two lanes.  Three stream-ordering races
+were found in rounds 2-3 (a DG share overwriting partial slots, a first-round dense prefix not
+waiting for the context stream, a q(u) Gram on the wrong lane).
+
+gpar_ctx_set_schedule("serialize", 1) routes every launch of the same schedule to the context's one
+stream, in issue order, with the same Gram plans, CU shares of work items and workspaces: an
+order-free reference.  Any missing dependency in the concurrent schedule shows up as a difference.
+Every other schedule knob (round overlap, the dense prefix, the split round head, batched q(u),
+prediction lanes) only reorders or re-places the same launches, so it must give bit-identical
+results too.  Sizes: the headline test's (N = 4e5, M = 512: the auto CU split, the pipelined Gram
+stage, the distance cache down to D = 1, five outputs: the round overlap).
+"""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+G = pytest.importorskip("gparatscale")
+from gparatscale import data as D  # noqa: E402
+
+N, M, NS, EV = 400_000, 512, 40_000, 6
+OUTS = [2, 3, 9, 17, 33]
+
+SETTINGS = [
+    {"serialize": 1},
+    {"overlap": 0},
+    {"overlap": 0, "serialize": 1},
+    {"overlap": 0, "dense_early": 0},
+    {"overlap": 0, "split_head": 0},
+    {"qu_batch": 0},
+    {"predict_lanes": 1},
+]
+DEFAULTS = {"serialize": 0, "overlap": 1, "dense_early": 1, "split_head": 1, "qu_batch": 1,
+            "predict_lanes": 2}
+
+
+@pytest.fixture(scope="module")
+def job():
+    import torch
+    dev = torch.device("cuda", 0)
+    ds = D.gpar_dataset(N, max(OUTS), seed=0, observation_noise=0.8, n_star=NS)
+    Y_d = torch.from_numpy(ds["Y"]).to(dev)
+    t_d = torch.from_numpy(ds["t"]).to(dev)
+    ts_d = torch.from_numpy(ds["t_star"]).to(dev)
+    Fs_d = torch.from_numpy(ds["F_star"]).to(dev)
+    probs, keep = [], []
+    for p in OUTS:
+        Z = torch.from_numpy(D.pseudo_inputs(ds["Y"][:, : p - 1], M, seed=p)).to(dev)
+        pr, k = G.make_problem(Y_d[:, : p - 1], Z, t_d, Y_d[:, p - 1].contiguous(), "matern52",
+                               "matern52", qu_kuu_noise=True)
+        probs.append(pr)
+        keep.append((k, Z))
+    x0 = np.tile([0.0, 0.0, 0.0, 0.0, -2.0], (len(OUTS), 1))
+    ctx = G.context(0)
+    ctx.set_cu_split(-1)
+    ctx.set_dist_cache(-1)
+    assert ctx.cu_split() == 8
+
+    def run(knobs):
+        for k, v in DEFAULTS.items():
+            ctx.set_schedule(k, v)
+        try:
+            for k, v in knobs.items():
+                ctx.set_schedule(k, v)
+            fr, means, stds = G.fit_predict_batch(probs, x0, ts_d, [Fs_d[:, : p - 1] for p in OUTS],
+                                                  max_evals=EV, g_tol=-1.0)
+            return fr, [m.cpu().numpy() for m in means], [s.cpu().numpy() for s in stds]
+        finally:
+            for k, v in DEFAULTS.items():
+                ctx.set_schedule(k, v)
+
+    base = run({})
+    return run, base, keep
+
+
+def test_schedule_knobs_round_trip():
+    ctx = G.context(0)
+    for k, v in DEFAULTS.items():
+        assert ctx.schedule(k) == v
+    ctx.set_schedule("serialize", 1)
+    assert ctx.schedule("serialize") == 1
+    ctx.set_schedule("serialize", 0)
+    with pytest.raises(G.DomainError):
+        ctx.set_schedule("no_such_knob", 1)
+    with pytest.raises(G.DomainError):
+        ctx.set_schedule("predict_lanes", 3)
+
+
+@pytest.mark.parametrize("knobs", SETTINGS, ids=lambda k: ",".join(f"{a}={b}" for a, b in k.items()))
+def test_schedule_is_bit_identical(job, knobs):
+    run, (fr0, m0, s0), _ = job
+    fr, m, s = run(knobs)
+    np.testing.assert_array_equal(fr.theta, fr0.theta)
+    np.testing.assert_array_equal(fr.nlml, fr0.nlml)
+    np.testing.assert_array_equal(fr.evals, fr0.evals)
+    for i in range(len(OUTS)):
+        np.testing.assert_array_equal(m[i], m0[i])
+        np.testing.assert_array_equal(s[i], s0[i])

@@ -243,3 +243,23 @@ def test_multi_output_driver_binds_the_batched_entry_points():
         assert k in kw, k
     assert "get_gpar_scaled_predictions_batch" in re.search(r"export ([\w,\s]+)\n", src).group(1)
     assert "return means, stds" in body
+
+
+def test_prediction_modes_map_explicitly():
+    """every gpar_predict_mode the header declares has a Julia constant of the same
+    value, and the mode keyword maps :analytic / :mc / :path explicitly (anything else is a
+    DomainError, not a silent ANALYTIC)."""
+    src = open(SHIM).read()
+    enum = re.search(r"typedef enum gpar_predict_mode \{(.*?)\}", _header(), re.S).group(1)
+    c_vals = dict(re.findall(r"(GPAR_PREDICT_\w+)\s*=\s*(\d+)", enum))
+    names = re.search(r"const (GPAR_PREDICT_\w+(?:, GPAR_PREDICT_\w+)*) = (.*)", src)
+    jl_vals = dict(zip([n.strip() for n in names.group(1).split(",")],
+                       re.findall(r"Int32\((\d+)\)", names.group(2))))
+    assert jl_vals == c_vals
+    body = re.search(r"function predict_mode\(mode::Symbol\)(.*?)\nend", src, re.S).group(1)
+    for sym, const in ((":mc", "GPAR_PREDICT_MC"), (":analytic", "GPAR_PREDICT_ANALYTIC"),
+                       (":path", "GPAR_PREDICT_PATH")):
+        assert f"mode === {sym} && return {const}" in body
+    assert "throw(DomainError(mode" in body
+    assert "mode === :mc ? " not in src
+    assert src.count("md = predict_mode(mode)") == 2
