@@ -8,11 +8,14 @@ QuOut run_q_u(gpar_ctx* c, const DevProblem& p, const Theta& th,
                      const GramCache* gc) {
   std::vector<DevProblem> P{p};
   std::vector<Theta> T{th};
-  // The extra beta fix-up pass is for the noise-free Cuu only; with qu_kuu_noise the factor is
-  // the objective's regularised Kuu + s2 I and the objective's correction-form Gram is enough --
-  // the very Gram the fit computed at this theta, when the caller hands it over (gc).
+  // G = beta^T beta and r = beta^T alpha do not depend on Cuu's jitter (only L_u does,
+  // gpar_scaled_inference.jl:157-187), so the Gram the fit computed at this theta is reused for
+  // either q(u) convention when the caller hands it over (gc: gpar_fit_predict).  Recomputed
+  // (gpar_predict, gpar_q_u), the noise-free Cuu takes the extra beta fix-up pass: a plain
+  // beta^T beta of the true beta carries ~10x less rounding than the correction form, which its
+  // cond(Cuu) up to ~1e10 amplifies.
   GramOut go;
-  if (gc && gc->G && p.qu_noise) {
+  if (gc && gc->G) {
     go.ldg = p.mp;
     go.npart = 1;
     go.G = const_cast<double*>(gc->G);
@@ -67,7 +70,7 @@ std::vector<QuPre> run_q_u_batch(gpar_ctx* c, const std::vector<DevProblem>& P,
   int64_t mpmax = 0, mmax = 0;
   for (const auto& p : P) { mpmax = std::max(mpmax, p.mp); mmax = std::max(mmax, p.m); }
   const bool qn = P[0].qu_noise;
-  bool kept = qn;
+  bool kept = true;   // the fit's Grams serve both q(u) conventions (run_q_u)
   for (int i = 0; i < np; ++i)
     kept = kept && i < (int)keep.valid.size() && keep.valid[i] && keep.gram[i].G;
   GramOut go;
@@ -688,4 +691,153 @@ int32_t gpar_lgssm_posterior_rand(gpar_ctx* ctx, int64_t n, const double* t, con
   sync(ctx);
   API_END(ctx)
 }
+}  // extern "C"
+
+// ---------------------------------------------------------------- posterior objects
+// gpar_fit_posterior keeps, per output, everything get_gpar_scaled_predictions computes before it
+// reads the inference inputs (gpar_scaled_inference.jl:20-73: the fit and q(u), :141-196), so a
+// caller whose inference inputs arrive later -- the chained sweep of GPAR_scaled_examples.jl:172,
+// eeg.jl:249,274, one owner per output across ranks -- runs only the V*-dependent prediction per
+// output (gpar_posterior_predict).
+struct gpar_posterior {
+  int device = 0;
+  int mem = GPAR_MEM_DEVICE;   // memory space of the problems (and of every predict call's I/O)
+  struct Out {
+    gpar::DevProblem p;        // t, v, z, y: borrowed (device problems) or owned (host problems)
+    gpar::Theta th;
+    gpar::QuPre q;             // me, w, X1, Vm, cov in owned device memory
+  };
+  std::vector<Out> outs;
+  std::vector<void*> owned;    // hipMalloc'd blocks, freed by gpar_posterior_destroy
+  ~gpar_posterior() {
+    (void)hipSetDevice(device);
+    for (void* b : owned) (void)hipFree(b);
+  }
+};
+
+namespace gpar {
+
+static double* post_alloc(gpar_posterior* post, size_t doubles) {
+  void* b = nullptr;
+  const hipError_t e = hipMalloc(&b, std::max<size_t>(doubles, 1) * sizeof(double));
+  if (e != hipSuccess) {
+    (void)hipGetLastError();
+    throw Error(e == hipErrorOutOfMemory ? GPAR_ERR_OOM : GPAR_ERR_HIP,
+                std::string("gpar_fit_posterior: hipMalloc: ") + hipGetErrorString(e));
+  }
+  post->owned.push_back(b);
+  return reinterpret_cast<double*>(b);
+}
+
+// device copy of `doubles` doubles on the context stream into posterior-owned memory
+static const double* post_keep(gpar_ctx* c, gpar_posterior* post, const double* src, size_t doubles) {
+  double* dst = post_alloc(post, doubles);
+  HIPCHECK(hipMemcpyAsync(dst, src, doubles * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
+  return dst;
+}
+
+}  // namespace gpar
+
+using namespace gpar;
+extern "C" {
+
+int32_t gpar_fit_posterior(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                           const double* log_theta0, const gpar_fit_options* opts,
+                           double* theta_out, double* nlml_out, int32_t* evals_out,
+                           gpar_posterior** out) {
+  if (out) *out = nullptr;
+  std::unique_ptr<gpar_posterior> post;
+  API_BEGIN(ctx)
+  ARGCHECK(probs && nprob >= 1 && log_theta0 && theta_out && out, "null argument");
+  check_batch(probs, nprob);
+  gpar_fit_options o{0, 1000, 1e-8, 0.0};
+  if (opts) o = *opts;
+  std::vector<DevProblem> P;
+  for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
+  FitKeep keep;
+  fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, &keep);
+  post.reset(new gpar_posterior());
+  post->device = ctx->device;
+  post->mem = probs[0].mem;
+  post->outs.resize(nprob);
+  for (int i = 0; i < nprob; ++i) {
+    const double* q = theta_out + 5 * i;
+    post->outs[i].th = Theta{q[0], q[1], q[2], q[3], q[4]};
+  }
+  // q(u) batched per convention (run_q_u_batch takes one), each batch copied out of the workspace
+  // before the next overwrites it
+  for (int qn : {0, 1}) {
+    std::vector<int> idx;
+    for (int i = 0; i < nprob; ++i)
+      if (P[i].qu_noise == qn) idx.push_back(i);
+    if (idx.empty()) continue;
+    std::vector<DevProblem> Pq;
+    std::vector<Theta> Tq;
+    FitKeep kq;
+    for (int i : idx) {
+      Pq.push_back(P[i]);
+      Tq.push_back(post->outs[i].th);
+      kq.gram.push_back(keep.gram[i]);
+      kq.valid.push_back(keep.valid[i]);
+    }
+    std::vector<QuPre> pre = run_q_u_batch(ctx, Pq, Tq, kq, /*want_cov=*/true);
+    for (size_t a = 0; a < idx.size(); ++a) {
+      const QuPre& s = pre[a];
+      const size_t sq = (size_t)s.ld * s.ld;
+      QuPre& d = post->outs[idx[a]].q;
+      d = s;
+      d.Lu = d.LD = nullptr;   // prediction reads w, X1, Vm (and me, cov: MC / path) only
+      d.me = post_keep(ctx, post.get(), s.me, s.ld);
+      d.w = post_keep(ctx, post.get(), s.w, s.ld);
+      d.X1 = post_keep(ctx, post.get(), s.X1, sq);
+      d.Vm = post_keep(ctx, post.get(), s.Vm, sq);
+      d.cov = post_keep(ctx, post.get(), s.cov, sq);
+    }
+    sync(ctx);
+  }
+  // the problems: device inputs stay the caller's (borrowed until gpar_posterior_destroy); host
+  // inputs were uploaded into workspace that later calls reuse, so they are copied
+  for (int i = 0; i < nprob; ++i) {
+    DevProblem d = P[i];
+    d.d2 = nullptr;   // the fit's distance cache is not the posterior's
+    d.cache_slot = -1;
+    d.zc = post_keep(ctx, post.get(), P[i].zc, (size_t)((d.mp + 255) / 256) * zc_stride((int)d.d));
+    if (probs[0].mem == GPAR_MEM_HOST) {
+      d.t = post_keep(ctx, post.get(), P[i].t, d.n);
+      d.y = post_keep(ctx, post.get(), P[i].y, d.n);
+      d.v = post_keep(ctx, post.get(), P[i].v, (size_t)d.n * d.ldv);
+      d.z = post_keep(ctx, post.get(), P[i].z, (size_t)d.m * d.ldz);
+    }
+    post->outs[i].p = d;
+  }
+  sync(ctx);
+  *out = post.release();
+  API_END(ctx)
+}
+
+int32_t gpar_posterior_predict(gpar_ctx* ctx, const gpar_posterior* post, int32_t i,
+                               int64_t n_star, const double* t_star, const double* v_star,
+                               int64_t ldvs, int32_t mode, int32_t samples, uint64_t seed,
+                               double* mean, double* std) {
+  API_BEGIN(ctx)
+  ARGCHECK(post && t_star && v_star && mean && std, "null argument");
+  ARGCHECK(post->device == ctx->device, "the posterior belongs to another device's context");
+  ARGCHECK(i >= 0 && i < (int32_t)post->outs.size(), "output index out of range");
+  const gpar_posterior::Out& o = post->outs[i];
+  ARGCHECK(n_star >= 1, "n_star must be >= 1");
+  ARGCHECK(ldvs >= o.p.d, "ldvs must be >= d");
+  ARGCHECK(mode == GPAR_PREDICT_ANALYTIC || mode == GPAR_PREDICT_MC || mode == GPAR_PREDICT_PATH,
+           "bad mode");
+  if (mode != GPAR_PREDICT_ANALYTIC)
+    ARGCHECK(samples >= 2 && samples <= kMaxSamples, "MC / path modes take 2..65536 samples");
+  predict_impl(ctx, o.p, o.th, post->mem, n_star, t_star, v_star, ldvs, mode, samples, seed, mean,
+               std, nullptr, false, &o.q);
+  API_END(ctx)
+}
+
+int32_t gpar_posterior_destroy(gpar_posterior* post) {
+  delete post;
+  return GPAR_OK;
+}
+
 }  // extern "C"

@@ -383,6 +383,78 @@ def fit_predict_batch(problems, log_theta0, t_star, V_stars, max_evals=0, max_it
     return FitResult(theta, nlml, evals), means, stds
 
 
+class Posterior:
+    """gpar_fit_posterior's result: the fitted theta of every output and its q(u), kept on the
+    device, so that predictions whose inference inputs arrive later (the chained sweep of
+    GPAR_scaled_examples.jl:172 / eeg.jl:249,274) run only the V*-dependent half of
+    get_gpar_scaled_predictions (gpar_posterior_predict).  Holds the problems' buffers (`keep`)
+    alive: device problems' inputs are borrowed by the posterior."""
+
+    def __init__(self, handle, fit, problems, keep, device):
+        self.h, self.fit, self.device = handle, fit, device
+        self._problems, self._keep = list(problems), keep
+
+    @property
+    def theta(self):
+        return self.fit.theta
+
+    def predict(self, i, t_star, V_star, mode="analytic", samples=100, seed=0):
+        """Output i's (mean, std) at (t_star, V_star): device tensors (V_star N* x D, rows =
+        points) for device problems, numpy (D x N* ColVecs) for host ones."""
+        p = self._problems[i]
+        keep = _Keep()
+        ctx, lib = context(self.device), _lib.load()
+        md = _mode_id(mode)
+        if p.mem == _lib.GPAR_MEM_DEVICE:
+            import torch
+            vsp, ldvs, ns, ds = _dev_points(V_star, keep)
+            tsp = _dev_vec(t_star, keep)
+            if ns != t_star.numel() or ds != p.d:
+                raise _arg_error("inference inputs must be N* x D with N* = len(t_star)")
+            mean = torch.empty(ns, dtype=torch.float64, device=t_star.device)
+            std = torch.empty(ns, dtype=torch.float64, device=t_star.device)
+            with _after_torch(ctx):
+                ctx.check(lib.gpar_posterior_predict(ctx.h, self.h, int(i), ns, tsp, vsp, ldvs, md,
+                                                     int(samples), int(seed), mean.data_ptr(),
+                                                     std.data_ptr()))
+            return mean, std
+        vsp, ldvs, ns, ds = _host_points(V_star, keep)
+        if ds != p.d or ns != len(np.asarray(t_star)):
+            raise _arg_error("inference inputs must be D x N* with N* = len(t_star)")
+        mean, std = np.zeros(ns), np.zeros(ns)
+        ctx.check(lib.gpar_posterior_predict(ctx.h, self.h, int(i), ns, _host_vec(t_star, keep), vsp,
+                                             ldvs, md, int(samples), int(seed), _ptr(mean), _ptr(std)))
+        return mean, std
+
+    def close(self):
+        if getattr(self, "h", None):
+            _lib.load().gpar_posterior_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def fit_posterior(problems, log_theta0, max_evals=0, max_iterations=1000, g_tol=1e-8,
+                  time_limit=0.0, device=0, keep=None):
+    """The fit and q(u) of get_gpar_scaled_predictions for a batch of outputs, kept on the device
+    for later predictions (gpar_fit_posterior) -> Posterior."""
+    ctx, lib = context(device), _lib.load()
+    P = len(problems)
+    arr = (GparProblem * P)(*problems)
+    x0 = np.ascontiguousarray(np.asarray(log_theta0, dtype=np.float64).reshape(P, 5))
+    opts = GparFitOptions(int(max_evals), int(max_iterations), float(g_tol), float(time_limit))
+    theta, nlml, evals = np.zeros((P, 5)), np.zeros(P), np.zeros(P, dtype=np.int32)
+    h = C.c_void_p()
+    with _after_torch(ctx, problems[0].mem == _lib.GPAR_MEM_DEVICE):
+        ctx.check(lib.gpar_fit_posterior(ctx.h, arr, P, _ptr(x0), C.byref(opts), _ptr(theta),
+                                         _ptr(nlml), _ptr(evals), C.byref(h)))
+    return Posterior(h, FitResult(theta, nlml, evals), problems, keep, device)
+
+
 def mc_normals(samples, m, seed, device=0):
     """The standard-normal draws MC-mode prediction uses for (samples, m, seed), samples x m
     (gpar_mc_normals): draw s maps to the pseudo-point sample m_e + chol(inv(D)).L xi_s

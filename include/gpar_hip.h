@@ -264,9 +264,11 @@ int32_t gpar_path_normals(gpar_ctx* ctx, int32_t samples, int64_t n, int32_t d, 
  * Replaces get_gpar_scaled_predictions (src/gp/gpar_scaled_inference.jl:20-136) -- the fit of
  * get_optim_scaled_gpar_params, then q(u) and the prediction at the fitted theta -- for `nprob`
  * outputs at once: the batched fit of gpar_fit, then per output exactly gpar_predict at its
- * fitted theta (theta_out row i).  With probs[i].qu_kuu_noise = 1, q(u)'s Gram at the fitted
- * theta is the one the fit already computed there (same kernels, same inputs: bit-identical), so
- * it is reused instead of recomputed; otherwise q(u) recomputes it.  Test inputs: t_star [n_star]
+ * fitted theta (theta_out row i).  q(u)'s Gram at the fitted theta is the one the fit already
+ * computed there (G = beta^T beta and r = beta^T alpha do not depend on Cuu's jitter), so it is
+ * reused instead of recomputed: with probs[i].qu_kuu_noise = 1 that is bit-identical to
+ * gpar_predict; with the reference's noise-free Cuu, gpar_predict recomputes the Gram from the
+ * fixed-up beta (less rounding for the ill-conditioned Cuu), so the two agree to ~1e-9.  Test inputs: t_star [n_star]
  * shared, output i's at v_star[i] (point k dim j at v_star[i][k*ldvs[i] + j]); mean_out[i],
  * std_out[i] [n_star]; all in probs[i].mem (one memory space for all outputs).  MC mode draws
  * output i with seed + i. */
@@ -292,6 +294,29 @@ int32_t gpar_fit_predict_chain(gpar_ctx* ctx, const gpar_problem* probs, int32_t
                                double* chain, int64_t ld_chain, const int32_t* chain_col,
                                double* theta_out, double* nlml_out, int32_t* evals_out,
                                double* const* mean_out, double* const* std_out);
+
+/* ---------------------------------------------------------------- posterior objects
+ * get_gpar_scaled_predictions (src/gp/gpar_scaled_inference.jl:20-136) split at the point where it
+ * first reads the inference inputs: gpar_fit_posterior runs the batched fit of gpar_fit and q(u)
+ * at every output's fitted theta (:63-73, compute_q_u :141-196; reusing the fit's Gram there, as
+ * gpar_fit_predict does) and keeps q(u) on the device; gpar_posterior_predict then runs output i's
+ * prediction for inference inputs that may arrive later -- the chained sweep of
+ * examples/GPAR_scaled_examples.jl:172 and examples/eeg.jl:249,274, where output p's inputs are
+ * the predicted means of outputs < p, possibly owned by other ranks.  gpar_posterior_predict
+ * equals the prediction half of gpar_fit_predict bit for bit.  Device problems' t, v, z, y are
+ * borrowed until gpar_posterior_destroy (host problems are copied to the device); the posterior
+ * holds ~3 Mp^2 doubles of device memory per output and belongs to ctx's device.  t_star, v_star,
+ * mean, std of a predict call are in the problems' memory space. */
+typedef struct gpar_posterior gpar_posterior;
+int32_t gpar_fit_posterior(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
+                           const double* log_theta0, const gpar_fit_options* opts,
+                           double* theta_out, double* nlml_out, int32_t* evals_out,
+                           gpar_posterior** out);
+int32_t gpar_posterior_predict(gpar_ctx* ctx, const gpar_posterior* post, int32_t i,
+                               int64_t n_star, const double* t_star, const double* v_star,
+                               int64_t ldvs, int32_t mode, int32_t samples, uint64_t seed,
+                               double* mean, double* std);
+int32_t gpar_posterior_destroy(gpar_posterior* post);
 
 /* ---------------------------------------------------------------- temporal-only (LGSSM) chains
  * `nchains` independent chains sharing the time grid t [n] (ascending); chain c's
