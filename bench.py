@@ -115,6 +115,10 @@ def main():
                          "recomputed by every fit, nothing is carried across steps) -- re-allocating "
                          "258 GB per step costs ~5.8 s on MI355X (fresh VRAM is cleared); 'release': "
                          "the library default, freed when each fit call returns")
+    ap.add_argument("--h2h-steps", type=int, default=2,
+                    help="after the timed device-resident steps, this many host->host steps "
+                         "(SURVEY §8d's unit: one pinned upload of t, Y, t*, F* and the pseudo-inputs "
+                         "per step, means / stds downloaded), reported as host_to_host beside value")
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-check-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--stub", action="store_true",
@@ -214,7 +218,7 @@ def main():
         shards = S.assign_outputs(P, w_)
         mine = shards[r_]
     gpar_out = [p for p in mine if p >= 2] if not temporal else []
-    Yh = Y_d.cpu().numpy() if gpar_out else None
+    Yh = Y_d.cpu().numpy() if (gpar_out or args.inference == "chained") else None
     # q(u) with Kuu + sigma^2 I (qu_kuu_noise) unless --qu-noise-free: the reference's jitter-free
     # Cuu (gpar_scaled_inference.jl:157) is numerically singular for M=512 pseudo-inputs drawn
     # from the data at fitted lengthscales; the objective itself is unchanged (dtc.jl:35,119).
@@ -269,6 +273,21 @@ def main():
         chain_d = Fs_d.clone()
         owners = S.owners_of(shards)
         gpar_all = list(range(2, P + 1))
+        if shard_of:
+            # untimed set-up of the one-rank chained measurement: every output's posterior (a short
+            # fit: the sweep's cost does not depend on theta), so the timed step can run the whole
+            # sweep the real job's ranks wait through
+            probs_all, keep_all = [], []
+            for p in gpar_all:
+                if p not in Zs:
+                    Zs[p] = torch.from_numpy(D.pseudo_inputs(Yh[:, : p - 1], M, seed=p)).to(dev)
+                    ycols[p] = Y_d[:, p - 1].contiguous()
+                pr, k = G.make_problem(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], cfg["out_kernel"],
+                                       "matern52", qu_kuu_noise=qn)
+                probs_all.append(pr)
+                keep_all.append(k)
+            post_all = G.fit_posterior(probs_all, np.tile(x0[0], (len(probs_all), 1)), max_evals=6,
+                                       g_tol=-1.0, device=local, keep=keep_all)
 
     ctx.set_dist_cache_keep(args.dist_cache == "keep")
     per_output = args.api == "per-output"
@@ -278,23 +297,25 @@ def main():
         """get_gpar_scaled_predictions for every owned GPAR output: one batched call, or one
         single-output call per output (--api per-output)."""
         if not per_output:
-            fr, _, _ = G.fit_predict_batch(problems, x0, ts, Vs, max_evals=EV, g_tol=-1.0,
-                                           mode=args.predict, samples=100, seed=gpar_out[0],
-                                           device=local)
-            return fr
+            return G.fit_predict_batch(problems, x0, ts, Vs, max_evals=EV, g_tol=-1.0,
+                                       mode=args.predict, samples=100, seed=gpar_out[0],
+                                       device=local)
         th, nl = np.zeros((len(problems), 5)), np.zeros(len(problems))
+        means, stds = [], []
         for i in range(len(problems)):
-            fr, _, _ = G.fit_predict_batch(problems[i:i + 1], x0[i:i + 1], ts, Vs[i:i + 1],
-                                           max_evals=EV, g_tol=-1.0, mode=args.predict, samples=100,
-                                           seed=gpar_out[0] + i, device=local)
+            fr, m, sd = G.fit_predict_batch(problems[i:i + 1], x0[i:i + 1], ts, Vs[i:i + 1],
+                                            max_evals=EV, g_tol=-1.0, mode=args.predict, samples=100,
+                                            seed=gpar_out[0] + i, device=local)
             th[i], nl[i] = fr.theta[0], fr.nlml[0]
-        return G.FitResult(th, nl, np.full(len(problems), EV, dtype=np.int32))
+            means.append(m[0])
+            stds.append(sd[0])
+        return G.FitResult(th, nl, np.full(len(problems), EV, dtype=np.int32)), means, stds
 
     def step():
         res = {}
         if host:
             if problems:
-                fr = fit_predict_outputs(ts_hh, Vs_h)
+                fr, _, _ = fit_predict_outputs(ts_hh, Vs_h)
                 last["fit"] = fr
                 for i, p in enumerate(gpar_out):
                     res[p] = fr.theta[i]
@@ -312,23 +333,40 @@ def main():
             for i, p in enumerate(gpar_out):
                 res[p] = fr.theta[i]
         elif chained:
-            # independent fits per rank, then the ordered prediction sweep across ranks: each
-            # predicted mean is broadcast by its owner as soon as it is ready (shard.py)
+            # independent fits per rank, each keeping its outputs' q(u) on the device
+            # (gpar_fit_posterior), then the ordered prediction sweep across ranks: only the
+            # inference-input-dependent predictions run inside it, and each predicted mean is
+            # broadcast by its owner as soon as it is ready (shard.py)
+            post = None
             if problems:
-                fr = G.fit_batch(problems, x0, max_evals=EV, g_tol=-1.0, device=local)
+                post = G.fit_posterior(problems, x0, max_evals=EV, g_tol=-1.0, device=local,
+                                       keep=keep)
                 for i, p in enumerate(gpar_out):
-                    res[p] = fr.theta[i]
-            S.chained_predictions(
-                gpar_all, owners,
-                lambda p, c: G.predict_scaled(Y_d[:, : p - 1], Zs[p], t_d, ycols[p], res[p], ts_d,
-                                              c[:, : p - 1], cfg["out_kernel"], "matern52",
-                                              mode=args.predict, samples=100, seed=p, device=local,
-                                              qu_kuu_noise=qn),
-                chain_d)
+                    res[p] = post.theta[i]
+            t_sw = time.perf_counter()
+            if shard_of:
+                # one rank of the W-way job on this GPU: its own fits above, then the whole
+                # P-output sweep (the other ranks' outputs from the untimed posteriors of the
+                # set-up) -- the serial part every rank of the real job waits through
+                S.chained_predictions(
+                    gpar_all, {p: 0 for p in gpar_all},
+                    lambda p, c: (post if p in gpar_out else post_all).predict(
+                        (gpar_out if p in gpar_out else gpar_all).index(p), ts_d, c[:, : p - 1],
+                        mode=args.predict, samples=100, seed=p),
+                    chain_d)
+            else:
+                idx = {p: i for i, p in enumerate(gpar_out)}
+                S.chained_predictions(
+                    gpar_all, owners,
+                    lambda p, c: post.predict(idx[p], ts_d, c[:, : p - 1], mode=args.predict,
+                                              samples=100, seed=p),
+                    chain_d)
+            torch.cuda.synchronize()
+            last.setdefault("sweep_s", []).append(time.perf_counter() - t_sw)
         elif problems and not args.separate_predict:
             # get_gpar_scaled_predictions for every owned output: batched fit, then predictions
-            fr = fit_predict_outputs(ts_d, [Fs_d[:, : p - 1] for p in gpar_out])
-            last["fit"] = fr
+            fr, means, stds = fit_predict_outputs(ts_d, [Fs_d[:, : p - 1] for p in gpar_out])
+            last["fit"], last["means"], last["stds"] = fr, means, stds
             for i, p in enumerate(gpar_out):
                 res[p] = fr.theta[i]
         elif problems:
@@ -339,6 +377,7 @@ def main():
             tk = cfg["out_kernel"] if temporal else "matern52"
             th1, m1, v1 = G.get_sde_predictions_device(t_d, y1, ts_d, tk, (0.0, 0.0, -2.0),
                                                        max_evals=EV, device=local)
+            last["temporal"] = (m1, v1)
             if temporal:
                 for i, p in enumerate(mine):
                     res[p] = np.array(list(np.atleast_2d(th1)[i]) + [0.0, 0.0])
@@ -516,6 +555,56 @@ def main():
                         "atol 1e-8 max|ref|; *_excess <= 1 passes) at N = N*, against the port")
         self_check = dict(self_check or {}, cpu_port=port)
         self_check["ok"] = bool(self_check.get("ok", True) and port["ok"])
+    h2h = None
+    if (rank == 0 and world == 1 and args.h2h_steps > 0 and problems and not host and not chained
+            and not temporal and not shard_of and not per_output and not args.separate_predict):
+        # SURVEY §8d's host->host unit ("host->host wall-clock, excluding setup"): the
+        # same job, every step starting from pinned host copies of its inputs -- t, Y (N x P), t*,
+        # F* (N* x P) and the pseudo-inputs, one upload each into the buffers the problems view --
+        # and ending with every output's mean / std (and output 1's smoothed marginals) in pinned
+        # host memory.  Untimed set-up: the pinned buffers.
+        t_pin, Y_pin = t_d.cpu().pin_memory(), Y_d.cpu().pin_memory()
+        ts_pin, Fs_pin = ts_d.cpu().pin_memory(), Fs_d.cpu().pin_memory()
+        Z_pin = {p: Zs[p].cpu().pin_memory() for p in gpar_out}
+        res_pin = torch.empty((2 * len(gpar_out) + 2, ns_eff), dtype=torch.float64).pin_memory()
+        up = 8 * (t_pin.numel() + Y_pin.numel() + ts_pin.numel() + Fs_pin.numel()
+                  + sum(z.numel() for z in Z_pin.values()))
+        th_dev = theta
+
+        def h2h_step():
+            for dst, src in ((t_d, t_pin), (Y_d, Y_pin), (ts_d, ts_pin), (Fs_d, Fs_pin)):
+                dst.copy_(src, non_blocking=True)
+            for p in gpar_out:   # the problems' views: pseudo-inputs uploaded, target columns
+                Zs[p].copy_(Z_pin[p], non_blocking=True)
+                ycols[p].copy_(Y_d[:, p - 1])
+            if y1 is not None:
+                y1.copy_(Y_d[:, 0])
+            th = step()
+            k = 0
+            for m_, s_ in zip(last["means"], last["stds"]):
+                res_pin[k].copy_(m_, non_blocking=True)
+                res_pin[k + 1].copy_(s_, non_blocking=True)
+                k += 2
+            if "temporal" in last:
+                res_pin[k].copy_(last["temporal"][0], non_blocking=True)
+                res_pin[k + 1].copy_(last["temporal"][1], non_blocking=True)
+                k += 2
+            torch.cuda.synchronize()
+            return th, k
+
+        torch.cuda.synchronize()
+        th0 = time.perf_counter()
+        for _ in range(args.h2h_steps):
+            th_h, nres = h2h_step()
+        el_h = (time.perf_counter() - th0) * 1e3 / args.h2h_steps
+        h2h = {"ms_per_step": el_h, "steps": args.h2h_steps, "value": n_eff * P / (el_h / 1e3),
+               "vs_device_resident": el_h / el, "bytes_up_per_step": up,
+               "bytes_down_per_step": 8 * nres * ns_eff,
+               "same_thetas_as_timed_steps": bool(np.array_equal(th_h, th_dev)),
+               "note": "after the timed device-resident steps: each step uploads t, Y, t*, F* and "
+                       "the pseudo-inputs from pinned host memory into the buffers the problems "
+                       "view, runs the job, and downloads every prediction to pinned host memory "
+                       "(SURVEY §8d host->host unit; value stays the device-resident figure)"}
     if cpu_child is not None:
         try:
             os.unlink(cpu_child.check_path)
@@ -629,6 +718,23 @@ def main():
                 pred["one_lane_probe"] = pred_probe
             out["roofline_predict"] = pred
         out["memory"] = memory
+        if h2h:
+            out["host_to_host_ms_per_step"] = h2h["ms_per_step"]
+            out["host_to_host"] = h2h
+        if last.get("sweep_s"):
+            sw = 1e3 * float(np.mean(last["sweep_s"][-args.steps:]))
+            out["chained_sweep"] = {
+                "ms_per_step": sw, "outputs": len(gpar_all),
+                "note": "wall time of the ordered chained prediction sweep inside each timed step "
+                        "(gpar_posterior_predict per output: q(u) ran with the fits)"}
+            if shard_of:
+                # the projected W-GPU chained step: this rank's fits (the slowest rank's: every rank
+                # fits the same number of equal-cost outputs) + the serial sweep + one 8 N* byte
+                # broadcast per output over xGMI (assumed 50 GB/s effective + 40 us latency)
+                bc = len(gpar_all) * (8.0 * ns_eff / 50e9 + 40e-6) * 1e3
+                out["chained_sweep"]["projected_step_ms"] = (el - sw) + sw + bc
+                out["chained_sweep"]["broadcast_ms_assumed"] = bc
+                out["chained_sweep"]["fit_ms_per_step"] = el - sw
         if self_check:
             out["self_check"] = self_check
         if probe:

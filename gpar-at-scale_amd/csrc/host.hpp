@@ -247,6 +247,12 @@ void check_sorted_host(const double* t, int64_t n);
 void check_problem(const gpar_problem& p);
 void check_batch(const gpar_problem* probs, int nprob);
 DevProblem prepare_problem(gpar_ctx* c, const gpar_problem& p, int idx);
+// prepare_problem for every problem of a batch; host inputs several problems share (t, the v base)
+// are uploaded once (upload_shared_block)
+std::vector<DevProblem> prepare_batch(gpar_ctx* c, const gpar_problem* probs, int nprob);
+std::pair<const double*, int64_t> upload_shared_block(gpar_ctx* c, const std::string& name,
+                                                      const double* src, int64_t ld, int64_t width,
+                                                      int64_t rows);
 
 struct Theta {
   double l_t, sv_t, l_o, sv_o, sigma;

@@ -356,7 +356,7 @@ int32_t gpar_dtc_objective(gpar_ctx* ctx, const gpar_problem* probs, int32_t npr
   ARGCHECK(probs && nprob >= 1 && theta && dtc_out, "null argument");
   check_batch(probs, nprob);
   std::vector<DevProblem> P;
-  for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
+  P = prepare_batch(ctx, probs, nprob);
   std::vector<Theta> th = thetas_from(theta, nprob);
   std::vector<int> st;
   eval_dtc(ctx, P, th, dtc_out, st);

@@ -193,6 +193,76 @@ DevProblem prepare_problem(gpar_ctx* c, const gpar_problem& p, int idx) {
   return d;
 }
 
+// Rows x width doubles of a host matrix (leading dimension ld) that several problems read as
+// column prefixes: uploaded once.  The whole ld-wide block goes up in one linear copy when it is
+// at most twice as wide as what they read (GPAR's outputs read the first p - 1 columns of one
+// N x P matrix of earlier outputs: ld = P, widest read P - 1), else the widest prefix (pitched).
+// Returns the device buffer and its leading dimension.
+std::pair<const double*, int64_t> upload_shared_block(gpar_ctx* c, const std::string& name,
+                                                      const double* src, int64_t ld, int64_t width,
+                                                      int64_t rows) {
+  const int64_t w = ld <= 2 * width ? ld : width;
+  double* dst = ws<double>(c, name, (size_t)rows * w);
+  h2d_rows(c, dst, src, ld, w, rows);
+  return {dst, w};
+}
+
+std::vector<DevProblem> prepare_batch(gpar_ctx* c, const gpar_problem* probs, int nprob) {
+  std::vector<DevProblem> P;
+  if (probs[0].mem != GPAR_MEM_HOST || nprob < 2) {
+    for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(c, probs[i], i));
+    return P;
+  }
+  // host inputs several problems share -- the time grid, the matrix of earlier outputs -- go up
+  // once; each problem then runs as a device problem over views of them
+  std::vector<gpar_problem> q(probs, probs + nprob);
+  std::vector<int> tgrp(nprob, -1), vgrp(nprob, -1);
+  int nt = 0, nv = 0;
+  for (int i = 0; i < nprob; ++i) {
+    for (int j = 0; j < i && tgrp[i] < 0; ++j)
+      if (probs[j].t == probs[i].t) tgrp[i] = tgrp[j];
+    if (tgrp[i] < 0) tgrp[i] = nt++;
+    for (int j = 0; j < i && vgrp[i] < 0; ++j)
+      if (probs[j].v == probs[i].v && probs[j].ldv == probs[i].ldv) vgrp[i] = vgrp[j];
+    if (vgrp[i] < 0) vgrp[i] = nv++;
+  }
+  std::vector<const double*> tdev(nt, nullptr);
+  std::vector<std::pair<const double*, int64_t>> vdev(nv, {nullptr, 0});
+  for (int g = 0; g < nv; ++g) {
+    int64_t wmax = 0, first = -1;
+    for (int i = 0; i < nprob; ++i)
+      if (vgrp[i] == g) {
+        wmax = std::max(wmax, probs[i].d);
+        if (first < 0) first = i;
+      }
+    const gpar_problem& r = probs[first];
+    vdev[g] = upload_shared_block(c, "pb_v" + std::to_string(g), r.v, r.ldv, wmax, r.n);
+  }
+  for (int i = 0; i < nprob; ++i) {
+    const int g = tgrp[i];
+    if (!tdev[g]) {
+      double* t = ws<double>(c, "pb_t" + std::to_string(g), probs[i].n);
+      h2d(c, t, probs[i].t, probs[i].n);
+      tdev[g] = t;
+    }
+    const std::string k = "prob" + std::to_string(i);
+    double* z = ws<double>(c, k + "_z", (size_t)probs[i].m * probs[i].d);
+    double* y = ws<double>(c, k + "_y", probs[i].n);
+    h2d(c, y, probs[i].y, probs[i].n);
+    h2d_rows(c, z, probs[i].z, probs[i].ldz, probs[i].d, probs[i].m);
+    q[i].t = tdev[g];
+    q[i].v = vdev[vgrp[i]].first;
+    q[i].ldv = vdev[vgrp[i]].second;
+    q[i].z = z;
+    q[i].ldz = probs[i].d;
+    q[i].y = y;
+    q[i].mem = GPAR_MEM_DEVICE;
+    P.push_back(prepare_problem(c, q[i], i));
+    P.back().t_user = probs[i].t;
+  }
+  return P;
+}
+
 // Data-independent per-step filter quantities for `nchains` chains sharing t (n steps).
 // With ys (one device data vector per chain): the chains' alpha_loc / chunk end states are
 // filtered inside the gains pass (alpha_loc: nchains x n, asend: nchains x nch x 4).

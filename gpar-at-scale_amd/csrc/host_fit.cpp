@@ -425,7 +425,7 @@ int32_t gpar_fit(gpar_ctx* ctx, const gpar_problem* probs, int32_t nprob,
   gpar_fit_options o{0, 1000, 1e-8, 0.0};
   if (opts) o = *opts;
   std::vector<DevProblem> P;
-  for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
+  P = prepare_batch(ctx, probs, nprob);
   fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, nullptr);
   API_END(ctx)
 }

@@ -9,13 +9,14 @@ QuOut run_q_u(gpar_ctx* c, const DevProblem& p, const Theta& th,
   std::vector<DevProblem> P{p};
   std::vector<Theta> T{th};
   // G = beta^T beta and r = beta^T alpha do not depend on Cuu's jitter (only L_u does,
-  // gpar_scaled_inference.jl:157-187), so the Gram the fit computed at this theta is reused for
-  // either q(u) convention when the caller hands it over (gc: gpar_fit_predict).  Recomputed
-  // (gpar_predict, gpar_q_u), the noise-free Cuu takes the extra beta fix-up pass: a plain
-  // beta^T beta of the true beta carries ~10x less rounding than the correction form, which its
-  // cond(Cuu) up to ~1e10 amplifies.
+  // gpar_scaled_inference.jl:157-187), but their rounding matters for the noise-free Cuu: it takes
+  // the extra beta fix-up pass (a plain beta^T beta of the true beta carries ~10x less rounding
+  // than the objective's correction form, and cond(Cuu) up to ~1e10 amplifies it -- reusing the
+  // fit's correction-form Gram there measured 1.5e-7 relative off the oracle's std, r04a).  With
+  // qu_kuu_noise the factor is the objective's regularised Kuu + s2 I and the correction-form Gram
+  // the fit computed at this theta is reused when the caller hands it over (gc).
   GramOut go;
-  if (gc && gc->G) {
+  if (gc && gc->G && p.qu_noise) {
     go.ldg = p.mp;
     go.npart = 1;
     go.G = const_cast<double*>(gc->G);
@@ -70,7 +71,7 @@ std::vector<QuPre> run_q_u_batch(gpar_ctx* c, const std::vector<DevProblem>& P,
   int64_t mpmax = 0, mmax = 0;
   for (const auto& p : P) { mpmax = std::max(mpmax, p.mp); mmax = std::max(mmax, p.m); }
   const bool qn = P[0].qu_noise;
-  bool kept = true;   // the fit's Grams serve both q(u) conventions (run_q_u)
+  bool kept = qn;   // the fit's Grams serve the regularised convention only (run_q_u)
   for (int i = 0; i < np; ++i)
     kept = kept && i < (int)keep.valid.size() && keep.valid[i] && keep.gram[i].G;
   GramOut go;
@@ -485,7 +486,7 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
   gpar_fit_options o{0, 1000, 1e-8, 0.0};
   if (opts) o = *opts;
   std::vector<DevProblem> P;
-  for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
+  P = prepare_batch(ctx, probs, nprob);
   FitKeep keep;
   const int mem = probs[0].mem;
   // Prediction lanes: with device-memory outputs and no chain between the predictions, outputs
@@ -493,7 +494,14 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
   // one output's memory-bound passes (merge, adjoint, rows) run beside the other's DP / MFMA work
   // (whitening, variance GEMM).  A lane's host syncs (q(u)'s Cholesky status) wait for that lane
   // only.
-  const bool lanes = mem == GPAR_MEM_DEVICE && !chain && nprob > 1 && ctx->predict_lanes > 1;
+  // Host-memory batches without a chain: the test inputs go up once after the fit (t* sorted once;
+  // every distinct v* base -- GPAR's outputs read column prefixes of one N* x P matrix -- in one
+  // linear copy), the predictions run on device buffers (with lanes), and the means / stds come
+  // down at the end.  (With a chain, later outputs read host columns the earlier predictions
+  // write: those predictions keep the per-output host path.)
+  const bool stage = mem == GPAR_MEM_HOST && !chain;
+  const bool lanes = (mem == GPAR_MEM_DEVICE || stage) && !chain && nprob > 1 &&
+                     ctx->predict_lanes > 1;
   // the predictions' workspace (named buffers, reused across the outputs: the largest counts)
   int64_t pred_bytes = 0;
   for (const auto& p : P)
@@ -501,7 +509,70 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
                                                           mode == GPAR_PREDICT_ANALYTIC &&
                                                               ctx->predict_fused &&
                                                               predict_var_tiles(p.mp) > 0));
-  fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, &keep, (lanes ? 2 : 1) * pred_bytes);
+  int64_t stage_bytes = 0;
+  if (stage) {
+    stage_bytes = 8 * n_star * (1 + 2 * (int64_t)nprob);
+    for (int i = 0; i < nprob; ++i) stage_bytes += 8 * n_star * ldvs[i];   // upper bound
+  }
+  fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, &keep,
+           (lanes ? 2 : 1) * pred_bytes + stage_bytes);
+  std::vector<int64_t> perm;
+  std::vector<const double*> vs_dev(nprob, nullptr);
+  std::vector<int64_t> lds_dev(nprob, 0);
+  const double* ts_dev = t_star;
+  double* res = nullptr;   // staged outputs: [nprob][mean, std][n_star]
+  if (stage) {
+    if (!std::is_sorted(t_star, t_star + n_star)) {
+      perm.resize(n_star);
+      for (int64_t k = 0; k < n_star; ++k) perm[k] = k;
+      std::stable_sort(perm.begin(), perm.end(),
+                       [&](int64_t a, int64_t b) { return t_star[a] < t_star[b]; });
+    }
+    std::vector<double> tmp;
+    double* tsd = ws<double>(ctx, "fph_ts", n_star);
+    if (perm.empty()) {
+      h2d(ctx, tsd, t_star, n_star);
+    } else {
+      tmp.resize(n_star);
+      for (int64_t k = 0; k < n_star; ++k) tmp[k] = t_star[perm[k]];
+      h2d(ctx, tsd, tmp.data(), n_star);
+      sync(ctx);
+    }
+    ts_dev = tsd;
+    std::vector<int> grp(nprob, -1);
+    int ng = 0;
+    for (int i = 0; i < nprob; ++i) {
+      for (int j = 0; j < i && grp[i] < 0; ++j)
+        if (v_star[j] == v_star[i] && ldvs[j] == ldvs[i]) grp[i] = grp[j];
+      if (grp[i] < 0) grp[i] = ng++;
+    }
+    for (int g = 0; g < ng; ++g) {
+      int64_t wmax = 0;
+      int first = -1;
+      for (int i = 0; i < nprob; ++i)
+        if (grp[i] == g) {
+          wmax = std::max(wmax, probs[i].d);
+          if (first < 0) first = i;
+        }
+      std::pair<const double*, int64_t> b;
+      if (perm.empty()) {
+        b = upload_shared_block(ctx, "fph_vs" + std::to_string(g), v_star[first], ldvs[first], wmax,
+                                n_star);
+      } else {   // the rows in t*'s ascending order, gathered on the host
+        tmp.assign((size_t)n_star * wmax, 0.0);
+        for (int64_t k = 0; k < n_star; ++k)
+          for (int64_t q = 0; q < wmax; ++q) tmp[k * wmax + q] = v_star[first][perm[k] * ldvs[first] + q];
+        b = upload_shared_block(ctx, "fph_vs" + std::to_string(g), tmp.data(), wmax, wmax, n_star);
+        sync(ctx);
+      }
+      for (int i = 0; i < nprob; ++i)
+        if (grp[i] == g) {
+          vs_dev[i] = b.first;
+          lds_dev[i] = b.second;
+        }
+    }
+    res = ws<double>(ctx, "fph_res", (size_t)nprob * 2 * n_star);
+  }
   struct LaneScope {   // a lane's stream and workspace names; restored on any exit
     gpar_ctx* c;
     hipStream_t saved;
@@ -538,10 +609,16 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
     const double* q = theta_out + 5 * i;
     const Theta th{q[0], q[1], q[2], q[3], q[4]};
     LaneScope lane_(ctx, lanes ? (i & 1) : 0);
-    predict_impl(ctx, P[i], th, mem, n_star, t_star, v_star[i], ldvs[i], mode, samples,
-                 seed + (uint64_t)i, mean_out[i], std_out[i],
-                 keep.valid[i] ? &keep.gram[i] : nullptr, /*defer=*/lanes,
-                 pre.empty() ? nullptr : &pre[i]);
+    if (stage)
+      predict_impl(ctx, P[i], th, GPAR_MEM_DEVICE, n_star, ts_dev, vs_dev[i], lds_dev[i], mode,
+                   samples, seed + (uint64_t)i, res + (size_t)(2 * i) * n_star,
+                   res + (size_t)(2 * i + 1) * n_star, keep.valid[i] ? &keep.gram[i] : nullptr,
+                   /*defer=*/true, pre.empty() ? nullptr : &pre[i]);
+    else
+      predict_impl(ctx, P[i], th, mem, n_star, t_star, v_star[i], ldvs[i], mode, samples,
+                   seed + (uint64_t)i, mean_out[i], std_out[i],
+                   keep.valid[i] ? &keep.gram[i] : nullptr, /*defer=*/lanes,
+                   pre.empty() ? nullptr : &pre[i]);
     if (chain && chain_col[i] >= 0) {
       double* dst = chain + chain_col[i];
       if (mem == GPAR_MEM_DEVICE) {   // stream-ordered before the next output's merge reads it
@@ -557,7 +634,25 @@ static void fit_predict_impl(gpar_ctx* ctx, const gpar_problem* probs, int32_t n
     HIPCHECK(hipStreamWaitEvent(ctx->main, ctx->ev_join, 0));
   }
   tm_pred.reset();
-  if (lanes || (chain && mem == GPAR_MEM_DEVICE)) sync(ctx);
+  if (lanes || stage || (chain && mem == GPAR_MEM_DEVICE)) sync(ctx);
+  if (stage) {   // the staged means / stds into the caller's host buffers, in t*'s input order
+    std::vector<double> h(perm.empty() ? 0 : (size_t)2 * n_star);
+    for (int i = 0; i < nprob; ++i) {
+      const double* src = res + (size_t)(2 * i) * n_star;
+      if (perm.empty()) {
+        d2h(ctx, mean_out[i], src, n_star);
+        d2h(ctx, std_out[i], src + n_star, n_star);
+      } else {
+        d2h(ctx, h.data(), src, (size_t)2 * n_star);
+        sync(ctx);
+        for (int64_t k = 0; k < n_star; ++k) {
+          mean_out[i][perm[k]] = h[k];
+          std_out[i][perm[k]] = h[n_star + k];
+        }
+      }
+    }
+    sync(ctx);
+  }
 }
 }  // namespace gpar
 using namespace gpar;
@@ -753,7 +848,7 @@ int32_t gpar_fit_posterior(gpar_ctx* ctx, const gpar_problem* probs, int32_t npr
   gpar_fit_options o{0, 1000, 1e-8, 0.0};
   if (opts) o = *opts;
   std::vector<DevProblem> P;
-  for (int i = 0; i < nprob; ++i) P.push_back(prepare_problem(ctx, probs[i], i));
+  P = prepare_batch(ctx, probs, nprob);
   FitKeep keep;
   fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, &keep);
   post.reset(new gpar_posterior());
@@ -796,16 +891,25 @@ int32_t gpar_fit_posterior(gpar_ctx* ctx, const gpar_problem* probs, int32_t npr
     sync(ctx);
   }
   // the problems: device inputs stay the caller's (borrowed until gpar_posterior_destroy); host
-  // inputs were uploaded into workspace that later calls reuse, so they are copied
+  // inputs were uploaded into workspace that later calls reuse, so they are copied (a time grid or
+  // input base several outputs share, once)
+  std::unordered_map<const double*, const double*> shared;
+  auto keep_once = [&](const double* src, size_t doubles) {
+    auto it = shared.find(src);
+    if (it != shared.end()) return it->second;
+    const double* dst = post_keep(ctx, post.get(), src, doubles);
+    shared[src] = dst;
+    return dst;
+  };
   for (int i = 0; i < nprob; ++i) {
     DevProblem d = P[i];
     d.d2 = nullptr;   // the fit's distance cache is not the posterior's
     d.cache_slot = -1;
     d.zc = post_keep(ctx, post.get(), P[i].zc, (size_t)((d.mp + 255) / 256) * zc_stride((int)d.d));
     if (probs[0].mem == GPAR_MEM_HOST) {
-      d.t = post_keep(ctx, post.get(), P[i].t, d.n);
+      d.t = keep_once(P[i].t, d.n);
       d.y = post_keep(ctx, post.get(), P[i].y, d.n);
-      d.v = post_keep(ctx, post.get(), P[i].v, (size_t)d.n * d.ldv);
+      d.v = keep_once(P[i].v, (size_t)d.n * d.ldv);
       d.z = post_keep(ctx, post.get(), P[i].z, (size_t)d.m * d.ldz);
     }
     post->outs[i].p = d;

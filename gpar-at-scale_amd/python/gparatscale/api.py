@@ -383,6 +383,66 @@ def fit_predict_batch(problems, log_theta0, t_star, V_stars, max_evals=0, max_it
     return FitResult(theta, nlml, evals), means, stds
 
 
+def get_gpar_scaled_predictions_batch(Y, pseudo_input_locations, time_loc, inference_time_loc, F,
+                                      chained=False, log_theta0=(0.0, 0.0, 0.0, 0.0, -2.0),
+                                      max_evals=0, g_tol=1e-8, time_limit=0.0, mode="analytic",
+                                      samples=100, seed=0, qu_kuu_noise=False, device=0):
+    """The Julia shim's matrix-form batch driver (julia/GPARatScaleHIP.jl): GPAR's per-output loop
+    (GPAR_scaled_examples.jl:132-175) for outputs 2..P of the host matrix Y (N x P, column i =
+    output i; output i's inputs are columns 1..i-1), ONE matrix passed for every output's inputs
+    (ldv = P; the library uploads it once) and one for the inference inputs F (N* x P; output i
+    reads its first i - 1 columns, given or -- chained -- F's column 1 then predicted means).
+    pseudo_input_locations[i - 2]: output i's D x M pseudo-inputs.  Returns (FitResult, means,
+    stds) for outputs 2..P."""
+    Y = np.ascontiguousarray(np.asarray(Y, dtype=np.float64))
+    F = np.ascontiguousarray(np.array(F, dtype=np.float64))   # a copy: the chain writes into it
+    n, P = Y.shape
+    ns = F.shape[0]
+    t = np.ascontiguousarray(np.asarray(time_loc, dtype=np.float64))
+    ts = np.ascontiguousarray(np.asarray(inference_time_loc, dtype=np.float64))
+    if P < 2 or F.shape[1] != P or len(t) != n or len(ts) != ns:
+        raise _arg_error("Y (N x P), F (N* x P), time_loc (N), inference_time_loc (N*) disagree")
+    if len(pseudo_input_locations) != P - 1:
+        raise _arg_error("one pseudo-input set per output 2..P")
+    keep = _Keep([Y, F, t, ts])
+    probs = []
+    for i in range(2, P + 1):
+        p = GparProblem()
+        p.z, p.ldz, m, dz = _host_points(pseudo_input_locations[i - 2], keep)
+        if dz != i - 1:
+            raise _arg_error(f"output {i}'s pseudo-inputs must have {i - 1} rows")
+        p.n, p.m, p.d = n, m, i - 1
+        p.t, p.v, p.ldv = t.ctypes.data, Y.ctypes.data, P
+        p.y = _host_vec(Y[:, i - 1], keep)
+        p.out_kernel = p.time_kernel = KERNEL_ID["matern52"]
+        p.kuu_noise, p.mem, p.qu_kuu_noise = 1, _lib.GPAR_MEM_HOST, 1 if qu_kuu_noise else 0
+        probs.append(p)
+    Q = P - 1
+    arr = (GparProblem * Q)(*probs)
+    x0 = np.ascontiguousarray(np.tile(np.asarray(log_theta0, dtype=np.float64), (Q, 1)))
+    opts = GparFitOptions(int(max_evals), 1000, float(g_tol), float(time_limit))
+    theta, nlml, evals = np.zeros((Q, 5)), np.zeros(Q), np.zeros(Q, dtype=np.int32)
+    means = [np.zeros(ns) for _ in range(Q)]
+    stds = [np.zeros(ns) for _ in range(Q)]
+    VP = (C.c_void_p * Q)(*([F.ctypes.data] * Q))
+    LD = (C.c_int64 * Q)(*([P] * Q))
+    MP = (C.c_void_p * Q)(*[a.ctypes.data for a in means])
+    SP = (C.c_void_p * Q)(*[a.ctypes.data for a in stds])
+    ctx, lib = context(device), _lib.load()
+    md = _mode_id(mode)
+    if chained:
+        CC = (C.c_int32 * Q)(*range(1, P))
+        ctx.check(lib.gpar_fit_predict_chain(ctx.h, arr, Q, _ptr(x0), C.byref(opts), ns,
+                                             ts.ctypes.data, VP, LD, md, int(samples), int(seed),
+                                             C.c_void_p(F.ctypes.data), P, CC, _ptr(theta),
+                                             _ptr(nlml), _ptr(evals), MP, SP))
+    else:
+        ctx.check(lib.gpar_fit_predict(ctx.h, arr, Q, _ptr(x0), C.byref(opts), ns, ts.ctypes.data,
+                                       VP, LD, md, int(samples), int(seed), _ptr(theta), _ptr(nlml),
+                                       _ptr(evals), MP, SP))
+    return FitResult(theta, nlml, evals), means, stds
+
+
 class Posterior:
     """gpar_fit_posterior's result: the fitted theta of every output and its q(u), kept on the
     device, so that predictions whose inference inputs arrive later (the chained sweep of

@@ -264,11 +264,11 @@ int32_t gpar_path_normals(gpar_ctx* ctx, int32_t samples, int64_t n, int32_t d, 
  * Replaces get_gpar_scaled_predictions (src/gp/gpar_scaled_inference.jl:20-136) -- the fit of
  * get_optim_scaled_gpar_params, then q(u) and the prediction at the fitted theta -- for `nprob`
  * outputs at once: the batched fit of gpar_fit, then per output exactly gpar_predict at its
- * fitted theta (theta_out row i).  q(u)'s Gram at the fitted theta is the one the fit already
- * computed there (G = beta^T beta and r = beta^T alpha do not depend on Cuu's jitter), so it is
- * reused instead of recomputed: with probs[i].qu_kuu_noise = 1 that is bit-identical to
- * gpar_predict; with the reference's noise-free Cuu, gpar_predict recomputes the Gram from the
- * fixed-up beta (less rounding for the ill-conditioned Cuu), so the two agree to ~1e-9.  Test inputs: t_star [n_star]
+ * fitted theta (theta_out row i).  With probs[i].qu_kuu_noise = 1, q(u)'s Gram at the fitted
+ * theta is the one the fit already computed there (same kernels, same inputs: bit-identical), so
+ * it is reused instead of recomputed; with the reference's noise-free Cuu q(u) recomputes it from
+ * the fixed-up beta (less rounding for the ill-conditioned Cuu: the fit's correction-form Gram
+ * measured 1.5e-7 relative off the oracle there).  Test inputs: t_star [n_star]
  * shared, output i's at v_star[i] (point k dim j at v_star[i][k*ldvs[i] + j]); mean_out[i],
  * std_out[i] [n_star]; all in probs[i].mem (one memory space for all outputs).  MC mode draws
  * output i with seed + i. */
@@ -298,8 +298,8 @@ int32_t gpar_fit_predict_chain(gpar_ctx* ctx, const gpar_problem* probs, int32_t
 /* ---------------------------------------------------------------- posterior objects
  * get_gpar_scaled_predictions (src/gp/gpar_scaled_inference.jl:20-136) split at the point where it
  * first reads the inference inputs: gpar_fit_posterior runs the batched fit of gpar_fit and q(u)
- * at every output's fitted theta (:63-73, compute_q_u :141-196; reusing the fit's Gram there, as
- * gpar_fit_predict does) and keeps q(u) on the device; gpar_posterior_predict then runs output i's
+ * at every output's fitted theta (:63-73, compute_q_u :141-196; with the fit's Gram where
+ * gpar_fit_predict reuses it) and keeps q(u) on the device; gpar_posterior_predict then runs output i's
  * prediction for inference inputs that may arrive later -- the chained sweep of
  * examples/GPAR_scaled_examples.jl:172 and examples/eeg.jl:249,274, where output p's inputs are
  * the predicted means of outputs < p, possibly owned by other ranks.  gpar_posterior_predict

@@ -425,6 +425,91 @@ function get_gpar_scaled_predictions_batch(input_locations, pseudo_input_locatio
     return means, stds
 end
 
+"""
+    get_gpar_scaled_predictions_batch(Y::AbstractMatrix, pseudo_input_locations, time_loc,
+                                      inference_time_loc, F::AbstractMatrix; chained = false, kw...)
+
+GPAR's own structure as one matrix (GPAR_scaled_examples.jl:132-175): column i of Y (N x P) is
+output i's observed targets, and output i's training inputs are columns 1..i-1 -- so every output's
+inputs are column prefixes of ONE matrix, passed once (the library uploads it once) instead of P
+copies.  Predicts outputs 2..P (output 1 is the temporal-only get_sde_predictions); output i's
+pseudo-inputs are `pseudo_input_locations[i - 1]` (D = i - 1).  Inference inputs: F (N* x P), output
+i reads its first i - 1 columns -- as given (`chained = false`), or with `chained = true` F's
+column 1 (test_y1) followed by the predicted means of outputs 2..i-1 (GPAR_scaled_examples.jl:172).
+Returns (means, stds) for outputs 2..P.
+"""
+function get_gpar_scaled_predictions_batch(Y::AbstractMatrix, pseudo_input_locations,
+        time_loc, inference_time_loc, F::AbstractMatrix;
+        chained::Bool = false,
+        i_log_time_l = nothing, i_log_time_var = nothing, i_log_out_l = nothing,
+        i_log_out_var = nothing, i_log_noise_sigma = nothing,
+        optimization_time_limit = 1000.0, debug::Bool = false,
+        mode::Symbol = :mc, samples::Integer = 100, seed::UInt64 = rand(UInt64))
+    N, P = size(Y)
+    P >= 2 || throw(DomainError(P, "Y needs at least two output columns"))
+    length(pseudo_input_locations) == P - 1 ||
+        throw(DomainError(P, "one pseudo-input set per output 2..P"))
+    size(F, 2) == P || throw(DomainError(size(F, 2), "F must have the P columns of Y"))
+    t = Vector{Float64}(time_loc)
+    ts = Vector{Float64}(inference_time_loc)
+    ns = length(ts)
+    length(t) == N && size(F, 1) == ns || throw(DomainError(N, "Y / F rows must match the times"))
+    # point-major: point k's outputs contiguous, so output i's inputs are a column prefix (ldv = P)
+    Yt = Matrix{Float64}(permutedims(Y))
+    Ft = Matrix{Float64}(permutedims(F))
+    Zs = [_colmat(z) for z in pseudo_input_locations]
+    ys = [Vector{Float64}(Y[:, i]) for i in 2:P]
+    probs = GparProblem[]
+    for i in 2:P
+        size(Zs[i - 1], 1) == i - 1 || throw(DomainError(i, "output $i's pseudo-inputs must have $(i - 1) rows"))
+        push!(probs, GparProblem(N, size(Zs[i - 1], 2), i - 1, pointer(t), pointer(Yt), P,
+                                 pointer(Zs[i - 1]), i - 1, pointer(ys[i - 1]),
+                                 kernel_id(Matern52()), kernel_id(Matern52()), Int32(1),
+                                 GPAR_MEM_HOST, Int32(0)))
+    end
+    Q = P - 1
+    x0 = reduce(vcat, [Vector{Float64}(parse_initial_gpar_params(i_log_time_l, i_log_time_var,
+                       i_log_out_l, i_log_out_var, i_log_noise_sigma)) for _ in 1:Q])
+    md = predict_mode(mode)
+    θ = zeros(5 * Q)
+    nlml = zeros(Q)
+    ev = zeros(Int32, Q)
+    means = [zeros(ns) for _ in 1:Q]
+    stds = [zeros(ns) for _ in 1:Q]
+    mptr = [pointer(m) for m in means]
+    sptr = [pointer(s) for s in stds]
+    vptr = fill(pointer(Ft), Q)
+    lds = fill(Int64(P), Q)
+    opts = Ref(fit_options(optimization_time_limit))
+    c = ctx()
+    GC.@preserve Yt Ft Zs ys t ts x0 θ nlml ev means stds probs begin
+        if chained
+            cols = Int32[i - 1 for i in 2:P]   # output i's mean -> column i (0-based i - 1)
+            check(c, ccall((:gpar_fit_predict_chain, libgpar), Int32,
+                           (Ptr{Cvoid}, Ptr{GparProblem}, Int32, Ptr{Float64}, Ref{GparFitOptions},
+                            Int64, Ptr{Float64}, Ptr{Ptr{Float64}}, Ptr{Int64}, Int32, Int32, UInt64,
+                            Ptr{Float64}, Int64, Ptr{Int32}, Ptr{Float64}, Ptr{Float64}, Ptr{Int32},
+                            Ptr{Ptr{Float64}}, Ptr{Ptr{Float64}}),
+                           c.h, probs, Int32(Q), x0, opts, ns, ts, vptr, lds, md, Int32(samples),
+                           seed, Ft, Int64(P), cols, θ, nlml, ev, mptr, sptr))
+        else
+            check(c, ccall((:gpar_fit_predict, libgpar), Int32,
+                           (Ptr{Cvoid}, Ptr{GparProblem}, Int32, Ptr{Float64}, Ref{GparFitOptions},
+                            Int64, Ptr{Float64}, Ptr{Ptr{Float64}}, Ptr{Int64}, Int32, Int32, UInt64,
+                            Ptr{Float64}, Ptr{Float64}, Ptr{Int32}, Ptr{Ptr{Float64}},
+                            Ptr{Ptr{Float64}}),
+                           c.h, probs, Int32(Q), x0, opts, ns, ts, vptr, lds, md, Int32(samples),
+                           seed, θ, nlml, ev, mptr, sptr))
+        end
+    end
+    if debug
+        for i in 1:Q
+            println("Output $(i + 1): optimum params $(Tuple(θ[5i-4:5i]))")
+        end
+    end
+    return means, stds
+end
+
 # ------------------------------------------------------------------ temporal_gp_inference.jl:45-114
 "Marginal of the latent f at one output location: `.m[1]` mean, `.P[1]` variance."
 struct Marginal

@@ -106,11 +106,10 @@ def test_sde_predictions_match_oracle():
 @pytest.mark.parametrize("qu_noise", [True, False])
 def test_fit_predict_equals_fit_then_predict(qu_noise):
     """gpar_fit_predict (get_gpar_scaled_predictions, gpar_scaled_inference.jl:20-136, batched
-    over outputs) == gpar_fit followed by one gpar_predict per output at the fitted theta.  q(u)
-    reuses the fit's Gram at that theta for both conventions.  With
-    qu_kuu_noise that is the computation gpar_predict redoes: bit for bit.  With the reference's
-    noise-free Cuu, gpar_predict recomputes the Gram from the fixed-up beta (less rounding for
-    the ill-conditioned Cuu), so the two agree to the q(u) tolerance."""
+    over outputs) == gpar_fit followed by one gpar_predict per output at the fitted theta --
+    bit for bit: with qu_kuu_noise q(u) reuses the fit's Gram at that theta, which is the same
+    computation it would redo; without, q(u) recomputes it (from the fixed-up beta: reusing the
+    fit's correction-form Gram for the noise-free Cuu measured 1.5e-7 off the oracle, r04a)."""
     import torch
     dev = torch.device("cuda", 0)
     t, Y = O.synthetic_gpar(900, 5, seed=23, noise=0.3)
@@ -135,14 +134,8 @@ def test_fit_predict_equals_fit_then_predict(qu_noise):
     for i, p in enumerate(outs):
         m2, s2 = G.predict_scaled(Y_d[:, : p - 1], Zs[p], t_d, Y_d[:, p - 1].contiguous(),
                                   fr.theta[i], ts_d, Fs_d[:, : p - 1], qu_kuu_noise=qu_noise)
-        a, b = means[i].cpu().numpy(), m2.cpu().numpy()
-        c, d = stds[i].cpu().numpy(), s2.cpu().numpy()
-        if qu_noise:
-            np.testing.assert_array_equal(a, b)
-            np.testing.assert_array_equal(c, d)
-        else:
-            np.testing.assert_allclose(a, b, rtol=1e-8, atol=1e-10 * np.abs(b).max())
-            np.testing.assert_allclose(c, d, rtol=1e-8, atol=1e-10 * np.abs(d).max())
+        np.testing.assert_array_equal(means[i].cpu().numpy(), m2.cpu().numpy())
+        np.testing.assert_array_equal(stds[i].cpu().numpy(), s2.cpu().numpy())
 
 
 @pytest.mark.parametrize("M,n,n_star,tk", [(30, 3000, 333, "matern32"), (140, 3000, 333, "matern32"),

@@ -262,4 +262,18 @@ def test_prediction_modes_map_explicitly():
         assert f"mode === {sym} && return {const}" in body
     assert "throw(DomainError(mode" in body
     assert "mode === :mc ? " not in src
-    assert src.count("md = predict_mode(mode)") == 2
+    assert src.count("md = predict_mode(mode)") == 3
+
+
+def test_matrix_batch_driver_passes_one_shared_input_matrix():
+    """the Julia batch driver's matrix form passes ONE point-major copy of the
+    N x P outputs (every output's inputs a column prefix, ldv = P) and one of the N* x P inference
+    inputs, which the library's host mode uploads once (prepare_batch / the staged test inputs)."""
+    src = open(SHIM).read()
+    m = re.search(r"function get_gpar_scaled_predictions_batch\(Y::AbstractMatrix,(.*?)\nend\n", src, re.S)
+    assert m, "matrix form missing"
+    body = m.group(1)
+    assert "Yt = Matrix{Float64}(permutedims(Y))" in body
+    assert "GparProblem(N, size(Zs[i - 1], 2), i - 1, pointer(t), pointer(Yt), P," in body
+    assert "vptr = fill(pointer(Ft), Q)" in body and "lds = fill(Int64(P), Q)" in body
+    assert body.count("ccall((:gpar_fit_predict") == 2
