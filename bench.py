@@ -433,6 +433,7 @@ def main():
         el = float(e[0])
     gram_n, gram_ms = ctx.kernel_stats("gram")
     wh_n, wh_ms = ctx.kernel_stats("whiten")
+    rnd_n, rnd_ms = ctx.kernel_stats("fit_round")   # round-by-round fits: entry -> values per round
     pred = {}
     for fam, bound in (("pred_whiten", "hbm"), ("pred_adjoint", "hbm"), ("pred_rows", "hbm"),
                        ("pred_gemm", "mfma"), ("pred_var", "mfma")):
@@ -677,6 +678,16 @@ def main():
                 "kernel": "Kfu assembly + Kalman whitening (whiten_kfu_d2x2 from the fit's distance "
                           "cache for D >= 17, fused whiten_kfu_mfma below)",
                 "bytes": "8 N (D + M + 20) per launch (M for D when cached), include/gpar_hip.h"}
+        if rnd_n and gram_n:
+            # what of the fit's rounds does not overlap a Gram: the round boundaries (dense tail
+            # after the last Gram, values to the host, the simplex step, the next round's gains and
+            # first whitening) plus any pipeline bubble
+            out["fit_rounds"] = {"rounds_per_step": rnd_n / args.steps,
+                                 "ms_per_step": rnd_ms / args.steps,
+                                 "gram_ms_per_step": gram_ms / args.steps,
+                                 "not_gram_ms_per_step": (rnd_ms - gram_ms) / args.steps,
+                                 "note": "HIP events on the context stream around each round-by-round "
+                                         "objective round (eval_dtc) vs the sum of its Gram spans"}
         if gram_n:
             # the whole job against its dominant kernel's floor: every Gram launch at the fp64
             # MFMA peak, nothing else, vs the measured step

@@ -391,6 +391,9 @@ std::vector<Theta> thetas_from(const double* theta, int np) {
 void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<Theta>& th,
                      double* out, std::vector<int>& status_out, GramOut* gram_out) {
   const int np = (int)P.size();
+  // one Nelder-Mead round of a batched fit, entry to values (the bench's round overhead: this
+  // span less the round's Gram spans is what does not overlap a Gram)
+  Timed tm_round(c, "fit_round");
   // On the CU-split pipeline the G-independent half of the dense tail (Kuu, its factor and
   // inverse) goes first on the Gram stream: it runs beside the gains and the first whitening,
   // while the Gram CUs would otherwise wait, instead of after the round's last Gram.

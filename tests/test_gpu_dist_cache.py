@@ -131,43 +131,49 @@ def test_cached_distances_match_direct_differences(kernel):
 
 
 def test_cache_survives_memory_pressure():
-    """A nearly full device (a blocker tensor) with an oversized explicit cache budget: the cache
-    takes what it can, the fit's own workspace then runs out of memory and evicts cache slots
-    (ws_bytes), and gpar_fit_predict completes with the unconstrained run's results."""
+    """A full device: the distance cache holds every slot (kept from an earlier call), a blocker
+    tensor takes the rest, and the next call's predictions need more workspace (more test points):
+    those allocations run out of memory, evict cache slots (ws_bytes) and retry, and
+    gpar_fit_predict completes with the unconstrained run's results."""
     import torch
     n, m = 200_000, 256
     t, probs, keep, data = _split_batch("matern52", n=n, m=m, dims=(2, 8, 20, 40))
-    ts = np.linspace(t[0], t[-1], 5000) + 1e-3
-    Vs = [np.vstack([np.interp(ts, t, V[q]) for q in range(V.shape[0])]) for V, _, _ in data]
+    ts_small = np.linspace(t[0], t[-1], 5000) + 1e-3
+    ts = np.linspace(t[0], t[-1], 60000) + 1e-3
+
+    def test_inputs(tt):
+        return [np.vstack([np.interp(tt, t, V[q]) for q in range(V.shape[0])]) for V, _, _ in data]
     x0 = np.tile(X0, (len(probs), 1))
     ctx = G.context(0)
-    cache_bytes = n * m * 8
     blocker = None
     try:
         ctx.set_cu_split(8)
         ctx.set_dist_cache(0)
         ctx.trim()
-        ref, rm, rs = G.fit_predict_batch(probs, x0, ts, Vs, max_evals=12, g_tol=-1.0)
-        work = ctx.workspace_bytes()                  # the call's workspace without the cache
+        ref, rm, rs = G.fit_predict_batch(probs, x0, ts, test_inputs(ts), max_evals=12, g_tol=-1.0)
         ctx.trim()
+        # every output cached and kept, with the workspace of the smaller call
+        ctx.set_dist_cache(1 << 40)
+        ctx.set_dist_cache_keep(True)
+        G.fit_predict_batch(probs, x0, ts_small, test_inputs(ts_small), max_evals=12, g_tol=-1.0)
+        held0 = ctx.dist_cache_stats()[2]
         torch.cuda.empty_cache()
         free = torch.cuda.mem_get_info(0)[0]
-        # leave the workspace plus 1.5 cache slots: the cache fills what it can, the workspace
-        # allocations then evict
-        leave = work + int(1.5 * cache_bytes)
-        blocker = torch.empty(free - leave, dtype=torch.uint8, device="cuda:0")
-        ctx.set_dist_cache(1 << 40)                   # explicit: far more than is free
+        blocker = torch.empty(free - (64 << 20), dtype=torch.uint8, device="cuda:0")
         ev0 = ctx.dist_cache_stats()[1]
-        got, gm, gs = G.fit_predict_batch(probs, x0, ts, Vs, max_evals=12, g_tol=-1.0)
+        got, gm, gs = G.fit_predict_batch(probs, x0, ts, test_inputs(ts), max_evals=12, g_tol=-1.0)
         cached, ev1, held = ctx.dist_cache_stats()
     finally:
         del blocker
         torch.cuda.empty_cache()
+        ctx.set_dist_cache_keep(False)
         ctx.set_cu_split(-1)
         ctx.set_dist_cache(-1)
         ctx.trim()
-    assert cached >= 1, cached
+    assert held0 == len(probs) * n * m * 8, held0
+    assert cached == len(probs), cached
     assert ev1 > ev0, (ev0, ev1)
+    assert held < held0, (held, held0)
     np.testing.assert_allclose(got.theta, ref.theta, rtol=1e-9)
     np.testing.assert_allclose(got.nlml, ref.nlml, rtol=1e-12)
     for a, b in zip(gm + gs, rm + rs):
