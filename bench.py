@@ -434,6 +434,8 @@ def main():
     gram_n, gram_ms = ctx.kernel_stats("gram")
     wh_n, wh_ms = ctx.kernel_stats("whiten")
     rnd_n, rnd_ms = ctx.kernel_stats("fit_round")   # round-by-round fits: entry -> values per round
+    rh_n, rh_ms = ctx.kernel_stats("round_head")    # ... entry -> first Gram start
+    rt_n, rt_ms = ctx.kernel_stats("round_tail")    # ... last Gram end -> values on the host
     pred = {}
     for fam, bound in (("pred_whiten", "hbm"), ("pred_adjoint", "hbm"), ("pred_rows", "hbm"),
                        ("pred_gemm", "mfma"), ("pred_var", "mfma")):
@@ -686,6 +688,10 @@ def main():
                                  "ms_per_step": rnd_ms / args.steps,
                                  "gram_ms_per_step": gram_ms / args.steps,
                                  "not_gram_ms_per_step": (rnd_ms - gram_ms) / args.steps,
+                                 "head_ms_per_step": rh_ms / args.steps if rh_n else None,
+                                 "tail_ms_per_step": rt_ms / args.steps if rt_n else None,
+                                 "between_grams_ms_per_step": ((rnd_ms - gram_ms - rh_ms - rt_ms)
+                                                               / args.steps if rh_n and rt_n else None),
                                  "note": "HIP events on the context stream around each round-by-round "
                                          "objective round (eval_dtc) vs the sum of its Gram spans"}
         if gram_n:

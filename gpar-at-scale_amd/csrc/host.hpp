@@ -100,6 +100,9 @@ struct gpar_ctx {
     double work = 0.0;
   };
   std::unordered_map<std::string, Stat> stats;
+  // profiling marks of a round-by-round fit round (eval_dtc): its first Gram's start and its last
+  // Gram's end on the Gram stream ("round_head" / "round_tail" stats)
+  hipEvent_t mark_first = nullptr, mark_last = nullptr;
 };
 
 // MC predictions: most draws a call takes (xi is samples x Mp doubles of workspace)
@@ -361,6 +364,7 @@ struct SplitPipe {
     {
       OnStream on_(c, c->s_g);
       HIPCHECK(hipStreamWaitEvent(c->s_g, c->ev_pc[i & 1], 0));
+      if (i == 0 && c->mark_first) HIPCHECK(hipEventRecord(c->mark_first, c->s_g));
       if (i >= 1) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[(i - 1) & 1], 0));
       stage_gram(c, pending, buf[i & 1], false, false, "", c->s_g2, gcus, c->s_w, c->ev_pw,
                  c->split_w);

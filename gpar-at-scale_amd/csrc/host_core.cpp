@@ -18,6 +18,7 @@ void flush_stats(gpar_ctx* c) {
     }
     kv.second.pending.clear();
   }
+  (void)hipGetLastError();   // an event pair that was never recorded must not fail a later launch check
 }
 
 void sync_all(gpar_ctx* c) {

@@ -234,6 +234,7 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     if (split_head) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr, 0));
     for (int i = 0; i < np; ++i) sp.push(job(i, sp.buf[i & 1]));
     sp.flush();
+    if (c->mark_last) HIPCHECK(hipEventRecord(c->mark_last, c->s_g));
     sp.join(c->stream);   // a prediction lane's q(u) runs this on the side stream
     if (split_head) {     // s_g2's gains precede the last Gram's correction, which join covers
       HIPCHECK(hipStreamWaitEvent(c->stream, c->ev_gr, 0));
@@ -394,6 +395,27 @@ void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<T
   // one Nelder-Mead round of a batched fit, entry to values (the bench's round overhead: this
   // span less the round's Gram spans is what does not overlap a Gram)
   Timed tm_round(c, "fit_round");
+  // with profiling: the round's head (entry -> first Gram) and tail (last Gram -> values)
+  hipEvent_t r0 = nullptr, r1 = nullptr;
+  int64_t mpm = 0;
+  for (const auto& p : P) mpm = std::max(mpm, p.mp);
+  if (c->profiling && fit_pipelined(c, P) && split_active(c, P[0].n, mpm)) {   // SplitPipe marks
+    HIPCHECK(hipEventCreate(&r0));
+    HIPCHECK(hipEventCreate(&r1));
+    HIPCHECK(hipEventCreate(&c->mark_first));
+    HIPCHECK(hipEventCreate(&c->mark_last));
+    HIPCHECK(hipEventRecord(r0, c->stream));
+  }
+  struct Marks {   // hands the events to the stats (flush_stats destroys them), on any exit
+    gpar_ctx* c;
+    hipEvent_t &r0, &r1;
+    ~Marks() {
+      if (!r0) return;
+      c->stats["round_head"].pending.push_back({r0, c->mark_first, 0.0});
+      c->stats["round_tail"].pending.push_back({c->mark_last, r1, 0.0});
+      c->mark_first = c->mark_last = nullptr;
+    }
+  } marks_{c, r0, r1};
   // On the CU-split pipeline the G-independent half of the dense tail (Kuu, its factor and
   // inverse) goes first on the Gram stream: it runs beside the gains and the first whitening,
   // while the Gram CUs would otherwise wait, instead of after the round's last Gram.
@@ -424,6 +446,7 @@ void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<T
   std::vector<int> st(2 * np);
   d2h(c, out, dout, np);
   d2h(c, st.data(), dn.status, 2 * np);
+  if (r1) HIPCHECK(hipEventRecord(r1, c->stream));
   sync(c);
   status_out.assign(np, 0);
   for (int i = 0; i < np; ++i) status_out[i] = st[2 * i] || st[2 * i + 1];
