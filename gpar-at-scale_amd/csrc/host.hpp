@@ -65,7 +65,7 @@ struct gpar_ctx {
     char* host = nullptr;
     size_t cap = 0, used = 0;
   };
-  Staging stage[2];
+  std::vector<Staging> stage;   // one per output group (deque-like: grown before use, never moved after)
   Staging* staging = nullptr;
   bool overlap = true;            // "overlap": round-overlapping batched fit (gpar_ctx_set_fit_overlap)
   int predict_lanes = 2;          // "predict_lanes": gpar_fit_predict's predictions over 1 or 2 streams
@@ -79,8 +79,12 @@ struct gpar_ctx {
   bool serialize = false;
   hipStream_t own_side = nullptr, own_s[4] = {nullptr, nullptr, nullptr, nullptr};
   std::string ws_suffix;          // appended to workspace names (a prediction lane's own buffers)
-  hipEvent_t ev_grp[2] = {nullptr, nullptr};   // fit_overlapped: a group's values are in
-  hipEvent_t ev_gn[2] = {nullptr, nullptr};    // fit_overlapped: a group's gains are done
+  std::vector<hipEvent_t> ev_grp;   // fit_overlapped: a group's values are in (one per group)
+  std::vector<hipEvent_t> ev_gn;    // fit_overlapped: a group's gains are done
+  // "overlap_group": outputs per group of the round overlap; 0 (auto) = groups of
+  // kOverlapGroupAuto in calls of 4..kOverlapMaxOutputs outputs, g > 0 = groups of g in any call
+  // of >= 4 outputs
+  int overlap_group = 0;
   std::string err;
   struct Buf {
     void* p = nullptr;

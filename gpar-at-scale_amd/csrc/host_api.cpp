@@ -81,13 +81,17 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
   return GPAR_OK;
 }
 
-static constexpr const char* kScheduleKnobs[] = {"overlap", "predict_fused", "qu_batch",
+static constexpr const char* kScheduleKnobs[] = {"overlap", "overlap_group", "predict_fused", "qu_batch",
                                                   "dense_early", "split_head", "predict_lanes",
                                                   "serialize"};
 
 // gpar_ctx_set_schedule / gpar_ctx_get_schedule (GPAR_ERR_ARG: unknown knob or value).
 static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
   if (k == "overlap") c->overlap = v != 0;
+  else if (k == "overlap_group") {
+    if (v < 0) return GPAR_ERR_ARG;
+    c->overlap_group = v;
+  }
   else if (k == "predict_fused") c->predict_fused = v != 0;
   else if (k == "qu_batch") c->qu_batch = v != 0;
   else if (k == "dense_early") c->dense_early = v != 0;
@@ -110,6 +114,7 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
 
 static int get_schedule(const gpar_ctx* c, const std::string& k, int32_t* v) {
   if (k == "overlap") *v = c->overlap;
+  else if (k == "overlap_group") *v = c->overlap_group;
   else if (k == "predict_fused") *v = c->predict_fused;
   else if (k == "qu_batch") *v = c->qu_batch;
   else if (k == "dense_early") *v = c->dense_early;
@@ -181,9 +186,11 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
         (void)hipStreamSynchronize(st);
         (void)hipStreamDestroy(st);
       }
-    for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_grp[0], ctx->ev_grp[1],
-                          ctx->ev_gn[0], ctx->ev_gn[1], ctx->ev_g0, ctx->ev_gr, ctx->ev_dn})
+    for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_g0, ctx->ev_gr, ctx->ev_dn})
       if (ev) (void)hipEventDestroy(ev);
+    for (const auto* evs : {&ctx->ev_grp, &ctx->ev_gn})
+      for (hipEvent_t ev : *evs)
+        if (ev) (void)hipEventDestroy(ev);
     for (auto& s : ctx->stage)
       if (s.host) (void)hipHostFree(s.host);
   }

@@ -155,11 +155,14 @@ struct OverlapGroup {
 };
 
 // Round overlap pays where the drain after each Nelder-Mead round is a large part of the round:
-// one 8-way shard of the north job (8 outputs per call) 2.70 -> 2.45 s per step; with all 63
-// north outputs in one call the round is long and the concurrent gains / dense tails on the
-// whitening CUs slow every Gram instead (5.13 -> 5.46 ms; 18.45 vs 18.75 s per job,
-// profiles/bench_r03d_*.json).
+// one 8-way shard of the north job (8 outputs per call, two groups of 4) 2.70 -> 2.45 s per step.
+// With all 63 north outputs in two groups of 32 the round is long and each group's burst of gains
+// and dense tails on the whitening CUs slowed every Gram instead (5.13 -> 5.46 ms; 18.45 vs
+// 18.75 s per job, profiles/bench_r03d_*.json); groups of gpar_ctx::overlap_group outputs spread
+// that work over the round.  Auto (overlap_group 0): groups of kOverlapGroupAuto in calls of up to
+// kOverlapMaxOutputs outputs; larger calls keep the round-by-round schedule.
 constexpr int kOverlapMaxOutputs = 16;
+constexpr int kOverlapGroupAuto = 8;
 
 using AcceptFn = std::function<void(int, double, const double*, const double*, int64_t)>;
 
@@ -170,16 +173,23 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
   int64_t mpmax = 0;
   for (auto& p : P) mpmax = std::max(mpmax, p.mp);
   const size_t sq = (size_t)mpmax * mpmax;
-  for (hipEvent_t* ev : {&c->ev_grp[0], &c->ev_grp[1], &c->ev_gn[0], &c->ev_gn[1]})
-    if (!*ev) HIPCHECK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
-  OverlapGroup grp[2];
-  // outputs dealt alternately (unequal groups measured slower at 63 outputs, r03w)
-  for (int i = 0; i < np; ++i) grp[i & 1].members.push_back(i);
-  for (int g = 0; g < 2; ++g) {
+  // K groups of about overlap_group outputs (at least two), dealt round-robin
+  const int gs = c->overlap_group > 0 ? c->overlap_group : kOverlapGroupAuto;
+  const int K = std::max(2, (np + gs - 1) / gs);
+  for (auto* evs : {&c->ev_grp, &c->ev_gn})
+    while ((int)evs->size() < K) {
+      hipEvent_t ev;
+      HIPCHECK(hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+      evs->push_back(ev);
+    }
+  if ((int)c->stage.size() < K) c->stage.resize(K);   // no arena is in use between calls
+  std::vector<OverlapGroup> grp(K);
+  for (int i = 0; i < np; ++i) grp[i % K].members.push_back(i);
+  for (int g = 0; g < K; ++g) {
     OverlapGroup& G = grp[g];
     G.id = g;
     const size_t cap = G.members.size();
-    const std::string sfx = g ? "B" : "A";
+    const std::string sfx = "g" + std::to_string(g);
     G.go.ldg = mpmax;
     G.go.npart = npart;
     G.go.G = ws<double>(c, "ovG" + sfx, cap * sq);
@@ -261,8 +271,8 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
     {
       OnStream on_(c, c->s_d);
       StagingScope st_(c, G.id);
-      gn = run_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, G.id ? "fitB" : "fitA", &ys,
-                     G.alpha_all, G.asend_all);
+      gn = run_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fitg" + std::to_string(G.id),
+                     &ys, G.alpha_all, G.asend_all);
       HIPCHECK(hipMemcpyAsync(G.go.logs, gn.logs, (size_t)na * nch * sizeof(double),
                               hipMemcpyDeviceToDevice, c->s_d));
       HIPCHECK(hipEventRecord(c->ev_gn[G.id], c->s_d));
@@ -312,9 +322,13 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
   };
   sp.start();
   HIPCHECK(hipStreamWaitEvent(c->s_d, c->ev_sp, 0));   // the inputs / distance cache on main
-  begin_round(grp[0]);
-  begin_round(grp[1]);
-  for (int g = 0; grp[0].in_flight || grp[1].in_flight; g ^= 1) {
+  for (auto& G : grp) begin_round(G);
+  auto any_in_flight = [&]() {
+    for (const auto& G : grp)
+      if (G.in_flight) return true;
+    return false;
+  };
+  for (int g = 0; any_in_flight(); g = (g + 1) % K) {
     if (!grp[g].in_flight) continue;
     finish_round(grp[g]);
     begin_round(grp[g]);
@@ -370,7 +384,8 @@ void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* lo
   };
   int64_t mpmax = 0;
   for (auto& p : P) mpmax = std::max(mpmax, p.mp);
-  if (ctx->overlap && nprob >= 4 && nprob <= kOverlapMaxOutputs && fit_pipelined(ctx, P) &&
+  if (ctx->overlap && nprob >= 4 && (nprob <= kOverlapMaxOutputs || ctx->overlap_group > 0) &&
+      fit_pipelined(ctx, P) &&
       split_active(ctx, P[0].n, mpmax))
     fit_overlapped(ctx, P, nm, accept);
   std::vector<double> vals;

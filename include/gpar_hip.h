@@ -147,6 +147,9 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
 /* Schedule knobs: each selects an order or a placement of the same launches, never different
  * arithmetic, so results are bit-identical with any setting (tests/test_gpu_schedule.py):
  *   "overlap"       1: round-overlapping batched fit, as gpar_ctx_set_fit_overlap (default 1)
+ *   "overlap_group" outputs per group of the round overlap: 0 (default) = groups of 8 in calls of
+ *                   4..16 outputs (larger calls: round by round); g > 0 = groups of g in any call
+ *                   of >= 4 outputs
  *   "qu_batch"      1: gpar_fit_predict runs q(u) batched over the outputs (default 1)
  *   "dense_early"   1: the G-independent half of the dense tail ahead of a split round's Grams (1)
  *   "split_head"    1: a split round's first whitening on the whole chip (default 1)

@@ -10,9 +10,9 @@ waiting for the context stream, a q(u) Gram on the wrong lane).
 gpar_ctx_set_schedule("serialize", 1) routes every launch of the same schedule to the context's one
 stream, in issue order, with the same Gram plans, CU shares of work items and workspaces: an
 order-free reference.  Any missing dependency in the concurrent schedule shows up as a difference.
-Every other schedule knob (round overlap, the dense prefix, the split round head, batched q(u),
-prediction lanes) only reorders or re-places the same launches, so it must give bit-identical
-results too.  Sizes: the headline test's (N = 4e5, M = 512: the auto CU split, the pipelined Gram
+Every other schedule knob (round overlap and its number of output groups, the dense prefix, the
+split round head, batched q(u), prediction lanes) only reorders or re-places the same launches, so
+it must give bit-identical results too.  Sizes: the headline test's (N = 4e5, M = 512: the auto CU split, the pipelined Gram
 stage, the distance cache down to D = 1, five outputs: the round overlap).
 """
 import numpy as np
@@ -29,14 +29,16 @@ OUTS = [2, 3, 9, 17, 33]
 SETTINGS = [
     {"serialize": 1},
     {"overlap": 0},
+    {"overlap_group": 2},                # three groups (2, 2, 1 outputs) take turns
+    {"overlap_group": 1},                # five groups of one
     {"overlap": 0, "serialize": 1},
     {"overlap": 0, "dense_early": 0},
     {"overlap": 0, "split_head": 0},
     {"qu_batch": 0},
     {"predict_lanes": 1},
 ]
-DEFAULTS = {"serialize": 0, "overlap": 1, "dense_early": 1, "split_head": 1, "qu_batch": 1,
-            "predict_lanes": 2}
+DEFAULTS = {"serialize": 0, "overlap": 1, "overlap_group": 0, "dense_early": 1, "split_head": 1,
+            "qu_batch": 1, "predict_lanes": 2}
 
 
 @pytest.fixture(scope="module")
