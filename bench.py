@@ -119,6 +119,9 @@ def main():
                     help="after the timed device-resident steps, this many host->host steps "
                          "(SURVEY §8d's unit: one pinned upload of t, Y, t*, F* and the pseudo-inputs "
                          "per step, means / stds downloaded), reported as host_to_host beside value")
+    ap.add_argument("--schedule", default="",
+                    help="schedule knobs as k=v,k=v (gpar_ctx_set_schedule: overlap, overlap_group, "
+                         "qu_batch, dense_early, split_head, predict_lanes, serialize); A/B only")
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-check-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--stub", action="store_true",
@@ -259,6 +262,11 @@ def main():
 
     ctx = G.context(local)
     ctx.set_lanes(args.lanes)
+    knobs = {}
+    for kv in filter(None, args.schedule.split(",")):
+        k, v = kv.split("=")
+        ctx.set_schedule(k.strip(), int(v))
+        knobs[k.strip()] = int(v)
     if args.cu_split is not None:
         ctx.set_cu_split(args.cu_split)
     cu_split = ctx.cu_split()
@@ -434,6 +442,7 @@ def main():
     gram_n, gram_ms = ctx.kernel_stats("gram")
     wh_n, wh_ms = ctx.kernel_stats("whiten")
     rnd_n, rnd_ms = ctx.kernel_stats("fit_round")   # round-by-round fits: entry -> values per round
+    fc_n, fc_ms = ctx.kernel_stats("fit_call")      # whole batched fits (any schedule)
     rh_n, rh_ms = ctx.kernel_stats("round_head")    # ... entry -> first Gram start
     rt_n, rt_ms = ctx.kernel_stats("round_tail")    # ... last Gram end -> values on the host
     pred = {}
@@ -649,6 +658,7 @@ def main():
                        "outputs_per_rank": shards, "inference": args.inference,
                        "inputs": args.inputs, "cu_split": cu_split, "qu_kuu_noise": qn,
                        "api": args.api, "dist_cache": args.dist_cache,
+                       **({"schedule": knobs} if knobs else {}),
                        **({"shard": f"{shard_of[0]}/{shard_of[1]}", "shard_outputs": mine}
                           if shard_of else {})},
             "qu_convention": ("q(u) and the predictions factor Cuu + sigma^2 I (qu_kuu_noise), the "
@@ -680,6 +690,12 @@ def main():
                 "kernel": "Kfu assembly + Kalman whitening (whiten_kfu_d2x2 from the fit's distance "
                           "cache for D >= 17, fused whiten_kfu_mfma below)",
                 "bytes": "8 N (D + M + 20) per launch (M for D when cached), include/gpar_hip.h"}
+        if fc_n and gram_n:
+            out["fit_calls"] = {"calls_per_step": fc_n / args.steps, "ms_per_step": fc_ms / args.steps,
+                                "not_gram_ms_per_step": (fc_ms - gram_ms) / args.steps,
+                                "note": "HIP events around each batched fit (after its distance cache) "
+                                        "vs the sum of the Gram spans: the fit's time off the Gram's "
+                                        "critical path (round boundaries, pipeline bubbles)"}
         if rnd_n and gram_n:
             # what of the fit's rounds does not overlap a Gram: the round boundaries (dense tail
             # after the last Gram, values to the host, the simplex step, the next round's gains and

@@ -354,6 +354,10 @@ void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* lo
   const std::vector<DevProblem> P =
       attach_dist_cache(ctx, P0, fit_ws_estimate(ctx, P0) + later_bytes);
   const int nprob = (int)P.size();
+  // the whole fit after its distance cache, on the context stream (every schedule ends joined to it
+  // or synchronised): the bench's fit time against its Gram spans
+  std::optional<Timed> tm_fit;
+  tm_fit.emplace(ctx, "fit_call");
   std::vector<NelderMead> nm;
   nm.reserve(nprob);
   for (int i = 0; i < nprob; ++i)
@@ -412,6 +416,7 @@ void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* lo
              keep ? go.r + a * go.ldg : nullptr, go.ldg);
     }
   }
+  tm_fit.reset();
   for (int i = 0; i < nprob; ++i) {
     const auto& x = nm[i].x_min();
     for (int j = 0; j < 5; ++j) theta_out[5 * i + j] = unpack(x[j]);

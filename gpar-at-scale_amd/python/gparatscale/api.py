@@ -461,6 +461,8 @@ class Posterior:
     def predict(self, i, t_star, V_star, mode="analytic", samples=100, seed=0):
         """Output i's (mean, std) at (t_star, V_star): device tensors (V_star N* x D, rows =
         points) for device problems, numpy (D x N* ColVecs) for host ones."""
+        if not 0 <= int(i) < len(self._problems):
+            raise _arg_error(f"output index {i} out of range (0..{len(self._problems) - 1})")
         p = self._problems[i]
         keep = _Keep()
         ctx, lib = context(self.device), _lib.load()
