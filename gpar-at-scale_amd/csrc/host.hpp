@@ -43,6 +43,7 @@ struct gpar_ctx {
   hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
   hipEvent_t ev_g0 = nullptr, ev_gr = nullptr;   // split round start: gains uploaded / the rest's gains done
   hipEvent_t ev_dn = nullptr;                    // split round start: the dense prefix follows the context stream
+  hipEvent_t ev_dp = nullptr;                    // split round: the dense prefix is done (on s_d)
   // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
   // the caller's stream, e.g. the copies that produce its device inputs
   bool has_input_stream = false;

@@ -417,23 +417,29 @@ void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<T
     }
   } marks_{c, r0, r1};
   // On the CU-split pipeline the G-independent half of the dense tail (Kuu, its factor and
-  // inverse) goes first on the Gram stream: it runs beside the gains and the first whitening,
-  // while the Gram CUs would otherwise wait, instead of after the round's last Gram.
+  // inverse) runs on the dense stream (the whitening CUs) from the round's start, beside the
+  // gains, the whitenings and the Grams, instead of after the round's last Gram.  (On the Gram
+  // stream ahead of the first Gram, r03, its ~5 ms latency-bound chain for 63 outputs held that
+  // Gram back: 8.6 ms from round entry to the first Gram, r04d.)
   int64_t mpmax = 0;
   for (const auto& p : P) mpmax = std::max(mpmax, p.mp);
   const bool early = c->dense_early && fit_pipelined(c, P) && split_active(c, P[0].n, mpmax);
   DenseOut dn{};
   if (early) {
-    // the Gram stream first follows everything queued on the context stream (host inputs' uploads,
-    // the pseudo-input centres, the distance cache), then factors Kuu beside the round's gains
+    // the dense stream first follows everything queued on the context stream (host inputs'
+    // uploads, the pseudo-input centres, the distance cache)
     HIPCHECK(hipEventRecord(c->ev_dn, c->stream));
-    HIPCHECK(hipStreamWaitEvent(c->s_g, c->ev_dn, 0));
-    OnStream on_(c, c->s_g);
+    HIPCHECK(hipStreamWaitEvent(c->s_d, c->ev_dn, 0));
+    OnStream on_(c, c->s_d);
     dn = run_dense_pre(c, P, th, mpmax, false);
+    HIPCHECK(hipEventRecord(c->ev_dp, c->s_d));
   }
   GramOut go = run_gram_stage(c, P, th);
   if (gram_out) *gram_out = go;
-  if (!early) dn = run_dense_pre(c, P, th, go.ldg, false);
+  if (early)
+    HIPCHECK(hipStreamWaitEvent(c->stream, c->ev_dp, 0));
+  else
+    dn = run_dense_pre(c, P, th, go.ldg, false);
   run_dense_post(c, P, go, dn);
   const int64_t nch = P[0].nch;
   std::vector<Finish2JobHost> fj(np);
