@@ -443,8 +443,13 @@ def main():
     wh_n, wh_ms = ctx.kernel_stats("whiten")
     rnd_n, rnd_ms = ctx.kernel_stats("fit_round")   # round-by-round fits: entry -> values per round
     fc_n, fc_ms = ctx.kernel_stats("fit_call")      # whole batched fits (any schedule)
-    rh_n, rh_ms = ctx.kernel_stats("round_head")    # ... entry -> first Gram start
-    rt_n, rt_ms = ctx.kernel_stats("round_tail")    # ... last Gram end -> values on the host
+    # ... and along each round (split fits): entry -> first output's gains -> its whitening -> its
+    # short chain -> the first Gram's start -> the last Gram's end -> the values on the host
+    marks = {k: ctx.kernel_stats(k) for k in ("head_gains", "head_w0", "head_p0", "head_gram_wait",
+                                               "round_grams", "round_tail")}
+    rh_n = marks["head_gains"][0]
+    rh_ms = sum(marks[k][1] for k in ("head_gains", "head_w0", "head_p0", "head_gram_wait"))
+    rt_n, rt_ms = marks["round_tail"]
     pred = {}
     for fam, bound in (("pred_whiten", "hbm"), ("pred_adjoint", "hbm"), ("pred_rows", "hbm"),
                        ("pred_gemm", "mfma"), ("pred_var", "mfma")):
@@ -708,6 +713,8 @@ def main():
                                  "tail_ms_per_step": rt_ms / args.steps if rt_n else None,
                                  "between_grams_ms_per_step": ((rnd_ms - gram_ms - rh_ms - rt_ms)
                                                                / args.steps if rh_n and rt_n else None),
+                                 "marks_ms_per_step": {k: v[1] / args.steps for k, v in marks.items()
+                                                       if v[0]},
                                  "note": "HIP events on the context stream around each round-by-round "
                                          "objective round (eval_dtc) vs the sum of its Gram spans"}
         if gram_n:

@@ -108,6 +108,13 @@ struct gpar_ctx {
   // profiling marks of a round-by-round fit round (eval_dtc): its first Gram's start and its last
   // Gram's end on the Gram stream ("round_head" / "round_tail" stats)
   hipEvent_t mark_first = nullptr, mark_last = nullptr;
+  hipEvent_t mark_h[3] = {nullptr, nullptr, nullptr};   // the round head's first job: gains, W, P
+  // event sequences: stats[names[i]] += time from ev[i - 1] to ev[i] (flush_stats)
+  struct MarkSeq {
+    std::vector<std::string> names;
+    std::vector<hipEvent_t> ev;
+  };
+  std::vector<MarkSeq> mark_seqs;
 };
 
 // MC predictions: most draws a call takes (xi is samples x Mp doubles of workspace)
@@ -348,8 +355,11 @@ struct SplitPipe {
       // nothing runs on the Gram CUs before the first Gram: the first whitening and its short
       // chain take the whole chip (the caller's unmasked stream, which the split streams follow
       // since start()); the whitening side continues after them
+      if (c->mark_h[0]) HIPCHECK(hipEventRecord(c->mark_h[0], c->stream));
       stage_whiten(c, j, buf[0]);
+      if (c->mark_h[1]) HIPCHECK(hipEventRecord(c->mark_h[1], c->stream));
       stage_post(c, j, buf[0], false);
+      if (c->mark_h[2]) HIPCHECK(hipEventRecord(c->mark_h[2], c->stream));
       HIPCHECK(hipEventRecord(c->ev_pc[0], c->stream));
       HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[0], 0));
     } else {

@@ -18,6 +18,18 @@ void flush_stats(gpar_ctx* c) {
     }
     kv.second.pending.clear();
   }
+  for (auto& q : c->mark_seqs) {
+    for (size_t i = 1; i < q.ev.size(); ++i) {
+      float ms = 0.f;
+      if (hipEventElapsedTime(&ms, q.ev[i - 1], q.ev[i]) == hipSuccess) {
+        auto& st = c->stats[q.names[i]];
+        st.ms += ms;
+        st.launches += 1;
+      }
+    }
+    for (hipEvent_t e : q.ev) (void)hipEventDestroy(e);
+  }
+  c->mark_seqs.clear();
   (void)hipGetLastError();   // an event pair that was never recorded must not fail a later launch check
 }
 

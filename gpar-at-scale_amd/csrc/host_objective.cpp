@@ -395,51 +395,55 @@ void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<T
   // one Nelder-Mead round of a batched fit, entry to values (the bench's round overhead: this
   // span less the round's Gram spans is what does not overlap a Gram)
   Timed tm_round(c, "fit_round");
-  // with profiling: the round's head (entry -> first Gram) and tail (last Gram -> values)
-  hipEvent_t r0 = nullptr, r1 = nullptr;
+  // with profiling: marks along the round (flush_stats turns consecutive marks into stats):
+  // entry -> the first output's gains ("head_gains") -> its whitening ("head_w0") -> its short
+  // chain ("head_p0") -> the first Gram's start ("head_gram_wait") -> the last Gram's end
+  // ("round_grams") -> the values on the host ("round_tail")
+  gpar_ctx::MarkSeq seq;
   int64_t mpm = 0;
   for (const auto& p : P) mpm = std::max(mpm, p.mp);
   if (c->profiling && fit_pipelined(c, P) && split_active(c, P[0].n, mpm)) {   // SplitPipe marks
-    HIPCHECK(hipEventCreate(&r0));
-    HIPCHECK(hipEventCreate(&r1));
-    HIPCHECK(hipEventCreate(&c->mark_first));
-    HIPCHECK(hipEventCreate(&c->mark_last));
-    HIPCHECK(hipEventRecord(r0, c->stream));
+    seq.names = {"", "head_gains", "head_w0", "head_p0", "head_gram_wait", "round_grams",
+                 "round_tail"};
+    seq.ev.assign(seq.names.size(), nullptr);
+    for (hipEvent_t& e : seq.ev) HIPCHECK(hipEventCreate(&e));
+    c->mark_h[0] = seq.ev[1];
+    c->mark_h[1] = seq.ev[2];
+    c->mark_h[2] = seq.ev[3];
+    c->mark_first = seq.ev[4];
+    c->mark_last = seq.ev[5];
+    HIPCHECK(hipEventRecord(seq.ev[0], c->stream));
   }
-  struct Marks {   // hands the events to the stats (flush_stats destroys them), on any exit
+  struct Marks {   // hands the sequence to the stats (flush_stats destroys its events), on any exit
     gpar_ctx* c;
-    hipEvent_t &r0, &r1;
+    gpar_ctx::MarkSeq& seq;
     ~Marks() {
-      if (!r0) return;
-      c->stats["round_head"].pending.push_back({r0, c->mark_first, 0.0});
-      c->stats["round_tail"].pending.push_back({c->mark_last, r1, 0.0});
+      if (seq.ev.empty()) return;
+      c->mark_seqs.push_back(std::move(seq));
       c->mark_first = c->mark_last = nullptr;
+      for (hipEvent_t& e : c->mark_h) e = nullptr;
     }
-  } marks_{c, r0, r1};
+  } marks_{c, seq};
   // On the CU-split pipeline the G-independent half of the dense tail (Kuu, its factor and
-  // inverse) runs on the dense stream (the whitening CUs) from the round's start, beside the
-  // gains, the whitenings and the Grams, instead of after the round's last Gram.  (On the Gram
-  // stream ahead of the first Gram, r03, its ~5 ms latency-bound chain for 63 outputs held that
-  // Gram back: 8.6 ms from round entry to the first Gram, r04d.)
+  // inverse) goes first on the Gram stream: it runs beside the gains and the first whitening,
+  // while the Gram CUs would otherwise wait, instead of after the round's last Gram.  (On the
+  // dense stream over the whitening CUs instead, r04e, it slowed every Gram 5.11 -> 5.16 ms: the
+  // Gram's diagonal-block share runs there.)
   int64_t mpmax = 0;
   for (const auto& p : P) mpmax = std::max(mpmax, p.mp);
   const bool early = c->dense_early && fit_pipelined(c, P) && split_active(c, P[0].n, mpmax);
   DenseOut dn{};
   if (early) {
-    // the dense stream first follows everything queued on the context stream (host inputs'
-    // uploads, the pseudo-input centres, the distance cache)
+    // the Gram stream first follows everything queued on the context stream (host inputs' uploads,
+    // the pseudo-input centres, the distance cache), then factors Kuu beside the round's gains
     HIPCHECK(hipEventRecord(c->ev_dn, c->stream));
-    HIPCHECK(hipStreamWaitEvent(c->s_d, c->ev_dn, 0));
-    OnStream on_(c, c->s_d);
+    HIPCHECK(hipStreamWaitEvent(c->s_g, c->ev_dn, 0));
+    OnStream on_(c, c->s_g);
     dn = run_dense_pre(c, P, th, mpmax, false);
-    HIPCHECK(hipEventRecord(c->ev_dp, c->s_d));
   }
   GramOut go = run_gram_stage(c, P, th);
   if (gram_out) *gram_out = go;
-  if (early)
-    HIPCHECK(hipStreamWaitEvent(c->stream, c->ev_dp, 0));
-  else
-    dn = run_dense_pre(c, P, th, go.ldg, false);
+  if (!early) dn = run_dense_pre(c, P, th, go.ldg, false);
   run_dense_post(c, P, go, dn);
   const int64_t nch = P[0].nch;
   std::vector<Finish2JobHost> fj(np);
@@ -452,7 +456,7 @@ void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<T
   std::vector<int> st(2 * np);
   d2h(c, out, dout, np);
   d2h(c, st.data(), dn.status, 2 * np);
-  if (r1) HIPCHECK(hipEventRecord(r1, c->stream));
+  if (!seq.ev.empty()) HIPCHECK(hipEventRecord(seq.ev.back(), c->stream));
   sync(c);
   status_out.assign(np, 0);
   for (int i = 0; i < np; ++i) status_out[i] = st[2 * i] || st[2 * i + 1];
