@@ -41,7 +41,6 @@ struct gpar_ctx {
   // s_d: the round-overlapping fit's dense tails, on the whitening CUs (fit_overlapped)
   hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr, s_d = nullptr;
   hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
-  hipEvent_t ev_g0 = nullptr, ev_gr = nullptr;   // split round start: gains uploaded / the rest's gains done
   hipEvent_t ev_dn = nullptr;                    // split round start: the dense prefix follows the context stream
   hipEvent_t ev_dp = nullptr;                    // split round: the dense prefix is done (on s_d)
   // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
@@ -214,6 +213,9 @@ constexpr int64_t kPipeMaxBetaBytes = (int64_t)8 << 30;   // second beta buffer 
 // default gpar_ctx_set_cu_split width: 8 of every XCD's 32 CUs whiten beside the Gram (north job
 // 20.66 -> 19.69 s per job in same-box pairs; 4 starves the whitening: 28.4 s)
 constexpr int kDefaultCuSplit = 8;
+// a split round's gains: the first kHeadGains outputs' on the context stream at the round's head,
+// then kHeadGains at a time on the whitening stream (run_gram_stage)
+constexpr int kHeadGains = 8;
 // the default split applies to batched fits whose Gram is big enough to amortise it: N Mp^2 >= 1e11
 // (north, N = 1e6, M = 512: 2.6e11; the N = 1e5 configs measured slower split: dtc 389 vs 297 ms
 // per job, eeg 3.09 vs 3.07 s)
@@ -278,12 +280,31 @@ struct GainsOut {
   double *rec, *g, *phi, *logs, *pf;
   int64_t recstride, gstride, phistride;
 };
+// The gains of `nchains` chains sharing t: uploads and workspace (plan_gains), launched over any
+// chain ranges on any streams (GainsPlan::launch) -- the split fit launches them group by group on
+// the whitening stream ahead of the whitenings that read them.
+struct GainsPlan {
+  gpar_ctx* c = nullptr;
+  int sdim = 0, nchains = 0;
+  const double* t = nullptr;
+  int64_t n = 0, nch = 0;
+  const double* noise = nullptr;
+  ChainParamsHost* dcps = nullptr;
+  double *agg = nullptr, *pst = nullptr;
+  GainsOut o{};
+  const double** dys = nullptr;
+  double *alpha_loc = nullptr, *asend = nullptr;
+  void launch(hipStream_t st, int first, int count) const;
+};
+GainsPlan plan_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
+                     const std::vector<ChainParamsHost>& cps, const double* noise, bool want_pf,
+                     const std::string& tag, const std::vector<const double*>* ys = nullptr,
+                     double* alpha_loc = nullptr, double* asend = nullptr);
 GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                           const std::vector<ChainParamsHost>& cps, const double* noise,
                           bool want_pf, const std::string& tag,
                           const std::vector<const double*>* ys = nullptr,
-                          double* alpha_loc = nullptr, double* asend = nullptr,
-                          hipStream_t st_rest = nullptr);
+                          double* alpha_loc = nullptr, double* asend = nullptr);
 void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const double* rec, const double* v,
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
                            int64_t ldb, double* send, const double* g, double* hsum);
@@ -339,6 +360,7 @@ struct SplitPipe {
   bool has_pending = false;   // job k - 1 whitened, its Gram not yet issued
   StageJob pending;
   std::function<void(const StageJob&, int64_t)> on_gram;   // right after job k's Gram is issued
+  std::function<void(int64_t)> pre_whiten;   // on the whitening stream, just before whitening k
 
   SplitPipe(gpar_ctx* c_, int64_t n, int64_t mpmax)
       : c(c_), gcus(8 * (32 - c_->split_w)) {
@@ -364,6 +386,7 @@ struct SplitPipe {
       HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[0], 0));
     } else {
       OnStream on_(c, c->s_w);
+      if (pre_whiten) pre_whiten(k);
       if (k >= 2) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[k & 1], 0));
       stage_whiten(c, j, buf[k & 1]);
       stage_post(c, j, buf[k & 1], false);

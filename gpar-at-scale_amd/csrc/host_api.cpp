@@ -70,8 +70,6 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
         (hipEventCreateWithFlags(&c->ev_gd[0], hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_gd[1], hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_sp, hipEventDisableTiming) != hipSuccess ||
-         hipEventCreateWithFlags(&c->ev_g0, hipEventDisableTiming) != hipSuccess ||
-         hipEventCreateWithFlags(&c->ev_gr, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_dn, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_dp, hipEventDisableTiming) != hipSuccess))
       return GPAR_ERR_HIP;
@@ -187,7 +185,7 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
         (void)hipStreamSynchronize(st);
         (void)hipStreamDestroy(st);
       }
-    for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_g0, ctx->ev_gr, ctx->ev_dn,
+    for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_dn,
                           ctx->ev_dp})
       if (ev) (void)hipEventDestroy(ev);
     for (const auto* evs : {&ctx->ev_grp, &ctx->ev_gn})

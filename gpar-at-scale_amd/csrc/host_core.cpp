@@ -279,21 +279,27 @@ std::vector<DevProblem> prepare_batch(gpar_ctx* c, const gpar_problem* probs, in
 // Data-independent per-step filter quantities for `nchains` chains sharing t (n steps).
 // With ys (one device data vector per chain): the chains' alpha_loc / chunk end states are
 // filtered inside the gains pass (alpha_loc: nchains x n, asend: nchains x nch x 4).
-GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
-                          const std::vector<ChainParamsHost>& cps, const double* noise,
-                          bool want_pf, const std::string& tag,
-                          const std::vector<const double*>* ys,
-                          double* alpha_loc, double* asend,
-                          hipStream_t st_rest) {
-  const int nchains = (int)cps.size();
-  const int64_t nch = (n + kChunk - 1) / kChunk;
+GainsPlan plan_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
+                     const std::vector<ChainParamsHost>& cps, const double* noise, bool want_pf,
+                     const std::string& tag, const std::vector<const double*>* ys,
+                     double* alpha_loc, double* asend) {
+  GainsPlan gp;
+  gp.c = c;
+  gp.sdim = sdim;
+  gp.t = t;
+  gp.n = n;
+  gp.nchains = (int)cps.size();
+  gp.nch = (n + kChunk - 1) / kChunk;
+  gp.noise = noise;
+  const int nchains = gp.nchains;
+  const int64_t nch = gp.nch;
   const int rs = rec_size(sdim);
   const int d2 = sdim * sdim;
-  ChainParamsHost* dcps = ws<ChainParamsHost>(c, tag + "_cps", nchains);
-  h2d(c, dcps, cps.data(), nchains);
-  double* agg = ws<double>(c, tag + "_agg", (size_t)nchains * nch * 3 * d2);
-  double* pst = ws<double>(c, tag + "_pstart", (size_t)nchains * nch * d2);
-  GainsOut o;
+  gp.dcps = ws<ChainParamsHost>(c, tag + "_cps", nchains);
+  h2d(c, gp.dcps, cps.data(), nchains);
+  gp.agg = ws<double>(c, tag + "_agg", (size_t)nchains * nch * 3 * d2);
+  gp.pst = ws<double>(c, tag + "_pstart", (size_t)nchains * nch * d2);
+  GainsOut& o = gp.o;
   o.recstride = n * rs;
   o.gstride = n * 4;
   o.phistride = nch * d2;
@@ -302,32 +308,39 @@ GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
   o.phi = ws<double>(c, tag + "_phi", (size_t)nchains * nch * d2);
   o.logs = ws<double>(c, tag + "_logs", (size_t)nchains * nch);
   o.pf = want_pf ? ws<double>(c, tag + "_pf", (size_t)nchains * n * d2) : nullptr;
-  const double** dys = nullptr;
   if (ys) {
-    dys = ws<const double*>(c, tag + "_ys", nchains);
-    h2d(c, dys, ys->data(), nchains);
+    gp.dys = ws<const double*>(c, tag + "_ys", nchains);
+    h2d(c, gp.dys, ys->data(), nchains);
   }
-  // st_rest: chain 0 on c->stream, chains 1.. on st_rest (after the uploads above), which then
-  // records c->ev_gr; the chains' arrays are strided per chain, so a range is a pointer offset
-  const int n0 = (st_rest && nchains > 1) ? 1 : nchains;
-  if (n0 < nchains) HIPCHECK(hipEventRecord(c->ev_g0, c->stream));
-  {
-    Timed tm_(c, "gains");
-    launch_gains(c->stream, sdim, t, n, kChunk, nch, n0, dcps, noise, agg, pst, o.rec, o.g,
-                 o.phi, o.logs, o.pf, dys, alpha_loc, asend);
-  }
-  if (n0 < nchains) {
-    HIPCHECK(hipStreamWaitEvent(st_rest, c->ev_g0, 0));
-    launch_gains(st_rest, sdim, t, n, kChunk, nch, nchains - n0, dcps + n0, noise,
-                 agg + (size_t)n0 * nch * 3 * d2, pst + (size_t)n0 * nch * d2,
-                 o.rec + (size_t)n0 * o.recstride, o.g + (size_t)n0 * o.gstride,
-                 o.phi + (size_t)n0 * o.phistride, o.logs + (size_t)n0 * nch,
-                 o.pf ? o.pf + (size_t)n0 * n * d2 : nullptr, dys ? dys + n0 : nullptr,
-                 alpha_loc ? alpha_loc + (size_t)n0 * n : nullptr,
-                 asend ? asend + (size_t)n0 * nch * kSStride : nullptr);
-    HIPCHECK(hipEventRecord(c->ev_gr, st_rest));
-  }
+  gp.alpha_loc = alpha_loc;
+  gp.asend = asend;
+  return gp;
+}
+
+// chains [first, first + count) on stream st; the chains' arrays are strided per chain, so a
+// range is a pointer offset
+void GainsPlan::launch(hipStream_t st, int first, int count) const {
+  if (count <= 0) return;
+  const int d2 = sdim * sdim;
+  OnStream on_(c, st);
+  Timed tm_(c, "gains");
+  launch_gains(st, sdim, t, n, kChunk, nch, count, dcps + first, noise,
+               agg + (size_t)first * nch * 3 * d2, pst + (size_t)first * nch * d2,
+               o.rec + (size_t)first * o.recstride, o.g + (size_t)first * o.gstride,
+               o.phi + (size_t)first * o.phistride, o.logs + (size_t)first * nch,
+               o.pf ? o.pf + (size_t)first * n * d2 : nullptr, dys ? dys + first : nullptr,
+               alpha_loc ? alpha_loc + (size_t)first * n : nullptr,
+               asend ? asend + (size_t)first * nch * kSStride : nullptr);
   check_launch("gains");
-  return o;
+}
+
+GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
+                          const std::vector<ChainParamsHost>& cps, const double* noise,
+                          bool want_pf, const std::string& tag,
+                          const std::vector<const double*>* ys,
+                          double* alpha_loc, double* asend) {
+  GainsPlan gp = plan_gains(c, sdim, t, n, cps, noise, want_pf, tag, ys, alpha_loc, asend);
+  gp.launch(c->stream, 0, gp.nchains);
+  return gp.o;
 }
 }  // namespace gpar

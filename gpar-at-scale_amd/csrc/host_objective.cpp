@@ -161,6 +161,7 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   const bool split_head = split_pipe && c->split_head && shared && np > 1;
   const double* logs_src = nullptr;
   std::vector<GainsOut> gains(np);
+  GainsPlan gplan;
   // shared gains: every output's alpha_loc (y filtered from zero per chunk) comes out of the
   // gains pass itself; only its chunk end states are copied into the carry's alpha column
   double* alpha_all = nullptr;
@@ -174,10 +175,14 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     }
     alpha_all = ws<double>(c, "alpha_all", (size_t)np * n);
     asend_all = ws<double>(c, "asend_all", (size_t)np * nch * kSStride);
-    // split pipeline: the first output's gains alone on the context stream, so its whitening can
-    // start, the others' on s_g2 (Gram CUs, idle until the first Gram's correction)
-    GainsOut g = run_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fit", &ys, alpha_all,
-                           asend_all, split_head ? c->s_g2 : nullptr);
+    // split pipeline: the first kHeadGains outputs' gains on the context stream, so the first
+    // whitening can start; every later group's on the whitening stream just ahead of its first
+    // whitening (SplitPipe::pre_whiten).  All of them at once -- the rest on the Gram CUs beside
+    // the first gains and whitening -- slowed those ~4x (round head 8.6 ms, r04f).
+    gplan = plan_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fit", &ys, alpha_all,
+                       asend_all);
+    gplan.launch(c->stream, 0, split_head ? std::min(np, kHeadGains) : np);
+    const GainsOut& g = gplan.o;
     for (int i = 0; i < np; ++i) {
       gains[i] = g;
       gains[i].rec = g.rec + (size_t)i * g.recstride;
@@ -185,7 +190,7 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
       gains[i].phi = g.phi + (size_t)i * g.phistride;
       gains[i].logs = g.logs + (size_t)i * nch;
     }
-    if (!split_head)   // else after the pipeline (the other outputs' gains run on s_g2)
+    if (!split_head)   // else after the pipeline (later groups' gains run on the whitening stream)
       HIPCHECK(hipMemcpyAsync(o.logs, g.logs, (size_t)np * nch * sizeof(double),
                               hipMemcpyDeviceToDevice, c->stream));
     logs_src = g.logs;
@@ -230,17 +235,18 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     SplitPipe sp(c, n, mpmax);
     sp.head = split_head;
     sp.start();
-    // the whitening side needs every output's gains from job 1 on
-    if (split_head) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr, 0));
+    if (split_head)   // group k's gains on the whitening stream ahead of whitening k kHeadGains
+      sp.pre_whiten = [&](int64_t k) {
+        if (k >= kHeadGains && k % kHeadGains == 0)
+          gplan.launch(c->s_w, (int)k, std::min<int>(kHeadGains, np - (int)k));
+      };
     for (int i = 0; i < np; ++i) sp.push(job(i, sp.buf[i & 1]));
     sp.flush();
     if (c->mark_last) HIPCHECK(hipEventRecord(c->mark_last, c->s_g));
     sp.join(c->stream);   // a prediction lane's q(u) runs this on the side stream
-    if (split_head) {     // s_g2's gains precede the last Gram's correction, which join covers
-      HIPCHECK(hipStreamWaitEvent(c->stream, c->ev_gr, 0));
+    if (split_head)       // every gains launch precedes the last whitening, which join covers
       HIPCHECK(hipMemcpyAsync(o.logs, logs_src, (size_t)np * nch * sizeof(double),
                               hipMemcpyDeviceToDevice, c->stream));
-    }
     return o;
   }
   StageBufs bufs[2];
