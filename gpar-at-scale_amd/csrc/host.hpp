@@ -42,6 +42,7 @@ struct gpar_ctx {
   hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr, s_d = nullptr;
   hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
   hipEvent_t ev_dn = nullptr;                    // split round start: the dense prefix follows the context stream
+  hipEvent_t ev_hw = nullptr, ev_gr = nullptr;   // split round: head whitening done / the other gains done
   hipEvent_t ev_dp = nullptr;                    // split round: the dense prefix is done (on s_d)
   // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
   // the caller's stream, e.g. the copies that produce its device inputs
@@ -213,9 +214,6 @@ constexpr int64_t kPipeMaxBetaBytes = (int64_t)8 << 30;   // second beta buffer 
 // default gpar_ctx_set_cu_split width: 8 of every XCD's 32 CUs whiten beside the Gram (north job
 // 20.66 -> 19.69 s per job in same-box pairs; 4 starves the whitening: 28.4 s)
 constexpr int kDefaultCuSplit = 8;
-// a split round's gains: the first kHeadGains outputs' on the context stream at the round's head,
-// then kHeadGains at a time on the whitening stream (run_gram_stage)
-constexpr int kHeadGains = 8;
 // the default split applies to batched fits whose Gram is big enough to amortise it: N Mp^2 >= 1e11
 // (north, N = 1e6, M = 512: 2.6e11; the N = 1e5 configs measured slower split: dtc 389 vs 297 ms
 // per job, eeg 3.09 vs 3.07 s)
@@ -360,7 +358,7 @@ struct SplitPipe {
   bool has_pending = false;   // job k - 1 whitened, its Gram not yet issued
   StageJob pending;
   std::function<void(const StageJob&, int64_t)> on_gram;   // right after job k's Gram is issued
-  std::function<void(int64_t)> pre_whiten;   // on the whitening stream, just before whitening k
+  std::function<void()> after_head_whiten;   // host hook right after the head job's whitening
 
   SplitPipe(gpar_ctx* c_, int64_t n, int64_t mpmax)
       : c(c_), gcus(8 * (32 - c_->split_w)) {
@@ -380,13 +378,13 @@ struct SplitPipe {
       if (c->mark_h[0]) HIPCHECK(hipEventRecord(c->mark_h[0], c->stream));
       stage_whiten(c, j, buf[0]);
       if (c->mark_h[1]) HIPCHECK(hipEventRecord(c->mark_h[1], c->stream));
+      if (after_head_whiten) after_head_whiten();
       stage_post(c, j, buf[0], false);
       if (c->mark_h[2]) HIPCHECK(hipEventRecord(c->mark_h[2], c->stream));
       HIPCHECK(hipEventRecord(c->ev_pc[0], c->stream));
       HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[0], 0));
     } else {
       OnStream on_(c, c->s_w);
-      if (pre_whiten) pre_whiten(k);
       if (k >= 2) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[k & 1], 0));
       stage_whiten(c, j, buf[k & 1]);
       stage_post(c, j, buf[k & 1], false);

@@ -175,13 +175,15 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     }
     alpha_all = ws<double>(c, "alpha_all", (size_t)np * n);
     asend_all = ws<double>(c, "asend_all", (size_t)np * nch * kSStride);
-    // split pipeline: the first kHeadGains outputs' gains on the context stream, so the first
-    // whitening can start; every later group's on the whitening stream just ahead of its first
-    // whitening (SplitPipe::pre_whiten).  All of them at once -- the rest on the Gram CUs beside
-    // the first gains and whitening -- slowed those ~4x (round head 8.6 ms, r04f).
+    // split pipeline: the first output's gains alone on the context stream, so its whitening can
+    // start on the whole chip; the others' on the Gram CUs' second stream once that whitening is
+    // done (SplitPipe::after_head_whiten), beside its short chain and the first Gram, ahead of
+    // the second whitening.  Beside the first gains and whitening they slowed those ~2-4x (round
+    // head 8.6 ms, r04f); in groups on the whitening stream they delayed the Grams' DG share
+    // (5.10 -> 5.24 ms per Gram, r04h).
     gplan = plan_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fit", &ys, alpha_all,
                        asend_all);
-    gplan.launch(c->stream, 0, split_head ? std::min(np, kHeadGains) : np);
+    gplan.launch(c->stream, 0, split_head ? 1 : np);
     const GainsOut& g = gplan.o;
     for (int i = 0; i < np; ++i) {
       gains[i] = g;
@@ -235,16 +237,19 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     SplitPipe sp(c, n, mpmax);
     sp.head = split_head;
     sp.start();
-    if (split_head)   // group k's gains on the whitening stream ahead of whitening k kHeadGains
-      sp.pre_whiten = [&](int64_t k) {
-        if (k >= kHeadGains && k % kHeadGains == 0)
-          gplan.launch(c->s_w, (int)k, std::min<int>(kHeadGains, np - (int)k));
+    if (split_head)   // the other outputs' gains after the first whitening; the second waits
+      sp.after_head_whiten = [&]() {
+        HIPCHECK(hipEventRecord(c->ev_hw, c->stream));
+        HIPCHECK(hipStreamWaitEvent(c->s_g2, c->ev_hw, 0));
+        gplan.launch(c->s_g2, 1, np - 1);
+        HIPCHECK(hipEventRecord(c->ev_gr, c->s_g2));
+        HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr, 0));
       };
     for (int i = 0; i < np; ++i) sp.push(job(i, sp.buf[i & 1]));
     sp.flush();
     if (c->mark_last) HIPCHECK(hipEventRecord(c->mark_last, c->s_g));
     sp.join(c->stream);   // a prediction lane's q(u) runs this on the side stream
-    if (split_head)       // every gains launch precedes the last whitening, which join covers
+    if (split_head)       // every gains launch precedes the second whitening, which join covers
       HIPCHECK(hipMemcpyAsync(o.logs, logs_src, (size_t)np * nch * sizeof(double),
                               hipMemcpyDeviceToDevice, c->stream));
     return o;
