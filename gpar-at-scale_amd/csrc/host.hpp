@@ -42,7 +42,7 @@ struct gpar_ctx {
   hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr, s_d = nullptr;
   hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
   hipEvent_t ev_dn = nullptr;                    // split round start: the dense prefix follows the context stream
-  hipEvent_t ev_hw = nullptr, ev_gr = nullptr;   // split round: head whitening done / the other gains done
+  hipEvent_t ev_gr = nullptr;                    // split round: the other outputs' gains done
   hipEvent_t ev_dp = nullptr;                    // split round: the dense prefix is done (on s_d)
   // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
   // the caller's stream, e.g. the copies that produce its device inputs
@@ -73,7 +73,7 @@ struct gpar_ctx {
   bool predict_fused = true;      // "predict_fused": predict_var (off: predict_rows + gemm_nt; last bits differ)
   bool qu_batch = true;           // "qu_batch": gpar_fit_predict's q(u) batched over the outputs
   bool dense_early = true;        // "dense_early": the G-independent dense tail ahead of the round's Grams
-  bool split_head = true;         // "split_head": the split round's first whitening whole-chip, gains on two streams
+  bool split_head = true;         // "split_head": the split round's gains on two streams (first output's on the whitening CUs)
   // "serialize": side, s_w, s_g, s_g2 and s_d all alias `main`, so every launch runs in issue order
   // on one stream (the created streams stay in own_*): the order-free reference the concurrent
   // schedule must equal bit for bit.  Plans, CU shares of work items and workspaces are unchanged.
@@ -358,7 +358,6 @@ struct SplitPipe {
   bool has_pending = false;   // job k - 1 whitened, its Gram not yet issued
   StageJob pending;
   std::function<void(const StageJob&, int64_t)> on_gram;   // right after job k's Gram is issued
-  std::function<void()> after_head_whiten;   // host hook right after the head job's whitening
 
   SplitPipe(gpar_ctx* c_, int64_t n, int64_t mpmax)
       : c(c_), gcus(8 * (32 - c_->split_w)) {
@@ -369,25 +368,15 @@ struct SplitPipe {
     HIPCHECK(hipEventRecord(c->ev_sp, c->stream));
     for (hipStream_t st : {c->s_w, c->s_g, c->s_g2}) HIPCHECK(hipStreamWaitEvent(st, c->ev_sp, 0));
   }
-  bool head = false;           // job 0 runs whole-chip on the caller's stream (split_head)
   void push(const StageJob& j) {
-    if (k == 0 && head) {
-      // nothing runs on the Gram CUs before the first Gram: the first whitening and its short
-      // chain take the whole chip (the caller's unmasked stream, which the split streams follow
-      // since start()); the whitening side continues after them
-      if (c->mark_h[0]) HIPCHECK(hipEventRecord(c->mark_h[0], c->stream));
-      stage_whiten(c, j, buf[0]);
-      if (c->mark_h[1]) HIPCHECK(hipEventRecord(c->mark_h[1], c->stream));
-      if (after_head_whiten) after_head_whiten();
-      stage_post(c, j, buf[0], false);
-      if (c->mark_h[2]) HIPCHECK(hipEventRecord(c->mark_h[2], c->stream));
-      HIPCHECK(hipEventRecord(c->ev_pc[0], c->stream));
-      HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[0], 0));
-    } else {
+    {
       OnStream on_(c, c->s_w);
       if (k >= 2) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[k & 1], 0));
+      if (k == 0 && c->mark_h[0]) HIPCHECK(hipEventRecord(c->mark_h[0], c->s_w));
       stage_whiten(c, j, buf[k & 1]);
+      if (k == 0 && c->mark_h[1]) HIPCHECK(hipEventRecord(c->mark_h[1], c->s_w));
       stage_post(c, j, buf[k & 1], false);
+      if (k == 0 && c->mark_h[2]) HIPCHECK(hipEventRecord(c->mark_h[2], c->s_w));
       HIPCHECK(hipEventRecord(c->ev_pc[k & 1], c->s_w));
     }
     if (has_pending) issue_gram();

@@ -71,7 +71,6 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
          hipEventCreateWithFlags(&c->ev_gd[1], hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_sp, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_dn, hipEventDisableTiming) != hipSuccess ||
-         hipEventCreateWithFlags(&c->ev_hw, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_gr, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_dp, hipEventDisableTiming) != hipSuccess))
       return GPAR_ERR_HIP;
@@ -188,7 +187,7 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
         (void)hipStreamDestroy(st);
       }
     for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_dn,
-                          ctx->ev_dp, ctx->ev_hw, ctx->ev_gr})
+                          ctx->ev_dp, ctx->ev_gr})
       if (ev) (void)hipEventDestroy(ev);
     for (const auto* evs : {&ctx->ev_grp, &ctx->ev_gn})
       for (hipEvent_t ev : *evs)

@@ -175,15 +175,15 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     }
     alpha_all = ws<double>(c, "alpha_all", (size_t)np * n);
     asend_all = ws<double>(c, "asend_all", (size_t)np * nch * kSStride);
-    // split pipeline: the first output's gains alone on the context stream, so its whitening can
-    // start on the whole chip; the others' on the Gram CUs' second stream once that whitening is
-    // done (SplitPipe::after_head_whiten), beside its short chain and the first Gram, ahead of
-    // the second whitening.  Beside the first gains and whitening they slowed those ~2-4x (round
-    // head 8.6 ms, r04f); in groups on the whitening stream they delayed the Grams' DG share
-    // (5.10 -> 5.24 ms per Gram, r04h).
+    // split pipeline (split_head): the first output's gains on the whitening CUs, ahead of its
+    // whitening there, and the others' at the same time on the Gram CUs, ahead of the first Gram;
+    // the second whitening waits for them (below).  Tried: the first whitening whole-chip, beside
+    // the others' gains (head 8.6 ms per round, r04f) or ahead of them (they then delayed the
+    // second whitening and every Gram after it, r04i); the others' gains in groups on the
+    // whitening stream (they delayed the Grams' DG share: 5.10 -> 5.24 ms per Gram, r04h).
     gplan = plan_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fit", &ys, alpha_all,
                        asend_all);
-    gplan.launch(c->stream, 0, split_head ? 1 : np);
+    if (!split_head) gplan.launch(c->stream, 0, np);
     const GainsOut& g = gplan.o;
     for (int i = 0; i < np; ++i) {
       gains[i] = g;
@@ -235,17 +235,16 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   };
   if (split_pipe) {
     SplitPipe sp(c, n, mpmax);
-    sp.head = split_head;
     sp.start();
-    if (split_head)   // the other outputs' gains after the first whitening; the second waits
-      sp.after_head_whiten = [&]() {
-        HIPCHECK(hipEventRecord(c->ev_hw, c->stream));
-        HIPCHECK(hipStreamWaitEvent(c->s_g2, c->ev_hw, 0));
-        gplan.launch(c->s_g2, 1, np - 1);
-        HIPCHECK(hipEventRecord(c->ev_gr, c->s_g2));
-        HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr, 0));
-      };
-    for (int i = 0; i < np; ++i) sp.push(job(i, sp.buf[i & 1]));
+    if (split_head) {
+      gplan.launch(c->s_w, 0, 1);
+      gplan.launch(c->s_g2, 1, np - 1);
+      HIPCHECK(hipEventRecord(c->ev_gr, c->s_g2));
+    }
+    for (int i = 0; i < np; ++i) {
+      if (i == 1 && split_head) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr, 0));
+      sp.push(job(i, sp.buf[i & 1]));
+    }
     sp.flush();
     if (c->mark_last) HIPCHECK(hipEventRecord(c->mark_last, c->s_g));
     sp.join(c->stream);   // a prediction lane's q(u) runs this on the side stream

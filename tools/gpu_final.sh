@@ -1,15 +1,19 @@
 # Round evidence: full GPU suite, smoke, PMC passes, rocprof kernel stats of the north bench, and
-# the default bench line (with cpu_baseline)
+# the default bench line (with cpu_baseline).  bash tools/gpu_final.sh <tag>, e.g. r04z: every
+# summary lands under gpurun_out/final_<tag>/ named as profiles/ wants it.
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-mkdir -p gpurun_out
+TAG=${1:?tag}
+OUT=gpurun_out/final_$TAG
+mkdir -p $OUT
 export TMPDIR=/tmp
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.txt 2>&1 || { echo PYTEST FAILED; tail -30 gpurun_out/pytest_gpu.txt; exit 1; }
-tail -1 gpurun_out/pytest_gpu.txt
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.txt 2>&1 || { echo SMOKE FAILED; tail -20 gpurun_out/smoke.txt; exit 1; }
-tail -1 gpurun_out/smoke.txt
-bash tools/pmc_passes.sh > gpurun_out/pmc_summary.txt 2>&1 || { echo PMC FAILED; tail -20 gpurun_out/pmc_summary.txt; exit 1; }
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > gpurun_out/bench_rocprof.json 2> gpurun_out/bench_rocprof.err || { echo ROCPROF BENCH FAILED; tail -20 gpurun_out/bench_rocprof.err; exit 1; }
-cp gpurun_out/pmc/summary.json profiles/pmc_gram_whiten_r02.json
-timeout -k 10 600 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo BENCH FAILED; tail -20 gpurun_out/bench.err; exit 1; }
-cat gpurun_out/bench.json
+timeout -k 10 1000 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $OUT/pytest_gpu_$TAG.txt 2>&1 || { echo PYTEST FAILED; tail -30 $OUT/pytest_gpu_$TAG.txt; exit 1; }
+tail -1 $OUT/pytest_gpu_$TAG.txt
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke_$TAG.txt 2>&1 || { echo SMOKE FAILED; tail -20 $OUT/smoke_$TAG.txt; exit 1; }
+tail -1 $OUT/smoke_$TAG.txt
+bash tools/pmc_passes.sh > $OUT/pmc_summary.txt 2>&1 || { echo PMC FAILED; tail -20 $OUT/pmc_summary.txt; exit 1; }
+cp gpurun_out/pmc/summary.json $OUT/pmc_gram_whiten_$TAG.json
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_${TAG}_north_rocprof_run.json 2> $OUT/bench_rocprof.err || { echo ROCPROF BENCH FAILED; tail -20 $OUT/bench_rocprof.err; exit 1; }
+find gpurun_out/prof -name '*kernel_stats.csv' -exec cp {} $OUT/rocprof_bench_${TAG}_north_stats.csv \;
+timeout -k 10 600 python bench.py > $OUT/bench_${TAG}_north.json 2> $OUT/bench.err || { echo BENCH FAILED; tail -20 $OUT/bench.err; exit 1; }
+cat $OUT/bench_${TAG}_north.json
