@@ -73,7 +73,7 @@ struct gpar_ctx {
   bool predict_fused = true;      // "predict_fused": predict_var (off: predict_rows + gemm_nt; last bits differ)
   bool qu_batch = true;           // "qu_batch": gpar_fit_predict's q(u) batched over the outputs
   bool dense_early = true;        // "dense_early": the G-independent dense tail ahead of the round's Grams
-  bool split_head = true;         // "split_head": the split round's gains on two streams (first output's on the whitening CUs)
+  int split_head = 1;             // "split_head": a split round's head (run_gram_stage: 0, 1, 2)
   // "serialize": side, s_w, s_g, s_g2 and s_d all alias `main`, so every launch runs in issue order
   // on one stream (the created streams stay in own_*): the order-free reference the concurrent
   // schedule must equal bit for bit.  Plans, CU shares of work items and workspaces are unchanged.
@@ -368,8 +368,20 @@ struct SplitPipe {
     HIPCHECK(hipEventRecord(c->ev_sp, c->stream));
     for (hipStream_t st : {c->s_w, c->s_g, c->s_g2}) HIPCHECK(hipStreamWaitEvent(st, c->ev_sp, 0));
   }
+  bool head = false;   // job 0's whitening and short chain whole-chip on the caller's stream
   void push(const StageJob& j) {
-    {
+    if (k == 0 && head) {
+      // nothing runs on the Gram CUs before the first Gram: the first whitening and its short
+      // chain take the whole chip (the caller's unmasked stream, which the split streams follow
+      // since start()); the whitening side continues after them
+      if (c->mark_h[0]) HIPCHECK(hipEventRecord(c->mark_h[0], c->stream));
+      stage_whiten(c, j, buf[0]);
+      if (c->mark_h[1]) HIPCHECK(hipEventRecord(c->mark_h[1], c->stream));
+      stage_post(c, j, buf[0], false);
+      if (c->mark_h[2]) HIPCHECK(hipEventRecord(c->mark_h[2], c->stream));
+      HIPCHECK(hipEventRecord(c->ev_pc[0], c->stream));
+      HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[0], 0));
+    } else {
       OnStream on_(c, c->s_w);
       if (k >= 2) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[k & 1], 0));
       if (k == 0 && c->mark_h[0]) HIPCHECK(hipEventRecord(c->mark_h[0], c->s_w));

@@ -158,7 +158,11 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   const bool shared = shares_grid(P);
   const bool pipe = fit_pipelined(c, P, fix_beta);
   const bool split_pipe = pipe && split_active(c, n, mpmax);
-  const bool split_head = split_pipe && c->split_head && shared && np > 1;
+  // a split round's head: 1 = the first output's gains on the whitening CUs and the others' beside
+  // them on the Gram CUs; 2 = every output's gains, then the first whitening and short chain,
+  // whole-chip; 0 = every output's gains whole-chip, the first whitening on the whitening CUs
+  const int head_mode = (split_pipe && shared && np > 1) ? c->split_head : 0;
+  const bool split_head = head_mode == 1;
   const double* logs_src = nullptr;
   std::vector<GainsOut> gains(np);
   GainsPlan gplan;
@@ -235,6 +239,7 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   };
   if (split_pipe) {
     SplitPipe sp(c, n, mpmax);
+    sp.head = head_mode == 2;
     sp.start();
     if (split_head) {
       gplan.launch(c->s_w, 0, 1);

@@ -34,6 +34,7 @@ SETTINGS = [
     {"overlap": 0, "serialize": 1},
     {"overlap": 0, "dense_early": 0},
     {"overlap": 0, "split_head": 0},
+    {"overlap": 0, "split_head": 2},
     {"qu_batch": 0},
     {"predict_lanes": 1},
 ]
