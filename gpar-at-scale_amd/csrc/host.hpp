@@ -74,6 +74,7 @@ struct gpar_ctx {
   bool qu_batch = true;           // "qu_batch": gpar_fit_predict's q(u) batched over the outputs
   bool dense_early = true;        // "dense_early": the G-independent dense tail ahead of the round's Grams
   int split_head = 1;             // "split_head": a split round's head (run_gram_stage: 0, 1, 2)
+  int dg_share = -1;              // "dg_share": 32nds of a split Gram's DG items on the whitening CUs (-1: split_w)
   // "serialize": side, s_w, s_g, s_g2 and s_d all alias `main`, so every launch runs in issue order
   // on one stream (the created streams stay in own_*): the order-free reference the concurrent
   // schedule must equal bit for bit.  Plans, CU shares of work items and workspaces are unchanged.
@@ -404,7 +405,7 @@ struct SplitPipe {
       if (i == 0 && c->mark_first) HIPCHECK(hipEventRecord(c->mark_first, c->s_g));
       if (i >= 1) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[(i - 1) & 1], 0));
       stage_gram(c, pending, buf[i & 1], false, false, "", c->s_g2, gcus, c->s_w, c->ev_pw,
-                 c->split_w);
+                 c->dg_share >= 0 ? c->dg_share : c->split_w);
       HIPCHECK(hipEventRecord(c->ev_gd[i & 1], c->s_g));
     }
     has_pending = false;

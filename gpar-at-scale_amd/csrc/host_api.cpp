@@ -83,7 +83,7 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
 
 static constexpr const char* kScheduleKnobs[] = {"overlap", "overlap_group", "predict_fused", "qu_batch",
                                                   "dense_early", "split_head", "predict_lanes",
-                                                  "serialize"};
+                                                  "serialize", "dg_share"};
 
 // gpar_ctx_set_schedule / gpar_ctx_get_schedule (GPAR_ERR_ARG: unknown knob or value).
 static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
@@ -99,7 +99,10 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
     if (v < 0 || v > 2) return GPAR_ERR_ARG;
     c->split_head = v;
   }
-  else if (k == "predict_lanes") {
+  else if (k == "dg_share") {
+    if (v < -1 || v > 32) return GPAR_ERR_ARG;
+    c->dg_share = v;
+  } else if (k == "predict_lanes") {
     if (v != 1 && v != 2) return GPAR_ERR_ARG;
     c->predict_lanes = v;
   } else if (k == "serialize") {
@@ -122,6 +125,7 @@ static int get_schedule(const gpar_ctx* c, const std::string& k, int32_t* v) {
   else if (k == "qu_batch") *v = c->qu_batch;
   else if (k == "dense_early") *v = c->dense_early;
   else if (k == "split_head") *v = c->split_head;
+  else if (k == "dg_share") *v = c->dg_share;
   else if (k == "predict_lanes") *v = c->predict_lanes;
   else if (k == "serialize") *v = c->serialize;
   else return GPAR_ERR_ARG;

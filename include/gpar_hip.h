@@ -152,8 +152,11 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *                   of >= 4 outputs
  *   "qu_batch"      1: gpar_fit_predict runs q(u) batched over the outputs (default 1)
  *   "dense_early"   1: the G-independent half of the dense tail ahead of a split round's Grams (1)
- *   "split_head"    1: a split round's gains on two streams: the first output's on the whitening
- *                      CUs, the others' on the Gram CUs (default 1; 0: all of them ahead of the round)
+ *   "split_head"    a split round's head: 1 = the first output's gains on the whitening CUs, the
+ *                   others' beside them on the Gram CUs (default); 2 = every output's gains, then the
+ *                   first whitening, whole-chip; 0 = every output's gains ahead of the round
+ *   "dg_share"      32nds of a split Gram's diagonal-block work items run on the whitening CUs
+ *                   (-1, the default: the CU split's own share, cus_per_xcd / 32)
  *   "predict_lanes" 1 or 2: streams gpar_fit_predict's predictions alternate over (default 2)
  *   "serialize"     1: every launch of every schedule on the context's one stream, in issue order,
  *                   with the same plans, CU shares of work items and workspaces: the order-free
