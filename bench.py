@@ -333,7 +333,7 @@ def main():
                                                   max_evals=EV, g_tol=-1.0, device=local)
                 res[1] = np.array(list(th1) + [0.0, 0.0])
             return S.gather_thetas(res, P, dev)
-        if chained and world == 1:
+        if chained and world == 1 and not shard_of:
             fr, _, _ = G.fit_predict_batch(problems, x0, ts_d, [None] * len(problems),
                                            max_evals=EV, g_tol=-1.0, mode=args.predict, samples=100,
                                            seed=gpar_out[0], device=local, chain=chain_d,

@@ -79,7 +79,10 @@ struct gpar_ctx {
   // on one stream (the created streams stay in own_*): the order-free reference the concurrent
   // schedule must equal bit for bit.  Plans, CU shares of work items and workspaces are unchanged.
   bool serialize = false;
-  hipStream_t own_side = nullptr, own_s[4] = {nullptr, nullptr, nullptr, nullptr};
+  // own_s[3..5]: the round overlap's dense tails and gains on the whitening CUs, the whole chip,
+  // the Gram CUs ("tail_cus" 0, 1, 2 picks s_d among them)
+  hipStream_t own_side = nullptr, own_s[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
+  int tail_cus = 0;
   std::string ws_suffix;          // appended to workspace names (a prediction lane's own buffers)
   std::vector<hipEvent_t> ev_grp;   // fit_overlapped: a group's values are in (one per group)
   std::vector<hipEvent_t> ev_gn;    // fit_overlapped: a group's gains are done

@@ -23,7 +23,8 @@ int fail(gpar_ctx* c, int code, const char* what) {
   c->err = what;
   c->stream = c->main;
   (void)hipStreamSynchronize(c->main);
-  for (hipStream_t st : {c->own_side, c->own_s[0], c->own_s[1], c->own_s[2], c->own_s[3]})
+  (void)hipStreamSynchronize(c->own_side);
+  for (hipStream_t st : c->own_s)
     if (st) (void)hipStreamSynchronize(st);
   (void)hipGetLastError();
   return code;
@@ -33,7 +34,10 @@ int fail(gpar_ctx* c, int code, const char* what) {
 static void route_streams(gpar_ctx* c) {
   c->side = c->serialize ? c->main : c->own_side;
   hipStream_t* act[4] = {&c->s_w, &c->s_g, &c->s_g2, &c->s_d};
-  for (int i = 0; i < 4; ++i) *act[i] = (c->serialize && c->own_s[i]) ? c->main : c->own_s[i];
+  for (int i = 0; i < 4; ++i) {
+    const hipStream_t own = c->own_s[i < 3 ? i : 3 + c->tail_cus];
+    *act[i] = (c->serialize && own) ? c->main : own;
+  }
 }
 
 // CU split of the pipelined fit (gpar_ctx_set_cu_split): CU-masked streams for the whitening
@@ -58,13 +62,12 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
     c->split_mask_w = 0;
     c->split_w = 0;
     // own_s: s_w (whitening), s_g (Gram), s_g2 (its co-running correction), s_d (dense tails)
-    uint32_t mw[8] = {0}, mg[8] = {0};
+    uint32_t mw[8] = {0}, mg[8] = {0}, ma[8];
     for (int i = 0; i < 256; ++i) (i < 8 * w ? mw : mg)[i / 32] |= 1u << (i % 32);
-    if (hipExtStreamCreateWithCUMask(&c->own_s[0], 8, mw) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&c->own_s[1], 8, mg) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&c->own_s[2], 8, mg) != hipSuccess ||
-        hipExtStreamCreateWithCUMask(&c->own_s[3], 8, mw) != hipSuccess)
-      return GPAR_ERR_HIP;
+    for (int i = 0; i < 8; ++i) ma[i] = ~0u;
+    const uint32_t* masks[6] = {mw, mg, mg, mw, ma, mg};
+    for (int i = 0; i < 6; ++i)
+      if (hipExtStreamCreateWithCUMask(&c->own_s[i], 8, masks[i]) != hipSuccess) return GPAR_ERR_HIP;
     route_streams(c);
     if (!c->ev_sp &&
         (hipEventCreateWithFlags(&c->ev_gd[0], hipEventDisableTiming) != hipSuccess ||
@@ -83,7 +86,7 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
 
 static constexpr const char* kScheduleKnobs[] = {"overlap", "overlap_group", "predict_fused", "qu_batch",
                                                   "dense_early", "split_head", "predict_lanes",
-                                                  "serialize", "dg_share"};
+                                                  "serialize", "dg_share", "tail_cus"};
 
 // gpar_ctx_set_schedule / gpar_ctx_get_schedule (GPAR_ERR_ARG: unknown knob or value).
 static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
@@ -108,9 +111,15 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
   } else if (k == "serialize") {
     // the streams about to be re-routed must not hold queued work
     (void)hipStreamSynchronize(c->main);
-    for (hipStream_t st : {c->own_side, c->own_s[0], c->own_s[1], c->own_s[2], c->own_s[3]})
+    (void)hipStreamSynchronize(c->own_side);
+    for (hipStream_t st : c->own_s)
       if (st) (void)hipStreamSynchronize(st);
     c->serialize = v != 0;
+    route_streams(c);
+  } else if (k == "tail_cus") {
+    if (v < 0 || v > 2) return GPAR_ERR_ARG;
+    if (c->s_d) (void)hipStreamSynchronize(c->s_d);
+    c->tail_cus = v;
     route_streams(c);
   } else {
     return GPAR_ERR_ARG;
@@ -126,6 +135,7 @@ static int get_schedule(const gpar_ctx* c, const std::string& k, int32_t* v) {
   else if (k == "dense_early") *v = c->dense_early;
   else if (k == "split_head") *v = c->split_head;
   else if (k == "dg_share") *v = c->dg_share;
+  else if (k == "tail_cus") *v = c->tail_cus;
   else if (k == "predict_lanes") *v = c->predict_lanes;
   else if (k == "serialize") *v = c->serialize;
   else return GPAR_ERR_ARG;
