@@ -19,7 +19,6 @@
 // are theta-independent, so gpar_host.cpp (attach_dist_cache) computes them once per fit for the
 // outputs it caches and every objective evaluation reads them.
 #include "device_common.hpp"
-#include "exp_table.hpp"
 
 namespace gpar {
 
@@ -223,7 +222,6 @@ __global__ __launch_bounds__(256, kW2Occ) void whiten_kfu_d2x2(
   constexpr int RS = Rec<SD>::size;
   __shared__ __attribute__((aligned(16))) double rl[kW2MaxL * RS];
   __shared__ __attribute__((aligned(16))) double gl[kW2MaxL * kGStride];
-  __shared__ double2 etab[256];
   const int tid = threadIdx.x;
   const int64_t j = blockIdx.x;
   const int64_t c = ((int64_t)blockIdx.y * 256 + tid) * 2;   // first of the thread's two columns
@@ -236,7 +234,6 @@ __global__ __launch_bounds__(256, kW2Occ) void whiten_kfu_d2x2(
   // the chunk's records and fix-up rows, once
   for (int e = tid; e < nk * RS; e += 256) rl[e] = rec[k0 * RS + e];
   for (int e = tid; e < nk * kGStride; e += 256) gl[e] = g[k0 * kGStride + e];
-  exp_table_stage(etab, tid, 256);
   double ma[SD], mb[SD], ha[SD], hb[SD];
 #pragma unroll
   for (int i = 0; i < SD; ++i) ma[i] = mb[i] = ha[i] = hb[i] = 0.0;
@@ -270,11 +267,11 @@ __global__ __launch_bounds__(256, kW2Occ) void whiten_kfu_d2x2(
         b = b > 0.0 ? b : 0.0;
       }
       if constexpr (RIN) {
-        x[r].x = v0 ? skappa_r_t<OK>(a, inv_lo, s_o, etab) : 0.0;
-        x[r].y = v1 ? skappa_r_t<OK>(b, inv_lo, s_o, etab) : 0.0;
+        x[r].x = v0 ? skappa_r_k<OK>(a, inv_lo, s_o, ek) : 0.0;
+        x[r].y = v1 ? skappa_r_k<OK>(b, inv_lo, s_o, ek) : 0.0;
       } else {
-        x[r].x = v0 ? skappa_sq_t<OK>(a, inv_lo, s_o, etab) : 0.0;
-        x[r].y = v1 ? skappa_sq_t<OK>(b, inv_lo, s_o, etab) : 0.0;
+        x[r].x = v0 ? skappa_sq_k<OK>(a, inv_lo, s_o, ek) : 0.0;
+        x[r].y = v1 ? skappa_sq_k<OK>(b, inv_lo, s_o, ek) : 0.0;
       }
     }
     auto step = [&](int r) __attribute__((always_inline)) {
