@@ -43,6 +43,7 @@ struct gpar_ctx {
   hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
   hipEvent_t ev_dn = nullptr;                    // split round start: the dense prefix follows the context stream
   hipEvent_t ev_gr = nullptr;                    // split round: the other outputs' gains done
+  hipEvent_t ev_wd = nullptr;                    // split job: its whitening is done (post_gram)
   hipEvent_t ev_dp = nullptr;                    // split round: the dense prefix is done (on s_d)
   // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
   // the caller's stream, e.g. the copies that produce its device inputs
@@ -74,6 +75,7 @@ struct gpar_ctx {
   bool qu_batch = true;           // "qu_batch": gpar_fit_predict's q(u) batched over the outputs
   bool dense_early = true;        // "dense_early": the G-independent dense tail ahead of the round's Grams
   int split_head = 1;             // "split_head": a split round's head (run_gram_stage: 0, 1, 2)
+  bool post_gram = false;         // "post_gram": a split job's short chain on the Gram CUs (s_g2), not the whitening CUs
   int dg_share = -1;              // "dg_share": 32nds of a split Gram's DG items on the whitening CUs (-1: split_w)
   // "serialize": side, s_w, s_g, s_g2 and s_d all alias `main`, so every launch runs in issue order
   // on one stream (the created streams stay in own_*): the order-free reference the concurrent
@@ -391,11 +393,24 @@ struct SplitPipe {
       if (k == 0 && c->mark_h[0]) HIPCHECK(hipEventRecord(c->mark_h[0], c->s_w));
       stage_whiten(c, j, buf[k & 1]);
       if (k == 0 && c->mark_h[1]) HIPCHECK(hipEventRecord(c->mark_h[1], c->s_w));
-      stage_post(c, j, buf[k & 1], false);
-      if (k == 0 && c->mark_h[2]) HIPCHECK(hipEventRecord(c->mark_h[2], c->s_w));
-      HIPCHECK(hipEventRecord(c->ev_pc[k & 1], c->s_w));
+      if (c->post_gram) {
+        HIPCHECK(hipEventRecord(c->ev_wd, c->s_w));
+      } else {
+        stage_post(c, j, buf[k & 1], false);
+        if (k == 0 && c->mark_h[2]) HIPCHECK(hipEventRecord(c->mark_h[2], c->s_w));
+        HIPCHECK(hipEventRecord(c->ev_pc[k & 1], c->s_w));
+      }
     }
     if (has_pending) issue_gram();
+    if (c->post_gram && !(k == 0 && head)) {
+      // the short chain on the Gram CUs' second stream, behind the previous Gram's co-running
+      // correction (issued just above), so the whitening side goes on with that Gram's DG share
+      OnStream on_(c, c->s_g2);
+      HIPCHECK(hipStreamWaitEvent(c->s_g2, c->ev_wd, 0));
+      stage_post(c, j, buf[k & 1], false);
+      if (k == 0 && c->mark_h[2]) HIPCHECK(hipEventRecord(c->mark_h[2], c->s_g2));
+      HIPCHECK(hipEventRecord(c->ev_pc[k & 1], c->s_g2));
+    }
     pending = j;
     has_pending = true;
     ++k;

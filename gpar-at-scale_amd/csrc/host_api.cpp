@@ -75,6 +75,7 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
          hipEventCreateWithFlags(&c->ev_sp, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_dn, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_gr, hipEventDisableTiming) != hipSuccess ||
+         hipEventCreateWithFlags(&c->ev_wd, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_dp, hipEventDisableTiming) != hipSuccess))
       return GPAR_ERR_HIP;
     c->split_mask_w = w;
@@ -86,7 +87,7 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
 
 static constexpr const char* kScheduleKnobs[] = {"overlap", "overlap_group", "predict_fused", "qu_batch",
                                                   "dense_early", "split_head", "predict_lanes",
-                                                  "serialize", "dg_share", "tail_cus"};
+                                                  "serialize", "dg_share", "tail_cus", "post_gram"};
 
 // gpar_ctx_set_schedule / gpar_ctx_get_schedule (GPAR_ERR_ARG: unknown knob or value).
 static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
@@ -102,6 +103,7 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
     if (v < 0 || v > 2) return GPAR_ERR_ARG;
     c->split_head = v;
   }
+  else if (k == "post_gram") c->post_gram = v != 0;
   else if (k == "dg_share") {
     if (v < -1 || v > 32) return GPAR_ERR_ARG;
     c->dg_share = v;
@@ -136,6 +138,7 @@ static int get_schedule(const gpar_ctx* c, const std::string& k, int32_t* v) {
   else if (k == "split_head") *v = c->split_head;
   else if (k == "dg_share") *v = c->dg_share;
   else if (k == "tail_cus") *v = c->tail_cus;
+  else if (k == "post_gram") *v = c->post_gram;
   else if (k == "predict_lanes") *v = c->predict_lanes;
   else if (k == "serialize") *v = c->serialize;
   else return GPAR_ERR_ARG;
@@ -204,7 +207,7 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
         (void)hipStreamDestroy(st);
       }
     for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_dn,
-                          ctx->ev_dp, ctx->ev_gr})
+                          ctx->ev_dp, ctx->ev_gr, ctx->ev_wd})
       if (ev) (void)hipEventDestroy(ev);
     for (const auto* evs : {&ctx->ev_grp, &ctx->ev_gn})
       for (hipEvent_t ev : *evs)
