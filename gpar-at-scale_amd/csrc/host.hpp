@@ -422,6 +422,9 @@ struct SplitPipe {
       HIPCHECK(hipStreamWaitEvent(c->s_g, c->ev_pc[i & 1], 0));
       if (i == 0 && c->mark_first) HIPCHECK(hipEventRecord(c->mark_first, c->s_g));
       if (i >= 1) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[(i - 1) & 1], 0));
+      // the DG share reads alpha after vec_fix and the zeroed beta tail: P(i) on the whitening
+      // stream orders it; on the Gram CUs' stream (post_gram) the share waits for it
+      if (c->post_gram) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[i & 1], 0));
       stage_gram(c, pending, buf[i & 1], false, false, "", c->s_g2, gcus, c->s_w, c->ev_pw,
                  c->dg_share >= 0 ? c->dg_share : c->split_w);
       HIPCHECK(hipEventRecord(c->ev_gd[i & 1], c->s_g));

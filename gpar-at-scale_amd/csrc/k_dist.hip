@@ -266,13 +266,20 @@ __global__ __launch_bounds__(256, kW2Occ) void whiten_kfu_d2x2(
         a = a > 0.0 ? a : 0.0;
         b = b > 0.0 ? b : 0.0;
       }
+      // evaluated for every column and selected after: a guarded evaluation compiles to one
+      // exec-masked branch per element, and the 16 independent exp chains of the 8-row block could
+      // then not interleave (padding columns read finite cache entries or the clamped rows; their
+      // values are dropped by the select)
+      double ka, kb;
       if constexpr (RIN) {
-        x[r].x = v0 ? skappa_r_k<OK>(a, inv_lo, s_o, ek) : 0.0;
-        x[r].y = v1 ? skappa_r_k<OK>(b, inv_lo, s_o, ek) : 0.0;
+        ka = skappa_r_k<OK>(a, inv_lo, s_o, ek);
+        kb = skappa_r_k<OK>(b, inv_lo, s_o, ek);
       } else {
-        x[r].x = v0 ? skappa_sq_k<OK>(a, inv_lo, s_o, ek) : 0.0;
-        x[r].y = v1 ? skappa_sq_k<OK>(b, inv_lo, s_o, ek) : 0.0;
+        ka = skappa_sq_k<OK>(a, inv_lo, s_o, ek);
+        kb = skappa_sq_k<OK>(b, inv_lo, s_o, ek);
       }
+      x[r].x = v0 ? ka : 0.0;
+      x[r].y = v1 ? kb : 0.0;
     }
     auto step = [&](int r) __attribute__((always_inline)) {
       const double* rr = rl + (r0 + r) * RS;
