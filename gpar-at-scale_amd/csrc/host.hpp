@@ -75,7 +75,7 @@ struct gpar_ctx {
   bool qu_batch = true;           // "qu_batch": gpar_fit_predict's q(u) batched over the outputs
   bool dense_early = true;        // "dense_early": the G-independent dense tail ahead of the round's Grams
   int split_head = 1;             // "split_head": a split round's head (run_gram_stage: 0, 1, 2)
-  bool post_gram = false;         // "post_gram": a split job's short chain on the Gram CUs (s_g2), not the whitening CUs
+  int post_gram = -1;             // "post_gram": a split job's short chain on the Gram CUs (s_g2): 1, 0, -1 = round overlap only
   int dg_share = -1;              // "dg_share": 32nds of a split Gram's DG items on the whitening CUs (-1: split_w)
   // "serialize": side, s_w, s_g, s_g2 and s_d all alias `main`, so every launch runs in issue order
   // on one stream (the created streams stay in own_*): the order-free reference the concurrent
@@ -375,6 +375,9 @@ struct SplitPipe {
     for (hipStream_t st : {c->s_w, c->s_g, c->s_g2}) HIPCHECK(hipStreamWaitEvent(st, c->ev_sp, 0));
   }
   bool head = false;   // job 0's whitening and short chain whole-chip on the caller's stream
+  // the short chains on the Gram CUs' second stream (gpar_ctx::post_gram; the round overlap's
+  // whitening CUs also run the other group's dense tails and gains)
+  bool post_gram = false;
   void push(const StageJob& j) {
     if (k == 0 && head) {
       // nothing runs on the Gram CUs before the first Gram: the first whitening and its short
@@ -393,7 +396,7 @@ struct SplitPipe {
       if (k == 0 && c->mark_h[0]) HIPCHECK(hipEventRecord(c->mark_h[0], c->s_w));
       stage_whiten(c, j, buf[k & 1]);
       if (k == 0 && c->mark_h[1]) HIPCHECK(hipEventRecord(c->mark_h[1], c->s_w));
-      if (c->post_gram) {
+      if (post_gram) {
         HIPCHECK(hipEventRecord(c->ev_wd, c->s_w));
       } else {
         stage_post(c, j, buf[k & 1], false);
@@ -402,7 +405,7 @@ struct SplitPipe {
       }
     }
     if (has_pending) issue_gram();
-    if (c->post_gram && !(k == 0 && head)) {
+    if (post_gram && !(k == 0 && head)) {
       // the short chain on the Gram CUs' second stream, behind the previous Gram's co-running
       // correction (issued just above), so the whitening side goes on with that Gram's DG share
       OnStream on_(c, c->s_g2);
@@ -424,7 +427,7 @@ struct SplitPipe {
       if (i >= 1) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[(i - 1) & 1], 0));
       // the DG share reads alpha after vec_fix and the zeroed beta tail: P(i) on the whitening
       // stream orders it; on the Gram CUs' stream (post_gram) the share waits for it
-      if (c->post_gram) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[i & 1], 0));
+      if (post_gram) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[i & 1], 0));
       stage_gram(c, pending, buf[i & 1], false, false, "", c->s_g2, gcus, c->s_w, c->ev_pw,
                  c->dg_share >= 0 ? c->dg_share : c->split_w);
       HIPCHECK(hipEventRecord(c->ev_gd[i & 1], c->s_g));

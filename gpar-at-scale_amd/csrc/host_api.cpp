@@ -103,7 +103,10 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
     if (v < 0 || v > 2) return GPAR_ERR_ARG;
     c->split_head = v;
   }
-  else if (k == "post_gram") c->post_gram = v != 0;
+  else if (k == "post_gram") {
+    if (v < -1 || v > 1) return GPAR_ERR_ARG;
+    c->post_gram = v;
+  }
   else if (k == "dg_share") {
     if (v < -1 || v > 32) return GPAR_ERR_ARG;
     c->dg_share = v;

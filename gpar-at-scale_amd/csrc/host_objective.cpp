@@ -240,6 +240,7 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   if (split_pipe) {
     SplitPipe sp(c, n, mpmax);
     sp.head = head_mode == 2;
+    sp.post_gram = c->post_gram == 1;
     sp.start();
     if (split_head) {
       gplan.launch(c->s_w, 0, 1);

@@ -158,7 +158,8 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *   "dg_share"      32nds of a split Gram's diagonal-block work items run on the whitening CUs
  *                   (-1, the default: the CU split's own share, cus_per_xcd / 32)
  *   "post_gram"     1: a split job's short chain (carry, vec_fix) on the Gram CUs behind the previous
- *                   Gram's correction instead of on the whitening CUs after its whitening (default 0)
+ *                   Gram's correction instead of on the whitening CUs after its whitening; 0: never;
+ *                   -1 (default): in the round-overlapping fit only
  *   "tail_cus"      the round overlap's dense tails and gains: 0 = on the whitening CUs (default),
  *                   1 = on the whole chip, 2 = on the Gram CUs
  *   "predict_lanes" 1 or 2: streams gpar_fit_predict's predictions alternate over (default 2)
