@@ -374,22 +374,26 @@ struct SplitPipe {
     HIPCHECK(hipEventRecord(c->ev_sp, c->stream));
     for (hipStream_t st : {c->s_w, c->s_g, c->s_g2}) HIPCHECK(hipStreamWaitEvent(st, c->ev_sp, 0));
   }
-  bool head = false;   // job 0's whitening and short chain whole-chip on the caller's stream
+  bool head = false;   // job 0's whitening and short chain on head_st (null: the caller's stream)
+  hipStream_t head_st = nullptr;
   // the short chains on the Gram CUs' second stream (gpar_ctx::post_gram; the round overlap's
   // whitening CUs also run the other group's dense tails and gains)
   bool post_gram = false;
   void push(const StageJob& j) {
     if (k == 0 && head) {
-      // nothing runs on the Gram CUs before the first Gram: the first whitening and its short
-      // chain take the whole chip (the caller's unmasked stream, which the split streams follow
-      // since start()); the whitening side continues after them
-      if (c->mark_h[0]) HIPCHECK(hipEventRecord(c->mark_h[0], c->stream));
+      // the first whitening and its short chain on head_st: the caller's unmasked stream (the whole
+      // chip: nothing runs on the Gram CUs before the first Gram; the whitening side continues
+      // after them) or the Gram stream (the Gram CUs whiten the first output while the whitening
+      // CUs run the other outputs' gains)
+      const hipStream_t hs = head_st ? head_st : c->stream;
+      OnStream on_(c, hs);
+      if (c->mark_h[0]) HIPCHECK(hipEventRecord(c->mark_h[0], hs));
       stage_whiten(c, j, buf[0]);
-      if (c->mark_h[1]) HIPCHECK(hipEventRecord(c->mark_h[1], c->stream));
+      if (c->mark_h[1]) HIPCHECK(hipEventRecord(c->mark_h[1], hs));
       stage_post(c, j, buf[0], false);
-      if (c->mark_h[2]) HIPCHECK(hipEventRecord(c->mark_h[2], c->stream));
-      HIPCHECK(hipEventRecord(c->ev_pc[0], c->stream));
-      HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[0], 0));
+      if (c->mark_h[2]) HIPCHECK(hipEventRecord(c->mark_h[2], hs));
+      HIPCHECK(hipEventRecord(c->ev_pc[0], hs));
+      if (!head_st) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[0], 0));
     } else {
       OnStream on_(c, c->s_w);
       if (k >= 2) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[k & 1], 0));

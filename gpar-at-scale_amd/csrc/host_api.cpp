@@ -100,7 +100,7 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
   else if (k == "qu_batch") c->qu_batch = v != 0;
   else if (k == "dense_early") c->dense_early = v != 0;
   else if (k == "split_head") {
-    if (v < 0 || v > 2) return GPAR_ERR_ARG;
+    if (v < 0 || v > 3) return GPAR_ERR_ARG;
     c->split_head = v;
   }
   else if (k == "post_gram") {

@@ -160,9 +160,11 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   const bool split_pipe = pipe && split_active(c, n, mpmax);
   // a split round's head: 1 = the first output's gains on the whitening CUs and the others' beside
   // them on the Gram CUs; 2 = every output's gains, then the first whitening and short chain,
-  // whole-chip; 0 = every output's gains whole-chip, the first whitening on the whitening CUs
+  // whole-chip; 3 = the first output's gains, whitening and short chain on the Gram CUs, the
+  // others' gains beside them on the whitening CUs; 0 = every output's gains whole-chip, the first
+  // whitening on the whitening CUs
   const int head_mode = (split_pipe && shared && np > 1) ? c->split_head : 0;
-  const bool split_head = head_mode == 1;
+  const bool split_head = head_mode == 1 || head_mode == 3;
   const double* logs_src = nullptr;
   std::vector<GainsOut> gains(np);
   GainsPlan gplan;
@@ -239,16 +241,20 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   };
   if (split_pipe) {
     SplitPipe sp(c, n, mpmax);
-    sp.head = head_mode == 2;
+    sp.head = head_mode == 2 || head_mode == 3;
+    sp.head_st = head_mode == 3 ? c->s_g : nullptr;
     sp.post_gram = c->post_gram == 1;
     sp.start();
-    if (split_head) {
+    if (head_mode == 1) {
       gplan.launch(c->s_w, 0, 1);
       gplan.launch(c->s_g2, 1, np - 1);
       HIPCHECK(hipEventRecord(c->ev_gr, c->s_g2));
+    } else if (head_mode == 3) {   // the second whitening follows the others' gains on s_w
+      gplan.launch(c->s_g, 0, 1);
+      gplan.launch(c->s_w, 1, np - 1);
     }
     for (int i = 0; i < np; ++i) {
-      if (i == 1 && split_head) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr, 0));
+      if (i == 1 && head_mode == 1) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr, 0));
       sp.push(job(i, sp.buf[i & 1]));
     }
     sp.flush();
@@ -452,9 +458,11 @@ void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<T
   if (early) {
     // the Gram stream first follows everything queued on the context stream (host inputs' uploads,
     // the pseudo-input centres, the distance cache), then factors Kuu beside the round's gains
+    // (split_head 3: on the Gram CUs' second stream, the Gram stream whitening the first output)
+    const hipStream_t ds = c->split_head == 3 ? c->s_g2 : c->s_g;
     HIPCHECK(hipEventRecord(c->ev_dn, c->stream));
-    HIPCHECK(hipStreamWaitEvent(c->s_g, c->ev_dn, 0));
-    OnStream on_(c, c->s_g);
+    HIPCHECK(hipStreamWaitEvent(ds, c->ev_dn, 0));
+    OnStream on_(c, ds);
     dn = run_dense_pre(c, P, th, mpmax, false);
   }
   GramOut go = run_gram_stage(c, P, th);

@@ -154,7 +154,9 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *   "dense_early"   1: the G-independent half of the dense tail ahead of a split round's Grams (1)
  *   "split_head"    a split round's head: 1 = the first output's gains on the whitening CUs, the
  *                   others' beside them on the Gram CUs (default); 2 = every output's gains, then the
- *                   first whitening, whole-chip; 0 = every output's gains ahead of the round
+ *                   first whitening, whole-chip; 3 = the first output's gains, whitening and
+ *                   short chain on the Gram CUs, the others' gains on the whitening CUs; 0 = every
+ *                   output's gains ahead of the round
  *   "dg_share"      32nds of a split Gram's diagonal-block work items run on the whitening CUs
  *                   (-1, the default: the CU split's own share, cus_per_xcd / 32)
  *   "post_gram"     1: a split job's short chain (carry, vec_fix) on the Gram CUs behind the previous
