@@ -13,6 +13,9 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smok
 tail -1 $OUT/smoke_$TAG.txt
 bash tools/pmc_passes.sh > $OUT/pmc_summary.txt 2>&1 || { echo PMC FAILED; tail -20 $OUT/pmc_summary.txt; exit 1; }
 cp gpurun_out/pmc/summary.json $OUT/pmc_gram_whiten_$TAG.json
+# the bench lines below read this round's traffic from profiles/ (bench.py PMC_FILE)
+PMC=$(python3 -c "import re;print(re.search(r'PMC_FILE = \"(.*)\"', open('bench.py').read()).group(1))")
+cp gpurun_out/pmc/summary.json profiles/$PMC
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline > $OUT/bench_${TAG}_north_rocprof_run.json 2> $OUT/bench_rocprof.err || { echo ROCPROF BENCH FAILED; tail -20 $OUT/bench_rocprof.err; exit 1; }
 find gpurun_out/prof -name '*kernel_stats.csv' -exec cp {} $OUT/rocprof_bench_${TAG}_north_stats.csv \;
 timeout -k 10 600 python bench.py > $OUT/bench_${TAG}_north.json 2> $OUT/bench.err || { echo BENCH FAILED; tail -20 $OUT/bench.err; exit 1; }
