@@ -356,19 +356,22 @@ def main():
                 # one rank of the W-way job on this GPU: its own fits above, then the whole
                 # P-output sweep (the other ranks' outputs from the untimed posteriors of the
                 # set-up) -- the serial part every rank of the real job waits through
+                def pick(p):
+                    return ((post, gpar_out.index(p)) if p in gpar_out else
+                            (post_all, gpar_all.index(p)))
                 S.chained_predictions(
                     gpar_all, {p: 0 for p in gpar_all},
-                    lambda p, c: (post if p in gpar_out else post_all).predict(
-                        (gpar_out if p in gpar_out else gpar_all).index(p), ts_d, c[:, : p - 1],
-                        mode=args.predict, samples=100, seed=p),
-                    chain_d)
+                    lambda p, c: pick(p)[0].predict(pick(p)[1], ts_d, c[:, : p - 1],
+                                                    mode=args.predict, samples=100, seed=p),
+                    chain_d,
+                    prepare_fn=lambda p: pick(p)[0].prepare(pick(p)[1], ts_d))
             else:
                 idx = {p: i for i, p in enumerate(gpar_out)}
                 S.chained_predictions(
                     gpar_all, owners,
                     lambda p, c: post.predict(idx[p], ts_d, c[:, : p - 1], mode=args.predict,
                                               samples=100, seed=p),
-                    chain_d)
+                    chain_d, prepare_fn=lambda p: post.prepare(idx[p], ts_d))
             torch.cuda.synchronize()
             last.setdefault("sweep_s", []).append(time.perf_counter() - t_sw)
         elif problems and not args.separate_predict:

@@ -24,6 +24,10 @@
 #include "launch.hpp"
 #include "nelder_mead.hpp"
 
+namespace gpar {
+struct PredPrep;
+}
+
 struct gpar_ctx {
   int device = 0;
   hipStream_t stream = nullptr;   // the stream every launch goes to (see OnStream)
@@ -44,6 +48,11 @@ struct gpar_ctx {
   hipEvent_t ev_dn = nullptr;                    // split round start: the dense prefix follows the context stream
   hipEvent_t ev_gr = nullptr;                    // split round: the other outputs' gains done
   hipEvent_t ev_wd = nullptr;                    // split job: its whitening is done (post_gram)
+  // gpar_posterior_prepare's two slots (PredPrep, host.hpp): ready on the side stream / free again
+  // (their prediction done on the context stream)
+  hipEvent_t ev_prep_ready[2] = {nullptr, nullptr}, ev_prep_free[2] = {nullptr, nullptr};
+  std::vector<gpar::PredPrep> prep;   // the two slots (sized on first use)
+  int prep_next = 0;
   hipEvent_t ev_dp = nullptr;                    // split round: the dense prefix is done (on s_d)
   // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
   // the caller's stream, e.g. the copies that produce its device inputs
@@ -510,6 +519,18 @@ struct QuPre {
   int64_t ld;
   int nb;
 };
+// The part of one output's prediction that does not read the inference inputs, queued ahead on
+// the side stream (gpar_posterior_prepare): the merged grid's gains and the adjoint's fix-up
+// vectors h for given test times.  A slot is consumed by the matching gpar_posterior_predict.
+struct PredPrep {
+  const void* post = nullptr;
+  int out = -1;
+  const double* ts = nullptr;
+  int64_t n_star = 0;
+  GainsOut g{};
+  double* h = nullptr;
+  bool valid = false;
+};
 std::vector<QuPre> run_q_u_batch(gpar_ctx* c, const std::vector<DevProblem>& P,
                                         const std::vector<Theta>& T, const FitKeep& keep,
                                         bool want_cov);
@@ -528,7 +549,7 @@ void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
                          int64_t n_star, const double* t_star_in, const double* v_star_in,
                          int64_t ldvs, int mode, int samples, uint64_t seed, double* mean_out,
                          double* std_out, const GramCache* gc = nullptr, bool defer = false,
-                         const QuPre* pre = nullptr);
+                         const QuPre* pre = nullptr, const PredPrep* prep = nullptr);
 void chains_smooth(gpar_ctx* c, int nchains, int64_t n, const double* t, const double* y,
                           int64_t ldy, const double* noise, int sdim,
                           const std::vector<ChainParamsHost>& cps, double* mean, double* var,

@@ -210,7 +210,8 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
         (void)hipStreamDestroy(st);
       }
     for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_dn,
-                          ctx->ev_dp, ctx->ev_gr, ctx->ev_wd})
+                          ctx->ev_dp, ctx->ev_gr, ctx->ev_wd, ctx->ev_prep_ready[0],
+                          ctx->ev_prep_ready[1], ctx->ev_prep_free[0], ctx->ev_prep_free[1]})
       if (ev) (void)hipEventDestroy(ev);
     for (const auto* evs : {&ctx->ev_grp, &ctx->ev_gn})
       for (hipEvent_t ev : *evs)

@@ -212,7 +212,7 @@ void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
                          int64_t n_star, const double* t_star_in, const double* v_star_in,
                          int64_t ldvs, int mode, int samples, uint64_t seed, double* mean_out,
                          double* std_out, const GramCache* gc, bool defer,
-                         const QuPre* pre) {
+                         const QuPre* pre, const PredPrep* prep) {
   const int64_t n = P.n, m = P.m, d = P.d, mp = P.mp, mc = P.mc;
   if (mode == GPAR_PREDICT_PATH)   // path draw (s, k, i): counter index k (sdim + 1) + i, 32 bits
     ARGCHECK((n + n_star) * (P.sdim + 1) <= ((int64_t)1 << 32),
@@ -330,7 +330,13 @@ void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
   // ---- gains on the merged grid (noise sigma^2 train / 1e10 test)
   std::vector<ChainParamsHost> cps{{1.0 / th.l_t, th.l_t, th.sv_t * th.sv_t, s2}};
   const bool path = mode == GPAR_PREDICT_PATH;
-  GainsOut g = run_gains(c, P.sdim, tm, nt, cps, rm, false, "pred");
+  GainsOut g;
+  if (prep) {   // computed ahead on the side stream (gpar_posterior_prepare)
+    HIPCHECK(hipStreamWaitEvent(c->stream, c->ev_prep_ready[prep - c->prep.data()], 0));
+    g = prep->g;
+  } else {
+    g = run_gains(c, P.sdim, tm, nt, cps, rm, false, "pred");
+  }
   double* dmean = ws<double>(c, "pr_mean", n_star);
   double* dstd = ws<double>(c, "pr_std", n_star);
   if (path) {
@@ -363,7 +369,7 @@ void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
     double* cin = ws<double>(c, "pr_cin", (size_t)nch * mc * 4);
     double* bend = ws<double>(c, "pr_bend", (size_t)nch * mc * 4);
     double* chat = ws<double>(c, "pr_chat", (size_t)nch * mc * 4);
-    double* h = ws<double>(c, "pr_h", (size_t)nt * 4);
+    double* h = prep ? prep->h : ws<double>(c, "pr_h", (size_t)nt * 4);
     {   // algorithmic HBM bytes: merged inputs V* (d) read, gains records + fix-up rows (20), the
         // m whitened Cf*u columns written, per merged row
       Timed tm_(c, "pred_whiten", 8.0 * (double)nt * ((double)d + (double)m + 20.0));
@@ -374,7 +380,7 @@ void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
     check_launch("predict: whiten");
     run_carry(c, P.sdim, g.phi, 0, send, cin, 0, nch, mc, mc, 1, "predf");
     // ---- adjoint: Sigma^{-1} x = W^T (W x)
-    launch_gains_adjoint(c->stream, P.sdim, g.rec, nt, kChunk, nch, 1, h);
+    if (!prep) launch_gains_adjoint(c->stream, P.sdim, g.rec, nt, kChunk, nch, 1, h);
     // u is read back only at the test rows (predict_rows), where rm = 1e10
     {   // bytes: the mc whitened columns read per merged row, records + fix-up rows + R (21), u
         // written at the test rows
@@ -438,6 +444,8 @@ void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
     check_launch("predict: gemm");
   }
 outputs:
+  // the prepared slot may be refilled once this prediction has read it
+  if (prep) HIPCHECK(hipEventRecord(c->ev_prep_free[prep - c->prep.data()], c->stream));
   // ---- outputs
   if (mem == GPAR_MEM_DEVICE) {
     HIPCHECK(hipMemcpyAsync(mean_out, dmean, n_star * sizeof(double), hipMemcpyDeviceToDevice, c->stream));
@@ -919,6 +927,58 @@ int32_t gpar_fit_posterior(gpar_ctx* ctx, const gpar_problem* probs, int32_t npr
   API_END(ctx)
 }
 
+int32_t gpar_posterior_prepare(gpar_ctx* ctx, const gpar_posterior* post, int32_t i,
+                               int64_t n_star, const double* t_star) {
+  API_BEGIN(ctx)
+  ARGCHECK(post && t_star, "null argument");
+  ARGCHECK(post->device == ctx->device, "the posterior belongs to another device's context");
+  ARGCHECK(post->mem == GPAR_MEM_DEVICE, "gpar_posterior_prepare: device-memory posteriors only");
+  ARGCHECK(i >= 0 && i < (int32_t)post->outs.size(), "output index out of range");
+  ARGCHECK(n_star >= 1, "n_star must be >= 1");
+  const gpar_posterior::Out& o = post->outs[i];
+  const DevProblem& P = o.p;
+  if (ctx->prep.empty()) ctx->prep.resize(2);
+  for (int k = 0; k < 2; ++k)
+    for (hipEvent_t* ev : {&ctx->ev_prep_ready[k], &ctx->ev_prep_free[k]})
+      if (!*ev) HIPCHECK(hipEventCreateWithFlags(ev, hipEventDisableTiming));
+  const int slot = ctx->prep_next;
+  ctx->prep_next ^= 1;
+  PredPrep& s = ctx->prep[slot];
+  s.valid = false;
+  // the side stream follows the context stream (inputs, earlier calls) and the slot's last reader
+  HIPCHECK(hipEventRecord(ctx->ev_fork, ctx->main));
+  HIPCHECK(hipStreamWaitEvent(ctx->side, ctx->ev_fork, 0));
+  HIPCHECK(hipStreamWaitEvent(ctx->side, ctx->ev_prep_free[slot], 0));
+  const std::string tag = "prep" + std::to_string(slot);
+  const int64_t nt = P.n + n_star;
+  const int64_t nch = (nt + kChunk - 1) / kChunk;
+  {
+    OnStream on_(ctx, ctx->side);
+    // the merged grid's times and noise (predict_impl merges the inputs again, identically)
+    double* tm = ws<double>(ctx, tag + "_tm", nt);
+    double* ym = ws<double>(ctx, tag + "_ym", nt);
+    double* rm = ws<double>(ctx, tag + "_rm", nt);
+    const double s2 = o.th.sigma * o.th.sigma;
+    launch_merge_side(ctx->stream, P.t, P.n, t_star, n_star, 0, P.y, s2, nullptr, 0, 0, tm, ym, rm,
+                      nullptr, 0, nullptr);
+    launch_merge_side(ctx->stream, t_star, n_star, P.t, P.n, 1, nullptr, 1e10, nullptr, 0, 0, tm, ym,
+                      rm, nullptr, 0, nullptr);
+    check_launch("prepare: merge");
+    std::vector<ChainParamsHost> cps{{1.0 / o.th.l_t, o.th.l_t, o.th.sv_t * o.th.sv_t, s2}};
+    s.g = run_gains(ctx, P.sdim, tm, nt, cps, rm, false, tag);
+    s.h = ws<double>(ctx, tag + "_h", (size_t)nt * 4);
+    launch_gains_adjoint(ctx->stream, P.sdim, s.g.rec, nt, kChunk, nch, 1, s.h);
+    check_launch("prepare: gains");
+    HIPCHECK(hipEventRecord(ctx->ev_prep_ready[slot], ctx->side));
+  }
+  s.post = post;
+  s.out = i;
+  s.ts = t_star;
+  s.n_star = n_star;
+  s.valid = true;
+  API_END(ctx)
+}
+
 int32_t gpar_posterior_predict(gpar_ctx* ctx, const gpar_posterior* post, int32_t i,
                                int64_t n_star, const double* t_star, const double* v_star,
                                int64_t ldvs, int32_t mode, int32_t samples, uint64_t seed,
@@ -934,8 +994,15 @@ int32_t gpar_posterior_predict(gpar_ctx* ctx, const gpar_posterior* post, int32_
            "bad mode");
   if (mode != GPAR_PREDICT_ANALYTIC)
     ARGCHECK(samples >= 2 && samples <= kMaxSamples, "MC / path modes take 2..65536 samples");
+  // a slot gpar_posterior_prepare filled for this output and these test times
+  const PredPrep* prep = nullptr;
+  for (PredPrep& s : ctx->prep)
+    if (s.valid && s.post == post && s.out == i && s.ts == t_star && s.n_star == n_star) {
+      s.valid = false;
+      prep = &s;
+    }
   predict_impl(ctx, o.p, o.th, post->mem, n_star, t_star, v_star, ldvs, mode, samples, seed, mean,
-               std, nullptr, false, &o.q);
+               std, nullptr, false, &o.q, prep);
   API_END(ctx)
 }
 

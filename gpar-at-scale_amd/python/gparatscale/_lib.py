@@ -27,7 +27,7 @@ EXPORTED = (
     "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_kernel_work", "gpar_ctx_reset_stats",
     "gpar_ctx_set_lanes", "gpar_ctx_set_cu_split", "gpar_ctx_set_fit_overlap", "gpar_ctx_get_cu_split", "gpar_ctx_set_dist_cache", "gpar_ctx_set_dist_cache_keep", "gpar_ctx_dist_cache_stats",
     "gpar_pairwise_distances", "gpar_ctx_set_predict_fused", "gpar_ctx_set_input_stream", "gpar_ctx_set_schedule", "gpar_ctx_get_schedule",
-    "gpar_fit_posterior", "gpar_posterior_predict", "gpar_posterior_destroy",
+    "gpar_fit_posterior", "gpar_posterior_predict", "gpar_posterior_prepare", "gpar_posterior_destroy",
     "gpar_nm_create", "gpar_nm_destroy", "gpar_nm_ask", "gpar_nm_tell", "gpar_nm_result",
 )
 
@@ -121,6 +121,7 @@ def load(path: str | None = None):
                                          dp, dp, dp, C.POINTER(vp)]),
             "gpar_posterior_predict": (i32, [vp, vp, i32, i64, vp, vp, i64, i32, i32, C.c_uint64,
                                              vp, vp]),
+            "gpar_posterior_prepare": (i32, [vp, vp, i32, i64, vp]),
             "gpar_posterior_destroy": (i32, [vp]),
             "gpar_mc_normals": (i32, [vp, i32, i64, C.c_uint64, dp]),
             "gpar_path_normals": (i32, [vp, i32, i64, i32, C.c_uint64, dp]),

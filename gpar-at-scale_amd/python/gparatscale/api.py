@@ -488,6 +488,20 @@ class Posterior:
                                              ldvs, md, int(samples), int(seed), _ptr(mean), _ptr(std)))
         return mean, std
 
+    def prepare(self, i, t_star):
+        """Queue output i's inference-input-independent prediction work for device test times
+        t_star (gpar_posterior_prepare) on the context's side stream; the next predict(i, t_star,
+        ...) with the same tensor uses it.  Device problems only."""
+        if not 0 <= int(i) < len(self._problems):
+            raise _arg_error(f"output index {i} out of range (0..{len(self._problems) - 1})")
+        if self._problems[i].mem != _lib.GPAR_MEM_DEVICE:
+            raise _arg_error("prepare: device-memory posteriors only")
+        keep = _Keep()
+        ctx, lib = context(self.device), _lib.load()
+        tsp = _dev_vec(t_star, keep)
+        with _after_torch(ctx):
+            ctx.check(lib.gpar_posterior_prepare(ctx.h, self.h, int(i), t_star.numel(), tsp))
+
     def close(self):
         if getattr(self, "h", None):
             _lib.load().gpar_posterior_destroy(self.h)

@@ -74,7 +74,7 @@ def owners_of(shards: list[list[int]]) -> dict[int, int]:
     return {p: r for r, owned in enumerate(shards) for p in owned}
 
 
-def chained_predictions(outputs, owners: dict, predict_fn, chain):
+def chained_predictions(outputs, owners: dict, predict_fn, chain, prepare_fn=None):
     """Predictions with chained inference inputs across ranks (GPAR_scaled_examples.jl:172,
     eeg.jl:249,274: output p's inference inputs include the predicted means of earlier outputs).
 
@@ -84,6 +84,9 @@ def chained_predictions(outputs, owners: dict, predict_fn, chain):
     (mean, std) and then broadcasts the mean (8 N* bytes over RCCL / gloo) from itself, and every
     rank stores it in chain[:, p - 1] before the next output starts.  The fits are independent
     and run before this on each rank; only this ordered sweep is serial across ranks.
+    prepare_fn(p) (optional, e.g. Posterior.prepare) queues the part of p's prediction that does
+    not read the chain; each rank calls it for its next output before predicting the current one
+    (and for its first output up front), so that part runs beside the sweep.
     Returns {p: (mean, std)} for this rank's outputs."""
     import torch
     import torch.distributed as dist
@@ -91,9 +94,15 @@ def chained_predictions(outputs, owners: dict, predict_fn, chain):
     rank = dist.get_rank() if on else 0
     col = torch.empty(chain.shape[0], dtype=chain.dtype, device=chain.device)
     mine = {}
+    own = [p for p in outputs if owners[p] == rank]
+    nxt = {a: b for a, b in zip(own, own[1:])}
+    if prepare_fn is not None and own:
+        prepare_fn(own[0])
     for p in outputs:
         owner = owners[p]
         if owner == rank:
+            if prepare_fn is not None and p in nxt:
+                prepare_fn(nxt[p])
             mean, std = predict_fn(p, chain)
             mine[p] = (mean, std)
             col.copy_(torch.as_tensor(mean, dtype=chain.dtype).to(chain.device))

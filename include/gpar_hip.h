@@ -330,6 +330,15 @@ int32_t gpar_posterior_predict(gpar_ctx* ctx, const gpar_posterior* post, int32_
                                int64_t n_star, const double* t_star, const double* v_star,
                                int64_t ldvs, int32_t mode, int32_t samples, uint64_t seed,
                                double* mean, double* std);
+/* Queue the part of output i's prediction that does not read the inference inputs -- the merged
+ * train + test grid's gains and adjoint fix-up rows for the (device, ascending) test times t_star
+ * -- on the context's side stream, and return.  The next gpar_posterior_predict for the same
+ * posterior, output, t_star pointer and n_star uses it (bit-identical results) instead of
+ * computing it in line; a chained sweep prepares output p + 1 before predicting output p, so the
+ * two overlap.  Two slots per context: a third prepare reuses the oldest (its predict falls back to
+ * the in-line path).  Device-memory posteriors only. */
+int32_t gpar_posterior_prepare(gpar_ctx* ctx, const gpar_posterior* post, int32_t i,
+                               int64_t n_star, const double* t_star);
 int32_t gpar_posterior_destroy(gpar_posterior* post);
 
 /* ---------------------------------------------------------------- temporal-only (LGSSM) chains
