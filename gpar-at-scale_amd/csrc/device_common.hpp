@@ -16,6 +16,9 @@ constexpr double kLog2Pi = 1.8378770664093454836;
 
 // Per-step gains record: A (d x d, row-major) | K (d) | rs = 1/sqrt(S) ; padded.
 template <int D> struct Rec { static constexpr int size = D == 3 ? 16 : (D == 2 ? 8 : 4); };
+// compact gains record {K_k (D), rs_k, pad}: A_k is recomputed from the step's time difference by
+// the one consumer that takes it (whiten_kfu_d2x2)
+template <int D> struct CRec { static constexpr int size = D == 1 ? 2 : 4; };
 // Per-step fix-up vector g_k (d), padded to 4 doubles.
 constexpr int kGStride = 4;
 // Carry / end-state vectors (d), padded to 4 doubles.

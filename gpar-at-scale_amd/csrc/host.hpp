@@ -292,6 +292,9 @@ struct Theta {
 struct GainsOut {
   double *rec, *g, *phi, *logs, *pf;
   int64_t recstride, gstride, phistride;
+  // compact records {K, rs} (CRec): the whitening recomputes A_k from t (whiten_kfu_any)
+  bool compact = false;
+  const double* t = nullptr;
 };
 // The gains of `nchains` chains sharing t: uploads and workspace (plan_gains), launched over any
 // chain ranges on any streams (GainsPlan::launch) -- the split fit launches them group by group on
@@ -312,15 +315,18 @@ struct GainsPlan {
 GainsPlan plan_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                      const std::vector<ChainParamsHost>& cps, const double* noise, bool want_pf,
                      const std::string& tag, const std::vector<const double*>* ys = nullptr,
-                     double* alpha_loc = nullptr, double* asend = nullptr);
+                     double* alpha_loc = nullptr, double* asend = nullptr, bool compact = false);
 GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                           const std::vector<ChainParamsHost>& cps, const double* noise,
                           bool want_pf, const std::string& tag,
                           const std::vector<const double*>* ys = nullptr,
-                          double* alpha_loc = nullptr, double* asend = nullptr);
-void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const double* rec, const double* v,
+                          double* alpha_loc = nullptr, double* asend = nullptr,
+                          bool compact = false);
+// gi: the output's gains (compact records: the whitening goes through whiten_kfu_d2x2, the
+// distances of an uncached output through a separate pass)
+void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const GainsOut& gi, const double* v,
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
-                           int64_t ldb, double* send, const double* g, double* hsum);
+                           int64_t ldb, double* send, double* hsum);
 
 // --------------------------------------------------------------------------- Gram stage
 struct GramOut {

@@ -282,7 +282,7 @@ std::vector<DevProblem> prepare_batch(gpar_ctx* c, const gpar_problem* probs, in
 GainsPlan plan_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                      const std::vector<ChainParamsHost>& cps, const double* noise, bool want_pf,
                      const std::string& tag, const std::vector<const double*>* ys,
-                     double* alpha_loc, double* asend) {
+                     double* alpha_loc, double* asend, bool compact) {
   GainsPlan gp;
   gp.c = c;
   gp.sdim = sdim;
@@ -293,7 +293,7 @@ GainsPlan plan_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
   gp.noise = noise;
   const int nchains = gp.nchains;
   const int64_t nch = gp.nch;
-  const int rs = rec_size(sdim);
+  const int rs = compact ? crec_size(sdim) : rec_size(sdim);
   const int d2 = sdim * sdim;
   gp.dcps = ws<ChainParamsHost>(c, tag + "_cps", nchains);
   h2d(c, gp.dcps, cps.data(), nchains);
@@ -308,6 +308,8 @@ GainsPlan plan_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
   o.phi = ws<double>(c, tag + "_phi", (size_t)nchains * nch * d2);
   o.logs = ws<double>(c, tag + "_logs", (size_t)nchains * nch);
   o.pf = want_pf ? ws<double>(c, tag + "_pf", (size_t)nchains * n * d2) : nullptr;
+  o.compact = compact;
+  o.t = t;
   if (ys) {
     gp.dys = ws<const double*>(c, tag + "_ys", nchains);
     h2d(c, gp.dys, ys->data(), nchains);
@@ -330,7 +332,7 @@ void GainsPlan::launch(hipStream_t st, int first, int count) const {
                o.phi + (size_t)first * o.phistride, o.logs + (size_t)first * nch,
                o.pf ? o.pf + (size_t)first * n * d2 : nullptr, dys ? dys + first : nullptr,
                alpha_loc ? alpha_loc + (size_t)first * n : nullptr,
-               asend ? asend + (size_t)first * nch * kSStride : nullptr);
+               asend ? asend + (size_t)first * nch * kSStride : nullptr, o.compact);
   check_launch("gains");
 }
 
@@ -338,8 +340,8 @@ GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                           const std::vector<ChainParamsHost>& cps, const double* noise,
                           bool want_pf, const std::string& tag,
                           const std::vector<const double*>* ys,
-                          double* alpha_loc, double* asend) {
-  GainsPlan gp = plan_gains(c, sdim, t, n, cps, noise, want_pf, tag, ys, alpha_loc, asend);
+                          double* alpha_loc, double* asend, bool compact) {
+  GainsPlan gp = plan_gains(c, sdim, t, n, cps, noise, want_pf, tag, ys, alpha_loc, asend, compact);
   gp.launch(c->stream, 0, gp.nchains);
   return gp.o;
 }

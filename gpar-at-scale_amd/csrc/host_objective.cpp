@@ -10,18 +10,22 @@ namespace gpar {
 // Inputs wider than kFusedMaxD (the fused kernels keep a column's pseudo-input in registers):
 // the squared distances are a separate MFMA (or direct-difference) pass into beta itself, which
 // the whitening then reads and overwrites in place (k_dist.hip).
-void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const double* rec, const double* v,
+void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const GainsOut& gi, const double* v,
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
-                           int64_t ldb, double* send, const double* g, double* hsum) {
+                           int64_t ldb, double* send, double* hsum) {
   const double s_o = th.sv_o * th.sv_o;
+  const double* rec = gi.rec;
+  const double* g = gi.g;
+  // compact records: A_k recomputed from t inside whiten_kfu_d2x2 (the only whitening that can)
+  const double* tc = gi.compact ? gi.t : nullptr;
   const double* d2 = cached_d2(c, p);
   if (d2 && v == p.v) {   // the fit's training inputs, distances cached (fit_impl)
     launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, d2, p.mp, p.m, p.mp, n, kChunk, nch,
-                         1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum, p.d2_is_r);
-  } else if (p.d > kFusedMaxD) {
+                         1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum, p.d2_is_r, tc, th.l_t);
+  } else if (p.d > kFusedMaxD || gi.compact) {
     launch_dist2(c->stream, p.ok, v, ldv, n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, beta, ldb);
     launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, beta, ldb, p.m, p.mp, n, kChunk, nch,
-                         1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum);
+                         1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum, false, tc, th.l_t);
   } else if (p.ok == GPAR_MATERN12) {
     launch_whiten_kfu(c->stream, p.tk, p.ok, rec, v, ldv, (int)p.d, p.z, p.ldz, p.m, p.mp, n,
                       kChunk, nch, 1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum);
@@ -52,8 +56,7 @@ void stage_whiten(gpar_ctx* c, const StageJob& j, const StageBufs& b) {
   // fix-up rows (16 + 4 doubles per step), beta written (m columns)
   const double in_cols = cached_d2(c, p) ? (double)p.m : (double)p.d;
   Timed tm_(c, "whiten", 8.0 * (double)p.n * (in_cols + (double)p.m + 20.0));
-  whiten_kfu_any(c, p, j.gi.rec, p.v, p.ldv, p.n, p.nch, *j.th, b.beta, p.mp, b.send, j.gi.g,
-                 b.hsum);
+  whiten_kfu_any(c, p, j.gi, p.v, p.ldv, p.n, p.nch, *j.th, b.beta, p.mp, b.send, b.hsum);
   check_launch("whiten_kfu");
 }
 
@@ -187,8 +190,9 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     // the others' gains (head 8.6 ms per round, r04f) or ahead of them (they then delayed the
     // second whitening and every Gram after it, r04i); the others' gains in groups on the
     // whitening stream (they delayed the Grams' DG share: 5.10 -> 5.24 ms per Gram, r04h).
+    // compact records on the split pipeline, whose every whitening is whiten_kfu_d2x2
     gplan = plan_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fit", &ys, alpha_all,
-                       asend_all);
+                       asend_all, /*compact=*/split_pipe);
     if (!split_head) gplan.launch(c->stream, 0, np);
     const GainsOut& g = gplan.o;
     for (int i = 0; i < np; ++i) {

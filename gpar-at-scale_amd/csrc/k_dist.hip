@@ -212,12 +212,15 @@ constexpr int kW2T = 8;     // rows of d2 prefetched per thread
 constexpr int kW2Occ = 2;   // workgroups per CU
 
 // RIN: src holds the distances r = sqrt_pos(d2) (the fit's cache, Matern kernels) instead of d2.
-template <int TK, int OK, bool RIN>
+// CR: rec holds compact records {K, rs} (gains_phase3<D, true>); each step's transition A_k is
+// recomputed here from t (tau = (t_k - t_{k-1}) / l_t, as the gains pass computes it) while the
+// chunk's records are staged, which cuts the gains pass's HBM writes by more than half.
+template <int TK, int OK, bool RIN, bool CR>
 __global__ __launch_bounds__(256, kW2Occ) void whiten_kfu_d2x2(
     const double* __restrict__ rec, const double* src, int64_t lds, int64_t m, int64_t mp,
     int64_t n, int L, double inv_lo, double s_o, double* beta, int64_t ldb,
     double* __restrict__ send, int64_t mc, const double* __restrict__ g,
-    double* __restrict__ hsum, ExpNegConsts ek) {
+    double* __restrict__ hsum, ExpNegConsts ek, const double* __restrict__ tt, double l_t) {
   constexpr int SD = Sde<TK>::d;
   constexpr int RS = Rec<SD>::size;
   __shared__ __attribute__((aligned(16))) double rl[kW2MaxL * RS];
@@ -232,7 +235,22 @@ __global__ __launch_bounds__(256, kW2Occ) void whiten_kfu_d2x2(
   const int64_t k1 = (k0 + L < n) ? k0 + L : n;
   const int nk = (int)(k1 - k0);
   // the chunk's records and fix-up rows, once
-  for (int e = tid; e < nk * RS; e += 256) rl[e] = rec[k0 * RS + e];
+  if constexpr (CR) {
+    constexpr int CS = CRec<SD>::size;
+    for (int e = tid; e < nk; e += 256) {
+      const int64_t k = k0 + e;
+      double A[SD][SD];
+      sde_transition<SD>((k == 0) ? 1.0 : (tt[k] - tt[k - 1]) / l_t, A);
+#pragma unroll
+      for (int i = 0; i < SD; ++i)
+#pragma unroll
+        for (int q = 0; q < SD; ++q) rl[e * RS + i * SD + q] = A[i][q];
+#pragma unroll
+      for (int i = 0; i <= SD; ++i) rl[e * RS + SD * SD + i] = rec[k * CS + i];
+    }
+  } else {
+    for (int e = tid; e < nk * RS; e += 256) rl[e] = rec[k0 * RS + e];
+  }
   for (int e = tid; e < nk * kGStride; e += 256) gl[e] = g[k0 * kGStride + e];
   double ma[SD], mb[SD], ha[SD], hb[SD];
 #pragma unroll
@@ -395,19 +413,25 @@ template <int TK, int OK, bool RIN>
 static void launch_wd2_k(hipStream_t st, dim3 grid, const double* rec, const double* src,
                          int64_t lds, int64_t m, int64_t mp, int64_t n, int L, double inv_lo,
                          double s_o, double* beta, int64_t ldb, double* send, int64_t mc,
-                         const double* g, double* hsum) {
+                         const double* g, double* hsum, const double* tt, double l_t) {
   if (L > kW2MaxL || (lds & 1) || (ldb & 1))
     throw std::runtime_error("whiten_kfu_d2x2: chunk length > 256 or odd leading dimension");
-  whiten_kfu_d2x2<TK, OK, RIN><<<grid, 256, 0, st>>>(rec, src, lds, m, mp, n, L, inv_lo, s_o, beta,
-                                                     ldb, send, mc, g, hsum, exp_neg_consts());
+  if (tt)
+    whiten_kfu_d2x2<TK, OK, RIN, true><<<grid, 256, 0, st>>>(rec, src, lds, m, mp, n, L, inv_lo,
+                                                             s_o, beta, ldb, send, mc, g, hsum,
+                                                             exp_neg_consts(), tt, l_t);
+  else
+    whiten_kfu_d2x2<TK, OK, RIN, false><<<grid, 256, 0, st>>>(rec, src, lds, m, mp, n, L, inv_lo,
+                                                              s_o, beta, ldb, send, mc, g, hsum,
+                                                              exp_neg_consts(), nullptr, 0.0);
 }
 
 template <int TK>
 static void launch_wd2_t(hipStream_t st, int ok, bool rin, dim3 grid, const double* rec,
                          const double* src, int64_t lds, int64_t m, int64_t mp, int64_t n, int L,
                          double inv_lo, double s_o, double* beta, int64_t ldb, double* send,
-                         int64_t mc, const double* g, double* hsum) {
-#define WD2_ARGS st, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum
+                         int64_t mc, const double* g, double* hsum, const double* tt, double l_t) {
+#define WD2_ARGS st, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum, tt, l_t
   if (rin) {
     switch (ok) {
       case KM12: launch_wd2_k<TK, KM12, true>(WD2_ARGS); break;
@@ -430,9 +454,10 @@ static void launch_wd2_t(hipStream_t st, int ok, bool rin, dim3 grid, const doub
 void launch_whiten_kfu_d2(hipStream_t st, int time_kind, int out_kind, const double* rec,
                           const double* src, int64_t lds, int64_t m, int64_t mp, int64_t n, int L,
                           int64_t nch, double inv_lo, double s_o, double* beta, int64_t ldb,
-                          double* send, int64_t mc, const double* g, double* hsum, bool src_is_r) {
+                          double* send, int64_t mc, const double* g, double* hsum, bool src_is_r,
+                          const double* t_compact, double l_t) {
   dim3 grid((unsigned)nch, (unsigned)((mp + 511) / 512));
-#define WD2T_ARGS st, out_kind, src_is_r, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum
+#define WD2T_ARGS st, out_kind, src_is_r, grid, rec, src, lds, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum, t_compact, l_t
   switch (time_kind) {
     case KM12: launch_wd2_t<KM12>(WD2T_ARGS); break;
     case KM32: launch_wd2_t<KM32>(WD2T_ARGS); break;

@@ -298,7 +298,7 @@ __global__ __launch_bounds__(256) void gains_phase2(int64_t nch, const double* _
 // With `ys` (the DTC objective): the chain's own data vector ys[p] is filtered from a zero state
 // in the same pass, with the record still in registers (what whiten_vec would do in a second pass
 // over rec): alpha_loc[p * n + k] and the chunk end state asend[(p * nch + j) * 4 + i].
-template <int D>
+template <int D, bool COMPACT>
 __global__ __launch_bounds__(256, 2) void gains_phase3(const double* __restrict__ t, int64_t n,
                                                     int L, int64_t nch,
                                                     const ChainParams* __restrict__ cps,
@@ -312,13 +312,15 @@ __global__ __launch_bounds__(256, 2) void gains_phase3(const double* __restrict_
                                                     const double* const* __restrict__ ys,
                                                     double* __restrict__ alpha_loc,
                                                     double* __restrict__ asend) {
-  constexpr int RS = Rec<D>::size;
+  // COMPACT: the record written is {K_k, rs_k} (CRec), its A_k recomputed by the consumer from the
+  // step's time difference (whiten_kfu_d2x2's staging); RP stays the full record's pitch
+  constexpr int RS = COMPACT ? CRec<D>::size : Rec<D>::size;
   // Output staging: thread = chunk, so a plain per-thread store of step s's record writes 64
   // lines 32 KB apart per instruction (measured: the stores were 5.6 of the 6.9 ms of a
   // 63-chain launch).  Each wave parks its 64 records (and the g rows) in LDS and writes them
   // back 16 bytes per lane, RS/2 lanes per record; the alpha values are parked 16 steps at a
   // time and written back as whole 128-byte lines the same way.
-  constexpr int RP = RS + 1;
+  constexpr int RP = Rec<D>::size + 1;
   constexpr int AS = 16;        // alpha steps per flush
   __shared__ double rbuf[4][64 * RP];
   __shared__ double abuf[4][64 * (AS + 1)];
@@ -379,16 +381,19 @@ __global__ __launch_bounds__(256, 2) void gains_phase3(const double* __restrict_
     for (int i = 0; i < D; ++i) Kg[i] = Pm[i][0] / S;
     double AP[D][D];
     mat_mul(A, Phi, AP);
-    // park the record {A, K, rs, pad} and g_k = -rs (A Phi)[0, :]
+    // park the record {A, K, rs, pad} (COMPACT: {K, rs, pad}) and g_k = -rs (A Phi)[0, :]
+    constexpr int KO = COMPACT ? 0 : D * D;   // K's offset in the record
+    if constexpr (!COMPACT) {
 #pragma unroll
-    for (int i = 0; i < D; ++i)
+      for (int i = 0; i < D; ++i)
 #pragma unroll
-      for (int q = 0; q < D; ++q) rb[lane * RP + i * D + q] = A[i][q];
+        for (int q = 0; q < D; ++q) rb[lane * RP + i * D + q] = A[i][q];
+    }
 #pragma unroll
-    for (int i = 0; i < D; ++i) rb[lane * RP + D * D + i] = Kg[i];
-    rb[lane * RP + D * D + D] = rs;
+    for (int i = 0; i < D; ++i) rb[lane * RP + KO + i] = Kg[i];
+    rb[lane * RP + KO + D] = rs;
 #pragma unroll
-    for (int e = D * D + D + 1; e < RS; ++e) rb[lane * RP + e] = 0.0;
+    for (int e = KO + D + 1; e < RS; ++e) rb[lane * RP + e] = 0.0;
     double gk[kGStride];
 #pragma unroll
     for (int q = 0; q < kGStride; ++q) gk[q] = q < D ? -rs * AP[0][q] : 0.0;
@@ -1651,14 +1656,18 @@ void launch_gains(hipStream_t st, int sdim, const double* t, int64_t n, int L, i
                   int nchains, const ChainParamsHost* cps_dev, const double* noise,
                   double* agg, double* pstart, double* rec, double* g, double* phi,
                   double* logs, double* pf, const double* const* ys, double* alpha_loc,
-                  double* asend) {
+                  double* asend, bool compact) {
   const ChainParams* cps = reinterpret_cast<const ChainParams*>(cps_dev);
   dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
   GPAR_DISPATCH_D(sdim, {
     gains_phase1<DD><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, agg);
     gains_phase2<DD><<<nchains, 256, 0, st>>>(nch, agg, pstart);
-    gains_phase3<DD><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, pstart, rec, g, phi, logs, pf,
-                                           ys, alpha_loc, asend);
+    if (compact)
+      gains_phase3<DD, true><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, pstart, rec, g, phi,
+                                                   logs, pf, ys, alpha_loc, asend);
+    else
+      gains_phase3<DD, false><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, pstart, rec, g, phi,
+                                                    logs, pf, ys, alpha_loc, asend);
   });
 }
 

@@ -88,7 +88,9 @@ void launch_gains(hipStream_t st, int sdim, const double* t, int64_t n, int L, i
                   int nchains, const ChainParamsHost* cps_dev, const double* noise,
                   double* agg, double* pstart, double* rec, double* g, double* phi,
                   double* logs, double* pf, const double* const* ys = nullptr,
-                  double* alpha_loc = nullptr, double* asend = nullptr);
+                  double* alpha_loc = nullptr, double* asend = nullptr, bool compact = false);
+// compact gains records {K, rs, pad} (gains_phase3<D, true>): doubles per step
+inline int crec_size(int sdim) { return sdim == 1 ? 2 : 4; }
 int dp_bucket(int d);
 void launch_whiten_kfu(hipStream_t st, int time_kind, int out_kind, const double* rec,
                        const double* v, int64_t ldv, int d, const double* z, int64_t ldz,
@@ -122,7 +124,8 @@ void launch_whiten_kfu_d2(hipStream_t st, int time_kind, int out_kind, const dou
                           const double* src, int64_t lds, int64_t m, int64_t mp, int64_t n, int L,
                           int64_t nch, double inv_lo, double s_o, double* beta, int64_t ldb,
                           double* send, int64_t mc, const double* g, double* hsum,
-                          bool src_is_r = false);
+                          bool src_is_r = false, const double* t_compact = nullptr,
+                          double l_t = 0.0);
 void launch_whiten_vec(hipStream_t st, int sdim, const double* rec, int64_t recstride,
                        const double* y, int64_t ldy, int64_t n, int L, int64_t nch, int nchains,
                        double* alpha, int64_t lda, double* send, int64_t sendstride, int64_t mc,
