@@ -87,7 +87,8 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
 
 static constexpr const char* kScheduleKnobs[] = {"overlap", "overlap_group", "predict_fused", "qu_batch",
                                                   "dense_early", "split_head", "predict_lanes",
-                                                  "serialize", "dg_share", "tail_cus", "post_gram"};
+                                                  "serialize", "dg_share", "tail_cus", "post_gram",
+                                                  "compact_rec"};
 
 // gpar_ctx_set_schedule / gpar_ctx_get_schedule (GPAR_ERR_ARG: unknown knob or value).
 static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
@@ -103,6 +104,7 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
     if (v < 0 || v > 3) return GPAR_ERR_ARG;
     c->split_head = v;
   }
+  else if (k == "compact_rec") c->compact_rec = v != 0;
   else if (k == "post_gram") {
     if (v < -1 || v > 1) return GPAR_ERR_ARG;
     c->post_gram = v;
@@ -142,6 +144,7 @@ static int get_schedule(const gpar_ctx* c, const std::string& k, int32_t* v) {
   else if (k == "dg_share") *v = c->dg_share;
   else if (k == "tail_cus") *v = c->tail_cus;
   else if (k == "post_gram") *v = c->post_gram;
+  else if (k == "compact_rec") *v = c->compact_rec;
   else if (k == "predict_lanes") *v = c->predict_lanes;
   else if (k == "serialize") *v = c->serialize;
   else return GPAR_ERR_ARG;

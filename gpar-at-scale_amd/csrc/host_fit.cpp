@@ -276,7 +276,7 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
       OnStream on_(c, c->s_d);
       StagingScope st_(c, G.id);
       gn = run_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fitg" + std::to_string(G.id),
-                     &ys, G.alpha_all, G.asend_all, /*compact=*/true);
+                     &ys, G.alpha_all, G.asend_all, /*compact=*/c->compact_rec);
       HIPCHECK(hipMemcpyAsync(G.go.logs, gn.logs, (size_t)na * nch * sizeof(double),
                               hipMemcpyDeviceToDevice, c->s_d));
       HIPCHECK(hipEventRecord(c->ev_gn[G.id], c->s_d));

@@ -192,7 +192,7 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     // whitening stream (they delayed the Grams' DG share: 5.10 -> 5.24 ms per Gram, r04h).
     // compact records on the split pipeline, whose every whitening is whiten_kfu_d2x2
     gplan = plan_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fit", &ys, alpha_all,
-                       asend_all, /*compact=*/split_pipe);
+                       asend_all, /*compact=*/split_pipe && c->compact_rec);
     if (!split_head) gplan.launch(c->stream, 0, np);
     const GainsOut& g = gplan.o;
     for (int i = 0; i < np; ++i) {
