@@ -104,7 +104,10 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
     if (v < 0 || v > 3) return GPAR_ERR_ARG;
     c->split_head = v;
   }
-  else if (k == "compact_rec") c->compact_rec = v != 0;
+  else if (k == "compact_rec") {
+    if (v < -1 || v > 1) return GPAR_ERR_ARG;
+    c->compact_rec = v;
+  }
   else if (k == "post_gram") {
     if (v < -1 || v > 1) return GPAR_ERR_ARG;
     c->post_gram = v;

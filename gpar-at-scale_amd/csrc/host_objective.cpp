@@ -190,9 +190,11 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     // the others' gains (head 8.6 ms per round, r04f) or ahead of them (they then delayed the
     // second whitening and every Gram after it, r04i); the others' gains in groups on the
     // whitening stream (they delayed the Grams' DG share: 5.10 -> 5.24 ms per Gram, r04h).
-    // compact records on the split pipeline, whose every whitening is whiten_kfu_d2x2
+    // compact records (split pipeline only: its every whitening is whiten_kfu_d2x2) when asked:
+    // in the round-by-round fit they made the round head's first whitening slower beside the
+    // other outputs' (now faster) gains, 5.6 -> 8.6 ms per round, 17.77 -> 17.91 s per job (r04x)
     gplan = plan_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fit", &ys, alpha_all,
-                       asend_all, /*compact=*/split_pipe && c->compact_rec);
+                       asend_all, /*compact=*/split_pipe && c->compact_rec == 1);
     if (!split_head) gplan.launch(c->stream, 0, np);
     const GainsOut& g = gplan.o;
     for (int i = 0; i < np; ++i) {
