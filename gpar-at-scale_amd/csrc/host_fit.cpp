@@ -220,6 +220,12 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
     ~StagingScope() { c->staging = nullptr; }
   };
 
+  // compact gains records (compact_rec -1 = auto) when every output already whitens through
+  // whiten_kfu_d2x2 (cached distances, or inputs wider than the fused kernels take): an uncached
+  // narrow output would otherwise switch from the fused whitening to the distance pass (last bits)
+  bool all_d2 = true;
+  for (const auto& p : P) all_d2 = all_d2 && (cached_d2(c, p) || p.d > kFusedMaxD);
+  const bool compact = c->compact_rec == 1 || (c->compact_rec == -1 && all_d2);
   SplitPipe sp(c, n, mpmax);
   // the short chains on the Gram CUs: the whitening CUs also run the other group's dense tails and
   // gains here (one 8-output shard of the north job: 2.356 -> 2.329 s per step, r04p; the
@@ -278,7 +284,7 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
       OnStream on_(c, c->s_d);
       StagingScope st_(c, G.id);
       gn = run_gains(c, P[0].sdim, P[0].t, n, cps, nullptr, false, "fitg" + std::to_string(G.id),
-                     &ys, G.alpha_all, G.asend_all, /*compact=*/c->compact_rec != 0);
+                     &ys, G.alpha_all, G.asend_all, compact);
       HIPCHECK(hipMemcpyAsync(G.go.logs, gn.logs, (size_t)na * nch * sizeof(double),
                               hipMemcpyDeviceToDevice, c->s_d));
       HIPCHECK(hipEventRecord(c->ev_gn[G.id], c->s_d));

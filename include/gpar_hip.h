@@ -165,8 +165,10 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *   "tail_cus"      the round overlap's dense tails and gains: 0 = on the whitening CUs (default),
  *                   1 = on the whole chip, 2 = on the Gram CUs
  *   "compact_rec"   1: the CU-split fit's gains write compact records {K_k, rs_k} and the cached
- *                   whitening recomputes each step's transition A_k from t (the same bits); 0:
- *                   full records {A_k, K_k, rs_k}; -1 (default): in the round-overlapping fit only
+ *                   whitening recomputes each step's transition A_k from t (the same bits; an
+ *                   output whose distances are not cached then whitens through the distance pass
+ *                   instead of the fused kernel: last bits); 0: full records {A_k, K_k, rs_k};
+ *                   -1 (default): in the round-overlapping fit when every output is cached
  *   "predict_lanes" 1 or 2: streams gpar_fit_predict's predictions alternate over (default 2)
  *   "serialize"     1: every launch of every schedule on the context's one stream, in issue order,
  *                   with the same plans, CU shares of work items and workspaces: the order-free
