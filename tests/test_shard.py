@@ -114,9 +114,25 @@ def _chain_worker(rank, world, port, out):
         chain = torch.zeros((NS, P), dtype=torch.float64)
         chain[:, 0] = torch.from_numpy(F[:, 0])         # test_y1: the true first output
         owners = S.owners_of(S.assign_outputs(P, world))
-        mine = S.chained_predictions(range(2, P + 1), owners,
-                                     lambda p, c: _chain_predict(t, Y, ts, p, c.numpy()), chain)
+        calls = []
+
+        def predict(p, c):
+            calls.append(("predict", p))
+            return _chain_predict(t, Y, ts, p, c.numpy())
+
+        mine = S.chained_predictions(range(2, P + 1), owners, predict, chain,
+                                     prepare_fn=lambda p: calls.append(("prepare", p)))
         assert all(owners[p] == rank for p in mine)
+        # prepare_fn: every owned output once, the first up front, each next one before the
+        # current prediction (gpar_posterior_prepare's two slots hold both)
+        own = [p for p in range(2, P + 1) if owners[p] == rank]
+        assert [p for k, p in calls if k == "prepare"] == own
+        assert [p for k, p in calls if k == "predict"] == own
+        for i, p in enumerate(own):
+            pos = calls.index(("predict", p))
+            assert calls.index(("prepare", p)) < pos
+            if i + 1 < len(own):
+                assert calls.index(("prepare", own[i + 1])) < pos
         if rank == 0:
             np.save(out, chain.numpy())
     finally:
