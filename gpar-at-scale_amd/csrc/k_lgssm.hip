@@ -602,9 +602,7 @@ __global__ __launch_bounds__(256) void whiten_kfu(
 constexpr int kMT = 16;   // steps per sub-tile
 
 template <int TK, int OK, int DP>
-// DP = 64 at two workgroups per CU spilled 44 VGPRs (its B fragments alone are 128); at one it
-// holds everything in registers (317 VGPRs + 61 AGPRs)
-__global__ __launch_bounds__(256, DP >= 64 ? 1 : 2) void whiten_kfu_mfma(
+__global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     const double* __restrict__ rec, const double* __restrict__ v, int64_t ldv, int d,
     const double* __restrict__ z, int64_t ldz, const double* __restrict__ zc, int64_t m,
     int64_t mp, int64_t n, int L, double inv_lo, double s_o, double* __restrict__ beta,
