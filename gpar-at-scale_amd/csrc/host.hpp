@@ -47,6 +47,7 @@ struct gpar_ctx {
   hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
   hipEvent_t ev_dn = nullptr;                    // split round start: the dense prefix follows the context stream
   hipEvent_t ev_gr = nullptr;                    // split round: the other outputs' gains done
+  hipEvent_t ev_gr2 = nullptr;                   // split round (split_head 4): the late gains done
   hipEvent_t ev_wd = nullptr;                    // split job: its whitening is done (post_gram)
   // gpar_posterior_prepare's two slots (PredPrep, host.hpp): ready on the side stream / free again
   // (their prediction done on the context stream)

@@ -76,6 +76,7 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
          hipEventCreateWithFlags(&c->ev_dn, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_gr, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_wd, hipEventDisableTiming) != hipSuccess ||
+         hipEventCreateWithFlags(&c->ev_gr2, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_dp, hipEventDisableTiming) != hipSuccess))
       return GPAR_ERR_HIP;
     c->split_mask_w = w;
@@ -101,7 +102,7 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
   else if (k == "qu_batch") c->qu_batch = v != 0;
   else if (k == "dense_early") c->dense_early = v != 0;
   else if (k == "split_head") {
-    if (v < 0 || v > 3) return GPAR_ERR_ARG;
+    if (v < 0 || v > 4) return GPAR_ERR_ARG;
     c->split_head = v;
   }
   else if (k == "compact_rec") {
@@ -216,7 +217,7 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
         (void)hipStreamDestroy(st);
       }
     for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_dn,
-                          ctx->ev_dp, ctx->ev_gr, ctx->ev_wd, ctx->ev_prep_ready[0],
+                          ctx->ev_dp, ctx->ev_gr, ctx->ev_gr2, ctx->ev_wd, ctx->ev_prep_ready[0],
                           ctx->ev_prep_ready[1], ctx->ev_prep_free[0], ctx->ev_prep_free[1]})
       if (ev) (void)hipEventDestroy(ev);
     for (const auto* evs : {&ctx->ev_grp, &ctx->ev_gn})

@@ -167,7 +167,7 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   // others' gains beside them on the whitening CUs; 0 = every output's gains whole-chip, the first
   // whitening on the whitening CUs
   const int head_mode = (split_pipe && shared && np > 1) ? c->split_head : 0;
-  const bool split_head = head_mode == 1 || head_mode == 3;
+  const bool split_head = head_mode == 1 || head_mode == 3 || head_mode == 4;
   const double* logs_src = nullptr;
   std::vector<GainsOut> gains(np);
   GainsPlan gplan;
@@ -251,16 +251,29 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     sp.head_st = head_mode == 3 ? c->s_g : nullptr;
     sp.post_gram = c->post_gram == 1;
     sp.start();
-    if (head_mode == 1) {
+    // head_mode 4: as 1, but only the next quarter of the outputs' gains (at most 15) beside the
+    // first whitening; the rest's on the Gram CUs' second stream once the first Gram (and its
+    // correction) is issued, well ahead of the whitening that first needs them
+    const int nhead = head_mode == 4 ? std::max(1, std::min(15, (np - 1) / 4)) : np - 1;
+    if (head_mode == 1 || head_mode == 4) {
       gplan.launch(c->s_w, 0, 1);
-      gplan.launch(c->s_g2, 1, np - 1);
+      gplan.launch(c->s_g2, 1, nhead);
       HIPCHECK(hipEventRecord(c->ev_gr, c->s_g2));
     } else if (head_mode == 3) {   // the second whitening follows the others' gains on s_w
       gplan.launch(c->s_g, 0, 1);
       gplan.launch(c->s_w, 1, np - 1);
     }
+    const bool late = head_mode == 4 && nhead < np - 1;
+    if (late)
+      sp.on_gram = [&](const StageJob&, int64_t k) {
+        if (k != 0) return;
+        gplan.launch(c->s_g2, 1 + nhead, np - 1 - nhead);
+        HIPCHECK(hipEventRecord(c->ev_gr2, c->s_g2));
+      };
     for (int i = 0; i < np; ++i) {
-      if (i == 1 && head_mode == 1) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr, 0));
+      if (i == 1 && (head_mode == 1 || head_mode == 4))
+        HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr, 0));
+      if (late && i == 1 + nhead) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr2, 0));
       sp.push(job(i, sp.buf[i & 1]));
     }
     sp.flush();

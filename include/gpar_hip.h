@@ -155,8 +155,9 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *   "split_head"    a split round's head: 1 = the first output's gains on the whitening CUs, the
  *                   others' beside them on the Gram CUs (default); 2 = every output's gains, then the
  *                   first whitening, whole-chip; 3 = the first output's gains, whitening and
- *                   short chain on the Gram CUs, the others' gains on the whitening CUs; 0 = every
- *                   output's gains ahead of the round
+ *                   short chain on the Gram CUs, the others' gains on the whitening CUs; 4 = as 1
+ *                   with only the next quarter of the outputs' gains (at most 15) beside the first
+ *                   whitening, the rest's after the first Gram; 0 = every output's gains ahead
  *   "dg_share"      32nds of a split Gram's diagonal-block work items run on the whitening CUs
  *                   (-1, the default: the CU split's own share, cus_per_xcd / 32)
  *   "post_gram"     1: a split job's short chain (carry, vec_fix) on the Gram CUs behind the previous

@@ -36,6 +36,7 @@ SETTINGS = [
     {"overlap": 0, "split_head": 0},
     {"overlap": 0, "split_head": 2},
     {"overlap": 0, "split_head": 3},
+    {"overlap": 0, "split_head": 4},
     {"dg_share": 12},
     {"post_gram": 0},
     {"post_gram": 1, "overlap": 0},
