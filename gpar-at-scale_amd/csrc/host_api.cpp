@@ -89,7 +89,7 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
 static constexpr const char* kScheduleKnobs[] = {"overlap", "overlap_group", "predict_fused", "qu_batch",
                                                   "dense_early", "split_head", "predict_lanes",
                                                   "serialize", "dg_share", "tail_cus", "post_gram",
-                                                  "compact_rec"};
+                                                  "compact_rec", "dg_rows_w"};
 
 // gpar_ctx_set_schedule / gpar_ctx_get_schedule (GPAR_ERR_ARG: unknown knob or value).
 static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
@@ -105,7 +105,10 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
     if (v < 0 || v > 4) return GPAR_ERR_ARG;
     c->split_head = v;
   }
-  else if (k == "compact_rec") {
+  else if (k == "dg_rows_w") {
+    if (v < -50 || v > 100) return GPAR_ERR_ARG;
+    c->dg_rows_w = v;
+  } else if (k == "compact_rec") {
     if (v < -1 || v > 1) return GPAR_ERR_ARG;
     c->compact_rec = v;
   }
@@ -149,6 +152,7 @@ static int get_schedule(const gpar_ctx* c, const std::string& k, int32_t* v) {
   else if (k == "tail_cus") *v = c->tail_cus;
   else if (k == "post_gram") *v = c->post_gram;
   else if (k == "compact_rec") *v = c->compact_rec;
+  else if (k == "dg_rows_w") *v = c->dg_rows_w;
   else if (k == "predict_lanes") *v = c->predict_lanes;
   else if (k == "serialize") *v = c->serialize;
   else return GPAR_ERR_ARG;

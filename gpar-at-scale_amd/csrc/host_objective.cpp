@@ -95,8 +95,22 @@ void stage_gram(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_bet
                        bool one_per_cu, const std::string& part_sfx, hipStream_t side, int cus,
                        hipStream_t st_w, hipEvent_t ev_w, int w_frac32) {
   const DevProblem& p = *j.p;
-  const GramPlan plan = gram_plan(p.n, p.mp, one_per_cu, cus, st_w ? 256 : cus);
+  GramPlan plan = gram_plan(p.n, p.mp, one_per_cu, cus, st_w ? 256 : cus);
   const int w_items = st_w ? plan.ndg * plan.sdg * w_frac32 / 32 : 0;
+  // dg_rows_w: the DG time splits that run on the whitening CUs take that many percent more rows
+  // (the rest fewer), moving diagonal-block work between the two sides in finer steps than whole
+  // rounds of items
+  if (st_w && w_items > 0 && c->dg_rows_w != 0 && plan.v3 && w_items % plan.ndg == 0) {
+    const int sw = w_items / plan.ndg;
+    auto up = [](int64_t r) { return (r + kBKRows - 1) / kBKRows * kBKRows; };
+    const int64_t rw = up(plan.rows_dg * (100 + c->dg_rows_w) / 100);
+    const int64_t rest = p.n - (int64_t)sw * rw;
+    if (rw > 0 && rest > 0 && plan.sdg > sw) {
+      plan.dg_sw = sw;
+      plan.dg_rows_w = rw;
+      plan.rows_dg = up((rest + plan.sdg - sw - 1) / (plan.sdg - sw));
+    }
+  }
   double* part = ws<double>(c, "gram_part" + part_sfx, (size_t)plan.part_doubles);
   double* rpart = ws<double>(c, "gram_rpart" + part_sfx, (size_t)plan.rpart_doubles);
   {

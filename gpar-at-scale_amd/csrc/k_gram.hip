@@ -773,10 +773,10 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
     const int64_t dslot0 = (int64_t)plan.noff * (plan.soff + ncs);
     if (st_w && w_items > 0) {   // the first w_items DG items on another stream (other CUs)
       launch_gram3_dg(st_w, 0, beta, ldb, n, alpha, plan.npan, plan.ndg, plan.sdg, plan.rows_dg,
-                      dslot0, part, rpart, 0, w_items);
+                      dslot0, part, rpart, 0, w_items, plan.dg_sw, plan.dg_rows_w);
       HIPCHECK_G(hipEventRecord(ev_w, st_w));
       launch_gram3_dg(st, 0, beta, ldb, n, alpha, plan.npan, plan.ndg, plan.sdg, plan.rows_dg,
-                      dslot0, part, rpart, w_items, -1);
+                      dslot0, part, rpart, w_items, -1, plan.dg_sw, plan.dg_rows_w);
       HIPCHECK_G(hipStreamWaitEvent(st, ev_w, 0));
     } else {
       launch_gram3_dg(st, ndgw, beta, ldb, n, alpha, plan.npan, plan.ndg, plan.sdg, plan.rows_dg,

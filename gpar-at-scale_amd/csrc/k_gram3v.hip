@@ -14,7 +14,7 @@ namespace gpar {
 __global__ __launch_bounds__(128) void gram3_dg_kernel(
     const double* __restrict__ beta, int64_t ldb, int64_t n, const double* __restrict__ alpha,
     int npan, int ndg, int sdg, int64_t rows, int64_t slot0, double* __restrict__ part,
-    double* __restrict__ rpart, int bt_lo, int bt_cnt) {
+    double* __restrict__ rpart, int bt_lo, int bt_cnt, int sw, int64_t rows_w) {
   __shared__ __attribute__((aligned(16))) double smem[4 * kPanelD + 2 * 2 * kBK];
   double* ringa = smem + 4 * kPanelD;
 
@@ -30,8 +30,11 @@ __global__ __launch_bounds__(128) void gram3_dg_kernel(
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int pA = 2 * gid + wave;
 
-  const int64_t kb = (int64_t)split * rows;
-  int64_t ke = kb + rows;
+  // the first sw splits take rows_w rows each (the share that runs on the whitening CUs can be
+  // sized apart from the rest), the others `rows`; both multiples of kBK
+  const int64_t kb = split < sw ? (int64_t)split * rows_w
+                                : (int64_t)sw * rows_w + (int64_t)(split - sw) * rows;
+  int64_t ke = kb + (split < sw ? rows_w : rows);
   if (ke > n) ke = n;
   const int nsteps = (int)(ke > kb ? (ke - kb + kBK - 1) / kBK : 0);
 
@@ -410,12 +413,13 @@ void launch_gram3_corr_slim(hipStream_t st, int sdim, const double* ecor, const 
 
 void launch_gram3_dg(hipStream_t st, int nwg, const double* beta, int64_t ldb, int64_t n,
                      const double* alpha, int npan, int ndg, int sdg, int64_t rows,
-                     int64_t slot0, double* part, double* rpart, int bt_lo, int bt_cnt) {
+                     int64_t slot0, double* part, double* rpart, int bt_lo, int bt_cnt, int sw,
+                     int64_t rows_w) {
   if (bt_cnt < 0) bt_cnt = ndg * sdg - bt_lo;
   if (bt_cnt <= 0) return;
   if (nwg <= 0) nwg = ((bt_cnt + 7) / 8) * 8;
   gram3_dg_kernel<<<nwg, 128, 0, st>>>(beta, ldb, n, alpha, npan, ndg, sdg, rows, slot0, part,
-                                       rpart, bt_lo, bt_cnt);
+                                       rpart, bt_lo, bt_cnt, sw, rows_w);
 }
 
 void launch_gram3_corr(hipStream_t st, int sdim, const double* ecor, const double* cin,

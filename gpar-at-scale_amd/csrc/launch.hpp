@@ -76,9 +76,13 @@ struct GramPlan {
   int v3 = 0;   // fat-wave kernels (gram3_*: 2-wave workgroups, 32-tile OFF waves)
   int ncs = 0;  // v3 chunk-correction splits
   int ncs_slim = 0;  // ... of the slim correction that runs beside the OFF kernel
+  // v3 DG time splits sized apart: the first dg_sw take dg_rows_w rows each (0: all rows_dg)
+  int dg_sw = 0;
+  int64_t dg_rows_w = 0;
 };
 
 constexpr int kGramTile = 128;
+constexpr int kBKRows = 16;   // the Gram kernels' time rows per K-step (gram_common.hpp kBK)
 constexpr int kRecStride3 = 16;
 
 inline int rec_size(int sdim) { return sdim == 3 ? 16 : (sdim == 2 ? 8 : 4); }
