@@ -88,7 +88,10 @@ struct gpar_ctx {
   int post_gram = -1;             // "post_gram": a split job's short chain on the Gram CUs (s_g2): 1, 0, -1 = round overlap only
   int compact_rec = -1;           // "compact_rec": compact gains records: 1, 0, -1 = round overlap only
   int dg_share = -1;
-  int dg_rows_w = 0;              // "dg_rows_w": percent more rows per DG split on the whitening CUs              // "dg_share": 32nds of a split Gram's DG items on the whitening CUs (-1: split_w)
+  // "dg_rows_w": percent more rows per DG split on the whitening CUs (fewer on the Gram CUs): with
+  // the whitening at 3.57 ms the Gram CUs' side set each split Gram's span; +10 % moves enough of
+  // the diagonal blocks across, 5.117 -> 5.080 ms per Gram (sweep 0..14 on one box, r04ac)
+  int dg_rows_w = 10;              // "dg_share": 32nds of a split Gram's DG items on the whitening CUs (-1: split_w)
   // "serialize": side, s_w, s_g, s_g2 and s_d all alias `main`, so every launch runs in issue order
   // on one stream (the created streams stay in own_*): the order-free reference the concurrent
   // schedule must equal bit for bit.  Plans, CU shares of work items and workspaces are unchanged.
