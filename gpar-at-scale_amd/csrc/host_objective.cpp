@@ -100,8 +100,10 @@ void stage_gram(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_bet
   // dg_rows_w: the DG time splits that run on the whitening CUs take that many percent more rows
   // (the rest fewer), moving diagonal-block work between the two sides in finer steps than whole
   // rounds of items
-  if (st_w && w_items > 0 && c->dg_rows_w != 0 && plan.v3 && w_items % plan.ndg == 0) {
-    const int sw = w_items / plan.ndg;
+  // (the split count follows the CU split's own share, not dg_share, so that dg_share only moves
+  // items between the sides and stays bit-identical)
+  if (st_w && w_items > 0 && c->dg_rows_w != 0 && plan.v3 && plan.sdg * c->split_w % 32 == 0) {
+    const int sw = plan.sdg * c->split_w / 32;
     auto up = [](int64_t r) { return (r + kBKRows - 1) / kBKRows * kBKRows; };
     const int64_t rw = up(plan.rows_dg * (100 + c->dg_rows_w) / 100);
     const int64_t rest = p.n - (int64_t)sw * rw;
