@@ -126,5 +126,7 @@ def test_dg_rows_w_is_a_plan_not_a_schedule(job):
     for i in range(len(OUTS)):
         np.testing.assert_array_equal(ma[i], mb[i])
         np.testing.assert_array_equal(sa[i], sb[i])
-    np.testing.assert_allclose(fa.nlml, fr0.nlml, rtol=1e-12)
-    np.testing.assert_allclose(fa.theta, fr0.theta, rtol=1e-8)
+    # the objective's tolerance against the checkers (rel 1e-9): output 3's fit is ill-conditioned
+    # (-nlml 1.7e9), and six simplex steps carry the last-bit difference of G to 1.7e-11
+    np.testing.assert_allclose(fa.nlml, fr0.nlml, rtol=1e-9)
+    np.testing.assert_allclose(fa.theta, fr0.theta, rtol=1e-6)
