@@ -26,6 +26,7 @@
 
 namespace gpar {
 struct PredPrep;
+constexpr int kDgRowsAuto = -100;   // gpar_ctx::dg_rows_w "auto"
 }
 
 struct gpar_ctx {
@@ -87,11 +88,13 @@ struct gpar_ctx {
   int split_head = 1;             // "split_head": a split round's head (run_gram_stage: 0, 1, 2)
   int post_gram = -1;             // "post_gram": a split job's short chain on the Gram CUs (s_g2): 1, 0, -1 = round overlap only
   int compact_rec = -1;           // "compact_rec": compact gains records: 1, 0, -1 = round overlap only
-  int dg_share = -1;
-  // "dg_rows_w": percent more rows per DG split on the whitening CUs (fewer on the Gram CUs): with
-  // the whitening at 3.57 ms the Gram CUs' side set each split Gram's span; +10 % moves enough of
-  // the diagonal blocks across, 5.117 -> 5.080 ms per Gram (sweep 0..14 on one box, r04ac)
-  int dg_rows_w = 10;              // "dg_share": 32nds of a split Gram's DG items on the whitening CUs (-1: split_w)
+  int dg_share = -1;              // "dg_share": 32nds of a split Gram's DG items on the whitening CUs (-1: split_w)
+  // "dg_rows_w": percent more rows per DG split on the whitening CUs (fewer on the Gram CUs);
+  // kDgRowsAuto: +10 in the round-by-round fit, where the whitening side (3.57 ms whitening) has
+  // time to spare and the Gram CUs' side sets the span (5.117 -> 5.080 ms per Gram, r04ac), 0 in
+  // the round overlap, whose whitening side also runs the other group's tails and gains (the
+  // 8-output shard: 2.353 s at +10, 2.329 at 0, r04ad)
+  int dg_rows_w = gpar::kDgRowsAuto;
   // "serialize": side, s_w, s_g, s_g2 and s_d all alias `main`, so every launch runs in issue order
   // on one stream (the created streams stay in own_*): the order-free reference the concurrent
   // schedule must equal bit for bit.  Plans, CU shares of work items and workspaces are unchanged.
@@ -368,7 +371,8 @@ void stage_whiten(gpar_ctx* c, const StageJob& j, const StageBufs& b);
 void stage_post(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_beta);
 void stage_gram(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_beta,
                        bool one_per_cu, const std::string& part_sfx, hipStream_t side, int cus,
-                       hipStream_t st_w = nullptr, hipEvent_t ev_w = nullptr, int w_frac32 = 0);
+                       hipStream_t st_w = nullptr, hipEvent_t ev_w = nullptr, int w_frac32 = 0,
+                       int dg_rows_w = 0);
 void reserve_gram_parts(gpar_ctx* c, const std::vector<DevProblem>& P, int nlanes);
 
 // The CU-split pipeline: whitening + short chain of job k on w CUs of every XCD (s_w),
@@ -400,6 +404,7 @@ struct SplitPipe {
   // the short chains on the Gram CUs' second stream (gpar_ctx::post_gram; the round overlap's
   // whitening CUs also run the other group's dense tails and gains)
   bool post_gram = false;
+  int dg_rows_w = 0;   // percent more rows per DG split on the whitening CUs (stage_gram)
   void push(const StageJob& j) {
     if (k == 0 && head) {
       // the first whitening and its short chain on head_st: the caller's unmasked stream (the whole
@@ -454,7 +459,7 @@ struct SplitPipe {
       // stream orders it; on the Gram CUs' stream (post_gram) the share waits for it
       if (post_gram) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[i & 1], 0));
       stage_gram(c, pending, buf[i & 1], false, false, "", c->s_g2, gcus, c->s_w, c->ev_pw,
-                 c->dg_share >= 0 ? c->dg_share : c->split_w);
+                 c->dg_share >= 0 ? c->dg_share : c->split_w, dg_rows_w);
       HIPCHECK(hipEventRecord(c->ev_gd[i & 1], c->s_g));
     }
     has_pending = false;

@@ -106,7 +106,7 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
     c->split_head = v;
   }
   else if (k == "dg_rows_w") {
-    if (v < -50 || v > 100) return GPAR_ERR_ARG;
+    if ((v < -50 || v > 100) && v != kDgRowsAuto) return GPAR_ERR_ARG;
     c->dg_rows_w = v;
   } else if (k == "compact_rec") {
     if (v < -1 || v > 1) return GPAR_ERR_ARG;

@@ -93,7 +93,7 @@ void stage_post(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_bet
 // there (ev_w joins them).  one_per_cu: the two-lane plan (one Gram workgroup per CU).
 void stage_gram(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_beta,
                        bool one_per_cu, const std::string& part_sfx, hipStream_t side, int cus,
-                       hipStream_t st_w, hipEvent_t ev_w, int w_frac32) {
+                       hipStream_t st_w, hipEvent_t ev_w, int w_frac32, int dg_rows_w) {
   const DevProblem& p = *j.p;
   GramPlan plan = gram_plan(p.n, p.mp, one_per_cu, cus, st_w ? 256 : cus);
   const int w_items = st_w ? plan.ndg * plan.sdg * w_frac32 / 32 : 0;
@@ -102,10 +102,10 @@ void stage_gram(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_bet
   // rounds of items
   // (the split count follows the CU split's own share, not dg_share, so that dg_share only moves
   // items between the sides and stays bit-identical)
-  if (st_w && w_items > 0 && c->dg_rows_w != 0 && plan.v3 && plan.sdg * c->split_w % 32 == 0) {
+  if (st_w && w_items > 0 && dg_rows_w != 0 && plan.v3 && plan.sdg * c->split_w % 32 == 0) {
     const int sw = plan.sdg * c->split_w / 32;
     auto up = [](int64_t r) { return (r + kBKRows - 1) / kBKRows * kBKRows; };
-    const int64_t rw = up(plan.rows_dg * (100 + c->dg_rows_w) / 100);
+    const int64_t rw = up(plan.rows_dg * (100 + dg_rows_w) / 100);
     const int64_t rest = p.n - (int64_t)sw * rw;
     if (rw > 0 && rest > 0 && plan.sdg > sw) {
       plan.dg_sw = sw;
@@ -266,6 +266,7 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     sp.head = head_mode == 2 || head_mode == 3;
     sp.head_st = head_mode == 3 ? c->s_g : nullptr;
     sp.post_gram = c->post_gram == 1;
+    sp.dg_rows_w = c->dg_rows_w == kDgRowsAuto ? 10 : c->dg_rows_w;
     sp.start();
     // head_mode 4: as 1, but only the next quarter of the outputs' gains (at most 15) beside the
     // first whitening; the rest's on the Gram CUs' second stream once the first Gram (and its

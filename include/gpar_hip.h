@@ -176,8 +176,9 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *                   reference the concurrent schedule equals bit for bit (default 0)
  *   "predict_fused" as gpar_ctx_set_predict_fused (changes the summation order: last bits)
  *   "dg_rows_w"     percent more rows per diagonal-block time split on the whitening CUs of a
- *                   split Gram, fewer on the Gram CUs (default 10; changes G's summation
- *                   grouping: last bits, like predict_fused)
+ *                   split Gram, fewer on the Gram CUs; -100 (default) = auto: 10 in the
+ *                   round-by-round fit, 0 in the round overlap (changes G's summation grouping:
+ *                   last bits, like predict_fused)
  * The environment variable GPAR_<KNOB> (upper case) sets a knob at context creation.
  * GPAR_ERR_ARG for an unknown knob or value. */
 int32_t gpar_ctx_set_schedule(gpar_ctx* ctx, const char* knob, int32_t value);

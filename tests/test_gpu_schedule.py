@@ -48,7 +48,7 @@ SETTINGS = [
     {"predict_lanes": 1},
 ]
 DEFAULTS = {"serialize": 0, "overlap": 1, "overlap_group": 0, "dense_early": 1, "split_head": 1,
-            "dg_share": -1, "tail_cus": 0, "post_gram": -1, "compact_rec": -1, "dg_rows_w": 10, "qu_batch": 1, "predict_lanes": 2}
+            "dg_share": -1, "tail_cus": 0, "post_gram": -1, "compact_rec": -1, "dg_rows_w": -100, "qu_batch": 1, "predict_lanes": 2}
 
 
 @pytest.fixture(scope="module")
