@@ -96,6 +96,8 @@ def test_overlapped_rounds_equal_round_by_round(ctx):
     probs, keep, ref = _batch(2500, outs, Ms, 61)
     x0 = np.tile([0.0, 0.0, 0.0, 0.0, -2.0], (len(outs), 1))
     ctx.set_cu_split(8)
+    # a fixed DG plan: dg_rows_w's auto value differs between the two fits (a summation grouping)
+    ctx.set_schedule("dg_rows_w", 10)
     res = {}
     try:
         for on in (False, True):
@@ -110,6 +112,7 @@ def test_overlapped_rounds_equal_round_by_round(ctx):
     finally:
         ctx.set_fit_overlap(True)
         ctx.set_cu_split(-1)
+        ctx.set_schedule("dg_rows_w", -100)
     (a0, b0, c0, cm0, cs0), (a1, b1, c1, cm1, cs1) = res[False], res[True]
     assert len(set(b0.evals)) > 1          # the groups shrink at different rounds
     for x, y in ((a0, a1), (b0, b1), (c0, c1)):
