@@ -44,7 +44,7 @@ struct gpar_ctx {
   int split_w = 0, split_mask_w = 0;
   bool split_forced = false;      // set explicitly: no problem-size gate (split_active)
   // s_d: the round-overlapping fit's dense tails, on the whitening CUs (fit_overlapped)
-  hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr, s_d = nullptr;
+  hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr, s_d = nullptr, s_dp = nullptr;
   hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
   hipEvent_t ev_dn = nullptr;                    // split round start: the dense prefix follows the context stream
   hipEvent_t ev_gr = nullptr;                    // split round: the other outputs' gains done
@@ -55,7 +55,7 @@ struct gpar_ctx {
   hipEvent_t ev_prep_ready[2] = {nullptr, nullptr}, ev_prep_free[2] = {nullptr, nullptr};
   std::vector<gpar::PredPrep> prep;   // the two slots (sized on first use)
   int prep_next = 0;
-  hipEvent_t ev_dp = nullptr;                    // split round: the dense prefix is done (on s_d)
+  hipEvent_t ev_dp = nullptr;                    // split round (dense_early 2): the dense prefix is done (on s_dp)
   // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
   // the caller's stream, e.g. the copies that produce its device inputs
   bool has_input_stream = false;
@@ -84,7 +84,9 @@ struct gpar_ctx {
   int predict_lanes = 2;          // "predict_lanes": gpar_fit_predict's predictions over 1 or 2 streams
   bool predict_fused = true;      // "predict_fused": predict_var (off: predict_rows + gemm_nt; last bits differ)
   bool qu_batch = true;           // "qu_batch": gpar_fit_predict's q(u) batched over the outputs
-  bool dense_early = true;        // "dense_early": the G-independent dense tail ahead of the round's Grams
+  // "dense_early": the G-independent dense tail ahead of the round's Grams: 1 on the Gram stream,
+  // 2 on a Gram-CU stream of its own (s_dp) beside the first Gram, 0 after the Grams
+  int dense_early = 1;
   int split_head = 1;             // "split_head": a split round's head (run_gram_stage: 0, 1, 2)
   int post_gram = -1;             // "post_gram": a split job's short chain on the Gram CUs (s_g2): 1, 0, -1 = round overlap only
   int compact_rec = -1;           // "compact_rec": compact gains records: 1, 0, -1 = round overlap only

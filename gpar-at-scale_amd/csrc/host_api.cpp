@@ -38,6 +38,7 @@ static void route_streams(gpar_ctx* c) {
     const hipStream_t own = c->own_s[i < 3 ? i : 3 + c->tail_cus];
     *act[i] = (c->serialize && own) ? c->main : own;
   }
+  c->s_dp = (c->serialize && c->own_s[5]) ? c->main : c->own_s[5];
 }
 
 // CU split of the pipelined fit (gpar_ctx_set_cu_split): CU-masked streams for the whitening
@@ -100,7 +101,10 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
   }
   else if (k == "predict_fused") c->predict_fused = v != 0;
   else if (k == "qu_batch") c->qu_batch = v != 0;
-  else if (k == "dense_early") c->dense_early = v != 0;
+  else if (k == "dense_early") {
+    if (v < 0 || v > 2) return GPAR_ERR_ARG;
+    c->dense_early = (int)v;
+  }
   else if (k == "split_head") {
     if (v < 0 || v > 4) return GPAR_ERR_ARG;
     c->split_head = v;

@@ -495,14 +495,17 @@ void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<T
     // the Gram stream first follows everything queued on the context stream (host inputs' uploads,
     // the pseudo-input centres, the distance cache), then factors Kuu beside the round's gains
     // (split_head 3: on the Gram CUs' second stream, the Gram stream whitening the first output)
-    const hipStream_t ds = c->split_head == 3 ? c->s_g2 : c->s_g;
+    // (dense_early 2: on a Gram-CU stream of its own, so the first Gram need not queue behind it)
+    const hipStream_t ds = c->dense_early == 2 ? c->s_dp : c->split_head == 3 ? c->s_g2 : c->s_g;
     HIPCHECK(hipEventRecord(c->ev_dn, c->stream));
     HIPCHECK(hipStreamWaitEvent(ds, c->ev_dn, 0));
     OnStream on_(c, ds);
     dn = run_dense_pre(c, P, th, mpmax, false);
+    if (c->dense_early == 2) HIPCHECK(hipEventRecord(c->ev_dp, ds));
   }
   GramOut go = run_gram_stage(c, P, th);
   if (gram_out) *gram_out = go;
+  if (early && c->dense_early == 2) HIPCHECK(hipStreamWaitEvent(c->stream, c->ev_dp, 0));
   if (!early) dn = run_dense_pre(c, P, th, go.ldg, false);
   run_dense_post(c, P, go, dn);
   const int64_t nch = P[0].nch;

@@ -151,7 +151,9 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *                   4..16 outputs (larger calls: round by round); g > 0 = groups of g in any call
  *                   of >= 4 outputs
  *   "qu_batch"      1: gpar_fit_predict runs q(u) batched over the outputs (default 1)
- *   "dense_early"   1: the G-independent half of the dense tail ahead of a split round's Grams (1)
+ *   "dense_early"   1: the G-independent half of the dense tail ahead of a split round's Grams, on
+ *                   the Gram stream (default); 2: the same on a Gram-CU stream of its own, beside
+ *                   the first Gram; 0: after the Grams
  *   "split_head"    a split round's head: 1 = the first output's gains on the whitening CUs, the
  *                   others' beside them on the Gram CUs (default); 2 = every output's gains, then the
  *                   first whitening, whole-chip; 3 = the first output's gains, whitening and

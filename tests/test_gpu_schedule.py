@@ -33,6 +33,7 @@ SETTINGS = [
     {"overlap_group": 1},                # five groups of one
     {"overlap": 0, "serialize": 1},
     {"overlap": 0, "dense_early": 0},
+    {"overlap": 0, "dense_early": 2},
     {"overlap": 0, "split_head": 0},
     {"overlap": 0, "split_head": 2},
     {"overlap": 0, "split_head": 3},
