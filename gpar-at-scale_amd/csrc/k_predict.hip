@@ -508,17 +508,34 @@ __global__ __launch_bounds__(256, 1) void predict_var(
       }
     }
     const double* B = &lb[0][0] + (s & 1) * (NC * 16);
-#pragma unroll
-    for (int t = T0; t < T; ++t)
+    // tile t's 4 fragments are read one tile ahead, each tile's reads in a scheduling region of
+    // their own: with two tiles' reads in one region the compiler paired them into
+    // ds_read2st64_b64, which banks by (a/4) mod 32 and 16-lane groups — 16 LDS cycles per pair
+    // with this layout's 2-way conflicts, against 4 for the two ds_read_b64 the layout is
+    // conflict-free for (PMC r04ag: 47 % of the LDS cycles were conflicts)
+    auto readB = [&](int t, double* bf) __attribute__((always_inline)) {
+      const int c = t * 16 + fcol;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
-        const int c = t * 16 + fcol, kk = ks * 4 + frow;
-        const double bf = B[c * 16 + (((kk >> 1) ^ ((c >> 1) & 7)) << 1) + (kk & 1)];
-        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[ks], bf, acc[t], 0, 0, 0);
-        // keep the scheduler's window to a few tiles: hoisting every fragment read of a
-        // 32-tile step ran out of VGPRs and spilled the accumulators
-        if (ks == 3 && (t & 1)) __builtin_amdgcn_sched_barrier(0);
+        const int kk = ks * 4 + frow;
+        bf[ks] = B[c * 16 + (((kk >> 1) ^ ((c >> 1) & 7)) << 1) + (kk & 1)];
       }
+    };
+    double bn[4];
+    readB(T0, bn);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int t = T0; t < T; ++t) {
+      double bc[4];
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks) bc[ks] = bn[ks];
+      if (t + 1 < T) readB(t + 1, bn);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+        acc[t] = __builtin_amdgcn_mfma_f64_16x16x4f64(fa[ks], bc[ks], acc[t], 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     if constexpr (PF) {
       // all but step s + 2's DMAs (issued last: X 2 per wave, the carries 1 more on wave 0) have
       // landed; a bare s_barrier (__syncthreads would first wait for every load, the prefetch

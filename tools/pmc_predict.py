@@ -19,6 +19,7 @@ ALGO = {  # algorithmic HBM bytes per launch (bench.py roofline_predict)
     "predict_rows": 16 * NS * MP,
     "gemm_nt_kernel": 8 * NS * MP,
 }
+FLOPS = {"predict_var": NS * M * (M + 1)}   # the variance product's triangle (bench.py pred_var)
 
 
 def load(d):
@@ -42,6 +43,7 @@ def load(d):
 
 def main(root):
     sq, fe, wr = load(root + "/sq1"), load(root + "/fetch"), load(root + "/write")
+    lds = load(root + "/lds")
     res = {"source": "tools/pmc_predict.sh: rocprofv3 --pmc passes over tools/predict_probe.py "
                      "--outputs 2 --dmin 62 (N = N* = 1e6, M = 512, D = 62, 63); per-dispatch averages"}
     for k in sorted(sq):
@@ -58,6 +60,11 @@ def main(root):
             e["wave_time_fraction"] = {"active_inst_any": c.get("SQ_ACTIVE_INST_ANY", 0) / w,
                                        "wait_inst_any (issue stall)": c.get("SQ_WAIT_INST_ANY", 0) / w,
                                        "wait_any (waitcnt/barrier)": c.get("SQ_WAIT_ANY", 0) / w}
+        if k in lds:
+            e["lds_counters"] = {a: b for a, b in lds[k].items() if a != "_dur"}
+        if k in FLOPS and t:
+            e["tflops"] = FLOPS[k] / t / 1e12
+            e["frac_of_fp64_peak"] = FLOPS[k] / t / 78.6e12
         f = fe.get(k, {}).get("FETCH_SIZE")
         wb = wr.get(k, {}).get("WRITE_SIZE")
         e["hbm_read_bytes"] = f * 1024 * 2 if f is not None else None
