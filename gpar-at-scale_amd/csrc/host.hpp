@@ -83,6 +83,9 @@ struct gpar_ctx {
   bool overlap = true;            // "overlap": round-overlapping batched fit (gpar_ctx_set_fit_overlap)
   int predict_lanes = 2;          // "predict_lanes": gpar_fit_predict's predictions over 1 or 2 streams
   bool predict_fused = true;      // "predict_fused": predict_var (off: predict_rows + gemm_nt; last bits differ)
+  // "predict_d2": the merged-grid whitening as a distance pass + whiten_kfu_d2x2 in place (the
+  // path inputs wider than kFusedMaxD take) instead of the fused whiten_kfu_mfma; last bits differ
+  bool predict_d2 = false;
   bool qu_batch = true;           // "qu_batch": gpar_fit_predict's q(u) batched over the outputs
   // "dense_early": the G-independent dense tail ahead of the round's Grams: 1 on the Gram stream,
   // 2 on a Gram-CU stream of its own (s_dp) beside the first Gram, 0 after the Grams
@@ -337,7 +340,7 @@ GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
 // distances of an uncached output through a separate pass)
 void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const GainsOut& gi, const double* v,
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
-                           int64_t ldb, double* send, double* hsum);
+                           int64_t ldb, double* send, double* hsum, bool force_d2 = false);
 
 // --------------------------------------------------------------------------- Gram stage
 struct GramOut {

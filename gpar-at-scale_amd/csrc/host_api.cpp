@@ -87,7 +87,7 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
   return GPAR_OK;
 }
 
-static constexpr const char* kScheduleKnobs[] = {"overlap", "overlap_group", "predict_fused", "qu_batch",
+static constexpr const char* kScheduleKnobs[] = {"overlap", "overlap_group", "predict_fused", "predict_d2", "qu_batch",
                                                   "dense_early", "split_head", "predict_lanes",
                                                   "serialize", "dg_share", "tail_cus", "post_gram",
                                                   "compact_rec", "dg_rows_w"};
@@ -100,6 +100,7 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
     c->overlap_group = v;
   }
   else if (k == "predict_fused") c->predict_fused = v != 0;
+  else if (k == "predict_d2") c->predict_d2 = v != 0;
   else if (k == "qu_batch") c->qu_batch = v != 0;
   else if (k == "dense_early") {
     if (v < 0 || v > 2) return GPAR_ERR_ARG;
@@ -149,6 +150,7 @@ static int get_schedule(const gpar_ctx* c, const std::string& k, int32_t* v) {
   if (k == "overlap") *v = c->overlap;
   else if (k == "overlap_group") *v = c->overlap_group;
   else if (k == "predict_fused") *v = c->predict_fused;
+  else if (k == "predict_d2") *v = c->predict_d2;
   else if (k == "qu_batch") *v = c->qu_batch;
   else if (k == "dense_early") *v = c->dense_early;
   else if (k == "split_head") *v = c->split_head;

@@ -12,7 +12,7 @@ namespace gpar {
 // the whitening then reads and overwrites in place (k_dist.hip).
 void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const GainsOut& gi, const double* v,
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
-                           int64_t ldb, double* send, double* hsum) {
+                           int64_t ldb, double* send, double* hsum, bool force_d2) {
   const double s_o = th.sv_o * th.sv_o;
   const double* rec = gi.rec;
   const double* g = gi.g;
@@ -22,7 +22,7 @@ void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const GainsOut& gi, const 
   if (d2 && v == p.v) {   // the fit's training inputs, distances cached (fit_impl)
     launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, d2, p.mp, p.m, p.mp, n, kChunk, nch,
                          1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum, p.d2_is_r, tc, th.l_t);
-  } else if (p.d > kFusedMaxD || gi.compact) {
+  } else if (p.d > kFusedMaxD || gi.compact || (force_d2 && p.d > 0)) {
     launch_dist2(c->stream, p.ok, v, ldv, n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, beta, ldb);
     launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, beta, ldb, p.m, p.mp, n, kChunk, nch,
                          1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum, false, tc, th.l_t);

@@ -373,7 +373,7 @@ void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
     {   // algorithmic HBM bytes: merged inputs V* (d) read, gains records + fix-up rows (20), the
         // m whitened Cf*u columns written, per merged row
       Timed tm_(c, "pred_whiten", 8.0 * (double)nt * ((double)d + (double)m + 20.0));
-      whiten_kfu_any(c, P, g, vm, d, nt, nch, th, X, ldx, send, nullptr);
+      whiten_kfu_any(c, P, g, vm, d, nt, nch, th, X, ldx, send, nullptr, c->predict_d2);
       launch_whiten_vec(c->stream, P.sdim, g.rec, 0, ym, 0, nt, kChunk, nch, 1, X + mp, 0, send, 0,
                         mc, mp, ldx);
     }

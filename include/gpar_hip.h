@@ -177,6 +177,8 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *                   with the same plans, CU shares of work items and workspaces: the order-free
  *                   reference the concurrent schedule equals bit for bit (default 0)
  *   "predict_fused" as gpar_ctx_set_predict_fused (changes the summation order: last bits)
+ *   "predict_d2"    1: the prediction's merged-grid whitening as a distance pass then the cached
+ *                   whitening kernel in place, instead of the fused kernel (0, default; last bits)
  *   "dg_rows_w"     percent more rows per diagonal-block time split on the whitening CUs of a
  *                   split Gram, fewer on the Gram CUs; -100 (default) = auto: 10 in the
  *                   round-by-round fit, 0 in the round overlap (changes G's summation grouping:

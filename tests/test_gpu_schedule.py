@@ -52,7 +52,8 @@ SETTINGS = [
 # between the round-by-round fit (+10 %) and the round overlap (0), which the settings switch
 PLAN = {"dg_rows_w": 10}
 DEFAULTS = {"serialize": 0, "overlap": 1, "overlap_group": 0, "dense_early": 1, "split_head": 1,
-            "dg_share": -1, "tail_cus": 0, "post_gram": -1, "compact_rec": -1, "dg_rows_w": -100, "qu_batch": 1, "predict_lanes": 2}
+            "dg_share": -1, "tail_cus": 0, "post_gram": -1, "compact_rec": -1, "dg_rows_w": -100, "qu_batch": 1, "predict_lanes": 2,
+            "predict_d2": 0}
 
 
 @pytest.fixture(scope="module")
@@ -134,3 +135,19 @@ def test_dg_rows_w_is_a_plan_not_a_schedule(job):
     # (-nlml 1.7e9), and six simplex steps carry the last-bit difference of G to 1.7e-11
     np.testing.assert_allclose(fa.nlml, fr0.nlml, rtol=1e-9)
     np.testing.assert_allclose(fa.theta, fr0.theta, rtol=1e-6)
+
+
+def test_predict_d2_is_a_path_not_a_schedule(job):
+    """predict_d2 whitens the prediction's merged grid by a distance pass + the cached whitening
+    kernel instead of the fused kernel (another rounding of the same Kfu): the fit is untouched,
+    the predictions agree to rounding, and the path is bit-identical to its serialized twin."""
+    run, (fr0, m0, s0), _ = job
+    fa, ma, sa = run({"predict_d2": 1})
+    fb, mb, sb = run({"predict_d2": 1, "serialize": 1})
+    np.testing.assert_array_equal(fa.theta, fr0.theta)
+    np.testing.assert_array_equal(fa.nlml, fr0.nlml)
+    for i in range(len(OUTS)):
+        np.testing.assert_array_equal(ma[i], mb[i])
+        np.testing.assert_array_equal(sa[i], sb[i])
+        np.testing.assert_allclose(ma[i], m0[i], rtol=1e-9, atol=1e-9 * np.abs(m0[i]).max())
+        np.testing.assert_allclose(sa[i], s0[i], rtol=1e-9, atol=1e-9 * np.abs(s0[i]).max())
