@@ -1286,8 +1286,11 @@ __global__ __launch_bounds__(CW) void adjoint_local_wide(double* __restrict__ X,
                                                          const double* __restrict__ wmask) {
   constexpr int RS = Rec<D>::size;
   constexpr int RU = D * D + D + 1;   // record entries used
-  __shared__ double lrec[256 * RU];
-  __shared__ double lg[256 * D];
+  // a step's record entries, then its fix-up row, padded to 16 bytes: the step's reads are 16-byte
+  // aligned broadcasts the compiler issues as ds_read_b128 (4 LDS cycles per 2 doubles; unaligned,
+  // they were ds_read2_b64 at 8, and the pass was LDS-bound: 63 % of the LDS array's cycles, r04ai)
+  constexpr int RP = (RU + D + 1) & ~1;
+  __shared__ __attribute__((aligned(16))) double lrec[256 * RP];
   __shared__ unsigned char lw[256];
   const int64_t j = blockIdx.x;
   const int tid = threadIdx.x;
@@ -1297,8 +1300,8 @@ __global__ __launch_bounds__(CW) void adjoint_local_wide(double* __restrict__ X,
   const int64_t k0 = j * L;
   const int64_t k1 = (k0 + L < n) ? k0 + L : n;
   const int nk = (int)(k1 - k0);
-  for (int e = tid; e < nk * RU; e += CW) lrec[e] = rec[(k0 + e / RU) * RS + e % RU];
-  for (int e = tid; e < nk * D; e += CW) lg[e] = g[(k0 + e / D) * kGStride + e % D];
+  for (int e = tid; e < nk * RU; e += CW) lrec[(e / RU) * RP + e % RU] = rec[(k0 + e / RU) * RS + e % RU];
+  for (int e = tid; e < nk * D; e += CW) lrec[(e / D) * RP + RU + e % D] = g[(k0 + e / D) * kGStride + e % D];
   if (tid < nk) lw[tid] = wmask ? (wmask[k0 + tid] >= 1e10) : 1;
   __syncthreads();
   if ((int64_t)blockIdx.y * CW + (tid & ~63) >= ncols) return;   // the whole wave is idle
@@ -1318,8 +1321,8 @@ __global__ __launch_bounds__(CW) void adjoint_local_wide(double* __restrict__ X,
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
   };
   auto stepfn = [&](int s, double w) {
-    const double* r = lrec + s * RU;
-    const double* gk = lg + s * D;
+    const double* r = lrec + s * RP;
+    const double* gk = r + RU;
 #pragma unroll
     for (int i = 0; i < D; ++i) w = fma(gk[i], cf[i], w);
     double u = w * r[D * D + D];
