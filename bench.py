@@ -24,11 +24,13 @@ line and exits with the first non-zero rank status.
 from __future__ import annotations
 
 import argparse
+import datetime
 import json
 import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -120,13 +122,15 @@ def main():
                          "(SURVEY §8d's unit: one pinned upload of t, Y, t*, F* and the pseudo-inputs "
                          "per step, means / stds downloaded), reported as host_to_host beside value")
     ap.add_argument("--schedule", default="",
-                    help="schedule knobs as k=v,k=v (gpar_ctx_set_schedule: overlap, overlap_group, "
-                         "qu_batch, dense_early, split_head, predict_lanes, serialize); A/B only")
+                    help="schedule knobs as k=v,k=v (gpar_ctx_set_schedule, include/gpar_hip.h: "
+                         "overlap, overlap_group, predict_fused, qu_batch, dense_early, "
+                         "predict_lanes, serialize, post_gram, compact_rec, dg_rows_w)")
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-check-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--stub", action="store_true",
                     help="launcher check without a GPU: ranks join a gloo group, take their output "
                          "shards and report them; no compute (tests/test_bench_launch.py)")
+    ap.add_argument("--stub-fail", default=None, help=argparse.SUPPRESS)
     args = ap.parse_args()
 
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
@@ -166,10 +170,13 @@ def main():
     dev = torch.device("cuda", local)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # a bounded collective timeout: a rank stuck waiting for a dead peer fails instead of
+        # sitting out torch's 10-minute default (the launcher also ends the job on the first
+        # failing rank)
         if args.rehearse:
-            dist.init_process_group("gloo")
+            dist.init_process_group("gloo", timeout=pg_timeout())
         else:
-            dist.init_process_group("nccl", device_id=dev)
+            dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout())
 
     # every rank's view of the job: the next SCALE record shows the backend (nccl = RCCL) and N
     # distinct devices
@@ -800,6 +807,16 @@ def main():
         dist.destroy_process_group()
 
 
+LAUNCH_KILL_GRACE_S = 10.0   # SIGTERM -> SIGKILL grace for the surviving ranks of a failed job
+
+
+def pg_timeout():
+    """The process group's collective timeout: 120 s (GPAR_PG_TIMEOUT_S overrides).  Every
+    collective of the bench waits at most one rank's step (a few seconds at 8 ranks) or the input
+    set-up on rank 0."""
+    return datetime.timedelta(seconds=float(os.environ.get("GPAR_PG_TIMEOUT_S", "120")))
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -849,26 +866,62 @@ def launch_ranks(n, argv, stub=False):
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
                                       stdout=subprocess.PIPE if r == 0 else sys.stderr,
                                       text=True))
-    out0, _ = procs[0].communicate()
-    codes = [procs[0].returncode] + [p.wait() for p in procs[1:]]
-    for line in out0.splitlines():   # the JSON line to stdout, anything a library printed to stderr
+    # rank 0's stdout is drained by a thread (a full pipe must never block it) while the parent
+    # polls every rank: the first rank to exit non-zero ends the job -- the others are terminated
+    # (SIGTERM, then SIGKILL after a grace period) instead of waiting in a collective for a peer
+    # that is gone until the process group's timeout
+    lines0 = []
+    reader = threading.Thread(target=lambda: lines0.extend(procs[0].stdout), daemon=True)
+    reader.start()
+    failed = None
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [(r, c) for r, c in enumerate(codes) if c not in (None, 0)]
+        if bad:
+            failed = bad[0]
+            break
+        if all(c is not None for c in codes):
+            break
+        time.sleep(0.1)
+    if failed is not None:
+        log(f"bench: rank {failed[0]} exited with status {failed[1]}; terminating the others")
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        deadline = time.monotonic() + LAUNCH_KILL_GRACE_S
+        for p in procs:
+            try:
+                p.wait(timeout=max(0.1, deadline - time.monotonic()))
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    reader.join(timeout=5)
+    for line in lines0:   # the JSON line to stdout, anything a library printed to stderr
+        line = line.rstrip("\n")
         print(line, file=sys.stdout if line.startswith("{") else sys.stderr, flush=True)
-    bad = [c for c in codes if c != 0]
-    if bad:
+    codes = [p.returncode for p in procs]
+    if failed is not None:
         log(f"bench: rank exit statuses {codes}")
-        return bad[0]
+        return failed[1] if failed[1] > 0 else 1
     return 0
 
 
 def stub_rank(args):
-    """One rank of the --stub launcher check: gloo group, output shards, no GPU and no compute."""
+    """One rank of the --stub launcher check: gloo group, output shards, no GPU and no compute.
+    --stub-fail R:CODE makes rank R exit with CODE before the gather (the launcher's fail-fast
+    test: the other ranks then wait in the collective until the launcher ends them)."""
     import torch.distributed as dist
     from gparatscale import shard as S
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     P = CONFIGS[args.config]["P"]
     if world > 1:
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.init_process_group("gloo", rank=rank, world_size=world, timeout=pg_timeout())
+    if args.stub_fail:
+        fr, fc = (int(x) for x in args.stub_fail.split(":"))
+        if fr == rank:
+            log(f"[rank {rank}] --stub-fail: exiting with {fc} before the gather")
+            os._exit(fc)
     mine = S.assign_outputs(P, world)[rank]
     got = [None] * world
     if world > 1:

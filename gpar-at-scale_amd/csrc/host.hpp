@@ -44,18 +44,16 @@ struct gpar_ctx {
   int split_w = 0, split_mask_w = 0;
   bool split_forced = false;      // set explicitly: no problem-size gate (split_active)
   // s_d: the round-overlapping fit's dense tails, on the whitening CUs (fit_overlapped)
-  hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr, s_d = nullptr, s_dp = nullptr;
+  hipStream_t s_w = nullptr, s_g = nullptr, s_g2 = nullptr, s_d = nullptr;
   hipEvent_t ev_gd[2] = {nullptr, nullptr}, ev_sp = nullptr;
   hipEvent_t ev_dn = nullptr;                    // split round start: the dense prefix follows the context stream
   hipEvent_t ev_gr = nullptr;                    // split round: the other outputs' gains done
-  hipEvent_t ev_gr2 = nullptr;                   // split round (split_head 4): the late gains done
   hipEvent_t ev_wd = nullptr;                    // split job: its whitening is done (post_gram)
   // gpar_posterior_prepare's two slots (PredPrep, host.hpp): ready on the side stream / free again
   // (their prediction done on the context stream)
   hipEvent_t ev_prep_ready[2] = {nullptr, nullptr}, ev_prep_free[2] = {nullptr, nullptr};
   std::vector<gpar::PredPrep> prep;   // the two slots (sized on first use)
   int prep_next = 0;
-  hipEvent_t ev_dp = nullptr;                    // split round (dense_early 2): the dense prefix is done (on s_dp)
   // gpar_ctx_set_input_stream: every call first waits (device side) for the work queued so far on
   // the caller's stream, e.g. the copies that produce its device inputs
   bool has_input_stream = false;
@@ -83,17 +81,12 @@ struct gpar_ctx {
   bool overlap = true;            // "overlap": round-overlapping batched fit (gpar_ctx_set_fit_overlap)
   int predict_lanes = 2;          // "predict_lanes": gpar_fit_predict's predictions over 1 or 2 streams
   bool predict_fused = true;      // "predict_fused": predict_var (off: predict_rows + gemm_nt; last bits differ)
-  // "predict_d2": the merged-grid whitening as a distance pass + whiten_kfu_d2x2 in place (the
-  // path inputs wider than kFusedMaxD take) instead of the fused whiten_kfu_mfma; last bits differ
-  bool predict_d2 = false;
   bool qu_batch = true;           // "qu_batch": gpar_fit_predict's q(u) batched over the outputs
-  // "dense_early": the G-independent dense tail ahead of the round's Grams: 1 on the Gram stream,
-  // 2 on a Gram-CU stream of its own (s_dp) beside the first Gram, 0 after the Grams
+  // "dense_early": the G-independent dense tail ahead of a split round's Grams on the Gram stream
+  // (1), or after the Grams (0)
   int dense_early = 1;
-  int split_head = 1;             // "split_head": a split round's head (run_gram_stage: 0, 1, 2)
   int post_gram = -1;             // "post_gram": a split job's short chain on the Gram CUs (s_g2): 1, 0, -1 = round overlap only
   int compact_rec = -1;           // "compact_rec": compact gains records: 1, 0, -1 = round overlap only
-  int dg_share = -1;              // "dg_share": 32nds of a split Gram's DG items on the whitening CUs (-1: split_w)
   // "dg_rows_w": percent more rows per DG split on the whitening CUs (fewer on the Gram CUs);
   // kDgRowsAuto: +10 in the round-by-round fit, where the whitening side (3.57 ms whitening) has
   // time to spare and the Gram CUs' side sets the span (5.117 -> 5.080 ms per Gram, r04ac), 0 in
@@ -104,10 +97,8 @@ struct gpar_ctx {
   // on one stream (the created streams stay in own_*): the order-free reference the concurrent
   // schedule must equal bit for bit.  Plans, CU shares of work items and workspaces are unchanged.
   bool serialize = false;
-  // own_s[3..5]: the round overlap's dense tails and gains on the whitening CUs, the whole chip,
-  // the Gram CUs ("tail_cus" 0, 1, 2 picks s_d among them)
-  hipStream_t own_side = nullptr, own_s[6] = {nullptr, nullptr, nullptr, nullptr, nullptr, nullptr};
-  int tail_cus = 0;
+  // own_s: s_w, s_g, s_g2 and s_d (the round overlap's dense tails and gains, on the whitening CUs)
+  hipStream_t own_side = nullptr, own_s[4] = {nullptr, nullptr, nullptr, nullptr};
   std::string ws_suffix;          // appended to workspace names (a prediction lane's own buffers)
   std::vector<hipEvent_t> ev_grp;   // fit_overlapped: a group's values are in (one per group)
   std::vector<hipEvent_t> ev_gn;    // fit_overlapped: a group's gains are done
@@ -340,7 +331,7 @@ GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
 // distances of an uncached output through a separate pass)
 void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const GainsOut& gi, const double* v,
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
-                           int64_t ldb, double* send, double* hsum, bool force_d2 = false);
+                           int64_t ldb, double* send, double* hsum);
 
 // --------------------------------------------------------------------------- Gram stage
 struct GramOut {
@@ -404,28 +395,12 @@ struct SplitPipe {
     HIPCHECK(hipEventRecord(c->ev_sp, c->stream));
     for (hipStream_t st : {c->s_w, c->s_g, c->s_g2}) HIPCHECK(hipStreamWaitEvent(st, c->ev_sp, 0));
   }
-  bool head = false;   // job 0's whitening and short chain on head_st (null: the caller's stream)
-  hipStream_t head_st = nullptr;
   // the short chains on the Gram CUs' second stream (gpar_ctx::post_gram; the round overlap's
   // whitening CUs also run the other group's dense tails and gains)
   bool post_gram = false;
   int dg_rows_w = 0;   // percent more rows per DG split on the whitening CUs (stage_gram)
   void push(const StageJob& j) {
-    if (k == 0 && head) {
-      // the first whitening and its short chain on head_st: the caller's unmasked stream (the whole
-      // chip: nothing runs on the Gram CUs before the first Gram; the whitening side continues
-      // after them) or the Gram stream (the Gram CUs whiten the first output while the whitening
-      // CUs run the other outputs' gains)
-      const hipStream_t hs = head_st ? head_st : c->stream;
-      OnStream on_(c, hs);
-      if (c->mark_h[0]) HIPCHECK(hipEventRecord(c->mark_h[0], hs));
-      stage_whiten(c, j, buf[0]);
-      if (c->mark_h[1]) HIPCHECK(hipEventRecord(c->mark_h[1], hs));
-      stage_post(c, j, buf[0], false);
-      if (c->mark_h[2]) HIPCHECK(hipEventRecord(c->mark_h[2], hs));
-      HIPCHECK(hipEventRecord(c->ev_pc[0], hs));
-      if (!head_st) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[0], 0));
-    } else {
+    {
       OnStream on_(c, c->s_w);
       if (k >= 2) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gd[k & 1], 0));
       if (k == 0 && c->mark_h[0]) HIPCHECK(hipEventRecord(c->mark_h[0], c->s_w));
@@ -440,7 +415,7 @@ struct SplitPipe {
       }
     }
     if (has_pending) issue_gram();
-    if (post_gram && !(k == 0 && head)) {
+    if (post_gram) {
       // the short chain on the Gram CUs' second stream, behind the previous Gram's co-running
       // correction (issued just above), so the whitening side goes on with that Gram's DG share
       OnStream on_(c, c->s_g2);
@@ -464,7 +439,7 @@ struct SplitPipe {
       // stream orders it; on the Gram CUs' stream (post_gram) the share waits for it
       if (post_gram) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_pc[i & 1], 0));
       stage_gram(c, pending, buf[i & 1], false, false, "", c->s_g2, gcus, c->s_w, c->ev_pw,
-                 c->dg_share >= 0 ? c->dg_share : c->split_w, dg_rows_w);
+                 c->split_w, dg_rows_w);
       HIPCHECK(hipEventRecord(c->ev_gd[i & 1], c->s_g));
     }
     has_pending = false;
@@ -544,8 +519,10 @@ struct QuPre {
 // The part of one output's prediction that does not read the inference inputs, queued ahead on
 // the side stream (gpar_posterior_prepare): the merged grid's gains and the adjoint's fix-up
 // vectors h for given test times.  A slot is consumed by the matching gpar_posterior_predict.
+// A slot is matched by the posterior's unique id (never by its address, which a later
+// gpar_fit_posterior may reuse after gpar_posterior_destroy), the output index and the test times.
 struct PredPrep {
-  const void* post = nullptr;
+  uint64_t post_id = 0;
   int out = -1;
   const double* ts = nullptr;
   int64_t n_star = 0;

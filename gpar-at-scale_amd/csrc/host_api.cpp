@@ -34,11 +34,7 @@ int fail(gpar_ctx* c, int code, const char* what) {
 static void route_streams(gpar_ctx* c) {
   c->side = c->serialize ? c->main : c->own_side;
   hipStream_t* act[4] = {&c->s_w, &c->s_g, &c->s_g2, &c->s_d};
-  for (int i = 0; i < 4; ++i) {
-    const hipStream_t own = c->own_s[i < 3 ? i : 3 + c->tail_cus];
-    *act[i] = (c->serialize && own) ? c->main : own;
-  }
-  c->s_dp = (c->serialize && c->own_s[5]) ? c->main : c->own_s[5];
+  for (int i = 0; i < 4; ++i) *act[i] = (c->serialize && c->own_s[i]) ? c->main : c->own_s[i];
 }
 
 // CU split of the pipelined fit (gpar_ctx_set_cu_split): CU-masked streams for the whitening
@@ -63,11 +59,10 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
     c->split_mask_w = 0;
     c->split_w = 0;
     // own_s: s_w (whitening), s_g (Gram), s_g2 (its co-running correction), s_d (dense tails)
-    uint32_t mw[8] = {0}, mg[8] = {0}, ma[8];
+    uint32_t mw[8] = {0}, mg[8] = {0};
     for (int i = 0; i < 256; ++i) (i < 8 * w ? mw : mg)[i / 32] |= 1u << (i % 32);
-    for (int i = 0; i < 8; ++i) ma[i] = ~0u;
-    const uint32_t* masks[6] = {mw, mg, mg, mw, ma, mg};
-    for (int i = 0; i < 6; ++i)
+    const uint32_t* masks[4] = {mw, mg, mg, mw};
+    for (int i = 0; i < 4; ++i)
       if (hipExtStreamCreateWithCUMask(&c->own_s[i], 8, masks[i]) != hipSuccess) return GPAR_ERR_HIP;
     route_streams(c);
     if (!c->ev_sp &&
@@ -76,9 +71,7 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
          hipEventCreateWithFlags(&c->ev_sp, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_dn, hipEventDisableTiming) != hipSuccess ||
          hipEventCreateWithFlags(&c->ev_gr, hipEventDisableTiming) != hipSuccess ||
-         hipEventCreateWithFlags(&c->ev_wd, hipEventDisableTiming) != hipSuccess ||
-         hipEventCreateWithFlags(&c->ev_gr2, hipEventDisableTiming) != hipSuccess ||
-         hipEventCreateWithFlags(&c->ev_dp, hipEventDisableTiming) != hipSuccess))
+         hipEventCreateWithFlags(&c->ev_wd, hipEventDisableTiming) != hipSuccess))
       return GPAR_ERR_HIP;
     c->split_mask_w = w;
   }
@@ -87,10 +80,13 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
   return GPAR_OK;
 }
 
-static constexpr const char* kScheduleKnobs[] = {"overlap", "overlap_group", "predict_fused", "predict_d2", "qu_batch",
-                                                  "dense_early", "split_head", "predict_lanes",
-                                                  "serialize", "dg_share", "tail_cus", "post_gram",
-                                                  "compact_rec", "dg_rows_w"};
+// Every knob's non-default values are supported modes (round 5 deleted the A/B-only ones: the
+// split round head's variants, the dense prefix on a stream of its own, the DG share, the round
+// overlap's tail placement and the prediction's distance-pass whitening, each measured slower).
+static constexpr const char* kScheduleKnobs[] = {"overlap", "overlap_group", "predict_fused",
+                                                  "qu_batch", "dense_early", "predict_lanes",
+                                                  "serialize", "post_gram", "compact_rec",
+                                                  "dg_rows_w"};
 
 // gpar_ctx_set_schedule / gpar_ctx_get_schedule (GPAR_ERR_ARG: unknown knob or value).
 static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
@@ -100,15 +96,10 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
     c->overlap_group = v;
   }
   else if (k == "predict_fused") c->predict_fused = v != 0;
-  else if (k == "predict_d2") c->predict_d2 = v != 0;
   else if (k == "qu_batch") c->qu_batch = v != 0;
   else if (k == "dense_early") {
-    if (v < 0 || v > 2) return GPAR_ERR_ARG;
+    if (v < 0 || v > 1) return GPAR_ERR_ARG;
     c->dense_early = (int)v;
-  }
-  else if (k == "split_head") {
-    if (v < 0 || v > 4) return GPAR_ERR_ARG;
-    c->split_head = v;
   }
   else if (k == "dg_rows_w") {
     if ((v < -50 || v > 100) && v != kDgRowsAuto) return GPAR_ERR_ARG;
@@ -121,10 +112,7 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
     if (v < -1 || v > 1) return GPAR_ERR_ARG;
     c->post_gram = v;
   }
-  else if (k == "dg_share") {
-    if (v < -1 || v > 32) return GPAR_ERR_ARG;
-    c->dg_share = v;
-  } else if (k == "predict_lanes") {
+  else if (k == "predict_lanes") {
     if (v != 1 && v != 2) return GPAR_ERR_ARG;
     c->predict_lanes = v;
   } else if (k == "serialize") {
@@ -134,11 +122,6 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
     for (hipStream_t st : c->own_s)
       if (st) (void)hipStreamSynchronize(st);
     c->serialize = v != 0;
-    route_streams(c);
-  } else if (k == "tail_cus") {
-    if (v < 0 || v > 2) return GPAR_ERR_ARG;
-    if (c->s_d) (void)hipStreamSynchronize(c->s_d);
-    c->tail_cus = v;
     route_streams(c);
   } else {
     return GPAR_ERR_ARG;
@@ -150,12 +133,8 @@ static int get_schedule(const gpar_ctx* c, const std::string& k, int32_t* v) {
   if (k == "overlap") *v = c->overlap;
   else if (k == "overlap_group") *v = c->overlap_group;
   else if (k == "predict_fused") *v = c->predict_fused;
-  else if (k == "predict_d2") *v = c->predict_d2;
   else if (k == "qu_batch") *v = c->qu_batch;
   else if (k == "dense_early") *v = c->dense_early;
-  else if (k == "split_head") *v = c->split_head;
-  else if (k == "dg_share") *v = c->dg_share;
-  else if (k == "tail_cus") *v = c->tail_cus;
   else if (k == "post_gram") *v = c->post_gram;
   else if (k == "compact_rec") *v = c->compact_rec;
   else if (k == "dg_rows_w") *v = c->dg_rows_w;
@@ -227,7 +206,7 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
         (void)hipStreamDestroy(st);
       }
     for (hipEvent_t ev : {ctx->ev_gd[0], ctx->ev_gd[1], ctx->ev_sp, ctx->ev_dn,
-                          ctx->ev_dp, ctx->ev_gr, ctx->ev_gr2, ctx->ev_wd, ctx->ev_prep_ready[0],
+                          ctx->ev_gr, ctx->ev_wd, ctx->ev_prep_ready[0],
                           ctx->ev_prep_ready[1], ctx->ev_prep_free[0], ctx->ev_prep_free[1]})
       if (ev) (void)hipEventDestroy(ev);
     for (const auto* evs : {&ctx->ev_grp, &ctx->ev_gn})

@@ -12,7 +12,7 @@ namespace gpar {
 // the whitening then reads and overwrites in place (k_dist.hip).
 void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const GainsOut& gi, const double* v,
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
-                           int64_t ldb, double* send, double* hsum, bool force_d2) {
+                           int64_t ldb, double* send, double* hsum) {
   const double s_o = th.sv_o * th.sv_o;
   const double* rec = gi.rec;
   const double* g = gi.g;
@@ -22,7 +22,7 @@ void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const GainsOut& gi, const 
   if (d2 && v == p.v) {   // the fit's training inputs, distances cached (fit_impl)
     launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, d2, p.mp, p.m, p.mp, n, kChunk, nch,
                          1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum, p.d2_is_r, tc, th.l_t);
-  } else if (p.d > kFusedMaxD || gi.compact || (force_d2 && p.d > 0)) {
+  } else if (p.d > kFusedMaxD || gi.compact) {
     launch_dist2(c->stream, p.ok, v, ldv, n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, beta, ldb);
     launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, beta, ldb, p.m, p.mp, n, kChunk, nch,
                          1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum, false, tc, th.l_t);
@@ -100,8 +100,6 @@ void stage_gram(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_bet
   // dg_rows_w: the DG time splits that run on the whitening CUs take that many percent more rows
   // (the rest fewer), moving diagonal-block work between the two sides in finer steps than whole
   // rounds of items
-  // (the split count follows the CU split's own share, not dg_share, so that dg_share only moves
-  // items between the sides and stays bit-identical)
   if (st_w && w_items > 0 && dg_rows_w != 0 && plan.v3 && plan.sdg * c->split_w % 32 == 0) {
     const int sw = plan.sdg * c->split_w / 32;
     auto up = [](int64_t r) { return (r + kBKRows - 1) / kBKRows * kBKRows; };
@@ -177,13 +175,10 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   const bool shared = shares_grid(P);
   const bool pipe = fit_pipelined(c, P, fix_beta);
   const bool split_pipe = pipe && split_active(c, n, mpmax);
-  // a split round's head: 1 = the first output's gains on the whitening CUs and the others' beside
-  // them on the Gram CUs; 2 = every output's gains, then the first whitening and short chain,
-  // whole-chip; 3 = the first output's gains, whitening and short chain on the Gram CUs, the
-  // others' gains beside them on the whitening CUs; 0 = every output's gains whole-chip, the first
-  // whitening on the whitening CUs
-  const int head_mode = (split_pipe && shared && np > 1) ? c->split_head : 0;
-  const bool split_head = head_mode == 1 || head_mode == 3 || head_mode == 4;
+  // a split round's head: the first output's gains on the whitening CUs and the others' beside
+  // them on the Gram CUs (r04j; the variants tried in r04 -- every gains first, whole-chip or not;
+  // the first job on the Gram CUs; the late gains beside the Grams -- measured slower)
+  const bool split_head = split_pipe && shared && np > 1;
   const double* logs_src = nullptr;
   std::vector<GainsOut> gains(np);
   GainsPlan gplan;
@@ -263,34 +258,16 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   };
   if (split_pipe) {
     SplitPipe sp(c, n, mpmax);
-    sp.head = head_mode == 2 || head_mode == 3;
-    sp.head_st = head_mode == 3 ? c->s_g : nullptr;
     sp.post_gram = c->post_gram == 1;
     sp.dg_rows_w = c->dg_rows_w == kDgRowsAuto ? 10 : c->dg_rows_w;
     sp.start();
-    // head_mode 4: as 1, but only the next quarter of the outputs' gains (at most 15) beside the
-    // first whitening; the rest's on the Gram CUs' second stream once the first Gram (and its
-    // correction) is issued, well ahead of the whitening that first needs them
-    const int nhead = head_mode == 4 ? std::max(1, std::min(15, (np - 1) / 4)) : np - 1;
-    if (head_mode == 1 || head_mode == 4) {
+    if (split_head) {
       gplan.launch(c->s_w, 0, 1);
-      gplan.launch(c->s_g2, 1, nhead);
+      gplan.launch(c->s_g2, 1, np - 1);
       HIPCHECK(hipEventRecord(c->ev_gr, c->s_g2));
-    } else if (head_mode == 3) {   // the second whitening follows the others' gains on s_w
-      gplan.launch(c->s_g, 0, 1);
-      gplan.launch(c->s_w, 1, np - 1);
     }
-    const bool late = head_mode == 4 && nhead < np - 1;
-    if (late)
-      sp.on_gram = [&](const StageJob&, int64_t k) {
-        if (k != 0) return;
-        gplan.launch(c->s_g2, 1 + nhead, np - 1 - nhead);
-        HIPCHECK(hipEventRecord(c->ev_gr2, c->s_g2));
-      };
     for (int i = 0; i < np; ++i) {
-      if (i == 1 && (head_mode == 1 || head_mode == 4))
-        HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr, 0));
-      if (late && i == 1 + nhead) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr2, 0));
+      if (i == 1 && split_head) HIPCHECK(hipStreamWaitEvent(c->s_w, c->ev_gr, 0));
       sp.push(job(i, sp.buf[i & 1]));
     }
     sp.flush();
@@ -494,18 +471,15 @@ void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<T
   if (early) {
     // the Gram stream first follows everything queued on the context stream (host inputs' uploads,
     // the pseudo-input centres, the distance cache), then factors Kuu beside the round's gains
-    // (split_head 3: on the Gram CUs' second stream, the Gram stream whitening the first output)
-    // (dense_early 2: on a Gram-CU stream of its own, so the first Gram need not queue behind it)
-    const hipStream_t ds = c->dense_early == 2 ? c->s_dp : c->split_head == 3 ? c->s_g2 : c->s_g;
+    // (on a Gram-CU stream of its own, r04ae, the first Gram no longer queued behind it but shared
+    // the Gram CUs with it: 17.67 -> 17.70 s per job)
     HIPCHECK(hipEventRecord(c->ev_dn, c->stream));
-    HIPCHECK(hipStreamWaitEvent(ds, c->ev_dn, 0));
-    OnStream on_(c, ds);
+    HIPCHECK(hipStreamWaitEvent(c->s_g, c->ev_dn, 0));
+    OnStream on_(c, c->s_g);
     dn = run_dense_pre(c, P, th, mpmax, false);
-    if (c->dense_early == 2) HIPCHECK(hipEventRecord(c->ev_dp, ds));
   }
   GramOut go = run_gram_stage(c, P, th);
   if (gram_out) *gram_out = go;
-  if (early && c->dense_early == 2) HIPCHECK(hipStreamWaitEvent(c->stream, c->ev_dp, 0));
   if (!early) dn = run_dense_pre(c, P, th, go.ldg, false);
   run_dense_post(c, P, go, dn);
   const int64_t nch = P[0].nch;

@@ -2,6 +2,8 @@
 // fit + predict driver, and their C-ABI entries.
 #include "host.hpp"
 
+#include <atomic>
+
 namespace gpar {
 
 QuOut run_q_u(gpar_ctx* c, const DevProblem& p, const Theta& th,
@@ -373,7 +375,7 @@ void predict_impl(gpar_ctx* c, const DevProblem& P, const Theta& th, int mem,
     {   // algorithmic HBM bytes: merged inputs V* (d) read, gains records + fix-up rows (20), the
         // m whitened Cf*u columns written, per merged row
       Timed tm_(c, "pred_whiten", 8.0 * (double)nt * ((double)d + (double)m + 20.0));
-      whiten_kfu_any(c, P, g, vm, d, nt, nch, th, X, ldx, send, nullptr, c->predict_d2);
+      whiten_kfu_any(c, P, g, vm, d, nt, nch, th, X, ldx, send, nullptr);
       launch_whiten_vec(c->stream, P.sdim, g.rec, 0, ym, 0, nt, kChunk, nch, 1, X + mp, 0, send, 0,
                         mc, mp, ldx);
     }
@@ -803,6 +805,9 @@ int32_t gpar_lgssm_posterior_rand(gpar_ctx* ctx, int64_t n, const double* t, con
 // eeg.jl:249,274, one owner per output across ranks -- runs only the V*-dependent prediction per
 // output (gpar_posterior_predict).
 struct gpar_posterior {
+  // unique over the process's lifetime: gpar_posterior_prepare's slots match on it, so a slot left
+  // by a destroyed posterior can never be taken for a new one at the same address
+  uint64_t id = 0;
   int device = 0;
   int mem = GPAR_MEM_DEVICE;   // memory space of the problems (and of every predict call's I/O)
   struct Out {
@@ -860,6 +865,8 @@ int32_t gpar_fit_posterior(gpar_ctx* ctx, const gpar_problem* probs, int32_t npr
   FitKeep keep;
   fit_impl(ctx, P, log_theta0, o, theta_out, nlml_out, evals_out, &keep);
   post.reset(new gpar_posterior());
+  static std::atomic<uint64_t> next_id{1};
+  post->id = next_id.fetch_add(1);
   post->device = ctx->device;
   post->mem = probs[0].mem;
   post->outs.resize(nprob);
@@ -971,7 +978,7 @@ int32_t gpar_posterior_prepare(gpar_ctx* ctx, const gpar_posterior* post, int32_
     check_launch("prepare: gains");
     HIPCHECK(hipEventRecord(ctx->ev_prep_ready[slot], ctx->side));
   }
-  s.post = post;
+  s.post_id = post->id;
   s.out = i;
   s.ts = t_star;
   s.n_star = n_star;
@@ -997,7 +1004,7 @@ int32_t gpar_posterior_predict(gpar_ctx* ctx, const gpar_posterior* post, int32_
   // a slot gpar_posterior_prepare filled for this output and these test times
   const PredPrep* prep = nullptr;
   for (PredPrep& s : ctx->prep)
-    if (s.valid && s.post == post && s.out == i && s.ts == t_star && s.n_star == n_star) {
+    if (s.valid && s.post_id == post->id && s.out == i && s.ts == t_star && s.n_star == n_star) {
       s.valid = false;
       prep = &s;
     }

@@ -273,9 +273,10 @@ class Context:
         self.check(load().gpar_ctx_set_predict_fused(self.h, 1 if on else 0))
 
     def set_schedule(self, knob, value):
-        """A schedule knob (gpar_ctx_set_schedule: pipeline, overlap, qu_batch, dense_early,
-        split_head, predict_lanes, serialize, predict_fused); results are bit-identical with any
-        setting except predict_fused."""
+        """A schedule knob (gpar_ctx_set_schedule: overlap, overlap_group, qu_batch, dense_early,
+        post_gram, compact_rec, predict_lanes, serialize, predict_fused, dg_rows_w; the header
+        lists their values); results are bit-identical with any setting except the plan knobs
+        predict_fused and dg_rows_w (last bits)."""
         self.check(load().gpar_ctx_set_schedule(self.h, knob.encode(), int(value)))
 
     def schedule(self, knob):

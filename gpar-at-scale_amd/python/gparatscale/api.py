@@ -393,7 +393,13 @@ def get_gpar_scaled_predictions_batch(Y, pseudo_input_locations, time_loc, infer
     (ldv = P; the library uploads it once) and one for the inference inputs F (N* x P; output i
     reads its first i - 1 columns, given or -- chained -- F's column 1 then predicted means).
     pseudo_input_locations[i - 2]: output i's D x M pseudo-inputs.  Returns (FitResult, means,
-    stds) for outputs 2..P."""
+    stds) for outputs 2..P.
+
+    Defaults differ from the Julia method on purpose, so that a call is reproducible: here
+    mode="analytic" (Julia: mode=:mc, the reference's estimator), seed=0 (Julia: rand(UInt64)), a
+    fixed log_theta0 (Julia: parse_initial_gpar_params, U(0,1) draws for missing values, util.jl:
+    128-134) and no time limit (Julia: optimization_time_limit=1000.0, dtc.jl:21).  Pass
+    mode="mc", a seed, log_theta0 and time_limit to reproduce a Julia call."""
     Y = np.ascontiguousarray(np.asarray(Y, dtype=np.float64))
     F = np.ascontiguousarray(np.array(F, dtype=np.float64))   # a copy: the chain writes into it
     n, P = Y.shape
@@ -453,6 +459,7 @@ class Posterior:
     def __init__(self, handle, fit, problems, keep, device):
         self.h, self.fit, self.device = handle, fit, device
         self._problems, self._keep = list(problems), keep
+        self._prepared = {}   # output -> the t_star tensor a pending prepare reads
 
     @property
     def theta(self):
@@ -479,6 +486,8 @@ class Posterior:
                 ctx.check(lib.gpar_posterior_predict(ctx.h, self.h, int(i), ns, tsp, vsp, ldvs, md,
                                                      int(samples), int(seed), mean.data_ptr(),
                                                      std.data_ptr()))
+            # the prepared slot is consumed (stream-ordered before any later use of the memory)
+            self._prepared.pop(int(i), None)
             return mean, std
         vsp, ldvs, ns, ds = _host_points(V_star, keep)
         if ds != p.d or ns != len(np.asarray(t_star)):
@@ -491,16 +500,24 @@ class Posterior:
     def prepare(self, i, t_star):
         """Queue output i's inference-input-independent prediction work for device test times
         t_star (gpar_posterior_prepare) on the context's side stream; the next predict(i, t_star,
-        ...) with the same tensor uses it.  Device problems only."""
+        ...) with the same tensor uses it.  Device problems only.  The queued kernels read t_star
+        asynchronously, so it must be contiguous (no temporary copy) and must not be freed or
+        written until that predict has run: the Posterior holds a reference to it until then."""
         if not 0 <= int(i) < len(self._problems):
             raise _arg_error(f"output index {i} out of range (0..{len(self._problems) - 1})")
         if self._problems[i].mem != _lib.GPAR_MEM_DEVICE:
             raise _arg_error("prepare: device-memory posteriors only")
-        keep = _Keep()
+        if not t_star.is_contiguous():
+            raise _arg_error("prepare: t_star must be a contiguous device tensor (the prepared "
+                             "kernels read it after this call returns)")
         ctx, lib = context(self.device), _lib.load()
-        tsp = _dev_vec(t_star, keep)
         with _after_torch(ctx):
-            ctx.check(lib.gpar_posterior_prepare(ctx.h, self.h, int(i), t_star.numel(), tsp))
+            ctx.check(lib.gpar_posterior_prepare(ctx.h, self.h, int(i), t_star.numel(),
+                                                 t_star.data_ptr()))
+        # alive until the matching predict (two slots per context: at most two pending)
+        self._prepared[int(i)] = t_star
+        while len(self._prepared) > 2:
+            self._prepared.pop(next(iter(self._prepared)))
 
     def close(self):
         if getattr(self, "h", None):
@@ -517,9 +534,16 @@ class Posterior:
 def fit_posterior(problems, log_theta0, max_evals=0, max_iterations=1000, g_tol=1e-8,
                   time_limit=0.0, device=0, keep=None):
     """The fit and q(u) of get_gpar_scaled_predictions for a batch of outputs, kept on the device
-    for later predictions (gpar_fit_posterior) -> Posterior."""
+    for later predictions (gpar_fit_posterior) -> Posterior.
+
+    Device problems' buffers are borrowed by the posterior until it is closed, so their `keep`
+    (the second value make_problem returns: the contiguous copies and columns the problems point
+    at) is required and held by the Posterior.  Host problems are copied to the device."""
     ctx, lib = context(device), _lib.load()
     P = len(problems)
+    if keep is None and any(p.mem == _lib.GPAR_MEM_DEVICE for p in problems):
+        raise _arg_error("fit_posterior: device problems need their keep (make_problem's second "
+                         "value): the posterior reads those buffers until it is closed")
     arr = (GparProblem * P)(*problems)
     x0 = np.ascontiguousarray(np.asarray(log_theta0, dtype=np.float64).reshape(P, 5))
     opts = GparFitOptions(int(max_evals), int(max_iterations), float(g_tol), float(time_limit))

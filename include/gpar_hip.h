@@ -152,21 +152,10 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *                   of >= 4 outputs
  *   "qu_batch"      1: gpar_fit_predict runs q(u) batched over the outputs (default 1)
  *   "dense_early"   1: the G-independent half of the dense tail ahead of a split round's Grams, on
- *                   the Gram stream (default); 2: the same on a Gram-CU stream of its own, beside
- *                   the first Gram; 0: after the Grams
- *   "split_head"    a split round's head: 1 = the first output's gains on the whitening CUs, the
- *                   others' beside them on the Gram CUs (default); 2 = every output's gains, then the
- *                   first whitening, whole-chip; 3 = the first output's gains, whitening and
- *                   short chain on the Gram CUs, the others' gains on the whitening CUs; 4 = as 1
- *                   with only the next quarter of the outputs' gains (at most 15) beside the first
- *                   whitening, the rest's after the first Gram; 0 = every output's gains ahead
- *   "dg_share"      32nds of a split Gram's diagonal-block work items run on the whitening CUs
- *                   (-1, the default: the CU split's own share, cus_per_xcd / 32)
+ *                   the Gram stream (default); 0: after the Grams
  *   "post_gram"     1: a split job's short chain (carry, vec_fix) on the Gram CUs behind the previous
  *                   Gram's correction instead of on the whitening CUs after its whitening; 0: never;
  *                   -1 (default): in the round-overlapping fit only
- *   "tail_cus"      the round overlap's dense tails and gains: 0 = on the whitening CUs (default),
- *                   1 = on the whole chip, 2 = on the Gram CUs
  *   "compact_rec"   1: the CU-split fit's gains write compact records {K_k, rs_k} and the cached
  *                   whitening recomputes each step's transition A_k from t (the same bits; an
  *                   output whose distances are not cached then whitens through the distance pass
@@ -177,14 +166,14 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *                   with the same plans, CU shares of work items and workspaces: the order-free
  *                   reference the concurrent schedule equals bit for bit (default 0)
  *   "predict_fused" as gpar_ctx_set_predict_fused (changes the summation order: last bits)
- *   "predict_d2"    1: the prediction's merged-grid whitening as a distance pass then the cached
- *                   whitening kernel in place, instead of the fused kernel (0, default; last bits)
  *   "dg_rows_w"     percent more rows per diagonal-block time split on the whitening CUs of a
  *                   split Gram, fewer on the Gram CUs; -100 (default) = auto: 10 in the
  *                   round-by-round fit, 0 in the round overlap (changes G's summation grouping:
  *                   last bits, like predict_fused)
  * The environment variable GPAR_<KNOB> (upper case) sets a knob at context creation.
- * GPAR_ERR_ARG for an unknown knob or value. */
+ * GPAR_ERR_ARG for an unknown knob or value.  Every non-default value is a supported schedule
+ * mode; the A/B-only knobs of round 4 (split_head, dg_share, tail_cus, predict_d2, dense_early 2)
+ * were measured slower at both the north job and the 8-output shard and deleted. */
 int32_t gpar_ctx_set_schedule(gpar_ctx* ctx, const char* knob, int32_t value);
 int32_t gpar_ctx_get_schedule(const gpar_ctx* ctx, const char* knob, int32_t* value);
 /* The CU split in effect (0 when off or unsupported). */
@@ -350,7 +339,10 @@ int32_t gpar_posterior_predict(gpar_ctx* ctx, const gpar_posterior* post, int32_
  * posterior, output, t_star pointer and n_star uses it (bit-identical results) instead of
  * computing it in line; a chained sweep prepares output p + 1 before predicting output p, so the
  * two overlap.  Two slots per context: a third prepare reuses the oldest (its predict falls back to
- * the in-line path).  Device-memory posteriors only. */
+ * the in-line path).  Device-memory posteriors only.  The kernels queued here read t_star
+ * asynchronously: t_star must stay allocated and unmodified until the matching
+ * gpar_posterior_predict has run (or the context is synchronised).  Slots are matched on the
+ * posterior's identity, not its address: a slot left by a destroyed posterior is never used. */
 int32_t gpar_posterior_prepare(gpar_ctx* ctx, const gpar_posterior* post, int32_t i,
                                int64_t n_star, const double* t_star);
 int32_t gpar_posterior_destroy(gpar_posterior* post);

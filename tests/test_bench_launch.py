@@ -83,3 +83,27 @@ def test_visible_gpu_count_reads_kfd_topology(tmp_path):
     assert bench.visible_gpu_count(str(tmp_path), env={"HIP_VISIBLE_DEVICES": "0,1"}) == 2
     assert bench.visible_gpu_count(str(tmp_path), env={"ROCR_VISIBLE_DEVICES": ""}) == 0
     assert bench.visible_gpu_count(str(tmp_path / "absent"), env={}) == 0
+
+
+def test_launcher_fails_fast_when_a_rank_dies():
+    """rank 1 exits with status 3 before its gather; rank 0 is then waiting in
+    the gloo all_gather for it.  The launcher must notice, terminate rank 0 and return 3 well before
+    the process group's timeout (set high here so only the launcher can end the wait)."""
+    import time
+    env_timeout = dict(GPAR_PG_TIMEOUT_S="600")
+    t0 = time.monotonic()
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_timeout)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--stub",
+                        "--stub-fail", "1:3"], env=env, capture_output=True, text=True, timeout=90)
+    dt = time.monotonic() - t0
+    assert r.returncode == 3, (r.returncode, r.stderr[-2000:])
+    assert dt < 30, dt
+    assert "rank 1 exited with status 3" in r.stderr
+    assert not r.stdout.strip()   # no JSON line from a failed job
+
+
+def test_launcher_fails_fast_when_rank0_dies():
+    r = _bench("--gpus", "3", "--stub", "--stub-fail", "0:5", timeout=90)
+    assert r.returncode == 5, r.stderr[-2000:]
+    assert "rank 0 exited with status 5" in r.stderr

@@ -59,8 +59,8 @@ def main():
     def ev(th):
         try:
             return G.dtc_objective_batch(prs, th)
-        except G.GparError:   # timing ablations (GPAR_LIB_PATH) compute garbage on purpose
-            if not os.environ.get("GPAR_LIB_PATH"):
+        except G.GparError:   # timing ablations (GPAR_HIP_LIB) compute garbage on purpose
+            if not os.environ.get("GPAR_HIP_LIB"):
                 raise
             return [float("nan")]
 
