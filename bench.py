@@ -109,7 +109,8 @@ def main():
                          "get_gpar_scaled_predictions makes them (GPAR_scaled_examples.jl:132-175)")
     ap.add_argument("--shard", default=None,
                     help="R/W: run exactly rank R's outputs of the W-way output assignment "
-                         "(gparatscale.shard.assign_outputs) on this one GPU, the code path of one "
+                         "(gparatscale.shard.assign_outputs; assign_chained with --inference "
+                         "chained) on this one GPU, the code path of one "
                          "rank of a W-GPU job, to predict the per-rank step time")
     ap.add_argument("--dist-cache", default="keep", choices=["keep", "release"],
                     help="'keep' (the bench default): the fit's distance-cache buffers stay allocated "
@@ -216,7 +217,11 @@ def main():
         ts_d.copy_(torch.from_numpy(ts_h)); Fs_d.copy_(torch.from_numpy(Fs_h))
     S.broadcast_inputs((t_d, Y_d, ts_d, Fs_d))   # RCCL broadcast of the shared inputs over xGMI
     temporal = cfg.get("temporal", False)
-    shards = S.assign_outputs(P, world) if not temporal else \
+    # chained inference inputs: contiguous output blocks, early ranks smaller, so the sweep starts
+    # on the first rank while the later ones still fit (shard.assign_chained); given inputs: LPT
+    chained_job = args.inference == "chained" and not temporal
+    assign = S.assign_chained if chained_job else S.assign_outputs
+    shards = assign(P, world) if not temporal else \
         [[p for p in range(1, P + 1) if (p - 1) % world == r] for r in range(world)]
     mine = shards[rank]
     shard_of = None
@@ -225,7 +230,7 @@ def main():
             sys.exit("--shard R/W: one process, the GPAR configs")
         r_, w_ = (int(x) for x in args.shard.split("/"))
         shard_of = (r_, w_)
-        shards = S.assign_outputs(P, w_)
+        shards = assign(P, w_)
         mine = shards[r_]
     gpar_out = [p for p in mine if p >= 2] if not temporal else []
     Yh = Y_d.cpu().numpy() if (gpar_out or args.inference == "chained") else None
@@ -373,9 +378,11 @@ def main():
                     chain_d,
                     prepare_fn=lambda p: pick(p)[0].prepare(pick(p)[1], ts_d))
             else:
+                # the staggered sweep: earlier blocks' means arrive point to point, this rank's
+                # block runs as soon as its own fits and those means are in (shard.py)
                 idx = {p: i for i, p in enumerate(gpar_out)}
-                S.chained_predictions(
-                    gpar_all, owners,
+                S.chained_sweep_blocks(
+                    shards,
                     lambda p, c: post.predict(idx[p], ts_d, c[:, : p - 1], mode=args.predict,
                                               samples=100, seed=p),
                     chain_d, prepare_fn=lambda p: post.prepare(idx[p], ts_d))
@@ -778,13 +785,29 @@ def main():
                 "note": "wall time of the ordered chained prediction sweep inside each timed step "
                         "(gpar_posterior_predict per output: q(u) ran with the fits)"}
             if shard_of:
-                # the projected W-GPU chained step: this rank's fits (the slowest rank's: every rank
-                # fits the same number of equal-cost outputs) + the serial sweep + one 8 N* byte
-                # broadcast per output over xGMI (assumed 50 GB/s effective + 40 us latency)
-                bc = len(gpar_all) * (8.0 * ns_eff / 50e9 + 40e-6) * 1e3
-                out["chained_sweep"]["projected_step_ms"] = (el - sw) + sw + bc
-                out["chained_sweep"]["broadcast_ms_assumed"] = bc
-                out["chained_sweep"]["fit_ms_per_step"] = el - sw
+                # the projected W-GPU chained step of the staggered schedule (shard.assign_chained):
+                # this rank's measured fits set the scale of the affine fit-time model of shard.py
+                # for every block size, the measured sweep gives the time per chained prediction,
+                # and each block's means reach the next owner over xGMI at ASSUMED figures (50 GB/s
+                # effective + 40 us; this pool never runs RCCL), plus the final broadcast of the
+                # whole chain from the last owner (assumed likewise)
+                fit_meas = el - sw
+                n_r = len(gpar_out)
+                model = lambda n: S.FIT_FIXED_MS + S.FIT_MS_PER_OUTPUT * n   # noqa: E731
+                fit_ms = lambda n: fit_meas * model(n) / model(n_r)        # noqa: E731
+                per = sw / len(gpar_all)
+                xfer = lambda k: 8.0 * ns_eff * k / (S.XFER_GBS_ASSUMED * 1e9) * 1e3 + \
+                    S.XFER_LAT_MS_ASSUMED                                   # noqa: E731
+                blocks = [len([p for p in o if p >= 2]) for o in shards]
+                mk, rows = S.chained_schedule(blocks, fit_ms, per, xfer)
+                final = 8.0 * ns_eff * P / (S.XFER_GBS_ASSUMED * 1e9) * 1e3 + S.XFER_LAT_MS_ASSUMED
+                out["chained_sweep"].update(
+                    projected_step_ms=mk + final, fit_ms_per_step=fit_meas, block_sizes=blocks,
+                    sweep_ms_per_output=per, final_broadcast_ms_assumed=final,
+                    schedule_ms=[[round(v, 1) for v in r] for r in rows],
+                    projection_note="staggered blocks (fit end, sweep start, sweep end per rank): "
+                                    "fits scaled from this rank's measured block by shard.py's "
+                                    "affine model, transfers at assumed xGMI figures")
         if self_check:
             out["self_check"] = self_check
         if probe:

@@ -110,3 +110,136 @@ def chained_predictions(outputs, owners: dict, predict_fn, chain, prepare_fn=Non
             dist.broadcast(col, owner)
         chain[:, p - 1].copy_(col)
     return mine
+
+
+# ---------------------------------------------------------------------------- chained, staggered
+# With chained inference inputs the fits are independent but the predictions are serial in output
+# order.  chained_predictions above runs the sweep after every rank's fits: each prediction then
+# runs on one GPU while the others wait (63 x 14.4 ms at north, the rank's fits 2.3 s before it).
+# assign_chained instead gives every rank a contiguous block of outputs, early blocks smaller, so
+# that the owner of the first block finishes its fits first and starts the sweep while the later
+# ranks are still fitting; each later block is sized so its fits end about when the sweep reaches
+# it.  chained_sweep_blocks then passes the means along block by block (point to point).
+# Defaults: one rank's batched fit + posterior at the north config, fit_ms(n) ~ FIT_FIXED_MS +
+# FIT_MS_PER_OUTPUT n (bench --shard; tools/chained_projection.py measures them), one chained
+# prediction SWEEP_MS_PER_OUTPUT (profiles/bench_r04s_shard1of8_chained_prepare.json).
+FIT_FIXED_MS = 150.0
+FIT_MS_PER_OUTPUT = 270.0
+SWEEP_MS_PER_OUTPUT = 14.4
+# a block of k means (8 N* bytes each) to the next owner: ASSUMED xGMI figures (never measured on
+# this pool, whose boxes have one GPU): 50 GB/s effective and 40 us per transfer
+XFER_GBS_ASSUMED = 50.0
+XFER_LAT_MS_ASSUMED = 0.04
+
+
+def chained_schedule(blocks, fit_ms, sweep_ms, xfer_ms):
+    """Timeline of a staggered chained job: blocks[r] = number of GPAR outputs of rank r (in output
+    order), fit_ms(n) its fit time, sweep_ms one prediction, xfer_ms(k) the transfer of k means to
+    the next owner.  Returns (makespan_ms, [(fit_end, sweep_start, sweep_end)] per rank)."""
+    t_prev, done, rows = None, 0, []
+    for n in blocks:
+        f = fit_ms(n) if n else 0.0
+        start = f if t_prev is None else max(f, t_prev + (xfer_ms(done) if done else 0.0))
+        end = start + sweep_ms * n
+        rows.append((f, start, end))
+        if n:
+            t_prev, done = end, done + n
+    return max(r[2] for r in rows), rows
+
+
+def assign_chained(P: int, world: int, fit_ms=None, sweep_ms: float = SWEEP_MS_PER_OUTPUT,
+                   xfer_ms=None) -> list[list[int]]:
+    """Contiguous output blocks for a chained job over `world` ranks: rank r owns GPAR outputs
+    a_r..b_r with a_{r+1} = b_r + 1 (output 1, the temporal-only chain whose inference inputs are
+    given, goes to rank 0).  The block sizes minimise chained_schedule's makespan (dynamic program
+    over ranks; every rank gets at least one output when P - 1 >= world).  Deterministic."""
+    fit_ms = fit_ms or (lambda n: FIT_FIXED_MS + FIT_MS_PER_OUTPUT * n)
+    xfer_ms = xfer_ms or (lambda k: 0.0)
+    G = P - 1
+    lo = 1 if G >= world else 0
+    INF = float("inf")
+    # best[r][k]: earliest end of the sweep through ranks 0..r owning the first k GPAR outputs
+    best = [[INF] * (G + 1) for _ in range(world)]
+    arg = [[0] * (G + 1) for _ in range(world)]
+    for k in range(lo, G + 1):
+        best[0][k] = (fit_ms(k) if k else 0.0) + sweep_ms * k
+        arg[0][k] = k
+    for r in range(1, world):
+        for k in range(G + 1):
+            for n in range(lo, k + 1):
+                prev = best[r - 1][k - n]
+                if prev == INF:
+                    continue
+                f = fit_ms(n) if n else 0.0
+                end = max(f, prev + (xfer_ms(k - n) if k - n else 0.0)) + sweep_ms * n if n else prev
+                if end < best[r][k] - 1e-9:
+                    best[r][k], arg[r][k] = end, n
+    sizes, k = [], G
+    for r in range(world - 1, -1, -1):
+        n = arg[r][k]
+        sizes.append(n)
+        k -= n
+    sizes.reverse()
+    owned, p = [], 2
+    for r, n in enumerate(sizes):
+        owned.append(([1] if r == 0 else []) + list(range(p, p + n)))
+        p += n
+    return owned
+
+
+def chained_sweep_blocks(shards, predict_fn, chain, prepare_fn=None, gather=True):
+    """The chained sweep over contiguous blocks (assign_chained): each rank receives the earlier
+    blocks' predicted means point to point from their owners, predicts its own block in order
+    (predict_fn(p, chain) -> (mean, std), its next output prepared ahead with prepare_fn), and
+    sends its block's means to every later rank.  No rank waits in a collective for a rank that is
+    still fitting.  gather: at the end the last rank broadcasts the whole chain, so every rank
+    holds every mean (as chained_predictions leaves it).  `chain` as chained_predictions'.
+    Returns {p: (mean, std)} for this rank's outputs."""
+    import torch
+    import torch.distributed as dist
+    on = dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+    rank = dist.get_rank() if on else 0
+    world = dist.get_world_size() if on else 1
+    gp = [[p for p in s if p >= 2] for s in shards]
+    for r in range(1, world):
+        prev = [p for s in gp[:r] for p in s]
+        if gp[r] and prev and min(gp[r]) < max(prev):
+            raise ValueError("chained_sweep_blocks: blocks must be contiguous in output order")
+    # gloo moves host tensors point to point; RCCL moves device tensors
+    host = on and dist.get_backend() == "gloo"
+
+    def cols(r):
+        return [p - 1 for p in gp[r]]
+
+    own = gp[rank]
+    if prepare_fn is not None and own:
+        prepare_fn(own[0])   # beside the wait for the earlier blocks
+    for r in range(rank):     # the earlier blocks, in order
+        if not gp[r]:
+            continue
+        buf = torch.empty((chain.shape[0], len(gp[r])), dtype=chain.dtype,
+                          device="cpu" if host else chain.device)
+        dist.recv(buf, src=r)
+        chain[:, cols(r)] = buf.to(chain.device)
+    mine = {}
+    for i, p in enumerate(own):
+        if prepare_fn is not None and i + 1 < len(own):
+            prepare_fn(own[i + 1])
+        mean, std = predict_fn(p, chain)
+        mine[p] = (mean, std)
+        chain[:, p - 1] = torch.as_tensor(mean, dtype=chain.dtype).to(chain.device)
+    works = []
+    if on and own:
+        blk = chain[:, cols(rank)].contiguous()
+        blk = blk.cpu() if host else blk
+        for r in range(rank + 1, world):
+            works.append(dist.isend(blk, dst=r))
+    for w in works:
+        w.wait()
+    if on and gather:
+        last = max((r for r in range(world) if gp[r]), default=0)
+        full = chain.contiguous()
+        full = full.cpu() if host else full
+        dist.broadcast(full, last)
+        chain.copy_(full.to(chain.device))
+    return mine

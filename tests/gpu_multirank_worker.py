@@ -3,8 +3,15 @@ WORLD_SIZE / MASTER_ADDR / MASTER_PORT in its environment; every rank uses cuda:
 
 The multi-GPU path of bench.py with the real GPU library: rank 0 builds the GPAR data and
 broadcasts it (shard.broadcast_inputs, over gloo here, RCCL in bench), each rank fits the GPAR
-outputs assign_outputs() gives it with one batched gpar_fit on device inputs, and
-shard.gather_thetas all-reduces the P x 5 rows.  Rank 0 writes the gathered rows to argv[1].
+outputs assign_outputs() gives it on device inputs, and shard.gather_thetas all-reduces the
+P x 5 rows.  Rank 0 writes the gathered rows to argv[1].
+
+argv[2] == "chained": the chained path of bench.py --inference chained across ranks
+(GPAR_scaled_examples.jl:172, eeg.jl:249,274): each rank's fits keep q(u) on the device
+(gpar_fit_posterior), then shard.chained_predictions walks outputs 2..P in order, the owner of
+output p predicting it (Posterior.predict, its next output prepared ahead with Posterior.prepare)
+from the chain's current columns and broadcasting the mean; every rank ends with every predicted
+mean in its chain.  Rank 0 also writes the means (from its chain) and the all-reduced stds.
 """
 import json
 import os
@@ -18,10 +25,11 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 N, P, M, EV = 3000, 6, 32, 20
+NS = 700          # test times of the chained sweep
 X0 = [0.0, 0.0, 0.0, 0.0, -2.0]
 
 
-def main(out):
+def main(out, mode="given"):
     from gparatscale import api as G
     from gparatscale import data as Dd
     from gparatscale import shard as S
@@ -30,34 +38,64 @@ def main(out):
     try:
         t_h = torch.zeros(N, dtype=torch.float64)
         Y_h = torch.zeros((N, P), dtype=torch.float64)
+        ts_h = torch.zeros(NS, dtype=torch.float64)
+        F_h = torch.zeros((NS, P), dtype=torch.float64)
         if rank == 0:
-            ds = Dd.gpar_dataset(N, P, seed=3, observation_noise=0.5)
+            ds = Dd.gpar_dataset(N, P, seed=3, observation_noise=0.5, n_star=NS)
             t_h.copy_(torch.from_numpy(ds["t"]))
             Y_h.copy_(torch.from_numpy(ds["Y"]))
-        S.broadcast_inputs((t_h, Y_h))
+            ts_h.copy_(torch.from_numpy(ds["t_star"]))
+            F_h.copy_(torch.from_numpy(ds["F_star"]))
+        S.broadcast_inputs((t_h, Y_h, ts_h, F_h))
         dev = torch.device("cuda", 0)
-        t_d, Y_d = t_h.to(dev), Y_h.to(dev)
-        mine = [p for p in S.assign_outputs(P, world)[rank] if p >= 2]
+        t_d, Y_d, ts_d = t_h.to(dev), Y_h.to(dev), ts_h.to(dev)
+        shards = S.assign_outputs(P, world)
+        mine = [p for p in shards[rank] if p >= 2]
         res = {}
-        if mine:
-            keep, problems = [], []
-            for p in mine:
-                Z = torch.from_numpy(Dd.pseudo_inputs(Y_h.numpy()[:, : p - 1], M, seed=p)).to(dev)
-                pr, k = G.make_problem(Y_d[:, : p - 1], Z, t_d, Y_d[:, p - 1].contiguous())
-                problems.append(pr)
-                keep.append(k)
+        keep, problems = [], []
+        for p in mine:
+            Z = torch.from_numpy(Dd.pseudo_inputs(Y_h.numpy()[:, : p - 1], M, seed=p)).to(dev)
+            pr, k = G.make_problem(Y_d[:, : p - 1], Z, t_d, Y_d[:, p - 1].contiguous(),
+                                   qu_kuu_noise=mode == "chained")
+            problems.append(pr)
+            keep.append((k, Z))
+        result = {"world": world, "shards": shards}
+        if mode == "chained":
+            post = None
+            if mine:
+                post = G.fit_posterior(problems, np.tile(X0, (len(mine), 1)), max_evals=EV,
+                                       g_tol=-1.0, device=0, keep=keep)
+                res = {p: post.theta[i] for i, p in enumerate(mine)}
+            idx = {p: i for i, p in enumerate(mine)}
+            chain = torch.zeros((NS, P), dtype=torch.float64, device=dev)
+            chain[:, 0] = F_h[:, 0].to(dev)     # output 1's true values (GPAR_scaled_examples.jl:172)
+            outs = list(range(2, P + 1))
+            got = S.chained_predictions(
+                outs, S.owners_of(shards),
+                lambda p, c: post.predict(idx[p], ts_d, c[:, : p - 1]), chain,
+                prepare_fn=lambda p: post.prepare(idx[p], ts_d))
+            torch.cuda.synchronize()
+            stds = torch.zeros((NS, P), dtype=torch.float64)
+            for p, (_, s) in got.items():
+                stds[:, p - 1] = s.cpu()
+            dist.all_reduce(stds)    # each output owned by one rank: a sum is a gather
+            result["means"] = chain.cpu().numpy()[:, 1:].T.tolist()
+            result["stds"] = stds.numpy()[:, 1:].T.tolist()
+            if post is not None:
+                post.close()
+        elif mine:
             fr = G.fit_batch(problems, np.tile(X0, (len(mine), 1)), max_evals=EV, g_tol=-1.0,
                              device=0)
             torch.cuda.synchronize()
             res = {p: fr.theta[i] for i, p in enumerate(mine)}
         th = S.gather_thetas(res, P)
+        result["theta"] = th.tolist()
         if rank == 0:
             with open(out, "w") as f:
-                json.dump({"world": world, "shards": S.assign_outputs(P, world),
-                           "theta": th.tolist()}, f)
+                json.dump(result, f)
     finally:
         dist.destroy_process_group()
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], sys.argv[2] if len(sys.argv) > 2 else "given")

@@ -7,6 +7,11 @@ independent of the batch it runs in, so the gathered hyperparameters must equal,
 one single-process batched fit of all outputs (GPAR_scaled_examples.jl:132-175 fits every output
 on its own).  The ranks are child processes started before they touch the GPU; the test waits
 for them under a timeout.
+
+The chained sweep across ranks: each rank fits its outputs into a
+posterior (gpar_fit_posterior), then the ordered sweep of shard.chained_predictions runs the real
+Posterior.predict / prepare in every rank and broadcasts each predicted mean from its owner; the
+means, stds and theta must equal one single-process gpar_fit_predict_chain bit for bit.
 """
 import json
 import os
@@ -32,13 +37,13 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _run_world(world, out):
+def _run_world(world, out, mode="given"):
     port = _free_port()
     procs = []
     for r in range(world):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK="0", WORLD_SIZE=str(world),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "gpu_multirank_worker.py"), out],
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "tests", "gpu_multirank_worker.py"), out, mode],
                                       env=env, cwd=ROOT))
     codes = []
     for pr in procs:
@@ -80,3 +85,37 @@ def test_sharded_gpu_fit_equals_single_process(world, tmp_path):
     th = np.array(got["theta"])
     np.testing.assert_array_equal(th[1:], _serial())
     assert np.all(th[1:] > 0)
+
+
+def _serial_chain():
+    from gparatscale import data as Dd
+    ds = Dd.gpar_dataset(W.N, W.P, seed=3, observation_noise=0.5, n_star=W.NS)
+    dev = torch.device("cuda", 0)
+    t_d = torch.from_numpy(ds["t"]).to(dev)
+    Y_d = torch.from_numpy(ds["Y"]).to(dev)
+    ts_d = torch.from_numpy(ds["t_star"]).to(dev)
+    keep, problems = [], []
+    outs = list(range(2, W.P + 1))
+    for p in outs:
+        Z = torch.from_numpy(Dd.pseudo_inputs(ds["Y"][:, : p - 1], W.M, seed=p)).to(dev)
+        pr, k = G.make_problem(Y_d[:, : p - 1], Z, t_d, Y_d[:, p - 1].contiguous(), qu_kuu_noise=True)
+        problems.append(pr)
+        keep.append((k, Z))
+    chain = torch.zeros((W.NS, W.P), dtype=torch.float64, device=dev)
+    chain[:, 0] = torch.from_numpy(ds["F_star"][:, 0]).to(dev)
+    fr, means, stds = G.fit_predict_batch(problems, np.tile(W.X0, (len(outs), 1)), ts_d,
+                                          [None] * len(outs), max_evals=W.EV, g_tol=-1.0,
+                                          chain=chain, chain_cols=[p - 1 for p in outs])
+    torch.cuda.synchronize()
+    return (fr.theta, np.array([m.cpu().numpy() for m in means]),
+            np.array([s.cpu().numpy() for s in stds]))
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_cross_rank_chained_sweep_equals_fit_predict_chain(world, tmp_path):
+    got = _run_world(world, str(tmp_path / "chain.json"), mode="chained")
+    th, means, stds = _serial_chain()
+    np.testing.assert_array_equal(np.array(got["theta"])[1:], th)
+    np.testing.assert_array_equal(np.array(got["means"]), means)
+    np.testing.assert_array_equal(np.array(got["stds"]), stds)
+    assert np.all(np.isfinite(means)) and np.all(stds > 0)

@@ -152,3 +152,72 @@ def test_chained_predictions_sharded_equal_serial(tmp_path):
         m, _ = _chain_predict(t, Y, ts, p, chain)
         chain = np.column_stack([chain, m])
     np.testing.assert_array_equal(got, chain)
+
+
+def test_assign_chained_blocks():
+    """Contiguous, complete blocks; early ranks own fewer outputs (they start the sweep while the
+    later ranks still fit), and the staggered makespan beats fits-then-sweep at the north costs."""
+    from gparatscale import shard as S
+    for world in (1, 2, 3, 8):
+        owned = S.assign_chained(64, world)
+        flat = [p for o in owned for p in o]
+        assert sorted(flat) == list(range(1, 65)) and flat == sorted(flat)
+        assert 1 in owned[0]
+        if world > 1:
+            sizes = [len([p for p in o if p >= 2]) for o in owned]
+            assert min(sizes) >= 1 and sizes[0] <= sizes[-1]
+    fit = lambda n: S.FIT_FIXED_MS + S.FIT_MS_PER_OUTPUT * n   # noqa: E731
+    sizes = [len([p for p in o if p >= 2]) for o in S.assign_chained(64, 8)]
+    stag, rows = S.chained_schedule(sizes, fit, S.SWEEP_MS_PER_OUTPUT, lambda k: 0.0)
+    flat_ms = fit(8) + 63 * S.SWEEP_MS_PER_OUTPUT        # every rank 8 outputs, then the sweep
+    assert stag < 0.93 * flat_ms, (stag, flat_ms, sizes)
+    # no rank's sweep waits on a later rank: starts are non-decreasing, each after its own fits
+    assert all(b[1] >= a[2] - 1e-9 for a, b in zip(rows, rows[1:]))
+    assert all(r[1] >= r[0] for r in rows)
+
+
+def _block_worker(rank, world, port, out):
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "gpar-at-scale_amd", "python"))
+    from gparatscale import shard as S
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        t, Y, ts, F = _chain_inputs()
+        chain = torch.zeros((NS, P), dtype=torch.float64)
+        chain[:, 0] = torch.from_numpy(F[:, 0])
+        shards = S.assign_chained(P, world)
+        calls = []
+
+        def predict(p, c):
+            calls.append(("predict", p))
+            # inputs of p: every earlier column must already hold its predicted mean
+            assert np.all(c[:, 1: p - 1].numpy() != 0.0)
+            return _chain_predict(t, Y, ts, p, c.numpy())
+
+        mine = S.chained_sweep_blocks(shards, predict, chain,
+                                      prepare_fn=lambda p: calls.append(("prepare", p)))
+        own = [p for p in shards[rank] if p >= 2]
+        assert sorted(mine) == own
+        assert [p for k, p in calls if k == "prepare"] == own
+        assert [p for k, p in calls if k == "predict"] == own
+        np.save(out + f".{rank}.npy", chain.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_chained_sweep_blocks_equal_serial(tmp_path, world):
+    """The staggered chained sweep (contiguous blocks, point-to-point block relay, final broadcast
+    from the last owner) over gloo: every rank ends with the serial reference chain, bit for bit."""
+    out = str(tmp_path / "chain")
+    mp.start_processes(_block_worker, args=(world, _free_port(), out), nprocs=world, join=True,
+                       start_method="spawn")
+    t, Y, ts, F = _chain_inputs()
+    chain = F[:, :1].copy()
+    for p in range(2, P + 1):
+        m, _ = _chain_predict(t, Y, ts, p, chain)
+        chain = np.column_stack([chain, m])
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(out + f".{r}.npy"), chain)
