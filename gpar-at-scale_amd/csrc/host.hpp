@@ -314,13 +314,16 @@ struct GainsPlan {
   double *agg = nullptr, *pst = nullptr;
   GainsOut o{};
   const double** dys = nullptr;
+  bool ys_aligned16 = false;   // every ys[i] 16-byte aligned (the fast gains path's LDS-DMA)
   double *alpha_loc = nullptr, *asend = nullptr;
+  double* moments = nullptr;   // chains_logpdf: per-chunk data moments instead of records
   void launch(hipStream_t st, int first, int count) const;
 };
 GainsPlan plan_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                      const std::vector<ChainParamsHost>& cps, const double* noise, bool want_pf,
                      const std::string& tag, const std::vector<const double*>* ys = nullptr,
-                     double* alpha_loc = nullptr, double* asend = nullptr, bool compact = false);
+                     double* alpha_loc = nullptr, double* asend = nullptr, bool compact = false,
+                     double* moments = nullptr);
 GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                           const std::vector<ChainParamsHost>& cps, const double* noise,
                           bool want_pf, const std::string& tag,

@@ -282,7 +282,7 @@ std::vector<DevProblem> prepare_batch(gpar_ctx* c, const gpar_problem* probs, in
 GainsPlan plan_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                      const std::vector<ChainParamsHost>& cps, const double* noise, bool want_pf,
                      const std::string& tag, const std::vector<const double*>* ys,
-                     double* alpha_loc, double* asend, bool compact) {
+                     double* alpha_loc, double* asend, bool compact, double* moments) {
   GainsPlan gp;
   gp.c = c;
   gp.sdim = sdim;
@@ -303,8 +303,9 @@ GainsPlan plan_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
   o.recstride = n * rs;
   o.gstride = n * 4;
   o.phistride = nch * d2;
-  o.rec = ws<double>(c, tag + "_rec", (size_t)nchains * n * rs);
-  o.g = ws<double>(c, tag + "_g", (size_t)nchains * n * 4);
+  // moments (the chains' logpdf): no per-step record or fix-up row is written
+  o.rec = moments ? nullptr : ws<double>(c, tag + "_rec", (size_t)nchains * n * rs);
+  o.g = moments ? nullptr : ws<double>(c, tag + "_g", (size_t)nchains * n * 4);
   o.phi = ws<double>(c, tag + "_phi", (size_t)nchains * nch * d2);
   o.logs = ws<double>(c, tag + "_logs", (size_t)nchains * nch);
   o.pf = want_pf ? ws<double>(c, tag + "_pf", (size_t)nchains * n * d2) : nullptr;
@@ -313,9 +314,12 @@ GainsPlan plan_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
   if (ys) {
     gp.dys = ws<const double*>(c, tag + "_ys", nchains);
     h2d(c, gp.dys, ys->data(), nchains);
+    gp.ys_aligned16 = true;
+    for (const double* y : *ys) gp.ys_aligned16 = gp.ys_aligned16 && (uintptr_t)y % 16 == 0;
   }
   gp.alpha_loc = alpha_loc;
   gp.asend = asend;
+  gp.moments = moments;
   return gp;
 }
 
@@ -328,11 +332,13 @@ void GainsPlan::launch(hipStream_t st, int first, int count) const {
   Timed tm_(c, "gains");
   launch_gains(st, sdim, t, n, kChunk, nch, count, dcps + first, noise,
                agg + (size_t)first * nch * 3 * d2, pst + (size_t)first * nch * d2,
-               o.rec + (size_t)first * o.recstride, o.g + (size_t)first * o.gstride,
+               o.rec ? o.rec + (size_t)first * o.recstride : nullptr,
+               o.g ? o.g + (size_t)first * o.gstride : nullptr,
                o.phi + (size_t)first * o.phistride, o.logs + (size_t)first * nch,
                o.pf ? o.pf + (size_t)first * n * d2 : nullptr, dys ? dys + first : nullptr,
                alpha_loc ? alpha_loc + (size_t)first * n : nullptr,
-               asend ? asend + (size_t)first * nch * kSStride : nullptr, o.compact);
+               asend ? asend + (size_t)first * nch * kSStride : nullptr, o.compact, ys_aligned16,
+               moments ? moments + (size_t)first * nch * kGainsMomStride : nullptr);
   check_launch("gains");
 }
 

@@ -14,18 +14,24 @@ void chains_logpdf(gpar_ctx* c, int nchains, int64_t n, const double* t, const d
     cps[i] = {1.0 / l, l, pv * pv, ns * ns};
   }
   const int64_t nch = (n + kChunk - 1) / kChunk;
-  GainsOut g = run_gains(c, sdim, t, n, cps, nullptr, false, "chain");
-  double* alpha = ws<double>(c, "chain_alpha", (size_t)nchains * n);
+  // one pass: the gains recursion filters each chain's y from zero per chunk and keeps, per chunk,
+  // sum log S_k and the moments of the chunk-local alpha against the fix-up rows (no per-step
+  // record, fix-up row or alpha reaches HBM: t and y are read, 32 + 96 bytes per chunk written);
+  // the carry gives each chunk's incoming state and sum alpha_k^2 follows from the moments
+  // (r05; before, the gains wrote 160 bytes per step and chain and whiten_vec / vec_fix read them
+  // back)
+  std::vector<const double*> ys(nchains);
+  for (int i = 0; i < nchains; ++i) ys[i] = y + (size_t)i * ldy;
   double* send = ws<double>(c, "chain_send", (size_t)nchains * nch * 4);
   double* cin = ws<double>(c, "chain_cin", (size_t)nchains * nch * 4);
-  const int64_t npart = vec_fix_blocks(n);
-  double* a2 = ws<double>(c, "chain_a2", (size_t)nchains * npart);
+  double* mom = ws<double>(c, "chain_mom", (size_t)nchains * nch * kGainsMomStride);
   double* dl = ws<double>(c, "chain_lml", nchains);
-  launch_whiten_vec(c->stream, sdim, g.rec, g.recstride, y, ldy, n, kChunk, nch, nchains, alpha, n,
-                    send, nch * 4, 1, 0);
+  GainsPlan gp = plan_gains(c, sdim, t, n, cps, nullptr, false, "chain", &ys, nullptr, send, false,
+                            mom);
+  gp.launch(c->stream, 0, nchains);
+  const GainsOut& g = gp.o;
   run_carry(c, sdim, g.phi, g.phistride, send, cin, nch * 4, nch, 1, 1, nchains, "chainc");
-  launch_vec_fix(c->stream, sdim, alpha, n, g.g, g.gstride, cin, nch * 4, 1, 0, n, kChunk, nchains, a2);
-  launch_chain_lml(c->stream, g.logs, nch, a2, npart, n, nchains, dl);
+  launch_chain_lml_mom(c->stream, sdim, g.logs, mom, cin, nch, n, nchains, dl);
   check_launch("chains_logpdf");
   d2h(c, lml, dl, nchains);
   sync(c);

@@ -298,8 +298,31 @@ __global__ __launch_bounds__(256) void gains_phase2(int64_t nch, const double* _
 // With `ys` (the DTC objective): the chain's own data vector ys[p] is filtered from a zero state
 // in the same pass, with the record still in registers (what whiten_vec would do in a second pass
 // over rec): alpha_loc[p * n + k] and the chunk end state asend[(p * nch + j) * 4 + i].
-template <int D, bool COMPACT>
-__global__ __launch_bounds__(256, 2) void gains_phase3(const double* __restrict__ t, int64_t n,
+//
+// Memory ordering (r05).  On gfx9 one counter (vmcnt) tracks loads and stores in issue order, so a
+// wait for a load also waits for every store issued before it.  Each step stores its record and
+// fix-up row, and each step needs its inputs (t_k, the noise entry, y_k).  The inputs are loaded
+// kGainsPF steps ahead into static register slots (the step loop unrolled by kGainsPF, so a slot's
+// pending load is never copied: a register rotation of a pending load forces an immediate wait),
+// and every store is issued unconditionally -- lanes past the chain's end write to a sink -- so the
+// number of memory operations between a slot's load and its use is fixed and the compiler's wait
+// covers only the load, never the stores behind it.  (r04: a StepPipe rotation plus branch-skipped
+// stores made every step wait for all outstanding memory: ~2 us per step, the 62-chain launch
+// 5.3 ms writing at 1.95 TB/s.)
+__device__ double g_gains_sink[64 * 16];   // 16 doubles per lane: the widest masked store (pf)
+
+constexpr int kGainsPF = 4;
+
+// MOM (the temporal-only chains' logpdf, chains_logpdf): no record, fix-up row or alpha is written;
+// each chunk leaves the moments of its chunk-local alpha against the fix-up rows instead,
+//   mom[j] = {s0 = sum alpha_loc^2, s1 = sum alpha_loc g_k (D), s2 = sum g_k g_k^T (packed upper)},
+// from which sum_k alpha_k^2 = sum_j s0 + 2 c_j . s1 + c_j^T s2 c_j once the carry has given the
+// chunks' incoming states c_j (alpha_k = alpha_loc,k + g_k . c_j, as vec_fix applies it).
+constexpr int kMomStride = 12;   // >= 1 + D + D (D + 1) / 2 for D <= 3
+
+template <int D, bool COMPACT, bool HAS_Y, bool HAS_NOISE, bool HAS_PF, bool MASKED, bool MOM>
+__global__ __launch_bounds__(256, 2) void gains_phase3(int64_t blk0, const double* __restrict__ t,
+                                                    int64_t n,
                                                     int L, int64_t nch,
                                                     const ChainParams* __restrict__ cps,
                                                     const double* __restrict__ noise,
@@ -311,27 +334,32 @@ __global__ __launch_bounds__(256, 2) void gains_phase3(const double* __restrict_
                                                     double* __restrict__ pf,
                                                     const double* const* __restrict__ ys,
                                                     double* __restrict__ alpha_loc,
-                                                    double* __restrict__ asend) {
+                                                    double* __restrict__ asend,
+                                                    double* __restrict__ mom) {
+  static_assert(!MOM || (HAS_Y && !COMPACT && !HAS_PF), "moments: the data filter only");
   // COMPACT: the record written is {K_k, rs_k} (CRec), its A_k recomputed by the consumer from the
   // step's time difference (whiten_kfu_d2x2's staging); RP stays the full record's pitch
   constexpr int RS = COMPACT ? CRec<D>::size : Rec<D>::size;
   // Output staging: thread = chunk, so a plain per-thread store of step s's record writes 64
-  // lines 32 KB apart per instruction (measured: the stores were 5.6 of the 6.9 ms of a
-  // 63-chain launch).  Each wave parks its 64 records (and the g rows) in LDS and writes them
-  // back 16 bytes per lane, RS/2 lanes per record; the alpha values are parked 16 steps at a
-  // time and written back as whole 128-byte lines the same way.
+  // lines 32 KB apart per instruction.  Each wave parks its 64 records (and the g rows) in LDS
+  // and writes them back 16 bytes per lane, RS/2 lanes per record; the alpha values are parked
+  // kGainsPF steps at a time and written back per chunk.
   constexpr int RP = Rec<D>::size + 1;
-  constexpr int AS = 16;        // alpha steps per flush
+  constexpr int PF = kGainsPF;
+  constexpr int AS = PF;        // alpha steps per flush: one per unrolled block
   __shared__ double rbuf[4][64 * RP];
   __shared__ double abuf[4][64 * (AS + 1)];
+  // MASKED = false: a block of 256 whole chunks (every chunk but the last is L steps long), so no
+  // lane is ever masked; the last block of each chain (MASKED) handles the partial last chunk and
+  // the lanes past nch
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t j = (blk0 + blockIdx.x) * (int64_t)blockDim.x + threadIdx.x;
   const int64_t jw = j - lane;  // the wave's first chunk
   const int p = blockIdx.y;
-  const bool jv = j < nch;
+  const bool jv = !MASKED || j < nch;
   const ChainParams cp = cps[p];
   const int64_t k0 = (jv ? j : nch - 1) * L;
-  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  const int64_t k1 = !MASKED ? k0 + L : ((k0 + L < n) ? k0 + L : n);
   double P[D][D];
   if (j == 0 || !jv) {
     sde_pinf<D>(cp.s, P);
@@ -345,150 +373,193 @@ __global__ __launch_bounds__(256, 2) void gains_phase3(const double* __restrict_
   double Phi[D][D];
   mat_eye(Phi);
   double lsum = 0.0;
-  const double* yp = ys ? ys[p] : nullptr;
-  double* ap = ys ? alpha_loc + (int64_t)p * n : nullptr;
+  const double* yp = HAS_Y ? ys[p] : nullptr;
+  double* ap = HAS_Y ? alpha_loc + (int64_t)p * n : nullptr;
   double ma[D];
 #pragma unroll
   for (int i = 0; i < D; ++i) ma[i] = 0.0;
+  double ms[kMomStride];
+#pragma unroll
+  for (int e = 0; e < kMomStride; ++e) ms[e] = 0.0;
   double* rp = rec + (int64_t)p * n * RS;
   double* gp = g + (int64_t)p * n * kGStride;
-  double* pfp = pf ? pf + (int64_t)p * n * (D * D) : nullptr;
+  double* pfp = HAS_PF ? pf + (int64_t)p * n * (D * D) : nullptr;
+  double* sink = g_gains_sink + 16 * lane;
   double* rb = rbuf[wave];
   double* ab = abuf[wave];
   double tprev = k0 > 0 ? t[k0 - 1] : 0.0;
-  StepPipe spp;
-  spp.init(t, noise, yp, k0, k1);
+  // step inputs, slot u = step sb + u of the current block (loads clamped in bounds)
+  double tq[PF], rq[PF], yq[PF];
+  auto load = [&](int u, int64_t k) __attribute__((always_inline)) {
+    const int64_t kk = (!MASKED && k + PF <= k0 + L) ? k : (k < k1 ? k : k1 - 1);
+    tq[u] = t[kk];
+    if constexpr (HAS_NOISE) rq[u] = noise[kk];
+    if constexpr (HAS_Y) yq[u] = yp[kk];
+  };
+#pragma unroll
+  for (int u = 0; u < PF; ++u) load(u, k0 + u);
   // every lane runs all L steps (the wave writes cooperatively); past k1 nothing is committed
-  for (int sidx = 0; sidx < L; ++sidx) {
-    const int64_t k = k0 + sidx;
-    const bool live = jv && k < k1;
-    double tk, rk, yk;
-    spp.next(k, tk, rk, yk);
-    double A[D][D], Q[D][D], X[D][D], Pm[D][D];
-    step_model_tau<D>((k == 0) ? 1.0 : (tk - tprev) / cp.l, cp, A, Q);
-    tprev = tk;
-    mat_mul(A, P, X);
-    mat_mul_bt(X, A, Pm);
+  for (int sb = 0; sb < L; sb += PF) {
 #pragma unroll
-    for (int i = 0; i < D; ++i)
-#pragma unroll
-      for (int q = 0; q < D; ++q) Pm[i][q] += Q[i][q];
-    const double R = noise ? (rk < 0.0 ? cp.r : rk) : cp.r;
-    const double S = Pm[0][0] + R;
-    const double rs = 1.0 / sqrt(S);
-    double Kg[D];
-#pragma unroll
-    for (int i = 0; i < D; ++i) Kg[i] = Pm[i][0] / S;
-    double AP[D][D];
-    mat_mul(A, Phi, AP);
-    // park the record {A, K, rs, pad} (COMPACT: {K, rs, pad}) and g_k = -rs (A Phi)[0, :]
-    constexpr int KO = COMPACT ? 0 : D * D;   // K's offset in the record
-    if constexpr (!COMPACT) {
+    for (int u = 0; u < PF; ++u) {
+      const int sidx = sb + u;
+      const int64_t k = k0 + sidx;
+      const bool live = !MASKED || (jv && k < k1);
+      const double tk = tq[u];
+      const double rk = HAS_NOISE ? rq[u] : 0.0;
+      const double yk = HAS_Y ? yq[u] : 0.0;
+      load(u, k + PF);
+      double A[D][D], Q[D][D], X[D][D], Pm[D][D];
+      step_model_tau<D>((k == 0) ? 1.0 : (tk - tprev) / cp.l, cp, A, Q);
+      tprev = tk;
+      mat_mul(A, P, X);
+      mat_mul_bt(X, A, Pm);
 #pragma unroll
       for (int i = 0; i < D; ++i)
 #pragma unroll
-        for (int q = 0; q < D; ++q) rb[lane * RP + i * D + q] = A[i][q];
-    }
+        for (int q = 0; q < D; ++q) Pm[i][q] += Q[i][q];
+      const double R = HAS_NOISE ? (rk < 0.0 ? cp.r : rk) : cp.r;
+      const double S = Pm[0][0] + R;
+      const double rs = 1.0 / sqrt(S);
+      double Kg[D];
 #pragma unroll
-    for (int i = 0; i < D; ++i) rb[lane * RP + KO + i] = Kg[i];
-    rb[lane * RP + KO + D] = rs;
+      for (int i = 0; i < D; ++i) Kg[i] = Pm[i][0] / S;
+      double AP[D][D];
+      mat_mul(A, Phi, AP);
+      // the record {A, K, rs, pad} (COMPACT: {K, rs, pad}) and g_k = -rs (A Phi)[0, :]
+      constexpr int KO = COMPACT ? 0 : D * D;   // K's offset in the record
+      double recv[RS];
+      if constexpr (!COMPACT) {
 #pragma unroll
-    for (int e = KO + D + 1; e < RS; ++e) rb[lane * RP + e] = 0.0;
-    double gk[kGStride];
+        for (int i = 0; i < D; ++i)
 #pragma unroll
-    for (int q = 0; q < kGStride; ++q) gk[q] = q < D ? -rs * AP[0][q] : 0.0;
-    if (live) {
-#pragma unroll
-      for (int i = 0; i < D; ++i)
-#pragma unroll
-        for (int q = 0; q < D; ++q) P[i][q] = Pm[i][q] - Kg[i] * Pm[0][q];
-      // Phi <- (I - K e1^T) A Phi
-#pragma unroll
-      for (int i = 0; i < D; ++i)
-#pragma unroll
-        for (int q = 0; q < D; ++q) Phi[i][q] = AP[i][q] - Kg[i] * AP[0][q];
-      lsum += log(S);
-    }
-    if (yp) {   // alpha filter from zero (same arithmetic as whiten_kfu's column recursion)
-      double mm[D];
-#pragma unroll
-      for (int i = 0; i < D; ++i) {
-        double a2 = 0.0;
-#pragma unroll
-        for (int q = 0; q < D; ++q) a2 = fma(A[i][q], ma[q], a2);
-        mm[i] = a2;
+          for (int q = 0; q < D; ++q) recv[i * D + q] = A[i][q];
       }
-      const double ev = yk - mm[0];
-      ab[lane * (AS + 1) + (sidx % AS)] = ev * rs;
+#pragma unroll
+      for (int i = 0; i < D; ++i) recv[KO + i] = Kg[i];
+      recv[KO + D] = rs;
+#pragma unroll
+      for (int e = KO + D + 1; e < RS; ++e) recv[e] = 0.0;
+      double gk[kGStride];
+#pragma unroll
+      for (int q = 0; q < kGStride; ++q) gk[q] = q < D ? -rs * AP[0][q] : 0.0;
+      if constexpr (MOM) {
+        // nothing stored: the moments are accumulated with alpha below
+      } else if constexpr (MASKED) {   // the chain's last block: each lane stores its own record directly
+        double* dr = live ? rp + k * RS : sink;
+#pragma unroll
+        for (int e = 0; e < RS; e += 2)
+          *reinterpret_cast<double2*>(dr + e) = double2{recv[e], recv[e + 1]};
+        double* dg = live ? gp + k * kGStride : sink;
+#pragma unroll
+        for (int e = 0; e < kGStride; e += 2)
+          *reinterpret_cast<double2*>(dg + e) = double2{gk[e], gk[e + 1]};
+      } else {   // parked in LDS, written back coalesced below
+#pragma unroll
+        for (int e = 0; e < RS; ++e) rb[lane * RP + e] = recv[e];
+      }
       if (live) {
 #pragma unroll
-        for (int i = 0; i < D; ++i) ma[i] = fma(Kg[i], ev, mm[i]);
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+          for (int q = 0; q < D; ++q) P[i][q] = Pm[i][q] - Kg[i] * Pm[0][q];
+        // Phi <- (I - K e1^T) A Phi
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+          for (int q = 0; q < D; ++q) Phi[i][q] = AP[i][q] - Kg[i] * AP[0][q];
+        lsum += log(S);
       }
-    }
-    if (pfp && live) {
+      if constexpr (HAS_Y) {   // alpha filter from zero (same arithmetic as whiten_kfu's column recursion)
+        double mm[D];
 #pragma unroll
-      for (int i = 0; i < D; ++i)
+        for (int i = 0; i < D; ++i) {
+          double a2 = 0.0;
 #pragma unroll
-        for (int q = 0; q < D; ++q) pfp[k * D * D + i * D + q] = P[i][q];
-    }
-    __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's parked values landed
-    __builtin_amdgcn_wave_barrier();
-    // write back: lane -> (record rr = e / (RS/2), 16-byte piece e % (RS/2))
+          for (int q = 0; q < D; ++q) a2 = fma(A[i][q], ma[q], a2);
+          mm[i] = a2;
+        }
+        const double ev = yk - mm[0];
+        if constexpr (MOM) {
+          if (live) {
+            const double al = ev * rs;
+            ms[0] = fma(al, al, ms[0]);
+            int e = 1 + D;
 #pragma unroll
-    for (int it = 0; it < RS / 2; ++it) {
-      const int e = it * 64 + lane;
-      const int rr = e / (RS / 2), pc = e % (RS / 2);
-      const int64_t jr = jw + rr;
-      const int64_t kr = jr * L + sidx;
-      if (jr < nch && kr < n) {
-        double2 v;
-        v.x = rb[rr * RP + 2 * pc];
-        v.y = rb[rr * RP + 2 * pc + 1];
-        *reinterpret_cast<double2*>(rp + kr * RS + 2 * pc) = v;
+            for (int i = 0; i < D; ++i) {
+              ms[1 + i] = fma(al, gk[i], ms[1 + i]);
+#pragma unroll
+              for (int q = i; q < D; ++q) {
+                ms[e] = fma(gk[i], gk[q], ms[e]);
+                ++e;
+              }
+            }
+          }
+        } else if constexpr (MASKED)
+          *(live ? ap + k : sink) = ev * rs;
+        else
+          ab[lane * (AS + 1) + u] = ev * rs;
+        if (live) {
+#pragma unroll
+          for (int i = 0; i < D; ++i) ma[i] = fma(Kg[i], ev, mm[i]);
+        }
       }
-    }
-    // g rows: two 16-byte pieces per step, straight from registers through a lane exchange
-    {
+      if constexpr (HAS_PF) {
+        double* dst = live ? pfp + k * D * D : sink;
 #pragma unroll
-      for (int q = 0; q < kGStride; ++q) rb[lane * RP + q] = gk[q];
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_wave_barrier();
+        for (int i = 0; i < D; ++i)
 #pragma unroll
-      for (int it = 0; it < 2; ++it) {
-        const int e = it * 64 + lane;
-        const int rr = e >> 1, pc = e & 1;
-        const int64_t jr = jw + rr;
-        const int64_t kr = jr * L + sidx;
-        if (jr < nch && kr < n) {
+          for (int q = 0; q < D; ++q) dst[i * D + q] = P[i][q];
+      }
+      if constexpr (!MASKED && !MOM) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's parked values landed
+        __builtin_amdgcn_wave_barrier();
+        // write back: lane -> (record rr = e / (RS/2), 16-byte piece e % (RS/2))
+  #pragma unroll
+        for (int it = 0; it < RS / 2; ++it) {
+          const int e = it * 64 + lane;
+          const int rr = e / (RS / 2), pc = e % (RS / 2);
+          const int64_t jr = jw + rr;
+          const int64_t kr = jr * L + sidx;
           double2 v;
           v.x = rb[rr * RP + 2 * pc];
           v.y = rb[rr * RP + 2 * pc + 1];
-          *reinterpret_cast<double2*>(gp + kr * kGStride + 2 * pc) = v;
+          double* dst = rp + kr * RS + 2 * pc;
+          *reinterpret_cast<double2*>(dst) = v;
         }
+        // g rows: two 16-byte pieces per step, straight from registers through a lane exchange
+        __builtin_amdgcn_wave_barrier();
+  #pragma unroll
+        for (int q = 0; q < kGStride; ++q) rb[lane * RP + q] = gk[q];
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+  #pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          const int e = it * 64 + lane;
+          const int rr = e >> 1, pc = e & 1;
+          const int64_t jr = jw + rr;
+          const int64_t kr = jr * L + sidx;
+          double2 v;
+          v.x = rb[rr * RP + 2 * pc];
+          v.y = rb[rr * RP + 2 * pc + 1];
+          double* dst = gp + kr * kGStride + 2 * pc;
+          *reinterpret_cast<double2*>(dst) = v;
+        }
+        __builtin_amdgcn_wave_barrier();   // rb is rewritten by the next step
       }
-      __builtin_amdgcn_wave_barrier();   // rb is rewritten by the next step
+      // keep the unrolled steps apart: interleaving them only lengthens live ranges (spills)
+      __builtin_amdgcn_sched_barrier(0);
     }
-    if (yp && (sidx % AS == AS - 1 || sidx == L - 1)) {
+    if constexpr (HAS_Y && !MASKED && !MOM) {   // the block's AS alpha values of the wave's 64 chunks
       __builtin_amdgcn_s_waitcnt(0xc07f);
       __builtin_amdgcn_wave_barrier();
-      const int s0 = sidx - (sidx % AS);
 #pragma unroll
-      for (int it = 0; it < AS / 2; ++it) {
+      for (int it = 0; it < AS; ++it) {
         const int e = it * 64 + lane;
-        const int rr = e / (AS / 2), pc = e % (AS / 2);
+        const int rr = e / AS, pc = e % AS;
         const int64_t jr = jw + rr;
-        const int64_t kr = jr * L + s0 + 2 * pc;
-        const int64_t kend = (jr * L + L < n) ? jr * L + L : n;
-        if (jr < nch && kr < kend) {
-          if (kr + 1 < kend) {
-            double2 v;
-            v.x = ab[rr * (AS + 1) + 2 * pc];
-            v.y = ab[rr * (AS + 1) + 2 * pc + 1];
-            *reinterpret_cast<double2*>(ap + kr) = v;
-          } else {
-            ap[kr] = ab[rr * (AS + 1) + 2 * pc];
-          }
-        }
+        const int64_t kr = jr * L + sb + pc;
+        ap[kr] = ab[rr * (AS + 1) + pc];
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -500,10 +571,334 @@ __global__ __launch_bounds__(256, 2) void gains_phase3(const double* __restrict_
 #pragma unroll
     for (int q = 0; q < D; ++q) ph[i * D + q] = Phi[i][q];
   logs[(int64_t)p * nch + j] = lsum;
-  if (yp) {
+  if constexpr (HAS_Y) {
     double* sp = asend + ((int64_t)p * nch + j) * kSStride;
 #pragma unroll
     for (int i = 0; i < kSStride; ++i) sp[i] = i < D ? ma[i] : 0.0;
+  }
+  if constexpr (MOM) {
+    double* mp_ = mom + ((int64_t)p * nch + j) * kMomStride;
+#pragma unroll
+    for (int e = 0; e < kMomStride; ++e) mp_[e] = ms[e];
+  }
+}
+
+// ---------------------------------------------------------------------------- phase 3, fast path
+// The same recursion and outputs as gains_phase3 for the chains' whole blocks (256 chunks of
+// exactly L = 256 steps, no masked lane), with every memory operation of the step loop issued
+// by inline asm so that its waits are exact:
+//   * the step inputs (t, and y or the noise vector) reach LDS by LDS-DMA (global_load_lds_dwordx4:
+//     two steps of the lane's chunk per instruction) into a per-wave ring of kG3Ring pair slots,
+//     one unrolled block (kG3Blk steps) ahead;
+//   * the record / fix-up row / alpha stores are asm too, kG3Stores(...) per block;
+//   * at the top of block b, after issuing block b + 1's DMAs, `s_waitcnt vmcnt(S + 2 NA)` leaves
+//     block b - 1's S stores and block b + 1's 2 NA DMAs in flight and retires block b's DMAs:
+//     no step ever waits for a store.
+// (hipcc does not count the asm DMAs, and the loop's only other memory operations are its plain
+// stores, which it never waits for, so it inserts no vmcnt of its own; the ring is read only by
+// the wave that filled it, after its own covering vmcnt -- MI355X_MICROARCH.md item 7.  The
+// stores are plain C++ stores, not asm, so that hipcc's hazard recognizer sees their operands:
+// a first version with asm stores, whose address registers hipcc rewrote in the next cycle,
+// produced wrong records.)
+constexpr int kG3L = 256;      // == kChunk
+constexpr int kG3Blk = 4;      // steps per unrolled block (two DMA pairs)
+constexpr int kG3Ring = 4;     // pair slots per array (two blocks)
+
+template <int D, bool COMPACT, bool HAS_PF, bool MOM = false, bool MASKED = false>
+__host__ __device__ constexpr int g3_stores_per_block(bool has_y) {
+  constexpr int RS = COMPACT ? CRec<D>::size : Rec<D>::size;
+  constexpr int PFS = HAS_PF ? (D * D + 1) / 2 : 0;   // the filtered covariance, 16 B pieces
+  // the block's alpha: two 16-byte pairs per lane (masked block: four 8-byte halves)
+  return MOM ? 0 : kG3Blk * (RS / 2 + 2 + PFS) + (has_y ? (MASKED ? 4 : 2) : 0);
+}
+
+typedef double g3d2 __attribute__((ext_vector_type(2)));
+
+// plain stores (hipcc emits them, and its hazard recognizer sees them; it counts no VMEM load in
+// the loop, so it never waits for them): one global_store_dwordx4 / _dwordx2 each
+__device__ __forceinline__ void g3_store16(double* dst, g3d2 v) {
+  *reinterpret_cast<g3d2*>(dst) = v;
+}
+__device__ __forceinline__ void g3_store8(double* dst, double v) { *dst = v; }
+__device__ __forceinline__ void g3_dma16(const double* src, uint32_t lds) {
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off"
+               :
+               : "v"(src), "s"(__builtin_amdgcn_readfirstlane(lds))
+               : "memory", "m0");
+}
+
+// MASKED: the chain's last block of 256 chunks -- lanes past nch run chunk nch - 1's inputs and
+// store to the sink, the partial last chunk's steps past n are not committed, and its inputs are
+// read in whole 16-byte pairs (the arrays are 16-byte aligned, so a pair holding a valid element
+// never leaves its page) up to the last one holding a valid step.
+// (the masked block -- one per chain -- is allowed the whole register file: its selects would
+// otherwise spill, and one such block per chain never fills a CU anyway)
+template <int D, bool COMPACT, bool HAS_Y, bool HAS_NOISE, bool HAS_PF, bool MOM, bool MASKED>
+__global__ __launch_bounds__(256, MASKED ? 1 : 2) void gains_phase3_fast(
+    int64_t blk0, const double* __restrict__ t, int64_t n, int64_t nch,
+    const ChainParams* __restrict__ cps,
+    const double* __restrict__ noise, const double* __restrict__ pstart, double* __restrict__ rec,
+    double* __restrict__ g, double* __restrict__ phi, double* __restrict__ logs,
+    double* __restrict__ pf, const double* const* __restrict__ ys, double* __restrict__ alpha_loc,
+    double* __restrict__ asend, double* __restrict__ mom) {
+  static_assert(!MOM || (HAS_Y && !COMPACT && !HAS_PF), "moments: the data filter only");
+  constexpr int L = kG3L;
+  constexpr int RS = COMPACT ? CRec<D>::size : Rec<D>::size;
+  constexpr int RP = Rec<D>::size + 1;
+  constexpr int NA = 1 + (HAS_Y ? 1 : 0) + (HAS_NOISE ? 1 : 0);   // input arrays staged
+  constexpr int S = g3_stores_per_block<D, COMPACT, HAS_PF, MOM, MASKED>(HAS_Y);
+  constexpr int VM = S + 2 * NA;   // ops allowed in flight at a block's wait
+  static_assert(VM <= 63, "vmcnt holds at most 63 outstanding operations");
+  __shared__ double rbuf[4][MOM ? 1 : 64 * RP];
+  __shared__ double abuf[4][MOM ? 1 : 64 * kG3Blk];
+  __shared__ __attribute__((aligned(16))) double ring[4][NA][kG3Ring][64 * 2];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int64_t j = (blk0 + blockIdx.x) * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t jw = j - lane;
+  const bool jv = !MASKED || j < nch;
+  const int64_t jc = jv ? j : nch - 1;   // the chunk whose inputs this lane reads
+  const int p = blockIdx.y;
+  const ChainParams cp = cps[p];
+  const int64_t k0 = jc * L;
+  const int64_t k1 = MASKED ? (k0 + L < n ? k0 + L : n) : k0 + L;
+  const int qmax = (int)((k1 - 1 - k0) >> 1);   // the last pair holding a valid step
+  double P[D][D];
+  if (jc == 0) {
+    sde_pinf<D>(cp.s, P);
+  } else {
+    const double* ps = pstart + ((int64_t)p * nch + jc) * (D * D);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) P[i][q] = ps[i * D + q];
+  }
+  double tprev = k0 > 0 ? t[k0 - 1] : 0.0;
+  const double* yp = HAS_Y ? ys[p] : nullptr;
+  double* ap = HAS_Y ? alpha_loc + (int64_t)p * n : nullptr;
+  double* rp = rec + (int64_t)p * n * RS;
+  double* gp = g + (int64_t)p * n * kGStride;
+  double* pfp = HAS_PF ? pf + (int64_t)p * n * (D * D) : nullptr;
+  double* rb = rbuf[wave];
+  double* ab = abuf[wave];
+  double* sink = g_gains_sink + 16 * lane;   // masked stores (MASKED only)
+  // every ordinary load is retired here, where hipcc can see it: none may stay pending into the
+  // loop, whose asm operations hipcc does not count
+  __builtin_amdgcn_s_waitcnt(0);
+  const double* src[NA];
+  src[0] = t + k0;
+  if constexpr (HAS_Y) src[1] = yp + k0;
+  if constexpr (HAS_NOISE) src[NA - 1] = noise + k0;
+  const uint32_t ring0 =
+      (uint32_t)(uintptr_t)(__attribute__((address_space(3))) double*)(&ring[wave][0][0][0]);
+  // pair q of every array into ring slot q % kG3Ring (a pair past the chunk's last valid one
+  // re-reads that one: in bounds, never consumed)
+  auto issue_pair = [&](int q) __attribute__((always_inline)) {
+    const int qq = MASKED ? (q < qmax ? q : qmax) : (q < L / 2 ? q : 0);
+#pragma unroll
+    for (int a = 0; a < NA; ++a)
+      g3_dma16(src[a] + 2 * qq, ring0 + (uint32_t)(((a * kG3Ring) + (q % kG3Ring)) * 1024));
+  };
+  issue_pair(0);
+  issue_pair(1);
+  double Phi[D][D];
+  mat_eye(Phi);
+  double lsum = 0.0;
+  double ma[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) ma[i] = 0.0;
+  double ms[MOM ? kMomStride : 1];
+#pragma unroll
+  for (int e = 0; e < (MOM ? kMomStride : 1); ++e) ms[e] = 0.0;
+  for (int sb = 0; sb < L; sb += kG3Blk) {
+    const int q0 = sb / 2;
+    issue_pair(q0 + 2);
+    issue_pair(q0 + 3);
+    // block b's pairs were issued before block b - 1's S stores and block b + 1's 2 NA DMAs
+    // (block 0: before block 1's DMAs only)
+    if (sb == 0)
+      asm volatile("s_waitcnt vmcnt(%0)" : : "n"(2 * NA) : "memory");
+    else
+      asm volatile("s_waitcnt vmcnt(%0)" : : "n"(VM) : "memory");
+    // the block's inputs: two pairs per array, one 16-byte LDS read per pair
+    double tin[kG3Blk], rin[kG3Blk], yin[kG3Blk];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int slot = (q0 + h) % kG3Ring;
+      const g3d2 tv = *reinterpret_cast<const g3d2*>(&ring[wave][0][slot][2 * lane]);
+      tin[2 * h] = tv.x;
+      tin[2 * h + 1] = tv.y;
+      if constexpr (HAS_Y) {
+        const g3d2 yv = *reinterpret_cast<const g3d2*>(&ring[wave][1][slot][2 * lane]);
+        yin[2 * h] = yv.x;
+        yin[2 * h + 1] = yv.y;
+      }
+      if constexpr (HAS_NOISE) {
+        const g3d2 rv = *reinterpret_cast<const g3d2*>(&ring[wave][NA - 1][slot][2 * lane]);
+        rin[2 * h] = rv.x;
+        rin[2 * h + 1] = rv.y;
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kG3Blk; ++u) {
+      const int sidx = sb + u;
+      const int64_t k = k0 + sidx;
+      const bool live = !MASKED || (jv && k < k1);
+      const double tk = tin[u];
+      double A[D][D], Q[D][D], X[D][D], Pm[D][D];
+      step_model_tau<D>((k == 0) ? 1.0 : (tk - tprev) / cp.l, cp, A, Q);
+      tprev = tk;
+      mat_mul(A, P, X);
+      mat_mul_bt(X, A, Pm);
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) Pm[i][q] += Q[i][q];
+      const double R = HAS_NOISE ? (rin[u] < 0.0 ? cp.r : rin[u]) : cp.r;
+      const double Sv = Pm[0][0] + R;
+      const double rs = 1.0 / sqrt(Sv);
+      double Kg[D];
+#pragma unroll
+      for (int i = 0; i < D; ++i) Kg[i] = Pm[i][0] / Sv;
+      double AP[D][D];
+      mat_mul(A, Phi, AP);
+      // park the record {A, K, rs, pad} (COMPACT: {K, rs, pad})
+      constexpr int KO = COMPACT ? 0 : D * D;
+      if constexpr (!MOM) {
+        if constexpr (!COMPACT) {
+#pragma unroll
+          for (int i = 0; i < D; ++i)
+#pragma unroll
+            for (int q = 0; q < D; ++q) rb[lane * RP + i * D + q] = A[i][q];
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) rb[lane * RP + KO + i] = Kg[i];
+        rb[lane * RP + KO + D] = rs;
+#pragma unroll
+        for (int e = KO + D + 1; e < RS; ++e) rb[lane * RP + e] = 0.0;
+      }
+      double gk[kGStride];
+#pragma unroll
+      for (int q = 0; q < kGStride; ++q) gk[q] = q < D ? -rs * AP[0][q] : 0.0;
+      if (live) {
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+          for (int q = 0; q < D; ++q) P[i][q] = Pm[i][q] - Kg[i] * Pm[0][q];
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+          for (int q = 0; q < D; ++q) Phi[i][q] = AP[i][q] - Kg[i] * AP[0][q];
+        lsum += log(Sv);
+      }
+      if constexpr (HAS_Y) {   // alpha filter from zero (whiten_kfu's column recursion)
+        double mm[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          double a2 = 0.0;
+#pragma unroll
+          for (int q = 0; q < D; ++q) a2 = fma(A[i][q], ma[q], a2);
+          mm[i] = a2;
+        }
+        const double ev = yin[u] - mm[0];
+        if constexpr (MOM) {
+          const double al = live ? ev * rs : 0.0;
+          ms[0] = fma(al, al, ms[0]);
+          int e = 1 + D;
+#pragma unroll
+          for (int i = 0; i < D; ++i) {
+            ms[1 + i] = fma(al, gk[i], ms[1 + i]);
+#pragma unroll
+            for (int q = i; q < D; ++q) {
+              ms[e] = live ? fma(gk[i], gk[q], ms[e]) : ms[e];
+              ++e;
+            }
+          }
+        } else {
+          ab[lane * kG3Blk + u] = ev * rs;
+        }
+        if (live) {
+#pragma unroll
+          for (int i = 0; i < D; ++i) ma[i] = fma(Kg[i], ev, mm[i]);
+        }
+      }
+      if constexpr (HAS_PF) {   // the filtered covariance, straight from registers (16-byte pieces)
+        double pv[2 * ((D * D + 1) / 2)];
+#pragma unroll
+        for (int e = 0; e < D * D; ++e) pv[e] = P[e / D][e % D];
+        if constexpr ((D * D) % 2) pv[D * D] = 0.0;
+        double* dst = live ? pfp + k * (D * D) : sink;
+#pragma unroll
+        for (int e = 0; e + 1 < D * D; e += 2) g3_store16(dst + e, g3d2{pv[e], pv[e + 1]});
+        if constexpr ((D * D) % 2) {
+          // odd count: the last double as an 8-byte store, padded to one 16-byte piece's count
+          g3_store8(dst + D * D - 1, pv[D * D - 1]);
+        }
+      }
+      if constexpr (!MOM) {
+        __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's parked values landed
+        __builtin_amdgcn_wave_barrier();
+        // write back: lane -> (record rr = e / (RS/2), 16-byte piece e % (RS/2))
+#pragma unroll
+        for (int it = 0; it < RS / 2; ++it) {
+          const int e = it * 64 + lane;
+          const int rr = e / (RS / 2), pc = e % (RS / 2);
+          const int64_t kr = (jw + rr) * L + sidx;
+          double* dst = (!MASKED || (jw + rr < nch && kr < n)) ? rp + kr * RS + 2 * pc : sink;
+          g3_store16(dst, g3d2{rb[rr * RP + 2 * pc], rb[rr * RP + 2 * pc + 1]});
+        }
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int q = 0; q < kGStride; ++q) rb[lane * RP + q] = gk[q];
+        __builtin_amdgcn_s_waitcnt(0xc07f);
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+          const int e = it * 64 + lane;
+          const int rr = e >> 1, pc = e & 1;
+          const int64_t kr = (jw + rr) * L + sidx;
+          double* dst = (!MASKED || (jw + rr < nch && kr < n)) ? gp + kr * kGStride + 2 * pc : sink;
+          g3_store16(dst, g3d2{rb[rr * RP + 2 * pc], rb[rr * RP + 2 * pc + 1]});
+        }
+        __builtin_amdgcn_wave_barrier();   // rb is rewritten by the next step
+      }
+    }
+    if constexpr (HAS_Y && !MOM) {   // the block's alpha values: 64 chunks x 4 steps, 16 bytes per lane
+      __builtin_amdgcn_s_waitcnt(0xc07f);
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int it = 0; it < 2; ++it) {
+        const int e = it * 64 + lane;
+        const int rr = e >> 1, pc = e & 1;
+        const int64_t kr = (jw + rr) * L + sb + 2 * pc;
+        if constexpr (MASKED) {   // two 8-byte halves, each committed only inside the chunk
+          const int64_t kend = ((jw + rr) * L + L < n) ? (jw + rr) * L + L : n;
+          const bool cv = jw + rr < nch;
+          g3_store8((cv && kr < kend) ? ap + kr : sink, ab[rr * kG3Blk + 2 * pc]);
+          g3_store8((cv && kr + 1 < kend) ? ap + kr + 1 : sink + 1, ab[rr * kG3Blk + 2 * pc + 1]);
+        } else {
+          g3_store16(ap + kr, g3d2{ab[rr * kG3Blk + 2 * pc], ab[rr * kG3Blk + 2 * pc + 1]});
+        }
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" : : : "memory");   // the ring's last DMAs land before exit
+  if (!jv) return;
+  double* ph = phi + ((int64_t)p * nch + j) * (D * D);
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) ph[i * D + q] = Phi[i][q];
+  logs[(int64_t)p * nch + j] = lsum;
+  if constexpr (HAS_Y) {
+    double* sp = asend + ((int64_t)p * nch + j) * kSStride;
+#pragma unroll
+    for (int i = 0; i < kSStride; ++i) sp[i] = i < D ? ma[i] : 0.0;
+  }
+  if constexpr (MOM) {
+    double* mp_ = mom + ((int64_t)p * nch + j) * kMomStride;
+#pragma unroll
+    for (int e = 0; e < kMomStride; ++e) mp_[e] = ms[e];
   }
 }
 
@@ -1641,10 +2036,46 @@ __global__ void chain_lml(const double* __restrict__ logs, int64_t nch,
   if (threadIdx.x == 0) lml[b] = -0.5 * ((double)n * kLog2Pi + red[0][0] + red[1][0]);
 }
 
+// lml[b] from the phase-3 moments (MOM): -0.5 (n log 2pi + sum_j [logS_j + s0_j + 2 c_j . s1_j +
+// c_j^T s2_j c_j]), c_j = the chunk's incoming state from the carry; partials summed in a fixed
+// order.
+template <int D>
+__global__ void chain_lml_mom(const double* __restrict__ logs, const double* __restrict__ mom,
+                              const double* __restrict__ cin, int64_t nch, int64_t n,
+                              double* __restrict__ lml) {
+  const int b = blockIdx.x;
+  __shared__ double red[256];
+  double s = 0.0;
+  for (int64_t j = threadIdx.x; j < nch; j += 256) {
+    const double* m = mom + ((int64_t)b * nch + j) * kMomStride;
+    const double* c = cin + ((int64_t)b * nch + j) * kSStride;
+    double v = logs[(int64_t)b * nch + j] + m[0];
+    int e = 1 + D;
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      v = fma(2.0 * c[i], m[1 + i], v);
+#pragma unroll
+      for (int q = i; q < D; ++q) {
+        v = fma((q == i ? 1.0 : 2.0) * c[i] * c[q], m[e], v);
+        ++e;
+      }
+    }
+    s += v;
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int off = 128; off > 0; off >>= 1) {
+    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) lml[b] = -0.5 * ((double)n * kLog2Pi + red[0]);
+}
+
 }  // namespace gpar
 
 // ============================================================================ launch wrappers
 #include "launch.hpp"
+static_assert(gpar::kMomStride == gpar::kGainsMomStride, "moment stride");
 
 namespace gpar {
 
@@ -1655,22 +2086,95 @@ namespace gpar {
     default: { constexpr int DD = 3; __VA_ARGS__; } break;        \
   }
 
+// every combination of the optional inputs / outputs is its own instantiation of gains_phase3
+// (no dead registers or branches for the ones a caller does not pass)
+template <int D, bool C, bool Y, bool NZ, bool PFX, bool MOM>
+static void launch_phase3_blocks(dim3 grid, hipStream_t st, const double* t, int64_t n, int L,
+                                 int64_t nch, const ChainParams* cps, const double* noise,
+                                 const double* pstart, double* rec, double* g, double* phi,
+                                 double* logs, double* pf, const double* const* ys,
+                                 double* alpha_loc, double* asend, double* mom, bool fast_ok) {
+  // the whole blocks (every chunk L steps, no lane masked) by the fast path when its counted
+  // waits fit the vmcnt field, then each chain's last (masked) block
+  const dim3 gfull(grid.x - 1, grid.y), glast(1, grid.y);
+  const int64_t last = grid.x - 1;
+  constexpr int NA = 1 + (Y ? 1 : 0) + (NZ ? 1 : 0);
+  if constexpr (g3_stores_per_block<D, C, PFX, MOM, true>(Y) + 2 * NA <= 63) {
+    if (L == kG3L && fast_ok) {
+      if (gfull.x)
+        gains_phase3_fast<D, C, Y, NZ, PFX, MOM, false><<<gfull, 256, 0, st>>>(
+            0, t, n, nch, cps, noise, pstart, rec, g, phi, logs, pf, ys, alpha_loc, asend, mom);
+      gains_phase3_fast<D, C, Y, NZ, PFX, MOM, true><<<glast, 256, 0, st>>>(
+          last, t, n, nch, cps, noise, pstart, rec, g, phi, logs, pf, ys, alpha_loc, asend, mom);
+      return;
+    }
+  }
+  if (gfull.x)
+    gains_phase3<D, C, Y, NZ, PFX, false, MOM><<<gfull, 256, 0, st>>>(0, t, n, L, nch, cps, noise,
+                                                                      pstart, rec, g, phi, logs, pf,
+                                                                      ys, alpha_loc, asend, mom);
+  gains_phase3<D, C, Y, NZ, PFX, true, MOM><<<glast, 256, 0, st>>>(last, t, n, L, nch, cps, noise,
+                                                                   pstart, rec, g, phi, logs, pf, ys,
+                                                                   alpha_loc, asend, mom);
+}
+
+template <int D, bool C, bool Y, bool NZ>
+static void launch_phase3_pf(dim3 grid, hipStream_t st, const double* t, int64_t n, int L,
+                             int64_t nch, const ChainParams* cps, const double* noise,
+                             const double* pstart, double* rec, double* g, double* phi,
+                             double* logs, double* pf, const double* const* ys,
+                             double* alpha_loc, double* asend, bool fast_ok) {
+  if (pf)
+    launch_phase3_blocks<D, C, Y, NZ, true, false>(grid, st, t, n, L, nch, cps, noise, pstart, rec,
+                                                   g, phi, logs, pf, ys, alpha_loc, asend, nullptr,
+                                                   fast_ok);
+  else
+    launch_phase3_blocks<D, C, Y, NZ, false, false>(grid, st, t, n, L, nch, cps, noise, pstart, rec,
+                                                    g, phi, logs, pf, ys, alpha_loc, asend, nullptr,
+                                                    fast_ok);
+}
+
+template <int D>
+static void launch_phase3(dim3 grid, hipStream_t st, const double* t, int64_t n, int L,
+                          int64_t nch, const ChainParams* cps, const double* noise,
+                          const double* pstart, double* rec, double* g, double* phi, double* logs,
+                          double* pf, const double* const* ys, double* alpha_loc, double* asend,
+                          bool compact, bool fast_ok, double* mom) {
+  if (mom) {   // the chains' logpdf: the data filter's moments only (no noise vector, no pf)
+    launch_phase3_blocks<D, false, true, false, false, true>(grid, st, t, n, L, nch, cps, nullptr,
+                                                             pstart, nullptr, nullptr, phi, logs,
+                                                             nullptr, ys, nullptr, asend, mom,
+                                                             fast_ok);
+    return;
+  }
+#define GPAR_P3(C, Y, NZ) \
+  launch_phase3_pf<D, C, Y, NZ>(grid, st, t, n, L, nch, cps, noise, pstart, rec, g, phi, logs, pf, \
+                                ys, alpha_loc, asend, fast_ok)
+  const bool y = ys != nullptr, nz = noise != nullptr;
+  if (compact) {
+    if (y) { if (nz) GPAR_P3(true, true, true); else GPAR_P3(true, true, false); }
+    else { if (nz) GPAR_P3(true, false, true); else GPAR_P3(true, false, false); }
+  } else {
+    if (y) { if (nz) GPAR_P3(false, true, true); else GPAR_P3(false, true, false); }
+    else { if (nz) GPAR_P3(false, false, true); else GPAR_P3(false, false, false); }
+  }
+#undef GPAR_P3
+}
+
 void launch_gains(hipStream_t st, int sdim, const double* t, int64_t n, int L, int64_t nch,
                   int nchains, const ChainParamsHost* cps_dev, const double* noise,
                   double* agg, double* pstart, double* rec, double* g, double* phi,
                   double* logs, double* pf, const double* const* ys, double* alpha_loc,
-                  double* asend, bool compact) {
+                  double* asend, bool compact, bool ys_aligned16, double* moments) {
   const ChainParams* cps = reinterpret_cast<const ChainParams*>(cps_dev);
   dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
   GPAR_DISPATCH_D(sdim, {
     gains_phase1<DD><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, agg);
     gains_phase2<DD><<<nchains, 256, 0, st>>>(nch, agg, pstart);
-    if (compact)
-      gains_phase3<DD, true><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, pstart, rec, g, phi,
-                                                   logs, pf, ys, alpha_loc, asend);
-    else
-      gains_phase3<DD, false><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, pstart, rec, g, phi,
-                                                    logs, pf, ys, alpha_loc, asend);
+    // the fast phase 3 stages its inputs by 16-byte LDS-DMA: every input array 16-byte aligned
+    const bool a16 = ((uintptr_t)t % 16 == 0) && ((uintptr_t)noise % 16 == 0) && (!ys || ys_aligned16);
+    launch_phase3<DD>(grid, st, t, n, L, nch, cps, noise, pstart, rec, g, phi, logs, pf, ys,
+                      alpha_loc, asend, compact, a16, moments);
   });
 }
 
@@ -1817,6 +2321,11 @@ void launch_carry(hipStream_t st, int sdim, const double* phi, int64_t phistride
     GPAR_CARRY_LAUNCH(false);
   }
 #undef GPAR_CARRY_LAUNCH
+}
+
+void launch_chain_lml_mom(hipStream_t st, int sdim, const double* logs, const double* mom,
+                          const double* cin, int64_t nch, int64_t n, int nchains, double* lml) {
+  GPAR_DISPATCH_D(sdim, chain_lml_mom<DD><<<nchains, 256, 0, st>>>(logs, mom, cin, nch, n, lml));
 }
 
 void launch_gains_adjoint(hipStream_t st, int sdim, const double* rec, int64_t n, int L,

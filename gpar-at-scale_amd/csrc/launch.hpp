@@ -92,7 +92,13 @@ void launch_gains(hipStream_t st, int sdim, const double* t, int64_t n, int L, i
                   int nchains, const ChainParamsHost* cps_dev, const double* noise,
                   double* agg, double* pstart, double* rec, double* g, double* phi,
                   double* logs, double* pf, const double* const* ys = nullptr,
-                  double* alpha_loc = nullptr, double* asend = nullptr, bool compact = false);
+                  double* alpha_loc = nullptr, double* asend = nullptr, bool compact = false,
+                  bool ys_aligned16 = false, double* moments = nullptr);
+// the chains' logpdf from the gains' moments (moments != null in launch_gains; kMomStride doubles
+// per chunk) and the carried chunk states cin [nchains][nch][4]
+constexpr int kGainsMomStride = 12;
+void launch_chain_lml_mom(hipStream_t st, int sdim, const double* logs, const double* mom,
+                          const double* cin, int64_t nch, int64_t n, int nchains, double* lml);
 // compact gains records {K, rs, pad} (gains_phase3<D, true>): doubles per step
 inline int crec_size(int sdim) { return sdim == 1 ? 2 : 4; }
 int dp_bucket(int d);
