@@ -145,8 +145,7 @@ def main():
     # the CPU baseline runs in a child process started before anything touches the GPU, so it
     # overlaps the inputs and the warm-up steps; it is joined before the timed region
     cpu_child = None
-    if (world0 == 1 and not args.no_cpu_baseline and not cfg0.get("temporal", False)
-            and args.shard is None and args.api == "batched"):
+    if (world0 == 1 and not args.no_cpu_baseline and args.shard is None and args.api == "batched"):
         cpu_child = start_cpu_baseline(args)
 
     import torch
@@ -559,6 +558,34 @@ def main():
                       "ok": bool(max(rels) <= 1e-9),
                       "what": "-nlml of the timed run's last step at its fitted theta vs a fresh "
                               "whole-chip single-output gpar_dtc_objective there (rel <= 1e-9)"}
+    if (rank == 0 and temporal and cpu_child is not None
+            and os.path.getsize(cpu_child.check_path) > 0):
+        # the C port's chain logpdfs (every chain, N) and chain 1's smoothed prediction on the merged
+        # grid at SSM_CHECK_THETA, computed by the CPU baseline child on this run's data, against
+        # gpar_lgssm_logpdf / gpar_lgssm_smooth (untimed)
+        ref = np.load(cpu_child.check_path)
+        t_h, ts_h = t_d.cpu().numpy(), ts_d.cpu().numpy()
+        Yc = Y_d[:, [p - 1 for p in mine]].T.contiguous().cpu().numpy()
+        th = np.tile(np.array([SSM_CHECK_THETA]), (len(mine), 1))
+        g_lml = np.asarray(G.lgssm_logpdf_batch(t_h, Yc, th, cfg["out_kernel"], device=local))
+        tm, order, is_test, _ = merged_sde_grid(t_h, ts_h, SSM_CHECK_THETA[2])
+        y0 = np.where(is_test, 0.0, np.concatenate([Yc[0], np.zeros(len(ts_h))])[order])
+        gm, gv = G.lgssm_smooth_batch(tm, y0[None, :], th[:1], cfg["out_kernel"],
+                                      noise=np.where(is_test, 1e10, -1.0), device=local)
+        gm, gv = np.asarray(gm)[0][is_test], np.asarray(gv)[0][is_test]
+        lrel = float(np.max(np.abs(g_lml - ref["lml"]) / np.abs(ref["lml"])))
+        mex = float(np.max(np.abs(gm - ref["mean"]) / (1e-9 * np.abs(ref["mean"]) + 1e-10 * np.abs(ref["mean"]).max())))
+        vex = float(np.max(np.abs(gv - ref["var"]) / (1e-9 * np.abs(ref["var"]) + 1e-12 * np.abs(ref["var"]).max())))
+        self_check = {"cpu_port": {
+            "reference": "C port (oracle/cpu_ref, pinned to the numpy oracle by tests/test_cpu_ref.py), "
+                         "run by the cpu_baseline child on this data",
+            "theta": list(SSM_CHECK_THETA), "chains": len(mine), "lml_max_rel": lrel,
+            "mean_excess": mex, "var_excess": vex,
+            "ok": bool(lrel <= 1e-10 and mex <= 1.0 and vex <= 1.0),
+            "what": "every chain's logpdf at N (rel <= 1e-10) and chain 1's smoothed mean / variance at "
+                    "t* on the merged grid (rtol 1e-9, atol 1e-10 / 1e-12 max|ref|; *_excess <= 1 "
+                    "passes), against the port"}}
+        self_check["ok"] = self_check["cpu_port"]["ok"]
     p_chk = check_output(P)
     if (rank == 0 and cpu_child is not None and p_chk in gpar_out and not host
             and os.path.getsize(cpu_child.check_path) > 0):
@@ -819,7 +846,30 @@ def main():
                                         "the other lane, not a kernel duration")
         if temporal:
             out["metric"] = "temporal-only LGSSM fit+smooth (Matern-3/2 chains), pts*chains/s"
+            out["unit"] = "pts*chains/s"
             out["roofline"] = None
+            out.pop("roofline_whiten", None)
+            for fam, key in (("chains_logpdf", "roofline"), ("chains_smooth", "roofline_smooth")):
+                fn, fms = ctx.kernel_stats(fam)
+                if fn:
+                    w = ctx.kernel_work(fam)
+                    ga = w / (fms * 1e-3) / 1e9
+                    out[key] = {"bound": "hbm", "achieved": ga, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                "frac": ga / HBM_PEAK_GBS, "traffic": None, "launches": fn,
+                                "avg_ms": fms / fn, "ms_per_step": fms / args.steps,
+                                "bytes_per_launch": w / fn}
+            if "roofline" in out and out["roofline"]:
+                out["roofline"].update(
+                    kernel="chains_logpdf: gains_phase1 + gains_phase2 + gains_phase3 (moments) + "
+                           "the carry + chain_lml_mom, one HIP-event span per NM round",
+                    bytes="8 N (t) + 8 N per active chain (y) per launch; the per-chunk outputs "
+                          "(~0.7 B per step and chain) not counted")
+            if out.get("roofline_smooth"):
+                out["roofline_smooth"].update(
+                    kernel="chains_smooth: gains with covariances + whiten_vec + carries + "
+                           "adjoint + smooth_mean + cov_smooth, one span on the merged grid",
+                    bytes="8 n (t) + 8 n (noise) + 24 n per chain (y in, mean and variance out), "
+                          "n = N + N*")
             out["config"]["workload"] = f"temporal-only chains fit+smooth ({args.config})"
             out["config"]["time_kernel"] = cfg["out_kernel"]
         if cpu_res is not None:
@@ -1028,6 +1078,10 @@ def cpu_baseline_child(args):
     cfg = dict(CONFIGS[args.config])
     if args.evals:
         cfg["evals"] = args.evals
+    if cfg.get("temporal", False):
+        print(json.dumps(ssm_cpu_baseline(cfg["N"], cfg["P"], cfg["evals"], cfg["out_kernel"],
+                                          check_path=args.cpu_check_file)), flush=True)
+        return
     res = cpu_baseline(cfg["N"], cfg["N"], cfg["M"], cfg["P"], cfg["evals"], cfg["out_kernel"],
                        qu_kuu_noise=not args.qu_noise_free, check_path=args.cpu_check_file)
     print(json.dumps(res), flush=True)
@@ -1170,6 +1224,69 @@ def cpu_baseline(N, NS, M, P, EV, out_kernel, n_ratio=100_000, qu_kuu_noise=True
                       f"(N={N}, M={M}) = {t_eval:.2f}s + 1 analytic predict (N={N}, N*={NS}) = "
                       f"{t_pred:.2f}s; job = {P - 1} outputs x ({EV} evals + 1 predict) = {t_job:.0f}s "
                       "(no extrapolation in N)"}
+
+
+# the fixed chain hyperparameters (l, process sd, noise sd) of the ssm config's CPU timing and
+# self-check
+SSM_CHECK_THETA = (1.5, 1.2, 0.4)
+
+
+def merged_sde_grid(t, t_star, noise_sd):
+    """get_sde_predictions' smoothing grid (temporal_gp_inference.jl:93-113): training and test
+    times merged (stable), R = sigma^2 on training steps and 1e10 on test steps.  Returns
+    (t_merged, order, is_test, R)."""
+    tc = np.concatenate([t, t_star])
+    order = np.argsort(tc, kind="stable")
+    is_test = order >= len(t)
+    R = np.where(is_test, 1e10, noise_sd * noise_sd)
+    return tc[order], order, is_test, R
+
+
+def ssm_cpu_baseline(N, P, EV, kind, check_path=None):
+    """The ssm config's CPU baseline: the C port (oracle/cpu_ref: gains, decorrelate, RTS smoother
+    mean and variance, pinned to the numpy oracle by tests/test_cpu_ref.py) on the bench's own P
+    chains, one chain per pool thread (ctypes releases the GIL; each chain's recursion is
+    sequential).  Timed: one NM round = every chain's logpdf at N (temporal_gp_inference.jl:78), and
+    the smoothing of every chain on the merged grid of N + N* steps (:93-113); job = EV rounds +
+    the smoothing, as the GPU job runs (g_tol = -1: exactly EV evaluations per chain).  The chain
+    logpdfs and chain 1's predicted mean / variance at SSM_CHECK_THETA go to check_path for the
+    bench's self-check."""
+    from concurrent.futures import ThreadPoolExecutor
+    sys.path.insert(0, ROOT)
+    from oracle import cpu_ref as CR
+    from gparatscale import data as D
+    ds = D.gpar_dataset(N, P, seed=0, observation_noise=0.8)
+    t, Y, ts = ds["t"], ds["Y"], ds["t_star"]
+    ys = [np.ascontiguousarray(Y[:, p]) for p in range(P)]
+    l, pv, ns = SSM_CHECK_THETA
+    workers = max(1, min(P, _cpu_threads()))
+    tm, order, is_test, R = merged_sde_grid(t, ts, ns)
+    ym = [np.where(is_test, 0.0, np.concatenate([y, np.zeros(len(ts))])[order]) for y in ys]
+    CR.lgssm_logpdf(kind, t[:4096], ys[0][:4096], l, pv * pv, ns * ns)   # warm-up, untimed
+    with ThreadPoolExecutor(workers) as ex:
+        rounds = []
+        for _ in range(3):
+            t0 = time.perf_counter()
+            lml = list(ex.map(lambda y: CR.lgssm_logpdf(kind, t, y, l, pv * pv, ns * ns), ys))
+            rounds.append(time.perf_counter() - t0)
+        t_round = float(np.median(rounds))
+        t0 = time.perf_counter()
+        sm = list(ex.map(lambda y: CR.lgssm_smooth(kind, tm, y, l, pv * pv, ns * ns, rvec=R), ym))
+        t_smooth = time.perf_counter() - t0
+    if check_path:
+        m0, v0 = sm[0]
+        np.savez(check_path, lml=np.array(lml), theta=np.array(SSM_CHECK_THETA),
+                 mean=m0[is_test], var=v0[is_test])
+    t_job = EV * t_round + t_smooth
+    return {"value": N * P / t_job, "unit": "pts*chains/s", "cores": workers, "kind": "port",
+            "host_cpu": _cpu_model(), "round_seconds": t_round, "smooth_seconds": t_smooth,
+            "job_seconds": t_job,
+            "ran": "in a child process beside the GPU warm-up (joined before the timed region)",
+            "sample": f"C restatement (oracle/cpu_ref), {P} chains over {workers} threads (one chain "
+                      f"per thread), the bench's own data at theta = {SSM_CHECK_THETA}: one NM round "
+                      f"(every chain's logpdf, N={N}) = {t_round:.3f}s (median of 3) + the smoothing "
+                      f"of every chain on the merged grid (N + N* = {len(tm)}) = {t_smooth:.2f}s; job "
+                      f"= {EV} rounds + smoothing = {t_job:.2f}s (no extrapolation in N)"}
 
 
 if __name__ == "__main__":

@@ -536,8 +536,8 @@ struct PredPrep {
 std::vector<QuPre> run_q_u_batch(gpar_ctx* c, const std::vector<DevProblem>& P,
                                         const std::vector<Theta>& T, const FitKeep& keep,
                                         bool want_cov);
-void chains_logpdf(gpar_ctx* c, int nchains, int64_t n, const double* t, const double* y,
-                          int64_t ldy, int kernel, int sdim, const double* theta, double* lml);
+void chains_logpdf(gpar_ctx* c, const std::vector<const double*>& ys, int64_t n, const double* t,
+                   int sdim, const double* theta, double* lml);
 
 
 // --------------------------------------------------------------------------- posterior paths

@@ -4,9 +4,12 @@
 
 namespace gpar {
 
-// logpdf of independent LGSSM chains sharing t (device pointers).
-void chains_logpdf(gpar_ctx* c, int nchains, int64_t n, const double* t, const double* y,
-                          int64_t ldy, int kernel, int sdim, const double* theta, double* lml) {
+// logpdf of independent LGSSM chains sharing t (device pointers; ys: each chain's data vector).
+// Timed "chains_logpdf": algorithmic bytes 8 n (t, once) + 8 n per chain (y); the per-chunk
+// outputs (about 0.7 bytes per step and chain) are not counted.
+void chains_logpdf(gpar_ctx* c, const std::vector<const double*>& ys, int64_t n, const double* t,
+                   int sdim, const double* theta, double* lml) {
+  const int nchains = (int)ys.size();
   std::vector<ChainParamsHost> cps(nchains);
   for (int i = 0; i < nchains; ++i) {
     const double l = theta[3 * i], pv = theta[3 * i + 1], ns = theta[3 * i + 2];
@@ -20,19 +23,20 @@ void chains_logpdf(gpar_ctx* c, int nchains, int64_t n, const double* t, const d
   // the carry gives each chunk's incoming state and sum alpha_k^2 follows from the moments
   // (r05; before, the gains wrote 160 bytes per step and chain and whiten_vec / vec_fix read them
   // back)
-  std::vector<const double*> ys(nchains);
-  for (int i = 0; i < nchains; ++i) ys[i] = y + (size_t)i * ldy;
   double* send = ws<double>(c, "chain_send", (size_t)nchains * nch * 4);
   double* cin = ws<double>(c, "chain_cin", (size_t)nchains * nch * 4);
   double* mom = ws<double>(c, "chain_mom", (size_t)nchains * nch * kGainsMomStride);
   double* dl = ws<double>(c, "chain_lml", nchains);
   GainsPlan gp = plan_gains(c, sdim, t, n, cps, nullptr, false, "chain", &ys, nullptr, send, false,
                             mom);
-  gp.launch(c->stream, 0, nchains);
-  const GainsOut& g = gp.o;
-  run_carry(c, sdim, g.phi, g.phistride, send, cin, nch * 4, nch, 1, 1, nchains, "chainc");
-  launch_chain_lml_mom(c->stream, sdim, g.logs, mom, cin, nch, n, nchains, dl);
-  check_launch("chains_logpdf");
+  {
+    Timed tm_(c, "chains_logpdf", 8.0 * (double)n * (1.0 + nchains));
+    gp.launch(c->stream, 0, nchains);
+    const GainsOut& g = gp.o;
+    run_carry(c, sdim, g.phi, g.phistride, send, cin, nch * 4, nch, 1, 1, nchains, "chainc");
+    launch_chain_lml_mom(c->stream, sdim, g.logs, mom, cin, nch, n, nchains, dl);
+    check_launch("chains_logpdf");
+  }
   d2h(c, lml, dl, nchains);
   sync(c);
 }
@@ -46,6 +50,9 @@ void chains_smooth(gpar_ctx* c, int nchains, int64_t n, const double* t, const d
                           const std::vector<ChainParamsHost>& cps, double* mean, double* var,
                           int64_t ldo) {
   const int64_t nch = (n + kChunk - 1) / kChunk;
+  // Timed "chains_smooth": algorithmic bytes 8 n (t) + 8 n (noise, when given) + 24 n per chain
+  // (y in, mean and variance out)
+  Timed tm_(c, "chains_smooth", 8.0 * (double)n * ((noise ? 2.0 : 1.0) + 3.0 * nchains));
   GainsOut g = run_gains(c, sdim, t, n, cps, noise, /*want_pf=*/true, "sm");
   double* u = ws<double>(c, "sm_u", (size_t)nchains * n);
   double* send = ws<double>(c, "sm_send", (size_t)nchains * nch * 4);
@@ -107,7 +114,9 @@ int32_t gpar_lgssm_logpdf(gpar_ctx* ctx, int32_t nchains, int64_t n, const doubl
     ldy = n;
   }
   std::vector<double> lml(nchains);
-  chains_logpdf(ctx, nchains, n, dt, dy, ldy, kernel, sdim, theta, lml.data());
+  std::vector<const double*> ys(nchains);
+  for (int i = 0; i < nchains; ++i) ys[i] = dy + (size_t)i * ldy;
+  chains_logpdf(ctx, ys, n, dt, sdim, theta, lml.data());
   for (int i = 0; i < nchains; ++i) lml_out[i] = lml[i];
   API_END(ctx)
 }
@@ -186,20 +195,21 @@ int32_t gpar_sde_predictions(gpar_ctx* ctx, int32_t nchains, int64_t n, const do
   for (int i = 0; i < nchains; ++i)
     nm.emplace_back(std::vector<double>(log_theta0 + 3 * i, log_theta0 + 3 * i + 3), o.max_evals,
                     o.max_iterations, o.g_tol, o.time_limit);
-  double* ysub = ws<double>(ctx, "sp_ysub", (size_t)nchains * n);
   while (true) {
     std::vector<int> act;
     for (int i = 0; i < nchains; ++i)
       if (!nm[i].done()) act.push_back(i);
     if (act.empty()) break;
+    // the active chains' own data columns (no copy into a packed block)
     std::vector<double> th(3 * act.size());
+    std::vector<const double*> ys(act.size());
     for (size_t a = 0; a < act.size(); ++a) {
       const auto& x = nm[act[a]].ask();
       for (int q = 0; q < 3; ++q) th[3 * a + q] = unpack(x[q]);
-      HIPCHECK(hipMemcpyAsync(ysub + a * n, dy + (size_t)act[a] * ldyd, n * sizeof(double), hipMemcpyDeviceToDevice, ctx->stream));
+      ys[a] = dy + (size_t)act[a] * ldyd;
     }
     std::vector<double> lml(act.size());
-    chains_logpdf(ctx, (int)act.size(), n, dt, ysub, n, kernel, sdim, th.data(), lml.data());
+    chains_logpdf(ctx, ys, n, dt, sdim, th.data(), lml.data());
     for (size_t a = 0; a < act.size(); ++a) {
       double f = -lml[a];
       if (!std::isfinite(f)) f = INFINITY;

@@ -245,6 +245,32 @@ static void inv3(int d, const double M[3][3], double R[3][3]) {
   }
 }
 
+/* RTS smoother gain G_k = Pf_k A_{k+1}^T Pp_{k+1}^{-1} (3x3 row-major, zero-padded), k < n - 1. */
+static void smoother_gain(int d, const double* rec, const double* pf, const double* pp, int64_t k,
+                          double* G) {
+  double Pf[3][3], A[3][3], Pp[3][3], Pi[3][3], T[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      Pf[i][j] = pf[k * 9 + i * 3 + j];
+      A[i][j] = rec[(k + 1) * 16 + i * 3 + j];
+      Pp[i][j] = pp[(k + 1) * 9 + i * 3 + j];
+    }
+  inv3(d, Pp, Pi);
+  for (int i = 0; i < d; ++i)
+    for (int j = 0; j < d; ++j) {
+      double a = 0.0;
+      for (int q = 0; q < d; ++q) a += Pf[i][q] * A[j][q];
+      T[i][j] = a;
+    }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double a = 0.0;
+      if (i < d && j < d)
+        for (int q = 0; q < d; ++q) a += T[i][q] * Pi[q][j];
+      G[i * 3 + j] = a;
+    }
+}
+
 /* RTS smoother over every column of X; out[k*ldo + c] = first component of the smoothed state
  * mean (the `.m[1]` the reference reads, gpar_scaled_inference.jl:117-127).
  * pf, pp: filtered / predicted covariances from gpar_cpu_gains.  Scratch: 3*n*ncol doubles. */
@@ -259,30 +285,7 @@ int gpar_cpu_smooth_first(int kind, const double* rec, const double* pf, const d
     return 1;
   }
   gpar_cpu_filter(kind, rec, n, X, ldx, ncol, al, ncol, mf, ncol);
-  /* G_k = Pf_k A_{k+1}^T Pp_{k+1}^{-1} */
-  for (int64_t k = 0; k + 1 < n; ++k) {
-    double Pf[3][3], A[3][3], Pp[3][3], Pi[3][3], T[3][3];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) {
-        Pf[i][j] = pf[k * 9 + i * 3 + j];
-        A[i][j] = rec[(k + 1) * 16 + i * 3 + j];
-        Pp[i][j] = pp[(k + 1) * 9 + i * 3 + j];
-      }
-    inv3(d, Pp, Pi);
-    for (int i = 0; i < d; ++i)
-      for (int j = 0; j < d; ++j) {
-        double a = 0.0;
-        for (int q = 0; q < d; ++q) a += Pf[i][q] * A[j][q];
-        T[i][j] = a;
-      }
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) {
-        double a = 0.0;
-        if (i < d && j < d)
-          for (int q = 0; q < d; ++q) a += T[i][q] * Pi[q][j];
-        G[k * 9 + i * 3 + j] = a;
-      }
-  }
+  for (int64_t k = 0; k + 1 < n; ++k) smoother_gain(d, rec, pf, pp, k, G + k * 9);
   const int64_t nb = (ncol + CB - 1) / CB;
 #pragma omp parallel for schedule(dynamic, 1)
   for (int64_t b = 0; b < nb; ++b) {
@@ -313,6 +316,37 @@ int gpar_cpu_smooth_first(int kind, const double* rec, const double* pf, const d
   }
   free(mf); free(al); free(G);
   return 0;
+}
+
+/* Smoothed marginal variance of the first state component (the `.P[1,1]` of TemporalGPs smooth,
+ * temporal_gp_inference.jl:109-114): P^s_{n-1} = Pf_{n-1},
+ * P^s_k = Pf_k + G_k (P^s_{k+1} - Pp_{k+1}) G_k^T.  Data-independent; var[k] = P^s_k[0][0]. */
+void gpar_cpu_smooth_var(int kind, const double* rec, const double* pf, const double* pp, int64_t n,
+                         double* var) {
+  const int d = sde_dim(kind);
+  double Ps[3][3];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Ps[i][j] = pf[(n - 1) * 9 + i * 3 + j];
+  var[n - 1] = Ps[0][0];
+  for (int64_t k = n - 2; k >= 0; --k) {
+    double G[9], D[3][3], GD[3][3];
+    smoother_gain(d, rec, pf, pp, k, G);
+    for (int i = 0; i < d; ++i)
+      for (int j = 0; j < d; ++j) D[i][j] = Ps[i][j] - pp[(k + 1) * 9 + i * 3 + j];
+    for (int i = 0; i < d; ++i)
+      for (int j = 0; j < d; ++j) {
+        double a = 0.0;
+        for (int q = 0; q < d; ++q) a += G[i * 3 + q] * D[q][j];
+        GD[i][j] = a;
+      }
+    for (int i = 0; i < d; ++i)
+      for (int j = 0; j < d; ++j) {
+        double a = 0.0;
+        for (int q = 0; q < d; ++q) a += GD[i][q] * G[j * 3 + q];
+        Ps[i][j] = pf[k * 9 + i * 3 + j] + a;
+      }
+    var[k] = Ps[0][0];
+  }
 }
 
 int gpar_cpu_threads(void) {

@@ -12,6 +12,7 @@ numpy/scipy, as the reference leaves it to Julia's OpenBLAS:
 * ``compute_gpar_dtc_objective``        src/gp/dtc.jl:83-128
 * ``compute_q_u``                        src/gp/gpar_scaled_inference.jl:141-196
 * ``get_gpar_scaled_predictions_fixed``  src/gp/gpar_scaled_inference.jl:20-136 (analytic mode)
+* ``lgssm_logpdf`` / ``lgssm_smooth``     src/gp/temporal_gp_inference.jl:78,109-114 (one chain)
 
 One stated deviation, shared with the oracle and the GPU path: logdet Sigma = sum_k log S_k
 instead of the dense N x N LU of dtc.jl:96-99,123 (same quantity; the dense form is O(N^3)).
@@ -44,6 +45,8 @@ def load():
         lib.gpar_cpu_filter.argtypes = [I, P, I64, P, I64, I64, P, I64, P, I64]
         lib.gpar_cpu_smooth_first.argtypes = [I, P, P, P, I64, P, I64, I64, P, I64]
         lib.gpar_cpu_smooth_first.restype = I
+        lib.gpar_cpu_smooth_var.argtypes = [I, P, P, P, I64, P]
+        lib.gpar_cpu_smooth_var.restype = None
         lib.gpar_cpu_threads.restype = I
         _lib = lib
     return _lib
@@ -102,6 +105,25 @@ def smooth_first(kind, rec, pf, pp, X):
     if load().gpar_cpu_smooth_first(KIND[kind], _p(rec), _p(pf), _p(pp), n, _p(X2), c, c, _p(out), c):
         raise MemoryError("gpar_cpu_smooth_first")
     return out if X.ndim == 2 else out[:, 0]
+
+
+def lgssm_logpdf(kind, t, y, l, s, r):
+    """TemporalGPs ``logpdf(lgssm, y)`` of one temporal-only chain (temporal_gp_inference.jl:78):
+    -1/2 (n log 2 pi + sum_k log S_k + sum_k alpha_k^2).  s: process variance, r: noise variance."""
+    y = np.ascontiguousarray(y, dtype=np.float64)
+    rec, logs, _, _ = gains(kind, t, l, s, r)
+    al = decorrelate(kind, rec, y)
+    return -0.5 * (y.shape[0] * LOG2PI + logs + float(al @ al))
+
+
+def lgssm_smooth(kind, t, y, l, s, r, rvec=None):
+    """TemporalGPs ``smooth`` of one chain (temporal_gp_inference.jl:109-114): the smoothed mean
+    and marginal variance of the first state component, (n,) each."""
+    rec, _, pf, pp = gains(kind, t, l, s, r, rvec=rvec, covs=True)
+    mean = smooth_first(kind, rec, pf, pp, np.ascontiguousarray(y, dtype=np.float64))
+    var = np.empty(rec.shape[0])
+    load().gpar_cpu_smooth_var(KIND[kind], _p(rec), _p(pf), _p(pp), rec.shape[0], _p(var))
+    return mean, var
 
 
 def compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel="matern52", time_kernel="matern52",

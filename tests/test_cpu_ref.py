@@ -81,3 +81,49 @@ def test_qu_kuu_noise_branch_matches_oracle(CR, data, ok):
 def test_rejects_unsorted_times(CR):
     with pytest.raises(ValueError):
         CR.gains("matern52", np.array([0.0, 2.0, 1.0]), 1.0, 1.0, 0.1)
+
+
+@pytest.mark.parametrize("kind", ["matern12", "matern32", "matern52"])
+def test_lgssm_logpdf_and_smooth_match_oracle(CR, data, kind):
+    """The temporal-only chain (bench.py --config ssm's CPU baseline): logpdf and the RTS
+    smoother's mean and marginal variance of the C port against the numpy oracle, with and
+    without a per-step noise vector (get_sde_predictions' R = sigma^2 train / 1e10 test)."""
+    t, V, y, Z = data
+    l, pv, ns = 0.9, 1.4, 0.3
+    lg = O.create_lgssm(t, l, pv, ns, kind)
+    assert abs(CR.lgssm_logpdf(kind, t, y, l, pv * pv, ns * ns) - O.lgssm_logpdf(lg, y)) <= \
+        1e-10 * abs(O.lgssm_logpdf(lg, y))
+    ms, Ps = O.rts_smooth(lg, y)
+    cm, cv = CR.lgssm_smooth(kind, t, y, l, pv * pv, ns * ns)
+    np.testing.assert_allclose(cm, ms[:, 0], rtol=1e-9, atol=1e-11)
+    np.testing.assert_allclose(cv, Ps[:, 0, 0], rtol=1e-9, atol=1e-12)
+    R = np.where(np.arange(len(t)) % 4 == 0, 1e10, ns * ns)
+    lgr = O.create_lgssm(t, l, pv, ns, kind, noise_vector=R)
+    ms, Ps = O.rts_smooth(lgr, y)
+    cm, cv = CR.lgssm_smooth(kind, t, y, l, pv * pv, ns * ns, rvec=R)
+    np.testing.assert_allclose(cm, ms[:, 0], rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(cv, Ps[:, 0, 0], rtol=1e-8, atol=1e-12)
+
+
+def test_ssm_cpu_baseline_check_file(CR, tmp_path):
+    """bench.py --config ssm's CPU baseline at a small N: the job figure and the self-check file
+    (every chain's logpdf, chain 1's prediction at t*) agree with the numpy oracle."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "gpar-at-scale_amd", "python"))
+    sys.path.insert(0, ROOT)
+    import bench
+    from gparatscale import data as D
+    n, P = 3000, 3
+    chk = tmp_path / "ssm.npz"
+    r = bench.ssm_cpu_baseline(n, P, 5, "matern32", check_path=str(chk))
+    assert r["value"] > 0 and r["kind"] == "port" and r["cores"] >= 1
+    assert abs(r["job_seconds"] - (5 * r["round_seconds"] + r["smooth_seconds"])) < 1e-9
+    ref = np.load(chk)
+    ds = D.gpar_dataset(n, P, seed=0, observation_noise=0.8)
+    l, pv, ns = bench.SSM_CHECK_THETA
+    for p in range(P):
+        lo = O.lgssm_logpdf(O.create_lgssm(ds["t"], l, pv, ns, "matern32"), ds["Y"][:, p])
+        assert abs(ref["lml"][p] - lo) <= 1e-10 * abs(lo)
+    m, v = O.sde_predict_fixed(ds["t"], ds["Y"][:, 0], ds["t_star"], (l, pv, ns), "matern32")
+    np.testing.assert_allclose(ref["mean"], m, rtol=1e-8, atol=1e-10)
+    np.testing.assert_allclose(ref["var"], v, rtol=1e-8, atol=1e-12)
