@@ -479,6 +479,9 @@ def main():
             pred[fam].update(launches=pn, avg_ms=pms / pn, ms_per_step=pms / args.steps,
                              work_per_launch=ctx.kernel_work(fam) / pn)
     pwall_n, pwall_ms = ctx.kernel_stats("predictions")   # wall span of each call's predictions
+    # the temporal chains' spans, read before the untimed self-check adds launches of its own
+    chain_stats = {fam: (ctx.kernel_stats(fam), ctx.kernel_work(fam))
+                   for fam in ("chains_logpdf", "chains_smooth")}
     gram_work = ctx.kernel_work("gram")      # flops, N*M*(M+1) per launch
     wh_work = ctx.kernel_work("whiten")      # algorithmic HBM bytes (include/gpar_hip.h)
     try:   # telemetry only: never fails the line
@@ -850,9 +853,8 @@ def main():
             out["roofline"] = None
             out.pop("roofline_whiten", None)
             for fam, key in (("chains_logpdf", "roofline"), ("chains_smooth", "roofline_smooth")):
-                fn, fms = ctx.kernel_stats(fam)
+                (fn, fms), w = chain_stats[fam]
                 if fn:
-                    w = ctx.kernel_work(fam)
                     ga = w / (fms * 1e-3) / 1e9
                     out[key] = {"bound": "hbm", "achieved": ga, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                 "frac": ga / HBM_PEAK_GBS, "traffic": None, "launches": fn,

@@ -585,12 +585,12 @@ __global__ __launch_bounds__(256, 2) void gains_phase3(int64_t blk0, const doubl
 
 // ---------------------------------------------------------------------------- phase 3, fast path
 // The same recursion and outputs as gains_phase3 for the chains' whole blocks (256 chunks of
-// exactly L = 256 steps, no masked lane), with every memory operation of the step loop issued
-// by inline asm so that its waits are exact:
+// exactly L = 256 steps) and, in the same launch, each chain's masked last block, with the step
+// loop's memory operations counted so that its waits are exact:
 //   * the step inputs (t, and y or the noise vector) reach LDS by LDS-DMA (global_load_lds_dwordx4:
 //     two steps of the lane's chunk per instruction) into a per-wave ring of kG3Ring pair slots,
 //     one unrolled block (kG3Blk steps) ahead;
-//   * the record / fix-up row / alpha stores are asm too, kG3Stores(...) per block;
+//   * the record / fix-up row / alpha stores, g3_stores_per_block(...) per block, are counted;
 //   * at the top of block b, after issuing block b + 1's DMAs, `s_waitcnt vmcnt(S + 2 NA)` leaves
 //     block b - 1's S stores and block b + 1's 2 NA DMAs in flight and retires block b's DMAs:
 //     no step ever waits for a store.
@@ -633,9 +633,19 @@ __device__ __forceinline__ void g3_dma16(const double* src, uint32_t lds) {
 // never leaves its page) up to the last one holding a valid step.
 // (the masked block -- one per chain -- is allowed the whole register file: its selects would
 // otherwise spill, and one such block per chain never fills a CU anyway)
+// the kernel's LDS, shared by its two bodies (whole blocks and the masked last block)
+template <int D, bool HAS_Y, bool HAS_NOISE, bool MOM>
+struct G3Lds {
+  static constexpr int RP = Rec<D>::size + 1;
+  static constexpr int NA = 1 + (HAS_Y ? 1 : 0) + (HAS_NOISE ? 1 : 0);   // input arrays staged
+  double rbuf[4][MOM ? 1 : 64 * RP];
+  double abuf[4][MOM ? 1 : 64 * kG3Blk];
+  alignas(16) double ring[4][NA][kG3Ring][64 * 2];
+};
+
 template <int D, bool COMPACT, bool HAS_Y, bool HAS_NOISE, bool HAS_PF, bool MOM, bool MASKED>
-__global__ __launch_bounds__(256, MASKED ? 1 : 2) void gains_phase3_fast(
-    int64_t blk0, const double* __restrict__ t, int64_t n, int64_t nch,
+__device__ __forceinline__ void g3_body(
+    G3Lds<D, HAS_Y, HAS_NOISE, MOM>& sh, const double* __restrict__ t, int64_t n, int64_t nch,
     const ChainParams* __restrict__ cps,
     const double* __restrict__ noise, const double* __restrict__ pstart, double* __restrict__ rec,
     double* __restrict__ g, double* __restrict__ phi, double* __restrict__ logs,
@@ -649,11 +659,11 @@ __global__ __launch_bounds__(256, MASKED ? 1 : 2) void gains_phase3_fast(
   constexpr int S = g3_stores_per_block<D, COMPACT, HAS_PF, MOM, MASKED>(HAS_Y);
   constexpr int VM = S + 2 * NA;   // ops allowed in flight at a block's wait
   static_assert(VM <= 63, "vmcnt holds at most 63 outstanding operations");
-  __shared__ double rbuf[4][MOM ? 1 : 64 * RP];
-  __shared__ double abuf[4][MOM ? 1 : 64 * kG3Blk];
-  __shared__ __attribute__((aligned(16))) double ring[4][NA][kG3Ring][64 * 2];
+  auto& rbuf = sh.rbuf;
+  auto& abuf = sh.abuf;
+  auto& ring = sh.ring;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int64_t j = (blk0 + blockIdx.x) * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const int64_t jw = j - lane;
   const bool jv = !MASKED || j < nch;
   const int64_t jc = jv ? j : nch - 1;   // the chunk whose inputs this lane reads
@@ -801,12 +811,14 @@ __global__ __launch_bounds__(256, MASKED ? 1 : 2) void gains_phase3_fast(
         }
         const double ev = yin[u] - mm[0];
         if constexpr (MOM) {
+          // every term selected on live: a step past the chunk's end re-runs stale inputs (its
+          // tau may be negative, S_k then negative and rs NaN), so no product of it may reach ms
           const double al = live ? ev * rs : 0.0;
           ms[0] = fma(al, al, ms[0]);
           int e = 1 + D;
 #pragma unroll
           for (int i = 0; i < D; ++i) {
-            ms[1 + i] = fma(al, gk[i], ms[1 + i]);
+            ms[1 + i] = live ? fma(al, gk[i], ms[1 + i]) : ms[1 + i];
 #pragma unroll
             for (int q = i; q < D; ++q) {
               ms[e] = live ? fma(gk[i], gk[q], ms[e]) : ms[e];
@@ -900,6 +912,35 @@ __global__ __launch_bounds__(256, MASKED ? 1 : 2) void gains_phase3_fast(
 #pragma unroll
     for (int e = 0; e < kMomStride; ++e) mp_[e] = ms[e];
   }
+}
+
+// one launch per chain group: blocks 0 .. gridDim.x - 2 are whole (256 chunks of L steps), the
+// last block of each chain runs the masked body, concurrently with the others (a separate
+// launch of it used to serialise one more 256-step recursion behind the whole blocks)
+// (the full-record data-filter variants of the 3-state model need the whole register file for
+// the masked body: under a 2-blocks bound they spill)
+template <int D, bool COMPACT, bool HAS_Y, bool HAS_NOISE, bool HAS_PF>
+constexpr int g3_min_blocks() {
+  return (D == 3 && !COMPACT && HAS_Y && !HAS_NOISE && !HAS_PF) ? 1 : 2;
+}
+
+template <int D, bool COMPACT, bool HAS_Y, bool HAS_NOISE, bool HAS_PF, bool MOM>
+__global__ __launch_bounds__(256, (g3_min_blocks<D, COMPACT, HAS_Y, HAS_NOISE, HAS_PF>())) void
+gains_phase3_fast(
+    const double* __restrict__ t, int64_t n, int64_t nch, const ChainParams* __restrict__ cps,
+    const double* __restrict__ noise, const double* __restrict__ pstart, double* __restrict__ rec,
+    double* __restrict__ g, double* __restrict__ phi, double* __restrict__ logs,
+    double* __restrict__ pf, const double* const* __restrict__ ys, double* __restrict__ alpha_loc,
+    double* __restrict__ asend, double* __restrict__ mom) {
+  __shared__ G3Lds<D, HAS_Y, HAS_NOISE, MOM> sh;
+  if (blockIdx.x + 1 == gridDim.x)
+    g3_body<D, COMPACT, HAS_Y, HAS_NOISE, HAS_PF, MOM, true>(sh, t, n, nch, cps, noise, pstart, rec,
+                                                             g, phi, logs, pf, ys, alpha_loc,
+                                                             asend, mom);
+  else
+    g3_body<D, COMPACT, HAS_Y, HAS_NOISE, HAS_PF, MOM, false>(sh, t, n, nch, cps, noise, pstart,
+                                                              rec, g, phi, logs, pf, ys, alpha_loc,
+                                                              asend, mom);
 }
 
 // ---------------------------------------------------------------------------- whitening of Kfu columns
@@ -1002,7 +1043,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     const double* __restrict__ z, int64_t ldz, const double* __restrict__ zc, int64_t m,
     int64_t mp, int64_t n, int L, double inv_lo, double s_o, double* __restrict__ beta,
     int64_t ldb, double* __restrict__ send, int64_t mc, const double* __restrict__ g,
-    double* __restrict__ hsum) {
+    double* __restrict__ hsum, const ExpNegConsts ek) {
   typedef double d4 __attribute__((ext_vector_type(4)));
   constexpr int SD = Sde<TK>::d;
   constexpr int RS = Rec<SD>::size;
@@ -1169,7 +1210,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
       for (int ct = 0; ct < 4; ++ct) {
         double d2 = vn + zn[ct] - 2.0 * acc[ct][r];
         if constexpr (OK == KEQ) d2 = d2 > 0.0 ? d2 : 0.0;   // the Matern forms clamp in sqrt_pos
-        xt[wave][fq + 4 * r][ct * 16 + fr] = skappa_sq<OK>(d2, inv_lo, s_o);
+        xt[wave][fq + 4 * r][ct * 16 + fr] = skappa_sq_k<OK>(d2, inv_lo, s_o, ek);
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
@@ -2101,11 +2142,8 @@ static void launch_phase3_blocks(dim3 grid, hipStream_t st, const double* t, int
   constexpr int NA = 1 + (Y ? 1 : 0) + (NZ ? 1 : 0);
   if constexpr (g3_stores_per_block<D, C, PFX, MOM, true>(Y) + 2 * NA <= 63) {
     if (L == kG3L && fast_ok) {
-      if (gfull.x)
-        gains_phase3_fast<D, C, Y, NZ, PFX, MOM, false><<<gfull, 256, 0, st>>>(
-            0, t, n, nch, cps, noise, pstart, rec, g, phi, logs, pf, ys, alpha_loc, asend, mom);
-      gains_phase3_fast<D, C, Y, NZ, PFX, MOM, true><<<glast, 256, 0, st>>>(
-          last, t, n, nch, cps, noise, pstart, rec, g, phi, logs, pf, ys, alpha_loc, asend, mom);
+      gains_phase3_fast<D, C, Y, NZ, PFX, MOM><<<grid, 256, 0, st>>>(
+          t, n, nch, cps, noise, pstart, rec, g, phi, logs, pf, ys, alpha_loc, asend, mom);
       return;
     }
   }
@@ -2172,7 +2210,10 @@ void launch_gains(hipStream_t st, int sdim, const double* t, int64_t n, int L, i
     gains_phase1<DD><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, agg);
     gains_phase2<DD><<<nchains, 256, 0, st>>>(nch, agg, pstart);
     // the fast phase 3 stages its inputs by 16-byte LDS-DMA: every input array 16-byte aligned
-    const bool a16 = ((uintptr_t)t % 16 == 0) && ((uintptr_t)noise % 16 == 0) && (!ys || ys_aligned16);
+    // (GPAR_GAINS_FAST=0: the general kernel everywhere, for the fast path's bit-identity test)
+    const char* fe = std::getenv("GPAR_GAINS_FAST");
+    const bool a16 = ((uintptr_t)t % 16 == 0) && ((uintptr_t)noise % 16 == 0) &&
+                     (!ys || ys_aligned16) && !(fe && fe[0] == '0');
     launch_phase3<DD>(grid, st, t, n, L, nch, cps, noise, pstart, rec, g, phi, logs, pf, ys,
                       alpha_loc, asend, compact, a16, moments);
   });
@@ -2223,10 +2264,10 @@ static void launch_whiten_mfma_k(hipStream_t st, int dp, dim3 grid, const double
                                  int L, double inv_lo, double s_o, double* beta, int64_t ldb,
                                  double* send, int64_t mc, const double* g, double* hsum) {
   switch (dp) {
-    case 16: whiten_kfu_mfma<TK, OK, 16><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
-    case 32: whiten_kfu_mfma<TK, OK, 32><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
-    case 48: whiten_kfu_mfma<TK, OK, 48><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
-    default: whiten_kfu_mfma<TK, OK, 64><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case 16: whiten_kfu_mfma<TK, OK, 16><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum, exp_neg_consts()); break;
+    case 32: whiten_kfu_mfma<TK, OK, 32><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum, exp_neg_consts()); break;
+    case 48: whiten_kfu_mfma<TK, OK, 48><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum, exp_neg_consts()); break;
+    default: whiten_kfu_mfma<TK, OK, 64><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum, exp_neg_consts()); break;
   }
 }
 

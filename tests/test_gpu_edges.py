@@ -152,3 +152,34 @@ def test_fresh_noncontiguous_device_inputs():
         tt = torch.from_numpy(t).to(dev) + 0.0
         got = G.compute_gpar_dtc_objective(Yt[:, :3], Zt, tt, Yt[:, 3], theta)
         assert abs(got - host) <= 1e-12 * abs(host), (got, host)
+
+
+@pytest.mark.parametrize("kind", ["matern12", "matern32", "matern52"])
+def test_gains_fast_path_bit_identical_to_general(kind, monkeypatch):
+    """The gains' phase-3 fast path (LDS-DMA staged inputs; its masked last block re-runs stale
+    inputs past each chunk's end) against the general kernel (GPAR_GAINS_FAST=0): chain logpdfs
+    (the moments form), smoothing with a noise vector, and a DTC objective are bit-identical, at
+    chunk counts inside one block and across blocks, with short last chunks, large time gaps
+    (negative stale steps) and short length scales."""
+    rng = np.random.default_rng(11)
+    for n in (1300, 256 * 300 + 7):
+        t = np.cumsum(rng.exponential(0.05, n) + np.where(rng.random(n) < 0.01, 3.0, 0.0))
+        Y = np.ascontiguousarray(rng.normal(size=(3, n)))
+        th = np.array([[0.05, 1.3, 0.2], [0.5, 0.7, 0.6], [4.0, 2.0, 0.05]])
+        noise = np.where(np.arange(n) % 5 == 0, 1e10, -1.0)
+        out = {}
+        for fast in ("1", "0"):
+            monkeypatch.setenv("GPAR_GAINS_FAST", fast)
+            lml = np.asarray(G.lgssm_logpdf_batch(t, Y, th, kind))
+            m, v = G.lgssm_smooth_batch(t, Y, th, kind, noise=noise)
+            out[fast] = (lml, np.asarray(m), np.asarray(v))
+        for a, b in zip(out["1"], out["0"]):
+            assert np.all(np.isfinite(a))
+            assert np.array_equal(a, b)
+    t, V, Z, y = _case(1300, 3, 40, 3)
+    vals = []
+    for fast in ("1", "0"):
+        monkeypatch.setenv("GPAR_GAINS_FAST", fast)
+        vals.append(G.compute_gpar_dtc_objective(V, Z, t, y, (1.2, 0.9, 1.1, 1.1, 0.3),
+                                                 time_kernel=kind))
+    assert np.isfinite(vals[0]) and vals[0] == vals[1]
