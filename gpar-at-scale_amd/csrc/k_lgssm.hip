@@ -1043,7 +1043,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     const double* __restrict__ z, int64_t ldz, const double* __restrict__ zc, int64_t m,
     int64_t mp, int64_t n, int L, double inv_lo, double s_o, double* __restrict__ beta,
     int64_t ldb, double* __restrict__ send, int64_t mc, const double* __restrict__ g,
-    double* __restrict__ hsum, const ExpNegConsts ek) {
+    double* __restrict__ hsum) {
   typedef double d4 __attribute__((ext_vector_type(4)));
   constexpr int SD = Sde<TK>::d;
   constexpr int RS = Rec<SD>::size;
@@ -1210,7 +1210,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
       for (int ct = 0; ct < 4; ++ct) {
         double d2 = vn + zn[ct] - 2.0 * acc[ct][r];
         if constexpr (OK == KEQ) d2 = d2 > 0.0 ? d2 : 0.0;   // the Matern forms clamp in sqrt_pos
-        xt[wave][fq + 4 * r][ct * 16 + fr] = skappa_sq_k<OK>(d2, inv_lo, s_o, ek);
+        xt[wave][fq + 4 * r][ct * 16 + fr] = skappa_sq<OK>(d2, inv_lo, s_o);
       }
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
@@ -2264,10 +2264,10 @@ static void launch_whiten_mfma_k(hipStream_t st, int dp, dim3 grid, const double
                                  int L, double inv_lo, double s_o, double* beta, int64_t ldb,
                                  double* send, int64_t mc, const double* g, double* hsum) {
   switch (dp) {
-    case 16: whiten_kfu_mfma<TK, OK, 16><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum, exp_neg_consts()); break;
-    case 32: whiten_kfu_mfma<TK, OK, 32><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum, exp_neg_consts()); break;
-    case 48: whiten_kfu_mfma<TK, OK, 48><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum, exp_neg_consts()); break;
-    default: whiten_kfu_mfma<TK, OK, 64><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum, exp_neg_consts()); break;
+    case 16: whiten_kfu_mfma<TK, OK, 16><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case 32: whiten_kfu_mfma<TK, OK, 32><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    case 48: whiten_kfu_mfma<TK, OK, 48><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
+    default: whiten_kfu_mfma<TK, OK, 64><<<grid, 256, 0, st>>>(rec, v, ldv, d, z, ldz, zc, m, mp, n, L, inv_lo, s_o, beta, ldb, send, mc, g, hsum); break;
   }
 }
 
