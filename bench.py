@@ -357,12 +357,15 @@ def main():
             # inference-input-dependent predictions run inside it, and each predicted mean is
             # broadcast by its owner as soon as it is ready (shard.py)
             post = None
+            t_fit0 = time.perf_counter()
             if problems:
                 post = G.fit_posterior(problems, x0, max_evals=EV, g_tol=-1.0, device=local,
                                        keep=keep)
                 for i, p in enumerate(gpar_out):
                     res[p] = post.theta[i]
+            torch.cuda.synchronize()
             t_sw = time.perf_counter()
+            last.setdefault("fit_s", []).append(t_sw - t_fit0)
             if shard_of:
                 # one rank of the W-way job on this GPU: its own fits above, then the whole
                 # P-output sweep (the other ranks' outputs from the untimed posteriors of the
@@ -448,6 +451,7 @@ def main():
     for _ in range(args.steps):
         theta = step()
     torch.cuda.synchronize()
+    busy = (time.perf_counter() - ts0) * 1e3 / args.steps   # this rank's own work, before the barrier
     if world > 1:
         dist.barrier()
     el = (time.perf_counter() - ts0) * 1e3 / args.steps
@@ -455,6 +459,18 @@ def main():
         e = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
         el = float(e[0])
+    # every rank's own times in the line (untimed gather): its step up to the closing barrier and,
+    # with chained inputs, its fits + posteriors and its part of the sweep (waits included)
+    mine_t = {"step_busy_ms": busy,
+              "fit_ms": 1e3 * float(np.mean(last["fit_s"][-args.steps:])) if last.get("fit_s") else None,
+              "sweep_ms": 1e3 * float(np.mean(last["sweep_s"][-args.steps:])) if last.get("sweep_s") else None,
+              "outputs": mine}
+    times_all = [mine_t]
+    if world > 1:
+        times_all = [None] * world
+        dist.all_gather_object(times_all, mine_t)
+    for ri, tt in zip(rank_info, times_all):
+        ri.update(tt)
     gram_n, gram_ms = ctx.kernel_stats("gram")
     wh_n, wh_ms = ctx.kernel_stats("whiten")
     rnd_n, rnd_ms = ctx.kernel_stats("fit_round")   # round-by-round fits: entry -> values per round

@@ -3,6 +3,7 @@
 // with VGPR-form MFMA accumulators).
 #pragma once
 #include "device_common.hpp"
+#include "launch.hpp"
 
 namespace gpar {
 
@@ -38,17 +39,22 @@ __device__ __forceinline__ int d2_base_of(int r) {
 // v3 partial-tile slots per wave (OFF: 4 x 8 tiles; DG: 18 of the 32 used)
 constexpr int kF3T = 32;
 
+// (GramGroupPtrs, the grouped Gram's per-output pointer table: launch.hpp)
+
 // v3 launchers living in k_gram3v.hip (VGPR-form MFMA accumulators)
 // sw / rows_w: the first sw time splits take rows_w rows each, the others `rows` (sw = 0: all)
 void launch_gram3_dg(hipStream_t st, int nwg, const double* beta, int64_t ldb, int64_t n,
                      const double* alpha, int npan, int ndg, int sdg, int64_t rows,
                      int64_t slot0, double* part, double* rpart, int bt_lo = 0, int bt_cnt = -1,
-                     int sw = 0, int64_t rows_w = 0);
+                     int sw = 0, int64_t rows_w = 0, const GramGroupPtrs* grp = nullptr,
+                     int ngrp = 1);
 void launch_gram3_corr_slim(hipStream_t st, int sdim, const double* ecor, const double* cin,
                             const double* qv, int64_t mc, int64_t nch, int npan, int noff, int ndg,
-                            int soff, int sdg, int ncs, double* part, double* rpart);
+                            int soff, int sdg, int ncs, double* part, double* rpart,
+                            const GramGroupPtrs* grp = nullptr, int ngrp = 1);
 void launch_gram3_corr(hipStream_t st, int sdim, const double* ecor, const double* cin,
                        const double* qv, int64_t mc, int64_t nch, int npan, int noff, int ndg,
-                       int soff, int sdg, int ncs, double* part, double* rpart);
+                       int soff, int sdg, int ncs, double* part, double* rpart,
+                       const GramGroupPtrs* grp = nullptr, int ngrp = 1);
 
 }  // namespace gpar

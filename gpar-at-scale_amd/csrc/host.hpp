@@ -87,6 +87,9 @@ struct gpar_ctx {
   int dense_early = 1;
   int post_gram = -1;             // "post_gram": a split job's short chain on the Gram CUs (s_g2): 1, 0, -1 = round overlap only
   int compact_rec = -1;           // "compact_rec": compact gains records: 1, 0, -1 = round overlap only
+  // "gram_group": outputs per grouped Gram launch set in an unsplit batched fit of small problems
+  // (run_gram_stage): 0 = off, >= 2 that many, 1 = off, -1 = auto (kGramGroupAuto below)
+  int gram_group = -1;
   // "dg_rows_w": percent more rows per DG split on the whitening CUs (fewer on the Gram CUs);
   // kDgRowsAuto: +10 in the round-by-round fit, where the whitening side (3.57 ms whitening) has
   // time to spare and the Gram CUs' side sets the span (5.117 -> 5.080 ms per Gram, r04ac), 0 in

@@ -49,6 +49,48 @@ StageBufs stage_bufs(gpar_ctx* c, int l, int64_t n, int64_t mpmax) {
   return b;
 }
 
+// The grouped Gram's per-output stage buffers: slot `slot` of a group, carry tags of stream lane
+// `lane` (its carry workspaces are reused output after output on that lane).
+static StageBufs stage_bufs_grp(gpar_ctx* c, int lane, int slot, int64_t n, int64_t mpmax) {
+  const int64_t nch = (n + kChunk - 1) / kChunk;
+  const std::string sfx = "_g" + std::to_string(slot);
+  StageBufs b;
+  b.idx = lane;
+  b.beta = ws<double>(c, "beta" + sfx, (size_t)(n + 16) * mpmax);
+  b.alpha = ws<double>(c, "alpha" + sfx, (size_t)n);
+  b.send = ws<double>(c, "send" + sfx, (size_t)nch * (mpmax + 1) * 4);
+  b.cin = ws<double>(c, "cin" + sfx, (size_t)nch * (mpmax + 1) * 4);
+  b.hsum = ws<double>(c, "hsum" + sfx, (size_t)nch * (mpmax + 1) * 4);
+  b.qv = ws<double>(c, "qv" + sfx, (size_t)nch * 4);
+  return b;
+}
+
+// Outputs per grouped Gram launch set (0: per-output Grams).  Small problems only: one output's
+// Gram (N Mp^2 <= kGramGroupMaxWork) has too few (group, split) items to fill the chip without
+// splitting time so finely that its partial sums and chunk correction cost as much as the GEMM
+// (N = 1e5, M = 256: 0.22 ms per launch against 0.084 ms of MFMA work, r05i); grouped, the same
+// items come from several outputs with 1/g of the time splits each.
+constexpr double kGramGroupMaxWork = 5e10;
+constexpr int kGramGroupAuto = 16;
+constexpr int64_t kGramGroupMaxBytes = (int64_t)24 << 30;   // the group's beta buffers
+static int gram_group_size(gpar_ctx* c, const std::vector<DevProblem>& P, int64_t n,
+                           int64_t mpmax, bool fix_beta, int nlanes, bool split_pipe) {
+  const int np = (int)P.size();
+  if (fix_beta || nlanes > 1 || split_pipe || np < 2) return 0;
+  for (const auto& p : P)
+    if (p.mp != mpmax || p.n != n) return 0;
+  int g = c->gram_group;
+  if (g == 0 || g == 1) return 0;
+  if (g < 0) {
+    if ((double)n * (double)mpmax * (double)mpmax > kGramGroupMaxWork) return 0;
+    g = kGramGroupAuto;
+  }
+  g = std::min(g, np);
+  const int64_t beta_bytes = (n + 16) * mpmax * (int64_t)sizeof(double);
+  while (g > 1 && (int64_t)g * beta_bytes > kGramGroupMaxBytes) --g;
+  return g >= 2 ? g : 0;
+}
+
 // Kfu assembly + chunk-local whitening of j's output into b.beta, on c->stream.
 void stage_whiten(gpar_ctx* c, const StageJob& j, const StageBufs& b) {
   const DevProblem& p = *j.p;
@@ -276,6 +318,64 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     if (split_head)       // every gains launch precedes the second whitening, which join covers
       HIPCHECK(hipMemcpyAsync(o.logs, logs_src, (size_t)np * nch * sizeof(double),
                               hipMemcpyDeviceToDevice, c->stream));
+    return o;
+  }
+  const int gsz = gram_group_size(c, P, n, mpmax, fix_beta, nlanes, split_pipe);
+  if (gsz >= 2) {
+    // Grouped Gram: per group of gsz outputs, their whitenings and short chains alternate over the
+    // context and side streams into buffers of their own, then one set of Gram launches covers the
+    // whole group (grid y = output, GramGroupPtrs table), its plan sized for 1/gsz of the chip per
+    // output.  A different split plan than the per-output Gram's: G moves within rounding.
+    const hipStream_t base = c->stream;
+    const int ngroups = (np + gsz - 1) / gsz;
+    auto* tab = ws<GramGroupPtrs>(c, "gram_grp_tab", (size_t)ngroups * gsz);
+    auto plan_of = [&](int cnt) {
+      const int cus = std::max(256 / cnt, 8);
+      return gram_plan(n, mpmax, false, cus, cus);
+    };
+    // the partials, sized once for every group's plan (no buffer may move under a running launch)
+    int64_t pd = 0, rd = 0;
+    for (int cnt : {gsz, np % gsz})
+      if (cnt > 0) {
+        const GramPlan pl = plan_of(cnt);
+        pd = std::max(pd, pl.part_doubles);
+        rd = std::max(rd, pl.rpart_doubles);
+      }
+    double* part = ws<double>(c, "gram_part_grp", (size_t)gsz * pd);
+    double* rpart = ws<double>(c, "gram_rpart_grp", (size_t)gsz * rd);
+    for (int g0 = 0, gi = 0; g0 < np; g0 += gsz, ++gi) {
+      const int cnt = std::min(gsz, np - g0);
+      const GramPlan plan = plan_of(cnt);
+      // the side lane starts after everything queued so far (the gains, the previous group's Gram,
+      // which still reads the buffers this group overwrites)
+      HIPCHECK(hipEventRecord(c->ev_fork, base));
+      HIPCHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
+      std::vector<StageBufs> gb(cnt);
+      std::vector<GramGroupPtrs> th_tab(cnt);
+      double work = 0.0;
+      for (int k = 0; k < cnt; ++k) {
+        const int i = g0 + k, lane = k & 1;
+        gb[k] = stage_bufs_grp(c, lane, k, n, mpmax);
+        OnStream on_(c, lane ? c->side : base);
+        const StageJob& j = job(i, gb[k]);
+        stage_whiten(c, j, gb[k]);
+        stage_post(c, j, gb[k], false);
+        th_tab[k] = {gb[k].beta, j.alpha, gb[k].hsum, gb[k].cin, gb[k].qv,
+                     part + (size_t)k * pd, rpart + (size_t)k * rd,
+                     j.G, j.r};
+        work += (double)P[i].n * (double)P[i].m * (double)(P[i].m + 1);
+      }
+      HIPCHECK(hipEventRecord(c->ev_join, c->side));
+      HIPCHECK(hipStreamWaitEvent(base, c->ev_join, 0));
+      GramGroupPtrs* dtab = tab + (size_t)gi * gsz;
+      h2d(c, dtab, th_tab.data(), (size_t)cnt);
+      {
+        Timed tm_(c, "gram", work);   // flops of every beta^T beta of the group
+        launch_gram_grouped(base, P[g0].sdim, plan, dtab, cnt, mpmax, n, P[g0].mc, kChunk, mpmax,
+                            c->side, c->ev_fork, c->ev_join);
+      }
+      check_launch("gram (grouped)");
+    }
     return o;
   }
   StageBufs bufs[2];

@@ -399,7 +399,12 @@ __global__ __launch_bounds__(256, 2) void gram2_kernel(
 __global__ __launch_bounds__(128) void gram3_off_kernel(const double* __restrict__ beta,
                                                         int64_t ldb, int64_t n, int noff,
                                                         int soff, int64_t rows,
-                                                        double* __restrict__ part) {
+                                                        double* __restrict__ part,
+                                                        const GramGroupPtrs* __restrict__ grp) {
+  if (grp) {
+    const GramGroupPtrs& q = grp[blockIdx.y];
+    beta = q.beta; part = q.part;
+  }
   __shared__ __attribute__((aligned(16))) double smem[8 * kPanelD];
 
   const int nty = noff * soff;
@@ -502,7 +507,12 @@ __global__ __launch_bounds__(256) void gram3_reduce(const double* __restrict__ p
                                                     const double* __restrict__ rpart, int npan,
                                                     int noff, int ndg, int soff, int sdg, int ncs,
                                                     double* __restrict__ G, int64_t ldg,
-                                                    double* __restrict__ r) {
+                                                    double* __restrict__ r,
+                                                    const GramGroupPtrs* __restrict__ grp) {
+  if (grp) {
+    const GramGroupPtrs& q = grp[blockIdx.y];
+    part = q.part; rpart = q.rpart; G = q.G; r = q.r;
+  }
   const int e = threadIdx.x;
   const int y = blockIdx.x;
   const int nrow_off = noff * 2 * kF3T, nrow_dg = ndg * 2 * kD2T;
@@ -565,7 +575,12 @@ __global__ __launch_bounds__(256) void gram2_reduce(const double* __restrict__ p
                                                     const double* __restrict__ rpart, int npan,
                                                     int noff, int ndg, int soff, int sdg,
                                                     double* __restrict__ G, int64_t ldg,
-                                                    double* __restrict__ r) {
+                                                    double* __restrict__ r,
+                                                    const GramGroupPtrs* __restrict__ grp) {
+  if (grp) {
+    const GramGroupPtrs& q = grp[blockIdx.y];
+    part = q.part; rpart = q.rpart; G = q.G; r = q.r;
+  }
   const int e = threadIdx.x;   // element of the 16 x 16 tile (C layout row-major 16 x 16)
   const int y = blockIdx.x;
   const int nbk = npan >> 1;
@@ -766,7 +781,8 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
       HIPCHECK_G(hipStreamWaitEvent(side, ev_a, 0));
     }
     if (noffw > 0)
-      gram3_off_kernel<<<noffw, 128, 0, st>>>(beta, ldb, n, plan.noff, plan.soff, plan.rows_off, part);
+      gram3_off_kernel<<<noffw, 128, 0, st>>>(beta, ldb, n, plan.noff, plan.soff, plan.rows_off, part,
+                                              nullptr);
     if (corun)
       launch_gram3_corr_slim(side, sdim, ecor, cin, qv, mc, nchk, plan.npan, plan.noff, plan.ndg,
                              plan.soff, plan.sdg, ncs, part, rpart);
@@ -791,7 +807,7 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
     }
     const int nrows = plan.noff * 2 * kF3T + plan.ndg * 2 * kD2T + 1;
     gram3_reduce<<<nrows, 256, 0, st>>>(part, rpart, plan.npan, plan.noff, plan.ndg, plan.soff,
-                                        plan.sdg, ncs, G, ldg, r);
+                                        plan.sdg, ncs, G, ldg, r, nullptr);
     return;
   }
   if (plan.v2) {
@@ -816,8 +832,45 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
     }
 #undef GRAM2_ARGS
     const int nrows = plan.noff * 4 * 16 + plan.ndg * 4 * kD2T + 1;
-    gram2_reduce<<<nrows, 256, 0, st>>>(part, rpart, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, G, ldg, r);
+    gram2_reduce<<<nrows, 256, 0, st>>>(part, rpart, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, G, ldg, r,
+                                        nullptr);
   }
+}
+
+// v3 over ngrp outputs of one size in one set of launches (grid y = output; per-output pointers
+// from the device table grp: GramGroupPtrs), with the chunk correction (the objective's form)
+void launch_gram_grouped(hipStream_t st, int sdim, const GramPlan& plan, const GramGroupPtrs* grp,
+                         int ngrp, int64_t ldb, int64_t n, int64_t mc, int L, int64_t ldg,
+                         hipStream_t side, hipEvent_t ev_a, hipEvent_t ev_b) {
+  const bool corun = side && plan.noff > 0;
+  const int ncs = corun ? plan.ncs_slim : plan.ncs;
+  const int noffw = ((plan.noff * plan.soff + 7) / 8) * 8;   // XCD deal (per grid row)
+  const int ndgw = ((plan.ndg * plan.sdg + 7) / 8) * 8;
+  const int64_t nchk = (n + L - 1) / L;
+  if (corun) {
+    HIPCHECK_G(hipEventRecord(ev_a, st));
+    HIPCHECK_G(hipStreamWaitEvent(side, ev_a, 0));
+  }
+  if (noffw > 0)
+    gram3_off_kernel<<<dim3((unsigned)noffw, (unsigned)ngrp), 128, 0, st>>>(
+        nullptr, ldb, n, plan.noff, plan.soff, plan.rows_off, nullptr, grp);
+  if (corun)
+    launch_gram3_corr_slim(side, sdim, nullptr, nullptr, nullptr, mc, nchk, plan.npan, plan.noff,
+                           plan.ndg, plan.soff, plan.sdg, ncs, nullptr, nullptr, grp, ngrp);
+  const int64_t dslot0 = (int64_t)plan.noff * (plan.soff + ncs);
+  launch_gram3_dg(st, ndgw, nullptr, ldb, n, nullptr, plan.npan, plan.ndg, plan.sdg, plan.rows_dg,
+                  dslot0, nullptr, nullptr, 0, -1, 0, 0, grp, ngrp);
+  if (corun) {
+    HIPCHECK_G(hipEventRecord(ev_b, side));
+    HIPCHECK_G(hipStreamWaitEvent(st, ev_b, 0));
+  } else {
+    launch_gram3_corr(st, sdim, nullptr, nullptr, nullptr, mc, nchk, plan.npan, plan.noff, plan.ndg,
+                      plan.soff, plan.sdg, ncs, nullptr, nullptr, grp, ngrp);
+  }
+  const int nrows = plan.noff * 2 * kF3T + plan.ndg * 2 * kD2T + 1;
+  gram3_reduce<<<dim3((unsigned)nrows, (unsigned)ngrp), 256, 0, st>>>(
+      nullptr, nullptr, plan.npan, plan.noff, plan.ndg, plan.soff, plan.sdg, ncs, nullptr, ldg,
+      nullptr, grp);
 }
 
 void launch_beta_fix(hipStream_t st, int sdim, double* beta, int64_t ldb, int64_t n,

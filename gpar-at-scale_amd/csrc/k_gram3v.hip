@@ -14,7 +14,12 @@ namespace gpar {
 __global__ __launch_bounds__(128) void gram3_dg_kernel(
     const double* __restrict__ beta, int64_t ldb, int64_t n, const double* __restrict__ alpha,
     int npan, int ndg, int sdg, int64_t rows, int64_t slot0, double* __restrict__ part,
-    double* __restrict__ rpart, int bt_lo, int bt_cnt, int sw, int64_t rows_w) {
+    double* __restrict__ rpart, int bt_lo, int bt_cnt, int sw, int64_t rows_w,
+    const GramGroupPtrs* __restrict__ grp) {
+  if (grp) {
+    const GramGroupPtrs& q = grp[blockIdx.y];
+    beta = q.beta; alpha = q.alpha; part = q.part; rpart = q.rpart;
+  }
   __shared__ __attribute__((aligned(16))) double smem[4 * kPanelD + 2 * 2 * kBK];
   double* ringa = smem + 4 * kPanelD;
 
@@ -156,7 +161,11 @@ template <int D>
 __global__ __launch_bounds__(256) void gram3_corr_kernel(
     const double* __restrict__ ecor, const double* __restrict__ cin, const double* __restrict__ qv,
     int64_t mc, int64_t nch, int npan, int noff, int ndg, int soff, int sdg, int ncs,
-    double* __restrict__ part, double* __restrict__ rpart) {
+    double* __restrict__ part, double* __restrict__ rpart, const GramGroupPtrs* __restrict__ grp) {
+  if (grp) {
+    const GramGroupPtrs& q = grp[blockIdx.y];
+    ecor = q.ecor; cin = q.cin; qv = q.qv; part = q.part; rpart = q.rpart;
+  }
   const int ng = noff + ndg;
   const int g = (int)blockIdx.x % ng, cs = (int)blockIdx.x / ng;
   const int64_t j0 = (int64_t)cs * nch / ncs, j1 = (int64_t)(cs + 1) * nch / ncs;
@@ -288,7 +297,11 @@ template <int D>
 __global__ __launch_bounds__(256) void gram3_corr_slim_kernel(
     const double* __restrict__ ecor, const double* __restrict__ cin, const double* __restrict__ qv,
     int64_t mc, int64_t nch, int npan, int noff, int ndg, int soff, int sdg, int ncs,
-    double* __restrict__ part, double* __restrict__ rpart) {
+    double* __restrict__ part, double* __restrict__ rpart, const GramGroupPtrs* __restrict__ grp) {
+  if (grp) {
+    const GramGroupPtrs& q = grp[blockIdx.y];
+    ecor = q.ecor; cin = q.cin; qv = q.qv; part = q.part; rpart = q.rpart;
+  }
   const int ng = noff + ndg;
   const int g = (int)blockIdx.x % ng;
   const int hw = ((int)blockIdx.x / ng) & 1, cs = (int)blockIdx.x / (2 * ng);
@@ -400,9 +413,10 @@ __global__ __launch_bounds__(256) void gram3_corr_slim_kernel(
 
 void launch_gram3_corr_slim(hipStream_t st, int sdim, const double* ecor, const double* cin,
                             const double* qv, int64_t mc, int64_t nch, int npan, int noff, int ndg,
-                            int soff, int sdg, int ncs, double* part, double* rpart) {
-  const int nwg = (noff + ndg) * 2 * ncs;
-#define GRAM3C_ARGS ecor, cin, qv, mc, nch, npan, noff, ndg, soff, sdg, ncs, part, rpart
+                            int soff, int sdg, int ncs, double* part, double* rpart,
+                            const GramGroupPtrs* grp, int ngrp) {
+  const dim3 nwg((unsigned)((noff + ndg) * 2 * ncs), (unsigned)ngrp);
+#define GRAM3C_ARGS ecor, cin, qv, mc, nch, npan, noff, ndg, soff, sdg, ncs, part, rpart, grp
   switch (sdim) {
     case 1: gram3_corr_slim_kernel<1><<<nwg, 256, 0, st>>>(GRAM3C_ARGS); break;
     case 2: gram3_corr_slim_kernel<2><<<nwg, 256, 0, st>>>(GRAM3C_ARGS); break;
@@ -414,19 +428,20 @@ void launch_gram3_corr_slim(hipStream_t st, int sdim, const double* ecor, const 
 void launch_gram3_dg(hipStream_t st, int nwg, const double* beta, int64_t ldb, int64_t n,
                      const double* alpha, int npan, int ndg, int sdg, int64_t rows,
                      int64_t slot0, double* part, double* rpart, int bt_lo, int bt_cnt, int sw,
-                     int64_t rows_w) {
+                     int64_t rows_w, const GramGroupPtrs* grp, int ngrp) {
   if (bt_cnt < 0) bt_cnt = ndg * sdg - bt_lo;
   if (bt_cnt <= 0) return;
   if (nwg <= 0) nwg = ((bt_cnt + 7) / 8) * 8;
-  gram3_dg_kernel<<<nwg, 128, 0, st>>>(beta, ldb, n, alpha, npan, ndg, sdg, rows, slot0, part,
-                                       rpart, bt_lo, bt_cnt, sw, rows_w);
+  gram3_dg_kernel<<<dim3((unsigned)nwg, (unsigned)ngrp), 128, 0, st>>>(
+      beta, ldb, n, alpha, npan, ndg, sdg, rows, slot0, part, rpart, bt_lo, bt_cnt, sw, rows_w, grp);
 }
 
 void launch_gram3_corr(hipStream_t st, int sdim, const double* ecor, const double* cin,
                        const double* qv, int64_t mc, int64_t nch, int npan, int noff, int ndg,
-                       int soff, int sdg, int ncs, double* part, double* rpart) {
-  const int nwg = (noff + ndg) * ncs;
-#define GRAM3C_ARGS ecor, cin, qv, mc, nch, npan, noff, ndg, soff, sdg, ncs, part, rpart
+                       int soff, int sdg, int ncs, double* part, double* rpart,
+                       const GramGroupPtrs* grp, int ngrp) {
+  const dim3 nwg((unsigned)((noff + ndg) * ncs), (unsigned)ngrp);
+#define GRAM3C_ARGS ecor, cin, qv, mc, nch, npan, noff, ndg, soff, sdg, ncs, part, rpart, grp
   switch (sdim) {
     case 1: gram3_corr_kernel<1><<<nwg, 256, 0, st>>>(GRAM3C_ARGS); break;
     case 2: gram3_corr_kernel<2><<<nwg, 256, 0, st>>>(GRAM3C_ARGS); break;

@@ -81,6 +81,20 @@ struct GramPlan {
   int64_t dg_rows_w = 0;
 };
 
+// Grouped Gram (one set of launches for several outputs of one size, grid y = output): each
+// kernel takes its per-output pointers from row blockIdx.y of this device table
+struct GramGroupPtrs {
+  const double* beta;
+  const double* alpha;
+  const double* ecor;
+  const double* cin;
+  const double* qv;
+  double* part;
+  double* rpart;
+  double* G;
+  double* r;
+};
+
 constexpr int kGramTile = 128;
 constexpr int kBKRows = 16;   // the Gram kernels' time rows per K-step (gram_common.hpp kBK)
 constexpr int kRecStride3 = 16;
@@ -187,6 +201,9 @@ void launch_gram(hipStream_t st, int sdim, const GramPlan& plan, const double* b
                  int64_t ldg, double* r, hipStream_t side = nullptr,
                  hipEvent_t ev_a = nullptr, hipEvent_t ev_b = nullptr,
                  hipStream_t st_w = nullptr, hipEvent_t ev_w = nullptr, int w_items = 0);
+void launch_gram_grouped(hipStream_t st, int sdim, const GramPlan& plan, const GramGroupPtrs* grp,
+                         int ngrp, int64_t ldb, int64_t n, int64_t mc, int L, int64_t ldg,
+                         hipStream_t side, hipEvent_t ev_a, hipEvent_t ev_b);
 void launch_beta_fix(hipStream_t st, int sdim, double* beta, int64_t ldb, int64_t n,
                      const double* g, const double* cin, int64_t mc, int L);
 

@@ -170,6 +170,11 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *                   split Gram, fewer on the Gram CUs; -100 (default) = auto: 10 in the
  *                   round-by-round fit, 0 in the round overlap (changes G's summation grouping:
  *                   last bits, like predict_fused)
+ *   "gram_group"    outputs per grouped Gram of an unsplit batched fit: the group's outputs whiten
+ *                   over two streams into buffers of their own and one set of Gram launches covers
+ *                   them all (grid y = output), each with 1/g of the time splits; -1 (default) =
+ *                   auto: groups of 16 when one output's N Mp^2 <= 5e10 (the dtc / eeg configs),
+ *                   0 = per-output Grams; a plan like dg_rows_w (G's summation grouping: last bits)
  * The environment variable GPAR_<KNOB> (upper case) sets a knob at context creation.
  * GPAR_ERR_ARG for an unknown knob or value.  Every non-default value is a supported schedule
  * mode; the A/B-only knobs of round 4 (split_head, dg_share, tail_cus, predict_d2, dense_early 2)

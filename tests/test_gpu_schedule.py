@@ -47,7 +47,7 @@ SETTINGS = [
 PLAN = {"dg_rows_w": 10}
 DEFAULTS = {"serialize": 0, "overlap": 1, "overlap_group": 0, "dense_early": 1, "post_gram": -1,
             "compact_rec": -1, "dg_rows_w": -100, "qu_batch": 1, "predict_lanes": 2,
-            "predict_fused": 1}
+            "predict_fused": 1, "gram_group": -1}
 DELETED = ["split_head", "dg_share", "tail_cus", "predict_d2"]
 
 
@@ -103,6 +103,8 @@ def test_schedule_knobs_round_trip():
         ctx.set_schedule("predict_lanes", 3)
     with pytest.raises(G.DomainError):
         ctx.set_schedule("dense_early", 2)
+    with pytest.raises(G.DomainError):
+        ctx.set_schedule("gram_group", 65)
     for k in DELETED:
         with pytest.raises(G.DomainError):
             ctx.set_schedule(k, 0)
@@ -135,3 +137,60 @@ def test_dg_rows_w_is_a_plan_not_a_schedule(job):
     # (-nlml 1.7e9), and six simplex steps carry the last-bit difference of G to 1.7e-11
     np.testing.assert_allclose(fa.nlml, fr0.nlml, rtol=1e-9)
     np.testing.assert_allclose(fa.theta, fr0.theta, rtol=1e-6)
+
+
+def test_grouped_gram_is_a_plan_not_a_schedule():
+    """gram_group: an unsplit batched fit of small problems (here N = 3e4, M = 128, five outputs of
+    one Mp) whitens every output of a group into buffers of its own over two streams and runs one
+    grouped set of Gram launches for the group, with 1/g of the time splits per output.  A plan (G
+    summed in another grouping): bit-identical to its serialized twin, for the auto groups (one
+    group of five) and groups of two (2 + 2 + 1), and within rounding of the per-output Grams."""
+    import torch
+    dev = torch.device("cuda", 0)
+    n, m, outs = 30_000, 128, [2, 3, 5, 9, 17]
+    ds = D.gpar_dataset(n, max(outs), seed=3, observation_noise=0.8, n_star=4_000)
+    Y_d = torch.from_numpy(ds["Y"]).to(dev)
+    t_d = torch.from_numpy(ds["t"]).to(dev)
+    ts_d = torch.from_numpy(ds["t_star"]).to(dev)
+    Fs_d = torch.from_numpy(ds["F_star"]).to(dev)
+    probs, keep = [], []
+    for p in outs:
+        Z = torch.from_numpy(D.pseudo_inputs(ds["Y"][:, : p - 1], m, seed=p)).to(dev)
+        pr, k = G.make_problem(Y_d[:, : p - 1], Z, t_d, Y_d[:, p - 1].contiguous(), "eq",
+                               "matern52", qu_kuu_noise=True)
+        probs.append(pr)
+        keep.append((k, Z))
+    x0 = np.tile([0.0, 0.0, 0.0, 0.0, -2.0], (len(outs), 1))
+    ctx = G.context(0)
+    ctx.set_cu_split(-1)
+    assert ctx.cu_split() == 0 or n * 128 * 128 < 1e11   # the auto split stays off at this size
+    th = np.tile([[1.1, 0.9, 1.3, 0.8, 0.3]], (len(outs), 1))
+
+    def run(knobs):
+        try:
+            for k, v in knobs.items():
+                ctx.set_schedule(k, v)
+            vals = G.dtc_objective_batch(probs, th)
+            fr, means, stds = G.fit_predict_batch(probs, x0, ts_d, [Fs_d[:, : p - 1] for p in outs],
+                                                  max_evals=8, g_tol=-1.0)
+            return np.asarray(vals), fr, [a.cpu().numpy() for a in means], [a.cpu().numpy() for a in stds]
+        finally:
+            for k, v in DEFAULTS.items():
+                ctx.set_schedule(k, v)
+
+    off = run({"gram_group": 0})
+    for g in (-1, 2):
+        a = run({"gram_group": g})
+        b = run({"gram_group": g, "serialize": 1})
+        np.testing.assert_array_equal(a[0], b[0])
+        np.testing.assert_array_equal(a[1].theta, b[1].theta)
+        np.testing.assert_array_equal(a[1].nlml, b[1].nlml)
+        for i in range(len(outs)):
+            np.testing.assert_array_equal(a[2][i], b[2][i])
+            np.testing.assert_array_equal(a[3][i], b[3][i])
+        np.testing.assert_allclose(a[0], off[0], rtol=1e-10)
+        np.testing.assert_allclose(a[1].nlml, off[1].nlml, rtol=1e-9)
+        np.testing.assert_allclose(a[1].theta, off[1].theta, rtol=1e-6)
+        for i in range(len(outs)):
+            np.testing.assert_allclose(a[2][i], off[2][i], rtol=1e-7, atol=1e-9)
+            np.testing.assert_allclose(a[3][i], off[3][i], rtol=1e-7, atol=1e-9)
