@@ -1,5 +1,5 @@
 # Kernel trace of a short north fit (8 evaluations, one step, no warm-up) and the round-boundary
-# timeline (tools/trace_rounds.py).
+# timeline (tools/trace_rounds.py), and the gains launches by grid size (tools/trace_kernels.py).
 set -o pipefail
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out
@@ -11,4 +11,6 @@ f=$(find gpurun_out/$tag -name "*kernel_trace.csv" | head -1)
 echo "trace: $f"
 python tools/trace_rounds.py "$f" --top 25 > gpurun_out/${tag}_rounds.txt
 cat gpurun_out/${tag}_rounds.txt | head -120
+python tools/trace_kernels.py "$f" --match gains --top 20 > gpurun_out/${tag}_gains.txt
+cat gpurun_out/${tag}_gains.txt
 rm -rf gpurun_out/$tag
