@@ -55,7 +55,7 @@ CONFIGS = {
 FP64_MFMA_PEAK_TFLOPS = 78.6
 HBM_PEAK_GBS = 8000.0
 # HBM bytes per launch from the PMC passes of this round's sources (tools/pmc_passes.sh, D = 32)
-PMC_FILE = "pmc_gram_whiten_r04.json"
+PMC_FILE = "pmc_gram_whiten_r05.json"
 
 
 def log(*a):
