@@ -1037,6 +1037,30 @@ __global__ __launch_bounds__(256) void whiten_kfu(
 // form (its kappa is not smooth in d^2 at 0).
 constexpr int kMT = 16;   // steps per sub-tile
 
+// acc + row[E] * m, where each 16-lane DPP row of the wave holds the same 16-double step row
+// {A_k, K_k, rs_k, g_k} (lane i: element i) and row_newbcast:E hands element E to every lane of
+// its row as the FMA's first source.  The step's record and fix-up row then reach all 64 lanes
+// from one ds_read_b64 (2 LDS cycles) instead of seven broadcast ds_read_b128 and two b64 reads
+// (≈ 34 cycles): the filter recursion was LDS-bound, eight waves per CU sharing one LDS.  The
+// source must not be written by a VALU in the two instructions before (DPP hazard): `row` comes
+// straight from LDS.  Same operation order and rounding as fma(row[E], m, acc).
+// f(std::integral_constant<int, i>) for i = 0 .. N-1 (compile-time indices for fmac_row's lane)
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
+template <int E>
+__device__ __forceinline__ double fmac_row(double acc, double row, double m) {
+  asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+      : "+v"(acc)
+      : "v"(row), "v"(m), "n"(E));
+  return acc;
+}
+
 template <int TK, int OK, int DP>
 __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     const double* __restrict__ rec, const double* __restrict__ v, int64_t ldv, int d,
@@ -1051,8 +1075,10 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
   constexpr int NKS = DP / 4;
   __shared__ __attribute__((aligned(16))) double vs[kMT * VS];
   __shared__ __attribute__((aligned(16))) double xt[4][kMT][65];
-  __shared__ __attribute__((aligned(16))) double rl[kMT * RS];   // the sub-tile's gains records
-  __shared__ __attribute__((aligned(16))) double gl[kMT * kGStride];   // and fix-up rows g_k
+  // the sub-tile's step rows {A_k (SD x SD), K_k (SD), rs_k, g_k (SD)}, 16 doubles each (fmac_row)
+  constexpr int RK = SD * SD, RR = SD * SD + SD, RG = SD * SD + SD + 1;
+  static_assert(RG + SD <= 16, "step row");
+  __shared__ __attribute__((aligned(16))) double rg[kMT * 16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int64_t j = blockIdx.x;
   const int64_t cw0 = (int64_t)blockIdx.y * 256 + wave * 64;   // wave's first column
@@ -1122,8 +1148,9 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
       if (e < kMT * DP)
         vs[pkk[q] * VS + pii[q]] = (pkk[q] < nt_ && pii[q] < d) ? pv[q] - pcg[q] : 0.0;
     }
-    if (tid < kMT * RS) rl[tid] = tid < nt_ * RS ? pr : 0.0;
-    if (tid < kMT * kGStride) gl[tid] = tid < nt_ * kGStride ? pg : 0.0;
+    if (tid < kMT * RS && tid % RS < RG) rg[tid / RS * 16 + tid % RS] = tid < nt_ * RS ? pr : 0.0;
+    if (tid < kMT * kGStride && tid % kGStride < SD)
+      rg[tid / kGStride * 16 + RG + tid % kGStride] = tid < nt_ * kGStride ? pg : 0.0;
   };
   // beta of a sub-tile is left in the wave's xt rows by the recursion and flushed to HBM at the
   // start of the next iteration, after commit's wait: the stores then drain behind a whole
@@ -1215,30 +1242,46 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     }
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes landed
     __builtin_amdgcn_wave_barrier();
-    auto step = [&](int kk) __attribute__((always_inline)) {
-      const double x = colv ? xt[wave][kk][lane] : 0.0;
-      const double* rr = rl + kk * RS;
+    auto step = [&](int kk, double x, double row) __attribute__((always_inline)) {
       double mm[SD];
-#pragma unroll
-      for (int i = 0; i < SD; ++i) {
+      static_for<SD>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
         double a2 = 0.0;
-#pragma unroll
-        for (int q = 0; q < SD; ++q) a2 = fma(rr[i * SD + q], mst[q], a2);
+        static_for<SD>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          a2 = fmac_row<i * SD + q>(a2, row, mst[q]);
+        });
         mm[i] = a2;
-      }
+      });
       const double ev = x - mm[0];
-      const double al = ev * rr[SD * SD + SD];
-#pragma unroll
-      for (int i = 0; i < SD; ++i) mst[i] = fma(rr[SD * SD + i], ev, mm[i]);
-#pragma unroll
-      for (int i = 0; i < SD; ++i) hs[i] = fma(al, gl[kk * kGStride + i], hs[i]);
+      const double al = ev * __builtin_amdgcn_update_dpp(0.0, row, 0x150 + RR, 0xf, 0xf, false);
+      static_for<SD>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        mst[i] = fmac_row<RK + i>(mm[i], row, ev);
+        hs[i] = fmac_row<RG + i>(hs[i], row, al);
+      });
       xt[wave][kk][lane] = al;
     };
-    if (nt == kMT) {   // unrolled: the next steps' LDS reads are issued under this step's chain
-#pragma unroll 4
-      for (int kk = 0; kk < kMT; ++kk) step(kk);
+    auto xval = [&](int kk) __attribute__((always_inline)) { return colv ? xt[wave][kk][lane] : 0.0; };
+    auto rval = [&](int kk) __attribute__((always_inline)) { return rg[kk * 16 + (lane & 15)]; };
+    if (nt == kMT) {   // unrolled, each step's x and row read kPW steps ahead of their use
+      constexpr int kPW = DP <= 32 ? 8 : 4;
+      double xs[kMT], rows[kMT];
+#pragma unroll
+      for (int kk = 0; kk < kPW; ++kk) {
+        xs[kk] = xval(kk);
+        rows[kk] = rval(kk);
+      }
+#pragma unroll
+      for (int kk = 0; kk < kMT; ++kk) {
+        if (kk + kPW < kMT) {
+          xs[kk + kPW] = xval(kk + kPW);
+          rows[kk + kPW] = rval(kk + kPW);
+        }
+        step(kk, xs[kk], rows[kk]);
+      }
     } else {
-      for (int kk = 0; kk < nt; ++kk) step(kk);
+      for (int kk = 0; kk < nt; ++kk) step(kk, xval(kk), rval(kk));
     }
     ntp = nt;
     ktp = kt;
