@@ -5,6 +5,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <type_traits>
 
 namespace gpar {
 
@@ -23,6 +24,37 @@ template <int D> struct CRec { static constexpr int size = D == 1 ? 2 : 4; };
 constexpr int kGStride = 4;
 // Carry / end-state vectors (d), padded to 4 doubles.
 constexpr int kSStride = 4;
+
+// f(std::integral_constant<int, i>) for i = 0 .. N-1 (compile-time indices for fmac_row's lane)
+template <int N, int I = 0, class F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (I < N) {
+    f(std::integral_constant<int, I>{});
+    static_for<N, I + 1>(f);
+  }
+}
+
+// acc + row[E] * m, where each 16-lane DPP row of the wave holds the same 16-double step row (a
+// gains record and its fix-up row, {A_k, K_k, rs_k, g_k}; lane i: element i) and row_newbcast:E
+// hands element E to every lane of its row as the FMA's first source.  A step's 16 values then
+// reach all 64 lanes from one ds_read_b64 (2 LDS cycles) instead of broadcast ds_read_b128 reads
+// (4 LDS cycles per 2 doubles, ≈ 34 per step): the filter recursions that read a record per step
+// were LDS-bound, 8-9 waves per CU sharing one LDS.  The source must not be written by a VALU in
+// the two instructions before (DPP hazard): `row` comes straight from an LDS read.  Same operation
+// order and rounding as fma(row[E], m, acc).
+template <int E>
+__device__ __forceinline__ double fmac_row(double acc, double row, double m) {
+  asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
+      : "+v"(acc)
+      : "v"(row), "v"(m), "n"(E));
+  return acc;
+}
+
+// row[E] in every lane of its 16-lane row (a v_mov_b64 with the same DPP source)
+template <int E>
+__device__ __forceinline__ double bcast_row(double row) {
+  return __builtin_amdgcn_update_dpp(0.0, row, 0x150 + E, 0xf, 0xf, false);
+}
 
 template <int KIND> struct Sde;
 template <> struct Sde<KM12> { static constexpr int d = 1; };

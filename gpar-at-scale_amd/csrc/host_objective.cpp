@@ -301,7 +301,7 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   if (split_pipe) {
     SplitPipe sp(c, n, mpmax);
     sp.post_gram = c->post_gram == 1;
-    sp.dg_rows_w = c->dg_rows_w == kDgRowsAuto ? 10 : c->dg_rows_w;
+    sp.dg_rows_w = c->dg_rows_w == kDgRowsAuto ? 40 : c->dg_rows_w;
     sp.start();
     if (split_head) {
       gplan.launch(c->s_w, 0, 1);

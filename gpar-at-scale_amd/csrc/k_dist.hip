@@ -223,8 +223,11 @@ __global__ __launch_bounds__(256, kW2Occ) void whiten_kfu_d2x2(
     double* __restrict__ hsum, ExpNegConsts ek, const double* __restrict__ tt, double l_t) {
   constexpr int SD = Sde<TK>::d;
   constexpr int RS = Rec<SD>::size;
-  __shared__ __attribute__((aligned(16))) double rl[kW2MaxL * RS];
-  __shared__ __attribute__((aligned(16))) double gl[kW2MaxL * kGStride];
+  // the chunk's step rows {A_k, K_k, rs_k, g_k}, 16 doubles each, read one double per lane and
+  // broadcast by DPP (fmac_row, device_common.hpp)
+  constexpr int RK = SD * SD, RR = SD * SD + SD, RG = SD * SD + SD + 1;
+  static_assert(RG + SD <= 16, "step row");
+  __shared__ __attribute__((aligned(16))) double rg[kW2MaxL * 16];
   const int tid = threadIdx.x;
   const int64_t j = blockIdx.x;
   const int64_t c = ((int64_t)blockIdx.y * 256 + tid) * 2;   // first of the thread's two columns
@@ -244,14 +247,16 @@ __global__ __launch_bounds__(256, kW2Occ) void whiten_kfu_d2x2(
 #pragma unroll
       for (int i = 0; i < SD; ++i)
 #pragma unroll
-        for (int q = 0; q < SD; ++q) rl[e * RS + i * SD + q] = A[i][q];
+        for (int q = 0; q < SD; ++q) rg[e * 16 + i * SD + q] = A[i][q];
 #pragma unroll
-      for (int i = 0; i <= SD; ++i) rl[e * RS + SD * SD + i] = rec[k * CS + i];
+      for (int i = 0; i <= SD; ++i) rg[e * 16 + RK + i] = rec[k * CS + i];
     }
   } else {
-    for (int e = tid; e < nk * RS; e += 256) rl[e] = rec[k0 * RS + e];
+    for (int e = tid; e < nk * RS; e += 256)
+      if (e % RS < RG) rg[e / RS * 16 + e % RS] = rec[k0 * RS + e];
   }
-  for (int e = tid; e < nk * kGStride; e += 256) gl[e] = g[k0 * kGStride + e];
+  for (int e = tid; e < nk * kGStride; e += 256)
+    if (e % kGStride < SD) rg[e / kGStride * 16 + RG + e % kGStride] = g[k0 * kGStride + e];
   double ma[SD], mb[SD], ha[SD], hb[SD];
 #pragma unroll
   for (int i = 0; i < SD; ++i) ma[i] = mb[i] = ha[i] = hb[i] = 0.0;
@@ -300,32 +305,29 @@ __global__ __launch_bounds__(256, kW2Occ) void whiten_kfu_d2x2(
       x[r].y = v1 ? kb : 0.0;
     }
     auto step = [&](int r) __attribute__((always_inline)) {
-      const double* rr = rl + (r0 + r) * RS;
-      const double* gg = gl + (r0 + r) * kGStride;
+      const double row = rg[(r0 + r) * 16 + (tid & 15)];
       double pa[SD], pb[SD];
-#pragma unroll
-      for (int i = 0; i < SD; ++i) {
+      static_for<SD>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
         double sa = 0.0, sb = 0.0;
-#pragma unroll
-        for (int q = 0; q < SD; ++q) {
-          sa = fma(rr[i * SD + q], ma[q], sa);
-          sb = fma(rr[i * SD + q], mb[q], sb);
-        }
+        static_for<SD>([&](auto qc) {
+          constexpr int q = decltype(qc)::value;
+          sa = fmac_row<i * SD + q>(sa, row, ma[q]);
+          sb = fmac_row<i * SD + q>(sb, row, mb[q]);
+        });
         pa[i] = sa;
         pb[i] = sb;
-      }
+      });
       const double ea = x[r].x - pa[0], eb = x[r].y - pb[0];
-      const double rs = rr[SD * SD + SD];
+      const double rs = bcast_row<RR>(row);
       const double aa = ea * rs, ab = eb * rs;
-#pragma unroll
-      for (int i = 0; i < SD; ++i) {
-        const double kg = rr[SD * SD + i];
-        ma[i] = fma(kg, ea, pa[i]);
-        mb[i] = fma(kg, eb, pb[i]);
-        const double gi = gg[i];
-        ha[i] = fma(aa, gi, ha[i]);
-        hb[i] = fma(ab, gi, hb[i]);
-      }
+      static_for<SD>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        ma[i] = fmac_row<RK + i>(pa[i], row, ea);
+        mb[i] = fmac_row<RK + i>(pb[i], row, eb);
+        ha[i] = fmac_row<RG + i>(ha[i], row, aa);
+        hb[i] = fmac_row<RG + i>(hb[i], row, ab);
+      });
       if (cola) {
         double2 o;
         o.x = aa;

@@ -1037,30 +1037,6 @@ __global__ __launch_bounds__(256) void whiten_kfu(
 // form (its kappa is not smooth in d^2 at 0).
 constexpr int kMT = 16;   // steps per sub-tile
 
-// acc + row[E] * m, where each 16-lane DPP row of the wave holds the same 16-double step row
-// {A_k, K_k, rs_k, g_k} (lane i: element i) and row_newbcast:E hands element E to every lane of
-// its row as the FMA's first source.  The step's record and fix-up row then reach all 64 lanes
-// from one ds_read_b64 (2 LDS cycles) instead of seven broadcast ds_read_b128 and two b64 reads
-// (≈ 34 cycles): the filter recursion was LDS-bound, eight waves per CU sharing one LDS.  The
-// source must not be written by a VALU in the two instructions before (DPP hazard): `row` comes
-// straight from LDS.  Same operation order and rounding as fma(row[E], m, acc).
-// f(std::integral_constant<int, i>) for i = 0 .. N-1 (compile-time indices for fmac_row's lane)
-template <int N, int I = 0, class F>
-__device__ __forceinline__ void static_for(F&& f) {
-  if constexpr (I < N) {
-    f(std::integral_constant<int, I>{});
-    static_for<N, I + 1>(f);
-  }
-}
-
-template <int E>
-__device__ __forceinline__ double fmac_row(double acc, double row, double m) {
-  asm("v_fmac_f64_dpp %0, %1, %2 row_newbcast:%3 row_mask:0xf bank_mask:0xf"
-      : "+v"(acc)
-      : "v"(row), "v"(m), "n"(E));
-  return acc;
-}
-
 template <int TK, int OK, int DP>
 __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     const double* __restrict__ rec, const double* __restrict__ v, int64_t ldv, int d,
@@ -1254,7 +1230,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
         mm[i] = a2;
       });
       const double ev = x - mm[0];
-      const double al = ev * __builtin_amdgcn_update_dpp(0.0, row, 0x150 + RR, 0xf, 0xf, false);
+      const double al = ev * bcast_row<RR>(row);
       static_for<SD>([&](auto ic) {
         constexpr int i = decltype(ic)::value;
         mst[i] = fmac_row<RK + i>(mm[i], row, ev);
@@ -1765,10 +1741,13 @@ __global__ __launch_bounds__(CW) void adjoint_local_wide(double* __restrict__ X,
                                                          const double* __restrict__ wmask) {
   constexpr int RS = Rec<D>::size;
   constexpr int RU = D * D + D + 1;   // record entries used
-  // a step's record entries, then its fix-up row, padded to 16 bytes: the step's reads are 16-byte
-  // aligned broadcasts the compiler issues as ds_read_b128 (4 LDS cycles per 2 doubles; unaligned,
-  // they were ds_read2_b64 at 8, and the pass was LDS-bound: 63 % of the LDS array's cycles, r04ai)
-  constexpr int RP = (RU + D + 1) & ~1;
+  // a step's record entries, then its fix-up row, in a 16-double row: lane i of every 16-lane DPP
+  // row reads element i (one ds_read_b64, 2 LDS cycles) and the FMAs take the element they need by
+  // row_newbcast (fmac_row).  The broadcast ds_read_b128 form cost 32 LDS cycles per wave-step
+  // against ≈ 70 DP cycles, with 9 waves of a workgroup on one CU's LDS (r04ai: 63 % of the LDS
+  // array's cycles with ds_read2_b64; r05q: the DPP row).
+  constexpr int RP = 16;
+  static_assert(RU + D <= RP, "step row");
   __shared__ __attribute__((aligned(16))) double lrec[256 * RP];
   __shared__ unsigned char lw[256];
   const int64_t j = blockIdx.x;
@@ -1799,23 +1778,29 @@ __global__ __launch_bounds__(CW) void adjoint_local_wide(double* __restrict__ X,
     const uint32_t off = (uint32_t)(s > 0 ? s : 0) * rowb + col;
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(xr, off, 0, 0));
   };
+  const int rl = tid & 15;
   auto stepfn = [&](int s, double w) {
-    const double* r = lrec + s * RP;
-    const double* gk = r + RU;
-#pragma unroll
-    for (int i = 0; i < D; ++i) w = fma(gk[i], cf[i], w);
-    double u = w * r[D * D + D];
-#pragma unroll
-    for (int i = 0; i < D; ++i) u = fma(r[D * D + i], lam[i], u);
+    const double row = lrec[s * RP + rl];
+    static_for<D>([&](auto ic) {   // w += g_k . c_j
+      constexpr int i = decltype(ic)::value;
+      w = fmac_row<RU + i>(w, row, cf[i]);
+    });
+    double u = w * bcast_row<D * D + D>(row);
+    static_for<D>([&](auto ic) {
+      constexpr int i = decltype(ic)::value;
+      u = fmac_row<D * D + i>(u, row, lam[i]);
+    });
     lam[0] -= u;
     double nl[D];
-#pragma unroll
-    for (int q = 0; q < D; ++q) {
+    static_for<D>([&](auto qc) {
+      constexpr int q = decltype(qc)::value;
       double acc = 0.0;
-#pragma unroll
-      for (int i = 0; i < D; ++i) acc = fma(r[i * D + q], lam[i], acc);
+      static_for<D>([&](auto ic) {
+        constexpr int i = decltype(ic)::value;
+        acc = fmac_row<i * D + q>(acc, row, lam[i]);
+      });
       nl[q] = acc;
-    }
+    });
 #pragma unroll
     for (int i = 0; i < D; ++i) lam[i] = nl[i];
     // u only where the caller reads it; elsewhere an out-of-range offset (dropped)
