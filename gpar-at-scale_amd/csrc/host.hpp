@@ -94,8 +94,9 @@ struct gpar_ctx {
   // kDgRowsAuto: +40 in the round-by-round fit, where the whitening side (3.19 ms whitening since
   // the DPP step rows, r05r) has time to spare and the Gram CUs' side sets the span (north, same
   // box, 3 pairs: 5.074 ms per Gram / 17.584 s per job at +10 with the r05p whitening, 5.012 ms /
-  // 17.384 s at +40; +60: 5.25 ms), 0 in the round overlap, whose whitening side also runs the
-  // other group's tails and gains (the 8-output shard: 2.353 s at +10, 2.329 at 0, r04ad)
+  // 17.384 s at +40; +60: 5.25 ms), +20 in the round overlap, whose whitening side also runs the
+  // other group's tails and gains (the 8-output shard 3/8, r05r: 2.278 s at 0, 2.244 at +20,
+  // 2.304 at +40; with the r04 whitening 0 was best, r04ad)
   int dg_rows_w = gpar::kDgRowsAuto;
   // "serialize": side, s_w, s_g, s_g2 and s_d all alias `main`, so every launch runs in issue order
   // on one stream (the created streams stay in own_*): the order-free reference the concurrent

@@ -231,7 +231,7 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
   // gains here (one 8-output shard of the north job: 2.356 -> 2.329 s per step, r04p; the
   // round-by-round 63-output fit is slower with it, 17.75 -> 18.69 s)
   sp.post_gram = c->post_gram != 0;
-  sp.dg_rows_w = c->dg_rows_w == kDgRowsAuto ? 0 : c->dg_rows_w;
+  sp.dg_rows_w = c->dg_rows_w == kDgRowsAuto ? 20 : c->dg_rows_w;
   // a group's dense tail + finish on the context stream as soon as its round's last Gram is
   // issued; its values land in pinned memory, ev_grp[g] marks them
   // (on the whitening CUs: beside the Gram on the whole chip it slowed every Gram by ~5 %)

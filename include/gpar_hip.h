@@ -168,7 +168,7 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *   "predict_fused" as gpar_ctx_set_predict_fused (changes the summation order: last bits)
  *   "dg_rows_w"     percent more rows per diagonal-block time split on the whitening CUs of a
  *                   split Gram, fewer on the Gram CUs; -100 (default) = auto: 40 in the
- *                   round-by-round fit, 0 in the round overlap (changes G's summation grouping:
+ *                   round-by-round fit, 20 in the round overlap (changes G's summation grouping:
  *                   last bits, like predict_fused)
  *   "gram_group"    outputs per grouped Gram of an unsplit batched fit: the group's outputs whiten
  *                   over two streams into buffers of their own and one set of Gram launches covers

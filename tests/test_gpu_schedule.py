@@ -43,7 +43,7 @@ SETTINGS = [
     {"predict_lanes": 1},
 ]
 # dg_rows_w (a plan: G's summation grouping) is pinned for the comparisons: its auto value differs
-# between the round-by-round fit (+40 %) and the round overlap (0), which the settings switch
+# between the round-by-round fit (+40 %) and the round overlap (+20 %), which the settings switch
 PLAN = {"dg_rows_w": 10}
 DEFAULTS = {"serialize": 0, "overlap": 1, "overlap_group": 0, "dense_early": 1, "post_gram": -1,
             "compact_rec": -1, "dg_rows_w": -100, "qu_batch": 1, "predict_lanes": 2,
