@@ -121,12 +121,13 @@ def chained_predictions(outputs, owners: dict, predict_fn, chain, prepare_fn=Non
 # ranks are still fitting; each later block is sized so its fits end about when the sweep reaches
 # it.  chained_sweep_blocks then passes the means along block by block (point to point).
 # Defaults: one rank's batched fit + posterior at the north config, fit_ms(n) ~ FIT_FIXED_MS +
-# FIT_MS_PER_OUTPUT n, and one chained prediction SWEEP_MS_PER_OUTPUT, fitted to the r05 one-GPU
-# shard lines (bench --shard R/8 --inference chained for blocks of 7, 8, 9 outputs: 1997, 2168,
-# 2486 ms of fits, 14.17 ms per chained prediction; profiles/chained_projection_r05l.json).
-FIT_FIXED_MS = 285.0
-FIT_MS_PER_OUTPUT = 245.0
-SWEEP_MS_PER_OUTPUT = 14.2
+# FIT_MS_PER_OUTPUT n, and one chained prediction SWEEP_MS_PER_OUTPUT, least-squares fitted to the
+# r05s one-GPU shard lines (bench --shard R/8 --inference chained, ranks 0 / 3 / 7 with 6 / 8 / 9
+# GPAR outputs: 1789, 2155, 2453 ms of fits, 13.71 ms per chained prediction;
+# profiles/chained_projection_r05s.json).  assign_chained picks the same blocks as with r05l's.
+FIT_FIXED_MS = 477.0
+FIT_MS_PER_OUTPUT = 216.0
+SWEEP_MS_PER_OUTPUT = 13.7
 # a block of k means (8 N* bytes each) to the next owner: ASSUMED xGMI figures (never measured on
 # this pool, whose boxes have one GPU): 50 GB/s effective and 40 us per transfer
 XFER_GBS_ASSUMED = 50.0
