@@ -2415,12 +2415,8 @@ void launch_adjoint_local_wide(hipStream_t st, int sdim, double* X, int64_t ldx,
                                const double* rec, const double* g, const double* cin, int64_t mc,
                                int64_t n, int L, int64_t nch, double* bend, const double* wmask) {
   // a prediction's Mp + 1 <= 576 columns in one workgroup per chunk: the whole row of X is read
-  // by one workgroup at a time (GPAR_ADJ_CW=256: 256-column workgroups, A/B)
-  static const int cw_env = [] {
-    const char* e = std::getenv("GPAR_ADJ_CW");
-    return e ? std::atoi(e) : 576;
-  }();
-  if (cw_env == 576 && ncols <= 576 && ncols > 256) {
+  // by one workgroup at a time (256-column workgroups otherwise)
+  if (ncols <= 576 && ncols > 256) {
     dim3 grid((unsigned)nch, 1u);
     GPAR_DISPATCH_D(sdim, (adjoint_local_wide<DD, 576><<<grid, 576, 0, st>>>(X, ldx, ncols, rec, g, cin, mc, n, L, bend, wmask)));
     return;
