@@ -47,19 +47,39 @@ struct TrsmJob {
 };
 
 // ---------------------------------------------------------------------------- Kuu
+// One 16 x 16 tile of K per workgroup.  The tile's 16 + 16 pseudo-inputs are staged in LDS 64
+// dimensions at a time (coalesced row reads), then each thread forms its d2 in the same order as a
+// plain loop over the dimensions: the per-element global reads of two strided rows took 0.94 ms
+// for the north batch's 63 x 512^2 entries, at the head of every Nelder-Mead round (r05y trace).
 __global__ __launch_bounds__(256) void kuu_kernel(const KuuJob* __restrict__ jobs) {
   const KuuJob jb = jobs[blockIdx.z];
-  const int i = blockIdx.y * 16 + (threadIdx.x >> 4);
-  const int j = blockIdx.x * 16 + (threadIdx.x & 15);
+  __shared__ double zi[16][65], zj[16][65];
+  const int tid = threadIdx.x, ti = tid >> 4, tj = tid & 15;
+  const int i0 = blockIdx.y * 16, j0 = blockIdx.x * 16;
+  if (i0 >= jb.mpad || j0 >= jb.mpad) return;   // workgroup-uniform
+  const int i = i0 + ti, j = j0 + tj;
+  double d2 = 0.0;
+  if (i0 < jb.m && j0 < jb.m) {   // workgroup-uniform: a tile with a real row and column
+    for (int q0 = 0; q0 < jb.d; q0 += 64) {
+      const int nq = (jb.d - q0 < 64) ? jb.d - q0 : 64;
+      __syncthreads();
+      for (int e = tid; e < 16 * 64; e += 256) {
+        const int r = e >> 6, q = e & 63;
+        const bool qv = q < nq;
+        zi[r][q] = (qv && i0 + r < jb.m) ? jb.z[(int64_t)(i0 + r) * jb.ldz + q0 + q] : 0.0;
+        zj[r][q] = (qv && j0 + r < jb.m) ? jb.z[(int64_t)(j0 + r) * jb.ldz + q0 + q] : 0.0;
+      }
+      __syncthreads();
+      for (int q = 0; q < nq; ++q) {
+        const double a = zi[ti][q] - zj[tj][q];
+        d2 = fma(a, a, d2);
+      }
+    }
+  }
   if (i >= jb.mpad || j >= jb.mpad) return;
   if (i >= jb.m || j >= jb.m) {
     jb.K[(int64_t)i * jb.ldk + j] = (i == j) ? 1.0 : 0.0;
     return;
-  }
-  double d2 = 0.0;
-  for (int q = 0; q < jb.d; ++q) {
-    const double a = jb.z[(int64_t)i * jb.ldz + q] - jb.z[(int64_t)j * jb.ldz + q];
-    d2 = fma(a, a, d2);
   }
   double v;
   if (jb.kind == KEQ)

@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 tag=${1:-trace}
 rm -rf gpurun_out/$tag
-timeout -k 10 400 rocprofv3 --kernel-trace -d gpurun_out/$tag -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --evals 8 --no-cpu-baseline --h2h-steps 0 > gpurun_out/${tag}.json 2> gpurun_out/${tag}.err || { echo TRACE FAILED; tail -20 gpurun_out/${tag}.err; exit 1; }
+timeout -k 10 400 rocprofv3 --kernel-trace -d gpurun_out/$tag -o run --output-format csv -- python3 bench.py --steps 1 --warmup 0 --evals ${EVALS:-8} --no-cpu-baseline --h2h-steps 0 > gpurun_out/${tag}.json 2> gpurun_out/${tag}.err || { echo TRACE FAILED; tail -20 gpurun_out/${tag}.err; exit 1; }
 f=$(find gpurun_out/$tag -name "*kernel_trace.csv" | head -1)
 echo "trace: $f"
 python tools/trace_rounds.py "$f" --top 25 > gpurun_out/${tag}_rounds.txt
