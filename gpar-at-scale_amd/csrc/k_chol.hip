@@ -61,6 +61,35 @@ __device__ __forceinline__ void load_b(double* S, const double* G, int64_t ld, i
     for (int e = tid; e < kNB * kNB; e += 256) S[(e & 63) * kSB + (e >> 6)] = G[(int64_t)(e >> 6) * ld + (e & 63)];
   }
 }
+// The same block loads split in two: global -> 16 registers per thread (issued before a block
+// product, so the next k-step's loads are in flight under its MFMAs), then registers -> LDS.
+struct BlkRegs {
+  double v[16];
+};
+__device__ __forceinline__ void fetch_blk(BlkRegs& r, const double* G, int64_t ld, int tid) {
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = tid + 256 * u;
+    r.v[u] = G[(int64_t)(e >> 6) * ld + (e & 63)];
+  }
+}
+__device__ __forceinline__ void put_a(double* S, const BlkRegs& r, int tid) {
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = tid + 256 * u;
+    S[(e >> 6) * kSA + (e & 63)] = r.v[u];
+  }
+}
+__device__ __forceinline__ void put_b(double* S, const BlkRegs& r, int tid, bool trans) {
+#pragma unroll
+  for (int u = 0; u < 16; ++u) {
+    const int e = tid + 256 * u;
+    if (!trans)
+      S[(e >> 6) * kSB + (e & 63)] = r.v[u];
+    else
+      S[(e & 63) * kSB + (e >> 6)] = r.v[u];
+  }
+}
 // store acc (optionally scaled) into a row-major global block: G = alpha * acc (+ G if add)
 __device__ __forceinline__ void store_c(double* G, int64_t ld, const d4 (&acc)[4], int lane, int wave,
                                         double alpha, bool add) {
@@ -227,11 +256,19 @@ __global__ __launch_bounds__(256) void tinv_step(const CholJob2* __restrict__ jo
   __shared__ double Bs[kNB * kSB];
   d4 acc[4];
   zero4(acc);
+  // L_ik and T_kj of step k + 1 are fetched into registers under step k's block product
+  BlkRegs ra, rb;
+  fetch_blk(ra, jb.A + (int64_t)i * kNB * ld + (int64_t)j * kNB, ld, tid);   // L_ij
+  fetch_blk(rb, jb.T + (int64_t)j * kNB * ld + (int64_t)j * kNB, ld, tid);   // T_jj
   for (int k = j; k < i; ++k) {
     __syncthreads();
-    load_a(As, jb.A + (int64_t)i * kNB * ld + (int64_t)k * kNB, ld, tid);   // L_ik
-    load_b(Bs, jb.T + (int64_t)k * kNB * ld + (int64_t)j * kNB, ld, tid, false);   // T_kj
+    put_a(As, ra, tid);
+    put_b(Bs, rb, tid, false);
     __syncthreads();
+    if (k + 1 < i) {
+      fetch_blk(ra, jb.A + (int64_t)i * kNB * ld + (int64_t)(k + 1) * kNB, ld, tid);
+      fetch_blk(rb, jb.T + (int64_t)(k + 1) * kNB * ld + (int64_t)j * kNB, ld, tid);
+    }
     mma64(As, Bs, acc, lane, wave, kNB);
   }
   __syncthreads();
@@ -275,16 +312,27 @@ __global__ __launch_bounds__(256) void tgt_kernel(const TgtJob* __restrict__ job
   d4 acc[4];
   zero4(acc);
   const int kend = (mode == 0) ? i : j;
+  // the operands of step k: mode 0 T_ik, G_kj; mode 1 X_ik, T_jk (transposed into LDS); step
+  // k + 1's are fetched into registers under step k's block product
+  auto src_a = [&](int k) {
+    return (mode == 0 ? jb.T : jb.X) + (int64_t)i * kNB * ld + (int64_t)k * kNB;
+  };
+  auto src_b = [&](int k) {
+    return mode == 0 ? jb.G + (int64_t)k * kNB * ld + (int64_t)j * kNB
+                     : jb.T + (int64_t)j * kNB * ld + (int64_t)k * kNB;
+  };
+  BlkRegs ra, rb;
+  fetch_blk(ra, src_a(0), ld, tid);
+  fetch_blk(rb, src_b(0), ld, tid);
   for (int k = 0; k <= kend; ++k) {
     __syncthreads();
-    if (mode == 0) {
-      load_a(As, jb.T + (int64_t)i * kNB * ld + (int64_t)k * kNB, ld, tid);          // T_ik
-      load_b(Bs, jb.G + (int64_t)k * kNB * ld + (int64_t)j * kNB, ld, tid, false);   // G_kj
-    } else {
-      load_a(As, jb.X + (int64_t)i * kNB * ld + (int64_t)k * kNB, ld, tid);          // X_ik
-      load_b(Bs, jb.T + (int64_t)j * kNB * ld + (int64_t)k * kNB, ld, tid, true);    // T_jk^T
-    }
+    put_a(As, ra, tid);
+    put_b(Bs, rb, tid, mode != 0);
     __syncthreads();
+    if (k + 1 <= kend) {
+      fetch_blk(ra, src_a(k + 1), ld, tid);
+      fetch_blk(rb, src_b(k + 1), ld, tid);
+    }
     mma64(As, Bs, acc, lane, wave, kNB);
   }
   if (mode == 0) {
