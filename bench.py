@@ -125,7 +125,7 @@ def main():
     ap.add_argument("--schedule", default="",
                     help="schedule knobs as k=v,k=v (gpar_ctx_set_schedule, include/gpar_hip.h: "
                          "overlap, overlap_group, predict_fused, qu_batch, dense_early, "
-                         "predict_lanes, serialize, post_gram, compact_rec, dg_rows_w)")
+                         "predict_lanes, serialize, post_gram, compact_rec, dg_rows_w, gram_group)")
     ap.add_argument("--cpu-baseline-child", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--cpu-check-file", default=None, help=argparse.SUPPRESS)
     ap.add_argument("--stub", action="store_true",

@@ -271,6 +271,13 @@ int32_t gpar_ctx_kernel_work(gpar_ctx* ctx, const char* name, double* work) {
   API_END(ctx)
 }
 
+int64_t gpar_debug_counter(const char* name) {
+  if (!name) return -1;
+  if (std::strcmp(name, "gains_fast") == 0) return g_gains_fast_launches.load();
+  if (std::strcmp(name, "gains_general") == 0) return g_gains_general_launches.load();
+  return -1;
+}
+
 int32_t gpar_ctx_set_input_stream(gpar_ctx* ctx, void* stream, int32_t enable) {
   if (!ctx) return GPAR_ERR_STATE;
   ctx->has_input_stream = enable != 0;

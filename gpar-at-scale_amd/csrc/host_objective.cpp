@@ -77,8 +77,10 @@ static int gram_group_size(gpar_ctx* c, const std::vector<DevProblem>& P, int64_
                            int64_t mpmax, bool fix_beta, int nlanes, bool split_pipe) {
   const int np = (int)P.size();
   if (fix_beta || nlanes > 1 || split_pipe || np < 2) return 0;
+  // the grouped launch takes one chunk-correction template (sdim) and carry stride (mc) for the
+  // whole group: outputs with another time kernel keep the per-output Grams
   for (const auto& p : P)
-    if (p.mp != mpmax || p.n != n) return 0;
+    if (p.mp != mpmax || p.n != n || p.sdim != P[0].sdim || p.mc != P[0].mc) return 0;
   int g = c->gram_group;
   if (g == 0 || g == 1) return 0;
   if (g < 0) {

@@ -19,6 +19,7 @@
 //    consumer: vec_fix_kernel here, the Gram loader in k_gram.hip).
 #include "device_common.hpp"
 
+#include <atomic>
 #include <cstdlib>
 
 namespace gpar {
@@ -2148,6 +2149,10 @@ static_assert(gpar::kMomStride == gpar::kGainsMomStride, "moment stride");
 
 namespace gpar {
 
+// phase-3 launches by path since the library was loaded (gpar_debug_counter "gains_fast" /
+// "gains_general"): lets a test assert which kernel a case actually ran
+std::atomic<int64_t> g_gains_fast_launches{0}, g_gains_general_launches{0};
+
 #define GPAR_DISPATCH_D(D, ...)                                   \
   switch (D) {                                                    \
     case 1: { constexpr int DD = 1; __VA_ARGS__; } break;         \
@@ -2172,6 +2177,7 @@ static void launch_phase3_blocks(dim3 grid, hipStream_t st, const double* t, int
     if (L == kG3L && fast_ok) {
       gains_phase3_fast<D, C, Y, NZ, PFX, MOM><<<grid, 256, 0, st>>>(
           t, n, nch, cps, noise, pstart, rec, g, phi, logs, pf, ys, alpha_loc, asend, mom);
+      g_gains_fast_launches.fetch_add(1, std::memory_order_relaxed);
       return;
     }
   }
@@ -2182,6 +2188,7 @@ static void launch_phase3_blocks(dim3 grid, hipStream_t st, const double* t, int
   gains_phase3<D, C, Y, NZ, PFX, true, MOM><<<glast, 256, 0, st>>>(last, t, n, L, nch, cps, noise,
                                                                    pstart, rec, g, phi, logs, pf, ys,
                                                                    alpha_loc, asend, mom);
+  g_gains_general_launches.fetch_add(1, std::memory_order_relaxed);
 }
 
 template <int D, bool C, bool Y, bool NZ>

@@ -1,6 +1,7 @@
 // launch.hpp -- host-callable launch wrappers of the gfx950 kernels (one per .hip file).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cstdint>
 
 namespace gpar {
@@ -102,6 +103,8 @@ constexpr int kRecStride3 = 16;
 inline int rec_size(int sdim) { return sdim == 3 ? 16 : (sdim == 2 ? 8 : 4); }
 
 // k_lgssm.hip
+// phase-3 launches of launch_gains by path (k_lgssm.hip; gpar_debug_counter)
+extern std::atomic<int64_t> g_gains_fast_launches, g_gains_general_launches;
 void launch_gains(hipStream_t st, int sdim, const double* t, int64_t n, int L, int64_t nch,
                   int nchains, const ChainParamsHost* cps_dev, const double* noise,
                   double* agg, double* pstart, double* rec, double* g, double* phi,

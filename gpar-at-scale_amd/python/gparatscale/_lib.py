@@ -24,7 +24,7 @@ EXPORTED = (
     "gpar_ctx_workspace_bytes", "gpar_ctx_trim", "gpar_dtc_objective", "gpar_dtc_objective_A",
     "gpar_fit", "gpar_fit_predict", "gpar_fit_predict_chain", "gpar_mc_normals", "gpar_path_normals", "gpar_lgssm_posterior_rand", "gpar_q_u", "gpar_predict", "gpar_lgssm_logpdf", "gpar_lgssm_smooth",
     "gpar_sde_predictions", "gpar_exact_logpdf", "gpar_exact_posterior",
-    "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_ctx_kernel_work", "gpar_ctx_reset_stats",
+    "gpar_ctx_set_profiling", "gpar_ctx_kernel_stats", "gpar_debug_counter", "gpar_ctx_kernel_work", "gpar_ctx_reset_stats",
     "gpar_ctx_set_lanes", "gpar_ctx_set_cu_split", "gpar_ctx_set_fit_overlap", "gpar_ctx_get_cu_split", "gpar_ctx_set_dist_cache", "gpar_ctx_set_dist_cache_keep", "gpar_ctx_dist_cache_stats",
     "gpar_pairwise_distances", "gpar_ctx_set_predict_fused", "gpar_ctx_set_input_stream", "gpar_ctx_set_schedule", "gpar_ctx_get_schedule",
     "gpar_fit_posterior", "gpar_posterior_predict", "gpar_posterior_prepare", "gpar_posterior_destroy",
@@ -97,6 +97,7 @@ def load(path: str | None = None):
             "gpar_ctx_kernel_stats": (i32, [vp, C.c_char_p, C.POINTER(i64), C.POINTER(C.c_double)]),
             "gpar_ctx_reset_stats": (i32, [vp]),
             "gpar_ctx_kernel_work": (i32, [vp, C.c_char_p, C.POINTER(C.c_double)]),
+            "gpar_debug_counter": (i64, [C.c_char_p]),
             "gpar_ctx_set_lanes": (i32, [vp, i32]),
             "gpar_ctx_set_cu_split": (i32, [vp, i32]),
             "gpar_ctx_get_cu_split": (i32, [vp, C.POINTER(C.c_int32)]),
@@ -177,6 +178,12 @@ def _torch_runtime_first():
         import torch  # noqa: F401
     except ImportError:
         pass
+
+
+def debug_counter(name):
+    """A process-wide diagnostic counter of the library (gpar_debug_counter): "gains_fast" /
+    "gains_general" = phase-3 gains launches by kernel path."""
+    return int(load().gpar_debug_counter(name.encode()))
 
 
 class Context:

@@ -115,6 +115,10 @@ int32_t gpar_ctx_reset_stats(gpar_ctx* ctx);
  * gains records + fix-up rows, beta written), with M in place of D when the distances come from the
  * fit's cache. */
 int32_t gpar_ctx_kernel_work(gpar_ctx* ctx, const char* name, double* work);
+/* Process-wide diagnostic counters (tests; no device work): "gains_fast" / "gains_general" = the
+ * gains' phase-3 launches that took the LDS-DMA fast kernel / the general kernels since the library
+ * was loaded.  -1 for an unknown name. */
+int64_t gpar_debug_counter(const char* name);
 /* Concurrency of batched calls (gpar_dtc_objective / gpar_fit with nprob > 1): lanes = 2
  * alternates the outputs' whitening + Gram between two HIP streams with separate workspaces so
  * one output's whitening overlaps another's Gram (~1 % faster at N = 1e6, M = 512, two beta

@@ -6,6 +6,11 @@ broadcasts it (shard.broadcast_inputs, over gloo here, RCCL in bench), each rank
 outputs assign_outputs() gives it on device inputs, and shard.gather_thetas all-reduces the
 P x 5 rows.  Rank 0 writes the gathered rows to argv[1].
 
+argv[2] == "chained_blocks": bench.py's real multi-rank chained path -- contiguous output blocks
+(shard.assign_chained) and the staggered point-to-point sweep (shard.chained_sweep_blocks: recv of
+the earlier blocks, isend of this rank's block, the final broadcast from the last owner), with the
+real Posterior.predict / prepare on device tensors (gloo stages them through host memory).
+
 argv[2] == "chained": the chained path of bench.py --inference chained across ranks
 (GPAR_scaled_examples.jl:172, eeg.jl:249,274): each rank's fits keep q(u) on the device
 (gpar_fit_posterior), then shard.chained_predictions walks outputs 2..P in order, the owner of
@@ -49,18 +54,19 @@ def main(out, mode="given"):
         S.broadcast_inputs((t_h, Y_h, ts_h, F_h))
         dev = torch.device("cuda", 0)
         t_d, Y_d, ts_d = t_h.to(dev), Y_h.to(dev), ts_h.to(dev)
-        shards = S.assign_outputs(P, world)
+        blocks = mode == "chained_blocks"
+        shards = S.assign_chained(P, world) if blocks else S.assign_outputs(P, world)
         mine = [p for p in shards[rank] if p >= 2]
         res = {}
         keep, problems = [], []
         for p in mine:
             Z = torch.from_numpy(Dd.pseudo_inputs(Y_h.numpy()[:, : p - 1], M, seed=p)).to(dev)
             pr, k = G.make_problem(Y_d[:, : p - 1], Z, t_d, Y_d[:, p - 1].contiguous(),
-                                   qu_kuu_noise=mode == "chained")
+                                   qu_kuu_noise=mode in ("chained", "chained_blocks"))
             problems.append(pr)
             keep.append((k, Z))
         result = {"world": world, "shards": shards}
-        if mode == "chained":
+        if mode in ("chained", "chained_blocks"):
             post = None
             if mine:
                 post = G.fit_posterior(problems, np.tile(X0, (len(mine), 1)), max_evals=EV,
@@ -70,10 +76,15 @@ def main(out, mode="given"):
             chain = torch.zeros((NS, P), dtype=torch.float64, device=dev)
             chain[:, 0] = F_h[:, 0].to(dev)     # output 1's true values (GPAR_scaled_examples.jl:172)
             outs = list(range(2, P + 1))
-            got = S.chained_predictions(
-                outs, S.owners_of(shards),
-                lambda p, c: post.predict(idx[p], ts_d, c[:, : p - 1]), chain,
-                prepare_fn=lambda p: post.prepare(idx[p], ts_d))
+            if blocks:
+                got = S.chained_sweep_blocks(
+                    shards, lambda p, c: post.predict(idx[p], ts_d, c[:, : p - 1]), chain,
+                    prepare_fn=lambda p: post.prepare(idx[p], ts_d))
+            else:
+                got = S.chained_predictions(
+                    outs, S.owners_of(shards),
+                    lambda p, c: post.predict(idx[p], ts_d, c[:, : p - 1]), chain,
+                    prepare_fn=lambda p: post.prepare(idx[p], ts_d))
             torch.cuda.synchronize()
             stds = torch.zeros((NS, P), dtype=torch.float64)
             for p, (_, s) in got.items():

@@ -162,7 +162,10 @@ def test_gains_fast_path_bit_identical_to_general(kind, monkeypatch):
     chunk counts inside one block and across blocks, with short last chunks, large time gaps
     (negative stale steps) and short length scales."""
     rng = np.random.default_rng(11)
-    for n in (1300, 256 * 300 + 7):
+    # 256 * 300 + 8: an even n, so every chain's row of Y (ldy = n) is 16-byte aligned and the
+    # multi-block case really takes the fast kernel with data (an odd n misaligns row 1 and the
+    # library falls back to the general kernel for both settings; ADVICE r05)
+    for n in (1300, 256 * 300 + 8):
         t = np.cumsum(rng.exponential(0.05, n) + np.where(rng.random(n) < 0.01, 3.0, 0.0))
         Y = np.ascontiguousarray(rng.normal(size=(3, n)))
         th = np.array([[0.05, 1.3, 0.2], [0.5, 0.7, 0.6], [4.0, 2.0, 0.05]])
@@ -170,16 +173,24 @@ def test_gains_fast_path_bit_identical_to_general(kind, monkeypatch):
         out = {}
         for fast in ("1", "0"):
             monkeypatch.setenv("GPAR_GAINS_FAST", fast)
+            f0 = G.debug_counter("gains_fast")
             lml = np.asarray(G.lgssm_logpdf_batch(t, Y, th, kind))
             m, v = G.lgssm_smooth_batch(t, Y, th, kind, noise=noise)
             out[fast] = (lml, np.asarray(m), np.asarray(v))
+            took = G.debug_counter("gains_fast") - f0
+            assert (took >= 1) if fast == "1" else (took == 0), (n, fast, took)
         for a, b in zip(out["1"], out["0"]):
             assert np.all(np.isfinite(a))
             assert np.array_equal(a, b)
-    t, V, Z, y = _case(1300, 3, 40, 3)
-    vals = []
-    for fast in ("1", "0"):
-        monkeypatch.setenv("GPAR_GAINS_FAST", fast)
-        vals.append(G.compute_gpar_dtc_objective(V, Z, t, y, (1.2, 0.9, 1.1, 1.1, 0.3),
-                                                 time_kernel=kind))
-    assert np.isfinite(vals[0]) and vals[0] == vals[1]
+    # DTC objectives (the shared gains with data, HAS_Y): inside one block and across blocks
+    for n in (1300, 256 * 300 + 8):
+        t, V, Z, y = _case(n, 3, 40, 3)
+        vals = []
+        for fast in ("1", "0"):
+            monkeypatch.setenv("GPAR_GAINS_FAST", fast)
+            f0 = G.debug_counter("gains_fast")
+            vals.append(G.compute_gpar_dtc_objective(V, Z, t, y, (1.2, 0.9, 1.1, 1.1, 0.3),
+                                                     time_kernel=kind))
+            took = G.debug_counter("gains_fast") - f0
+            assert (took >= 1) if fast == "1" else (took == 0), (n, fast, took)
+        assert np.isfinite(vals[0]) and vals[0] == vals[1], (n, vals)

@@ -119,3 +119,17 @@ def test_cross_rank_chained_sweep_equals_fit_predict_chain(world, tmp_path):
     np.testing.assert_array_equal(np.array(got["means"]), means)
     np.testing.assert_array_equal(np.array(got["stds"]), stds)
     assert np.all(np.isfinite(means)) and np.all(stds > 0)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_cross_rank_chained_blocks_equal_fit_predict_chain(world, tmp_path):
+    """bench.py's staggered chained path (assign_chained blocks, chained_sweep_blocks' point-to-point
+    relay and final broadcast) with the real posteriors on device tensors: bit-identical to one
+    single-process gpar_fit_predict_chain."""
+    got = _run_world(world, str(tmp_path / "blocks.json"), mode="chained_blocks")
+    flat = [p for s in got["shards"] for p in s]
+    assert sorted(flat) == list(range(1, W.P + 1))
+    th, means, stds = _serial_chain()
+    np.testing.assert_array_equal(np.array(got["theta"])[1:], th)
+    np.testing.assert_array_equal(np.array(got["means"]), means)
+    np.testing.assert_array_equal(np.array(got["stds"]), stds)

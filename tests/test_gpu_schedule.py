@@ -194,3 +194,38 @@ def test_grouped_gram_is_a_plan_not_a_schedule():
         for i in range(len(outs)):
             np.testing.assert_allclose(a[2][i], off[2][i], rtol=1e-7, atol=1e-9)
             np.testing.assert_allclose(a[3][i], off[3][i], rtol=1e-7, atol=1e-9)
+
+
+def test_grouped_gram_mixed_time_kernels_match_per_output():
+    """A batch of small problems with the same N and Mp but different time kernels (Matern-1/2
+    and Matern-5/2: different state dimension, so a different chunk correction in the Gram): the
+    grouped plan must not run them under one group's correction.  Auto grouping equals the
+    per-output Grams (gram_group = 0) within rounding, output by output."""
+    import torch
+    dev = torch.device("cuda", 0)
+    n, m, outs = 30_000, 128, [2, 3, 5, 9]
+    ds = D.gpar_dataset(n, max(outs), seed=4, observation_noise=0.8)
+    Y_d = torch.from_numpy(ds["Y"]).to(dev)
+    t_d = torch.from_numpy(ds["t"]).to(dev)
+    probs, keep = [], []
+    for i, p in enumerate(outs):
+        Z = torch.from_numpy(D.pseudo_inputs(ds["Y"][:, : p - 1], m, seed=p)).to(dev)
+        tk = "matern12" if i % 2 else "matern52"
+        pr, k = G.make_problem(Y_d[:, : p - 1], Z, t_d, Y_d[:, p - 1].contiguous(), "matern52",
+                               tk, qu_kuu_noise=True)
+        probs.append(pr)
+        keep.append((k, Z))
+    ctx = G.context(0)
+    ctx.set_cu_split(-1)
+    th = np.tile([[1.1, 0.9, 1.3, 0.8, 0.3]], (len(outs), 1))
+    vals = {}
+    try:
+        for g in (0, -1, 2):
+            ctx.set_schedule("gram_group", g)
+            vals[g] = np.asarray(G.dtc_objective_batch(probs, th))
+    finally:
+        for k, v in DEFAULTS.items():
+            ctx.set_schedule(k, v)
+    singles = np.array([G.dtc_objective_batch([pr], th[i:i + 1])[0] for i, pr in enumerate(probs)])
+    for g in (0, -1, 2):
+        np.testing.assert_allclose(vals[g], singles, rtol=1e-10)
