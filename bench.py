@@ -49,6 +49,10 @@ CONFIGS = {
     # configs[2]: state-space (Matern-3/2) temporal-only chains, N=1e6, P=16 (a9, batched over
     # chains: one NM over all chains, then RTS smoothing at N* = N test times)
     "ssm": dict(N=1_000_000, M=0, P=16, evals=50, out_kernel="matern32", temporal=True),
+    # configs[4] (stress): N=1e7, M=1024, P=256 DTC-GPAR, per-evaluation throughput only (SURVEY
+    # §8d: "one full fit would be hours"): each step is one batched Nelder-Mead fit of `evals`
+    # objective evaluations per GPAR output of the rank's shard (stress_main)
+    "stress": dict(N=10_000_000, M=1024, P=256, evals=6, out_kernel="matern52", per_eval=True),
 }
 # MI355X dense fp64 matrix peak: 1024 SIMDs x 2048 flop per v_mfma_f64_16x16x4_f64 / 64 cycles
 # (SQ_VALU_MFMA_BUSY_CYCLES / SQ_INSTS_MFMA = 64, profiles/) x 2.4 GHz = 78.6 TF/s (AMD spec value)
@@ -140,6 +144,8 @@ def main():
         return stub_rank(args)
     if args.cpu_baseline_child:
         return cpu_baseline_child(args)
+    if CONFIGS[args.config].get("per_eval"):
+        return stress_main(args)
     world0 = int(os.environ.get("WORLD_SIZE", "1"))
     cfg0 = CONFIGS[args.config]
     # the CPU baseline runs in a child process started before anything touches the GPU, so it
@@ -898,6 +904,223 @@ def main():
         dist.destroy_process_group()
 
 
+def stress_main(args):
+    """BASELINE config 5 (stress: N = 1e7, M = 1024, P = 256, DTC-GPAR, fp64), per-evaluation
+    throughput ("Per-evaluation throughput, 8 GPUs").  Outputs 2..P are
+    sharded over the ranks by LPT with the D-dependent cost model (shard.output_cost_sized); one
+    step = one batched Nelder-Mead fit of exactly `evals` objective evaluations (dtc.jl:83-128) per
+    GPAR output this rank owns, fixed init log theta = (0, 0, 0, 0, -2).  --shard R/W runs rank R's
+    outputs of a W-way job on this one GPU.  value = N x (evaluations in the step) / step time, the
+    whole job's evaluation throughput (summed over ranks).  The temporal-only output 1 (O(N)) is
+    not part of this per-evaluation figure."""
+    import torch
+    import torch.distributed as dist
+    import gparatscale as G
+    from gparatscale import data as D
+    from gparatscale import shard as S
+    cfg = dict(CONFIGS[args.config])
+    if args.evals:
+        cfg["evals"] = args.evals
+    N, M, P, EV = cfg["N"], cfg["M"], cfg["P"], cfg["evals"]
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = 0 if args.rehearse else int(os.environ.get("LOCAL_RANK", "0"))
+    cpu_child = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu_child = start_cpu_baseline(args)   # before this process touches the GPU
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        if args.rehearse:
+            dist.init_process_group("gloo", timeout=pg_timeout())
+        else:
+            dist.init_process_group("nccl", device_id=dev, timeout=pg_timeout())
+    cost = lambda p: S.output_cost_sized(p, N, M, EV)   # noqa: E731
+    gpar_all = list(range(2, P + 1))
+    w_ = world
+    r_ = rank
+    if args.shard:
+        if world > 1:
+            sys.exit("--shard R/W: one process")
+        r_, w_ = (int(x) for x in args.shard.split("/"))
+    shards = S.assign_outputs(P, w_, cost=cost)
+    mine = [p for p in shards[r_] if p >= 2]
+    # inputs (untimed): generated on the device (20 GB of Y), broadcast from rank 0 over RCCL
+    t0 = time.perf_counter()
+    t_d = torch.empty(N, dtype=torch.float64, device=dev)
+    Y_d = torch.empty((N, P), dtype=torch.float64, device=dev)
+    if rank == 0:
+        x, Y = D.gpar_dataset_device(N, P, seed=0, observation_noise=0.8, device=dev)
+        t_d.copy_(x)
+        Y_d.copy_(Y)
+        del x, Y
+    S.broadcast_inputs((t_d, Y_d))
+    problems, keep = [], []
+    for p in mine:
+        idx = torch.from_numpy(D.pseudo_index(N, M, seed=p)).to(dev)
+        Z = Y_d[idx, : p - 1].contiguous()
+        pr, k = G.make_problem(Y_d[:, : p - 1], Z, t_d, Y_d[:, p - 1].contiguous(),
+                               cfg["out_kernel"], "matern52")
+        problems.append(pr)
+        keep.append((k, Z))
+    x0 = np.tile(np.array([0.0, 0.0, 0.0, 0.0, -2.0]), (len(problems), 1))
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] stress inputs ready in {time.perf_counter() - t0:.1f}s: N={N} M={M} "
+        f"P={P} shard {r_}/{w_}: {len(mine)} outputs (D {min(mine) - 1}..{max(mine) - 1})")
+    ctx = G.context(local)
+    for kv in filter(None, args.schedule.split(",")):
+        k, v = kv.split("=")
+        ctx.set_schedule(k.strip(), int(v))
+    if args.cu_split is not None:
+        ctx.set_cu_split(args.cu_split)
+    ctx.set_dist_cache_keep(args.dist_cache == "keep")
+    last = {}
+
+    def step():
+        fr = G.fit_batch(problems, x0, max_evals=EV, g_tol=-1.0, device=local) if problems else None
+        last["fit"] = fr
+        return fr
+
+    for _ in range(args.warmup):
+        step()
+    cpu_res = join_cpu_baseline(cpu_child, timeout=1800) if cpu_child is not None else None
+    ctx.set_profiling(True)
+    ctx.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    ts0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    busy = (time.perf_counter() - ts0) * 1e3 / args.steps
+    if world > 1:
+        dist.barrier()
+    el = (time.perf_counter() - ts0) * 1e3 / args.steps
+    if world > 1:
+        e = torch.tensor([el], dtype=torch.float64, device=dev)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        el = float(e[0])
+    fams = {k: ctx.kernel_stats(k) for k in ("gram", "whiten", "dist2", "fit_call", "fit_round")}
+    works = {k: ctx.kernel_work(k) for k in ("gram", "whiten", "dist2")}
+    evals_rank = len(problems) * EV
+    evals_all = evals_rank
+    if world > 1:
+        e = torch.tensor([float(evals_rank)], dtype=torch.float64, device=dev)
+        dist.all_reduce(e)
+        evals_all = int(e[0])
+    elif args.shard:
+        evals_all = evals_rank   # this rank's share of the W-way job, measured alone
+    out = None
+    if rank == 0:
+        gn, gms = fams["gram"]
+        wn, wms = fams["whiten"]
+        dn, dms = fams["dist2"]
+        gach = works["gram"] / (gms * 1e-3) / 1e12 if gn else None
+        value = float(N) * evals_all / (el / 1e3)
+        per_eval_ms = el / max(evals_rank, 1)
+        # the whole stress job (every GPAR output, 50 evaluations each) projected from this rank's
+        # per-evaluation time and the LPT loads of the sized cost model
+        loads = [sum(cost(p) for p in sh if p >= 2) for sh in shards]
+        mine_load = loads[r_]
+        proj_s = (el / 1e3) * (50.0 / EV) * max(loads) / mine_load if mine_load else None
+        out = {
+            "metric": "GPAR-DTC objective evaluation throughput (pts\u00b7evaluations/s), "
+                      f"N={D.fmt_count(N)} M={M} P={P}",
+            "value": value, "unit": "pts\u00b7evaluations/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": el, "higher_is_better": True,
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (toy_data.jl big-set functions extended to P outputs, generated on "
+                    "the device with torch's seeded generator)",
+            "config": {"workload": "GPAR-DTC per-evaluation (stress)", "N": N, "M": M, "P": P,
+                       "evals_per_output": EV, "out_kernel": cfg["out_kernel"],
+                       "time_kernel": "matern52", "outputs": mine,
+                       "parallelism": f"outputs sharded over {w_} GPU(s) (LPT, D-dependent cost)",
+                       **({"shard": f"{r_}/{w_}"} if args.shard else {}),
+                       "cu_split": ctx.cu_split(), "dist_cache": args.dist_cache,
+                       **({"schedule": args.schedule} if args.schedule else {})},
+            "ms_per_evaluation": per_eval_ms,
+            "evaluations_per_step": evals_rank,
+            "roofline": {"bound": "mfma", "achieved": gach, "peak": FP64_MFMA_PEAK_TFLOPS,
+                         "unit": "TFLOP/s", "frac": gach / FP64_MFMA_PEAK_TFLOPS if gach else None,
+                         "traffic": None, "launches": gn, "avg_ms": gms / gn if gn else None,
+                         "flops_per_launch": float(N) * M * (M + 1),
+                         "kernel": "Gram beta^T beta + beta^T alpha, fp64 MFMA (gram3_off + gram3_dg "
+                                   "+ gram3_corr + gram3_reduce), HIP events per launch"},
+            "job_vs_gram_floor": {"floor_ms_per_step": works["gram"] / args.steps /
+                                  (FP64_MFMA_PEAK_TFLOPS * 1e12) * 1e3,
+                                  "frac": works["gram"] / args.steps /
+                                  (FP64_MFMA_PEAK_TFLOPS * 1e12) * 1e3 / el},
+            "projected_job": {"seconds": proj_s, "gpus": w_, "evals_per_output": 50,
+                              "note": "every GPAR output's 50-evaluation fit on W GPUs: this rank's "
+                                      "measured step x 50 / evals x (largest rank load / this "
+                                      "rank's load) under shard.output_cost_sized"},
+            "ranks": [{"rank": r, "outputs": len([p for p in sh if p >= 2]),
+                       "load_rel": loads[r] / max(loads)} for r, sh in enumerate(shards)],
+        }
+        if wn:
+            wa = works["whiten"] / (wms * 1e-3) / 1e9
+            out["roofline_whiten"] = {"bound": "hbm", "achieved": wa, "peak": HBM_PEAK_GBS,
+                                      "unit": "GB/s", "frac": wa / HBM_PEAK_GBS, "launches": wn,
+                                      "avg_ms": wms / wn, "bytes_per_launch": works["whiten"] / wn,
+                                      "kernel": "Kfu + Kalman whitening (whiten_kfu_d2x2 from cached "
+                                                "or freshly computed distances)"}
+        if dn:
+            da = works["dist2"] / (dms * 1e-3) / 1e12
+            out["roofline_dist"] = {"bound": "mfma", "achieved": da, "peak": FP64_MFMA_PEAK_TFLOPS,
+                                    "unit": "TFLOP/s", "frac": da / FP64_MFMA_PEAK_TFLOPS,
+                                    "launches": dn, "avg_ms": dms / dn,
+                                    "flops_per_launch": works["dist2"] / dn,
+                                    "kernel": "dist2_mfma_kernel: |v - z|^2 cross products 2 N Mp D "
+                                              "on MFMA (cache fill or per-evaluation pass)"}
+        fc_n, fc_ms = fams["fit_call"]
+        if fc_n and gn:
+            out["fit_calls"] = {"ms_per_step": fc_ms / args.steps,
+                                "not_gram_ms_per_step": (fc_ms - gms) / args.steps}
+        if cpu_res is not None:
+            out["cpu_baseline"] = cpu_res
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+def stress_cpu_baseline(N, M, P, out_kernel, n_sample=1_000_000, check_path=None):
+    """The stress config's CPU baseline: the C/OpenMP port (oracle/cpu_ref, pinned to the numpy
+    oracle by tests/test_cpu_ref.py) times ONE DTC objective evaluation of the widest output
+    (D = P - 1 = 255, M pseudo-points) at n_sample = 1e6 points, scaled linearly in N (every piece
+    of the evaluation is O(N): Kfu, the M + 1 filter sweeps, the N M^2 Gram; the M^3 tail is
+    negligible), so value = N / (that time x N / n_sample) pts*evaluations/s."""
+    sys.path.insert(0, ROOT)
+    from oracle import gpar_oracle as O
+    from oracle import cpu_ref as CR
+    try:
+        from threadpoolctl import threadpool_info
+        blas = max([x.get("num_threads", 1) for x in threadpool_info() if x.get("user_api") == "blas"] + [1])
+    except Exception:
+        blas = 1
+    cores = max(CR.threads(), blas)
+    d = P - 1
+    t, Y = O.synthetic_gpar(n_sample, d + 1, seed=1, noise=0.8)
+    V = np.ascontiguousarray(Y[:, :d].T)
+    y = np.ascontiguousarray(Y[:, d])
+    Z = O.pick_pseudo_inputs(V, M, 3)
+    theta = CHECK_THETA
+    CR.compute_gpar_dtc_objective(V[:, :4096], Z, t[:4096], y[:4096], theta, out_kernel, "matern52")
+    t0 = time.perf_counter()
+    val, _ = CR.compute_gpar_dtc_objective(V, Z, t, y, theta, out_kernel, "matern52")
+    t_eval = time.perf_counter() - t0
+    t_scaled = t_eval * N / n_sample
+    return {"value": N / t_scaled, "unit": "pts\u00b7evaluations/s", "cores": int(cores),
+            "kind": "port", "host_cpu": _cpu_model(), "eval_seconds_sample": t_eval,
+            "eval_seconds_at_N": t_scaled, "dtc_sample": float(val),
+            "ran": "in a child process beside the GPU warm-up (joined before the timed region)",
+            "sample": f"C/OpenMP + OpenBLAS restatement (oracle/cpu_ref), {int(cores)} threads: one DTC "
+                      f"objective evaluation at N = {n_sample}, M = {M}, D = {d} (the widest output) = "
+                      f"{t_eval:.2f}s, scaled linearly to N = {N}: {t_scaled:.1f}s per evaluation"}
+
+
 LAUNCH_KILL_GRACE_S = 10.0   # SIGTERM -> SIGKILL grace for the surviving ranks of a failed job
 
 
@@ -1099,6 +1322,10 @@ def cpu_baseline_child(args):
     if cfg.get("temporal", False):
         print(json.dumps(ssm_cpu_baseline(cfg["N"], cfg["P"], cfg["evals"], cfg["out_kernel"],
                                           check_path=args.cpu_check_file)), flush=True)
+        return
+    if cfg.get("per_eval"):
+        print(json.dumps(stress_cpu_baseline(cfg["N"], cfg["M"], cfg["P"], cfg["out_kernel"],
+                                             check_path=args.cpu_check_file)), flush=True)
         return
     res = cpu_baseline(cfg["N"], cfg["N"], cfg["M"], cfg["P"], cfg["evals"], cfg["out_kernel"],
                        qu_kuu_noise=not args.qu_noise_free, check_path=args.cpu_check_file)

@@ -90,6 +90,10 @@ struct gpar_ctx {
   // "gram_group": outputs per grouped Gram launch set in an unsplit batched fit of small problems
   // (run_gram_stage): 0 = off, >= 2 that many, 1 = off, -1 = auto (kGramGroupAuto below)
   int gram_group = -1;
+  // "fit_chunks": outputs per consecutive sub-batch of a gpar_fit whose distances the cache
+  // cannot all hold at once (fit_impl): -1 = auto (unpipelined fits of outputs with D >= 17, the
+  // stress config), 0 = off (one batch), k >= 1 = sub-batches of k outputs
+  int fit_chunks = -1;
   // "dg_rows_w": percent more rows per DG split on the whitening CUs (fewer on the Gram CUs);
   // kDgRowsAuto: +40 in the round-by-round fit, where the whitening side (3.19 ms whitening since
   // the DPP step rows, r05r) has time to spare and the Gram CUs' side sets the span (north, same
@@ -337,9 +341,10 @@ GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                           bool compact = false);
 // gi: the output's gains (compact records: the whitening goes through whiten_kfu_d2x2, the
 // distances of an uncached output through a separate pass)
+// d2_in_beta: the caller already wrote the distances into beta (a separately timed pass)
 void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const GainsOut& gi, const double* v,
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
-                           int64_t ldb, double* send, double* hsum);
+                           int64_t ldb, double* send, double* hsum, bool d2_in_beta = false);
 
 // --------------------------------------------------------------------------- Gram stage
 struct GramOut {

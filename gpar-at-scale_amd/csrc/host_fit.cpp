@@ -115,8 +115,11 @@ std::vector<DevProblem> attach_dist_cache(gpar_ctx* c, const std::vector<DevProb
     fresh -= need;
     if ((int)c->cache_valid.size() <= slot) c->cache_valid.resize(slot + 1, 0);
     c->cache_valid[slot] = 1;
-    launch_dist2(c->stream, p.ok, p.v, p.ldv, p.n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, d2, p.mp,
-                 /*take_sqrt=*/p.ok != GPAR_EQ);
+    {
+      Timed td_(c, "dist2", 2.0 * (double)p.n * (double)p.mp * (double)p.d);
+      launch_dist2(c->stream, p.ok, p.v, p.ldv, p.n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, d2,
+                   p.mp, /*take_sqrt=*/p.ok != GPAR_EQ);
+    }
     check_launch("dist2 (cache)");
     Q[i].d2 = d2;
     Q[i].d2_is_r = p.ok != GPAR_EQ;
@@ -350,9 +353,72 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
   sp.join(c->main);
 }
 
+// Cache-resident sub-batches.  The batched fit evaluates every output once per Nelder-Mead round,
+// so an output's cached distances are only reused if the cache holds the whole batch; where it
+// cannot (BASELINE config 5: N = 1e7, M = 1024, 82 GB of distances per output, 32 outputs per
+// rank), the uncached outputs recompute their distances every evaluation (a pass of 2 N Mp D
+// flops: at D = 255 half the Gram's).  Each output's fit is independent of the batch it runs in,
+// so the fit runs instead in consecutive sub-batches whose distances all fit, each computing them
+// once.  Returns the sub-batch size, or 0 for one batch: auto (fit_chunks -1) where the fit is not
+// pipelined (beta above kPipeMaxBetaBytes: the per-round batching then buys nothing but the
+// batched gains and dense-tail launches), every output is cacheable (D >= kDistCacheMinD) and the
+// free memory holds fewer outputs' distances than the batch has.
+static int cache_chunk_size(gpar_ctx* c, const std::vector<DevProblem>& P, int64_t later_bytes) {
+  const int np = (int)P.size();
+  if (np < 2 || c->dist_cache_bytes == 0 || c->fit_chunks == 0) return 0;
+  if (c->fit_chunks > 0) return c->fit_chunks < np ? c->fit_chunks : 0;
+  if (fit_pipelined(c, P)) return 0;
+  for (const auto& p : P)
+    if (p.d < kDistCacheMinD) return 0;
+  size_t fr = 0, tot = 0;
+  HIPCHECK(hipMemGetInfo(&fr, &tot));
+  int64_t held = 0;   // the context's buffers are reused by the sub-batches
+  for (auto& kv : c->bufs) held += (int64_t)kv.second.bytes;
+  const int64_t reserve = std::max<int64_t>((int64_t)1 << 30, (int64_t)(tot / 100));
+  const int64_t avail = (int64_t)fr + held - reserve;
+  if (c->dist_cache_bytes > 0) {   // an explicit budget: outputs it holds
+    int k = 0;
+    int64_t b = 0;
+    while (k < np) {
+      const int64_t bytes = P[k].n * P[k].mp * (int64_t)sizeof(double);
+      if (b + bytes > c->dist_cache_bytes) break;
+      b += bytes;
+      ++k;
+    }
+    return (k >= 1 && k < np) ? k : 0;
+  }
+  for (int k = np; k >= 1; --k) {
+    const std::vector<DevProblem> sub(P.begin(), P.begin() + k);
+    int64_t need = fit_ws_estimate(c, sub) + later_bytes;
+    for (const auto& p : sub) need += p.n * p.mp * (int64_t)sizeof(double);
+    if (need <= avail) return k < np ? k : 0;
+  }
+  return 0;
+}
+
 void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* log_theta0,
                      const gpar_fit_options& o, double* theta_out, double* nlml_out,
                      int32_t* evals_out, FitKeep* keep, int64_t later_bytes) {
+  if (!keep) {   // (the kept Grams are named by batch index: one batch when they are wanted)
+    const int k = cache_chunk_size(ctx, P0, later_bytes);
+    if (k >= 1) {
+      const int saved = ctx->fit_chunks;
+      ctx->fit_chunks = 0;   // each sub-batch is one batch
+      struct Restore {
+        gpar_ctx* c;
+        int v;
+        ~Restore() { c->fit_chunks = v; }
+      } restore_{ctx, saved};
+      for (size_t i0 = 0; i0 < P0.size(); i0 += (size_t)k) {
+        const size_t i1 = std::min(P0.size(), i0 + (size_t)k);
+        const std::vector<DevProblem> sub(P0.begin() + i0, P0.begin() + i1);
+        fit_impl(ctx, sub, log_theta0 + 5 * i0, o, theta_out + 5 * i0,
+                 nlml_out ? nlml_out + i0 : nullptr, evals_out ? evals_out + i0 : nullptr, nullptr,
+                 later_bytes);
+      }
+      return;
+    }
+  }
   // the cache lives for this fit call only, unless the caller keeps it (gpar_ctx_set_dist_cache_keep)
   struct CacheRelease {
     gpar_ctx* c;

@@ -12,7 +12,7 @@ namespace gpar {
 // the whitening then reads and overwrites in place (k_dist.hip).
 void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const GainsOut& gi, const double* v,
                            int64_t ldv, int64_t n, int64_t nch, const Theta& th, double* beta,
-                           int64_t ldb, double* send, double* hsum) {
+                           int64_t ldb, double* send, double* hsum, bool d2_in_beta) {
   const double s_o = th.sv_o * th.sv_o;
   const double* rec = gi.rec;
   const double* g = gi.g;
@@ -23,7 +23,8 @@ void whiten_kfu_any(gpar_ctx* c, const DevProblem& p, const GainsOut& gi, const 
     launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, d2, p.mp, p.m, p.mp, n, kChunk, nch,
                          1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum, p.d2_is_r, tc, th.l_t);
   } else if (p.d > kFusedMaxD || gi.compact) {
-    launch_dist2(c->stream, p.ok, v, ldv, n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, beta, ldb);
+    if (!d2_in_beta)   // else the caller's (timed) distance pass already wrote them
+      launch_dist2(c->stream, p.ok, v, ldv, n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, beta, ldb);
     launch_whiten_kfu_d2(c->stream, p.tk, p.ok, rec, beta, ldb, p.m, p.mp, n, kChunk, nch,
                          1.0 / th.l_o, s_o, beta, ldb, send, p.mc, g, hsum, false, tc, th.l_t);
   } else if (p.ok == GPAR_MATERN12) {
@@ -96,11 +97,21 @@ static int gram_group_size(gpar_ctx* c, const std::vector<DevProblem>& P, int64_
 // Kfu assembly + chunk-local whitening of j's output into b.beta, on c->stream.
 void stage_whiten(gpar_ctx* c, const StageJob& j, const StageBufs& b) {
   const DevProblem& p = *j.p;
-  // algorithmic HBM bytes: the inputs (V, or the cached distances), the gains records and
-  // fix-up rows (16 + 4 doubles per step), beta written (m columns)
-  const double in_cols = cached_d2(c, p) ? (double)p.m : (double)p.d;
+  // uncached inputs wider than the fused kernels take (or compact records): the distances go
+  // into beta first, a pass of its own ("dist2": 2 N Mp D flops of MFMA cross products)
+  const bool cached = cached_d2(c, p) != nullptr;
+  const bool pass = !cached && (p.d > kFusedMaxD || j.gi.compact);
+  if (pass) {
+    Timed td_(c, "dist2", 2.0 * (double)p.n * (double)p.mp * (double)p.d);
+    launch_dist2(c->stream, p.ok, p.v, p.ldv, p.n, p.z, p.ldz, p.m, p.mp, (int)p.d, p.zc, b.beta,
+                 p.mp);
+    check_launch("dist2");
+  }
+  // algorithmic HBM bytes: the inputs (V, or the distances), the gains records and fix-up rows
+  // (16 + 4 doubles per step), beta written (m columns)
+  const double in_cols = (cached || pass) ? (double)p.m : (double)p.d;
   Timed tm_(c, "whiten", 8.0 * (double)p.n * (in_cols + (double)p.m + 20.0));
-  whiten_kfu_any(c, p, j.gi, p.v, p.ldv, p.n, p.nch, *j.th, b.beta, p.mp, b.send, b.hsum);
+  whiten_kfu_any(c, p, j.gi, p.v, p.ldv, p.n, p.nch, *j.th, b.beta, p.mp, b.send, b.hsum, pass);
   check_launch("whiten_kfu");
 }
 

@@ -87,3 +87,35 @@ def pseudo_inputs(V_rows, M, seed):
     rng = np.random.default_rng(seed)
     idx = np.sort(rng.choice(V_rows.shape[0], size=M, replace=False))
     return np.ascontiguousarray(V_rows[idx])
+
+
+def pseudo_index(n, M, seed):
+    """The rows pseudo_inputs(V_rows, M, seed) takes from an n-row V (sorted)."""
+    rng = np.random.default_rng(seed)
+    return np.sort(rng.choice(n, size=M, replace=False))
+
+
+def gpar_dataset_device(n, P, seed=0, observation_noise=0.8, device="cuda"):
+    """gpar_dataset's training half generated on the GPU with torch (the stress config: N = 1e7,
+    P = 256 is 20 GB of Y, minutes of numpy): t (n,) and Y (n x P, observed = f_big chain + noise
+    with std observation_noise^2), both fp64 on `device`.  The same functions as gpar_dataset; the
+    noise comes from torch's device generator (seeded), so the values differ from the numpy
+    generator's -- synthetic inputs of the same shape and distribution."""
+    import torch
+    g = torch.Generator(device=device)
+    g.manual_seed(int(seed))
+    x = START + STEP_SIZE * torch.arange(n, dtype=torch.float64, device=device)
+    Y = torch.empty((n, P), dtype=torch.float64, device=device)
+    std = observation_noise ** 2
+    pi = float(np.pi)
+    for p in range(1, P + 1):
+        if p == 1:
+            f = 3.0 - torch.sin(pi / 10.0 * (x + 1.0)) - torch.pow(x, 0.3)
+        elif p == 2:
+            f = torch.cos(Y[:, 0]) ** 2 + torch.sin(pi / 20.0 * x)
+        elif p == 3:
+            f = Y[:, 1] * Y[:, 0] ** 2 + 0.1 * x
+        else:
+            f = torch.cos(Y[:, p - 2]) ** 2 + torch.sin(pi * x / (20.0 + p)) + 0.1 * Y[:, p - 3]
+        Y[:, p - 1] = f + std * torch.randn(n, dtype=torch.float64, device=device, generator=g)
+    return x, Y

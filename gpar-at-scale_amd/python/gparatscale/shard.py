@@ -28,16 +28,40 @@ def output_cost(p: int) -> float:
     return SDE_MS if p == 1 else OUTPUT_EVAL_MS
 
 
-def assign_outputs(P: int, world: int) -> list[list[int]]:
-    """Longest-processing-time-first assignment of outputs 1..P to `world` ranks.
+# fp64 MFMA peak (flop/s) and HBM bandwidth (B/s) of one MI355X: the sized cost model below
+# prices memory-bound bytes in flop-equivalents at their ratio
+_PEAK_FLOPS, _PEAK_BYTES = 78.6e12, 8.0e12
+
+
+def output_cost_sized(p: int, n: int, m: int, evals: int) -> float:
+    """Cost of output p's fit at n training points and m pseudo-points in flop-equivalents, where
+    the input width D = p - 1 matters (BASELINE config 5: N = 1e7, M = 1024, D up to 255).  Per
+    evaluation the Gram's N M (M + 1) flops and the cached whitening's 8 N (2 Mp + 20) bytes; once
+    per fit the distance pass, 2 N Mp D flops on MFMA (the fit computes an output's distances
+    once and every evaluation reads them, include/gpar_hip.h gpar_ctx_set_dist_cache), spread
+    over its `evals` evaluations.  The temporal-only output 1 is O(N)."""
+    mp = (m + 127) // 128 * 128
+    if p == 1:
+        return 400.0 * n
+    d = p - 1
+    gram = float(n) * m * (m + 1)
+    whiten = 8.0 * n * (2 * mp + 20) * _PEAK_FLOPS / _PEAK_BYTES
+    dist = 2.0 * n * mp * d / max(int(evals), 1)
+    return gram + whiten + dist
+
+
+def assign_outputs(P: int, world: int, cost=None) -> list[list[int]]:
+    """Longest-processing-time-first assignment of outputs 1..P to `world` ranks.  cost(p): an
+    output's relative cost (default output_cost, the north config's D-independent model).
 
     Deterministic (ties broken by rank), every output owned by exactly one rank."""
+    cost = cost or output_cost
     heap = [(0.0, r) for r in range(world)]
     owned: list[list[int]] = [[] for _ in range(world)]
-    for p in sorted(range(1, P + 1), key=lambda q: (-output_cost(q), q)):
+    for p in sorted(range(1, P + 1), key=lambda q: (-cost(q), q)):
         load, r = heapq.heappop(heap)
         owned[r].append(p)
-        heapq.heappush(heap, (load + output_cost(p), r))
+        heapq.heappush(heap, (load + cost(p), r))
     return [sorted(o) for o in owned]
 
 

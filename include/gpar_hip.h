@@ -113,7 +113,8 @@ int32_t gpar_ctx_reset_stats(gpar_ctx* ctx);
 /* Algorithmic work of the timed launches of a family since the last reset (for rooflines):
  * "gram": flops, N M (M + 1) per launch; "whiten": HBM bytes, 8 N (D + M + 20) per launch (V read,
  * gains records + fix-up rows, beta written), with M in place of D when the distances come from the
- * fit's cache. */
+ * fit's cache or a distance pass; "dist2": flops, 2 N Mp D per distance pass (the fit's cache fill,
+ * or the per-evaluation pass of an uncached output wider than 64). */
 int32_t gpar_ctx_kernel_work(gpar_ctx* ctx, const char* name, double* work);
 /* Process-wide diagnostic counters (tests; no device work): "gains_fast" / "gains_general" = the
  * gains' phase-3 launches that took the LDS-DMA fast kernel / the general kernels since the library
@@ -179,6 +180,16 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *                   them all (grid y = output), each with 1/g of the time splits; -1 (default) =
  *                   auto: groups of 16 when one output's N Mp^2 <= 5e10 (the dtc / eeg configs),
  *                   0 = per-output Grams; a plan like dg_rows_w (G's summation grouping: last bits)
+ *   "fit_chunks"    outputs per consecutive sub-batch of a gpar_fit whose outputs' distances the
+ *                   cache cannot hold all at once: each sub-batch computes its distances once
+ *                   and every evaluation reads them, instead of the outputs left uncached
+ *                   recomputing theirs every evaluation.  -1 (default) = auto: fits too large
+ *                   to pipeline (beta > 8 GB: the N = 1e7, M = 1024 stress config) whose outputs
+ *                   all have D >= 17, in sub-batches of as many outputs as the free memory (or
+ *                   an explicit gpar_ctx_set_dist_cache budget) holds; 0 = one batch; k >= 1 =
+ *                   sub-batches of k.  Not for gpar_fit_predict / gpar_fit_posterior.  Each
+ *                   output's fit is independent of its batch, so a sub-batched fit equals the
+ *                   one-batch fit with every output cached bit for bit
  * The environment variable GPAR_<KNOB> (upper case) sets a knob at context creation.
  * GPAR_ERR_ARG for an unknown knob or value.  Every non-default value is a supported schedule
  * mode; the A/B-only knobs of round 4 (split_head, dg_share, tail_cus, predict_d2, dense_early 2)

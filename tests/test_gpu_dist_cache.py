@@ -217,3 +217,35 @@ def test_cache_auto_budget_under_memory_pressure():
     assert ev1 == ev0
     np.testing.assert_allclose(got.theta, ref.theta, rtol=1e-9)
     np.testing.assert_allclose(got.nlml, ref.nlml, rtol=1e-12)
+
+
+def test_fit_chunks_equal_one_fully_cached_batch():
+    """fit_chunks (cache-resident sub-batches, the stress config's schedule): the outputs fitted in
+    consecutive sub-batches of k, each computing its distances once, equal one batch with every
+    output cached, bit for bit (per-output Grams: gram_group 0, whose grouping would otherwise
+    follow the batch size); the auto rule leaves this pipelined fit as one batch."""
+    t, Y = O.synthetic_gpar(20_000, 25, seed=52, noise=0.3)
+    probs, keep = [], []
+    for D in (17, 19, 21, 24, 18):
+        V = np.ascontiguousarray(Y[:, :D].T)
+        Z = O.pick_pseudo_inputs(V, 64, D)
+        pr, k = G.make_problem(V, Z, t, Y[:, D], "matern52", "matern52")
+        probs.append(pr)
+        keep.append(k)
+    ctx = G.context(0)
+    x0 = np.tile(X0, (len(probs), 1))
+    res = {}
+    try:
+        ctx.set_schedule("gram_group", 0)
+        for k in (0, 2, 1, -1):
+            ctx.set_schedule("fit_chunks", k)
+            res[k] = G.fit_batch(probs, x0, max_evals=14, g_tol=-1.0)
+            # outputs the last fit call (the last sub-batch) cached: 5 = 2 + 2 + 1 = 1 + ... + 1
+            assert ctx.dist_cache_stats()[0] == {0: 5, -1: 5, 2: 1, 1: 1}[k]
+    finally:
+        ctx.set_schedule("fit_chunks", -1)
+        ctx.set_schedule("gram_group", -1)
+    for k in (2, 1, -1):
+        np.testing.assert_array_equal(res[k].theta, res[0].theta)
+        np.testing.assert_array_equal(res[k].nlml, res[0].nlml)
+        np.testing.assert_array_equal(res[k].evals, res[0].evals)

@@ -221,3 +221,21 @@ def test_chained_sweep_blocks_equal_serial(tmp_path, world):
         chain = np.column_stack([chain, m])
     for r in range(world):
         np.testing.assert_array_equal(np.load(out + f".{r}.npy"), chain)
+
+
+def test_sized_cost_model_balances_the_stress_config():
+    """BASELINE config 5 (N = 1e7, M = 1024, P = 256): with the D-dependent cost (the distance
+    pass grows with D = p - 1) LPT still partitions every output once and the largest rank load
+    stays within 1 % of the mean; the cost grows with D and the once-per-fit distance pass
+    shrinks with more evaluations."""
+    from gparatscale import shard as S
+    N, M, P = 10_000_000, 1024, 256
+    cost = lambda p: S.output_cost_sized(p, N, M, 6)   # noqa: E731
+    sh = S.assign_outputs(P, 8, cost=cost)
+    assert sorted(p for s in sh for p in s) == list(range(1, P + 1))
+    loads = [sum(cost(p) for p in s) for s in sh]
+    assert max(loads) / (sum(loads) / 8) < 1.01
+    assert cost(256) > cost(100) > cost(2) > cost(1)
+    assert S.output_cost_sized(256, N, M, 50) < cost(256)
+    # without a cost model the north assignment is unchanged
+    assert S.assign_outputs(64, 8) == S.assign_outputs(64, 8, cost=S.output_cost)
