@@ -948,13 +948,11 @@ def stress_main(args):
     mine = [p for p in shards[r_] if p >= 2]
     # inputs (untimed): generated on the device (20 GB of Y), broadcast from rank 0 over RCCL
     t0 = time.perf_counter()
-    t_d = torch.empty(N, dtype=torch.float64, device=dev)
-    Y_d = torch.empty((N, P), dtype=torch.float64, device=dev)
     if rank == 0:
-        x, Y = D.gpar_dataset_device(N, P, seed=0, observation_noise=0.8, device=dev)
-        t_d.copy_(x)
-        Y_d.copy_(Y)
-        del x, Y
+        t_d, Y_d = D.gpar_dataset_device(N, P, seed=0, observation_noise=0.8, device=dev)
+    else:
+        t_d = torch.empty(N, dtype=torch.float64, device=dev)
+        Y_d = torch.empty((N, P), dtype=torch.float64, device=dev)
     S.broadcast_inputs((t_d, Y_d))
     problems, keep = [], []
     for p in mine:
@@ -966,6 +964,7 @@ def stress_main(args):
         keep.append((k, Z))
     x0 = np.tile(np.array([0.0, 0.0, 0.0, 0.0, -2.0]), (len(problems), 1))
     torch.cuda.synchronize()
+    torch.cuda.empty_cache()   # the generator's temporaries back to the device for the library
     log(f"[rank {rank}] stress inputs ready in {time.perf_counter() - t0:.1f}s: N={N} M={M} "
         f"P={P} shard {r_}/{w_}: {len(mine)} outputs (D {min(mine) - 1}..{max(mine) - 1})")
     ctx = G.context(local)
