@@ -357,51 +357,74 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
 // so an output's cached distances are only reused if the cache holds the whole batch; where it
 // cannot (BASELINE config 5: N = 1e7, M = 1024, 82 GB of distances per output, 32 outputs per
 // rank), the uncached outputs recompute their distances every evaluation (a pass of 2 N Mp D
-// flops: at D = 255 half the Gram's).  Each output's fit is independent of the batch it runs in,
-// so the fit runs instead in consecutive sub-batches whose distances all fit, each computing them
-// once.  Returns the sub-batch size, or 0 for one batch: auto (fit_chunks -1) where the fit is not
-// pipelined (beta above kPipeMaxBetaBytes: the per-round batching then buys nothing but the
-// batched gains and dense-tail launches), every output is cacheable (D >= kDistCacheMinD) and the
-// free memory holds fewer outputs' distances than the batch has.
-static int cache_chunk_size(gpar_ctx* c, const std::vector<DevProblem>& P, int64_t later_bytes) {
+// flops: at D = 255 more than half the Gram's; 27 % of the r06a stress step).  Each output's fit
+// is independent of the batch it runs in, so the fit runs instead in consecutive sub-batches whose
+// distances all fit, each computing them once.  Returns the sub-batches (output indices), or none
+// for one batch.  Auto (fit_chunks -1): where the fit is not pipelined (beta above
+// kPipeMaxBetaBytes: the per-round batching then buys only the batched gains and dense-tail
+// launches) and the free memory holds fewer of the cacheable outputs' (D >= kDistCacheMinD)
+// distances than the batch has: the narrower outputs (fused whitening, no cache) as one sub-batch,
+// then the cacheable ones k at a time.  fit_chunks = k >= 1: k consecutive outputs at a time.
+static std::vector<std::vector<int>> cache_chunks(gpar_ctx* c, const std::vector<DevProblem>& P,
+                                                  int64_t later_bytes) {
   const int np = (int)P.size();
-  if (np < 2 || c->dist_cache_bytes == 0 || c->fit_chunks == 0) return 0;
-  if (c->fit_chunks > 0) return c->fit_chunks < np ? c->fit_chunks : 0;
-  if (fit_pipelined(c, P)) return 0;
-  for (const auto& p : P)
-    if (p.d < kDistCacheMinD) return 0;
-  size_t fr = 0, tot = 0;
-  HIPCHECK(hipMemGetInfo(&fr, &tot));
-  int64_t held = 0;   // the context's buffers are reused by the sub-batches
-  for (auto& kv : c->bufs) held += (int64_t)kv.second.bytes;
-  const int64_t reserve = std::max<int64_t>((int64_t)1 << 30, (int64_t)(tot / 100));
-  const int64_t avail = (int64_t)fr + held - reserve;
-  if (c->dist_cache_bytes > 0) {   // an explicit budget: outputs it holds
-    int k = 0;
+  std::vector<std::vector<int>> out;
+  if (np < 2 || c->dist_cache_bytes == 0 || c->fit_chunks == 0) return out;
+  if (c->fit_chunks > 0) {
+    if (c->fit_chunks >= np) return out;
+    for (int i0 = 0; i0 < np; i0 += c->fit_chunks) {
+      out.emplace_back();
+      for (int i = i0; i < std::min(np, i0 + c->fit_chunks); ++i) out.back().push_back(i);
+    }
+    return out;
+  }
+  if (fit_pipelined(c, P)) return out;
+  std::vector<int> narrow, wide;
+  for (int i = 0; i < np; ++i) (P[i].d >= kDistCacheMinD ? wide : narrow).push_back(i);
+  if (wide.size() < 2) return out;
+  int k = 0;
+  if (c->dist_cache_bytes > 0) {   // an explicit budget: the cacheable outputs it holds
     int64_t b = 0;
-    while (k < np) {
-      const int64_t bytes = P[k].n * P[k].mp * (int64_t)sizeof(double);
+    for (int i : wide) {
+      const int64_t bytes = P[i].n * P[i].mp * (int64_t)sizeof(double);
       if (b + bytes > c->dist_cache_bytes) break;
       b += bytes;
       ++k;
     }
-    return (k >= 1 && k < np) ? k : 0;
+  } else {
+    size_t fr = 0, tot = 0;
+    HIPCHECK(hipMemGetInfo(&fr, &tot));
+    int64_t held = 0;   // the context's buffers are reused by the sub-batches
+    for (auto& kv : c->bufs) held += (int64_t)kv.second.bytes;
+    const int64_t reserve = std::max<int64_t>((int64_t)1 << 30, (int64_t)(tot / 100));
+    const int64_t avail = (int64_t)fr + held - reserve;
+    for (int kk = (int)wide.size(); kk >= 1; --kk) {
+      std::vector<DevProblem> sub;
+      int64_t need = later_bytes;
+      for (int a = 0; a < kk; ++a) {
+        sub.push_back(P[wide[a]]);
+        need += P[wide[a]].n * P[wide[a]].mp * (int64_t)sizeof(double);
+      }
+      need += fit_ws_estimate(c, sub);
+      if (need <= avail) {
+        k = kk;
+        break;
+      }
+    }
   }
-  for (int k = np; k >= 1; --k) {
-    const std::vector<DevProblem> sub(P.begin(), P.begin() + k);
-    int64_t need = fit_ws_estimate(c, sub) + later_bytes;
-    for (const auto& p : sub) need += p.n * p.mp * (int64_t)sizeof(double);
-    if (need <= avail) return k < np ? k : 0;
-  }
-  return 0;
+  if (k < 1 || k >= (int)wide.size()) return out;
+  if (!narrow.empty()) out.push_back(narrow);
+  for (size_t a = 0; a < wide.size(); a += (size_t)k)
+    out.emplace_back(wide.begin() + a, wide.begin() + std::min(wide.size(), a + (size_t)k));
+  return out;
 }
 
 void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* log_theta0,
                      const gpar_fit_options& o, double* theta_out, double* nlml_out,
                      int32_t* evals_out, FitKeep* keep, int64_t later_bytes) {
   if (!keep) {   // (the kept Grams are named by batch index: one batch when they are wanted)
-    const int k = cache_chunk_size(ctx, P0, later_bytes);
-    if (k >= 1) {
+    const std::vector<std::vector<int>> chunks = cache_chunks(ctx, P0, later_bytes);
+    if (!chunks.empty()) {
       const int saved = ctx->fit_chunks;
       ctx->fit_chunks = 0;   // each sub-batch is one batch
       struct Restore {
@@ -409,27 +432,25 @@ void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* lo
         int v;
         ~Restore() { c->fit_chunks = v; }
       } restore_{ctx, saved};
-      for (size_t i0 = 0; i0 < P0.size(); i0 += (size_t)k) {
-        const size_t i1 = std::min(P0.size(), i0 + (size_t)k);
-        const std::vector<DevProblem> sub(P0.begin() + i0, P0.begin() + i1);
-        fit_impl(ctx, sub, log_theta0 + 5 * i0, o, theta_out + 5 * i0,
-                 nlml_out ? nlml_out + i0 : nullptr, evals_out ? evals_out + i0 : nullptr, nullptr,
-                 later_bytes);
+      for (const auto& idx : chunks) {
+        const size_t k = idx.size();
+        std::vector<DevProblem> sub;
+        std::vector<double> x0(5 * k), th(5 * k), nl(k);
+        std::vector<int32_t> ev(k);
+        for (size_t a = 0; a < k; ++a) {
+          sub.push_back(P0[idx[a]]);
+          std::copy(log_theta0 + 5 * idx[a], log_theta0 + 5 * idx[a] + 5, x0.begin() + 5 * a);
+        }
+        fit_impl(ctx, sub, x0.data(), o, th.data(), nl.data(), ev.data(), nullptr, later_bytes);
+        for (size_t a = 0; a < k; ++a) {
+          std::copy(th.begin() + 5 * a, th.begin() + 5 * a + 5, theta_out + 5 * idx[a]);
+          if (nlml_out) nlml_out[idx[a]] = nl[a];
+          if (evals_out) evals_out[idx[a]] = ev[a];
+        }
       }
       return;
     }
   }
-  // the cache lives for this fit call only, unless the caller keeps it (gpar_ctx_set_dist_cache_keep)
-  struct CacheRelease {
-    gpar_ctx* c;
-    ~CacheRelease() {
-      if (c->dist_cache_keep) return;
-      try {
-        release_dist_cache(c);
-      } catch (...) {
-      }
-    }
-  } release_{ctx};
   const std::vector<DevProblem> P =
       attach_dist_cache(ctx, P0, fit_ws_estimate(ctx, P0) + later_bytes);
   const int nprob = (int)P.size();

@@ -76,8 +76,9 @@ void chains_smooth(gpar_ctx* c, int nchains, int64_t n, const double* t, const d
   double* gam = ws<double>(c, "sm_gam", (size_t)nchains * n * 4);
   double* agg = ws<double>(c, "sm_agg", (size_t)nchains * nch * 2 * sdim * sdim);
   double* phat = ws<double>(c, "sm_phat", (size_t)nchains * nch * sdim * sdim);
+  double* cscr = ws<double>(c, "sm_covscan", (size_t)cov_carry_scratch_doubles(sdim, nch, nchains));
   launch_cov_smooth(c->stream, sdim, t, g.rec, g.pf, dcps, n, kChunk, nch, nchains, vloc, gam, agg,
-                    phat, var, ldo);
+                    phat, var, ldo, cscr);
   check_launch("chains_smooth");
 }
 

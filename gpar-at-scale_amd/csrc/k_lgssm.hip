@@ -1721,6 +1721,61 @@ __global__ __launch_bounds__(64) void adjoint_local(double* __restrict__ X, int6
   }
 }
 
+// One column (the temporal chains' smoothing, gpar_lgssm_smooth): one lane per (chunk, chain)
+// instead of a 64-lane workgroup per chunk with one lane active (r05: 125 k workgroups, 3.6 ms for
+// the ssm config's 16 chains x 2e6 steps).  The same arithmetic per step as adjoint_local.
+template <int D>
+__global__ __launch_bounds__(256) void adjoint_local_col(double* __restrict__ X,
+                                                         const double* __restrict__ rec,
+                                                         const double* __restrict__ g,
+                                                         const double* __restrict__ cin, int64_t n,
+                                                         int L, int64_t nch,
+                                                         double* __restrict__ bend,
+                                                         int64_t xstride, int64_t sstride) {
+  constexpr int RS = Rec<D>::size;
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (j >= nch) return;
+  X += (int64_t)b * xstride;
+  rec += (int64_t)b * n * RS;
+  g += (int64_t)b * n * kGStride;
+  cin += (int64_t)b * sstride;
+  bend += (int64_t)b * sstride;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  double cf[D], lam[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    cf[i] = cin[j * kSStride + i];
+    lam[i] = 0.0;
+  }
+#pragma unroll 4
+  for (int64_t k = k1 - 1; k >= k0; --k) {
+    const double* r = rec + k * RS;
+    const double* gk = g + k * kGStride;
+    double w = X[k];
+#pragma unroll
+    for (int i = 0; i < D; ++i) w = fma(gk[i], cf[i], w);
+    double u = w * r[D * D + D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) u = fma(r[D * D + i], lam[i], u);
+    lam[0] -= u;
+    double nl[D];
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) acc = fma(r[i * D + q], lam[i], acc);
+      nl[q] = acc;
+    }
+#pragma unroll
+    for (int i = 0; i < D; ++i) lam[i] = nl[i];
+    X[k] = u;
+  }
+#pragma unroll
+  for (int i = 0; i < D; ++i) bend[j * kSStride + i] = lam[i];
+}
+
 // Wide form for the prediction's many columns: a 256-column workgroup per chunk stages the
 // chunk's gains records and fix-up rows in LDS once (read back as broadcasts; from memory they
 // were scalar loads waited on step by step), and with `wmask` writes u only at the rows the
@@ -1946,33 +2001,107 @@ __global__ __launch_bounds__(256) void cov_local(const double* __restrict__ t,
     }
 }
 
-// Backward carry over chunks (one thread per chain): Phat_{J-1} = 0,
-// Phat_{j-1} = Ps_loc(j) + Gamma_j Phat_j Gamma_j^T.
+// Backward carry over chunks: Phat_{J-1} = 0, Phat_{j-1} = f_j(Phat_j) = S_j + Gamma_j Phat_j
+// Gamma_j^T with S_j = the chunk's local smoothed covariance at its start and Gamma_j its
+// transfer (agg).  The maps compose, (S_a, Gamma_a) o (S_b, Gamma_b) = (S_a + Gamma_a S_b
+// Gamma_a^T, Gamma_a Gamma_b), so the carry is a two-level scan like the means' (carry_group_*):
+//   a) cov_group_local, per (group of GS chunks, chain): the group's composite map   -> gagg
+//   b) cov_group_scan, per chain: the groups right to left from Phat = 0              -> gin
+//   c) cov_group_apply, per (group, chain): Phat at each of the group's chunks        -> phat
+// (Round 5 ran the recursion serially, one thread per chain over all 7813 chunks of the ssm
+// config's merged grid: 3.7 ms of 16 threads on a 256-CU chip.)  The last group reproduces the
+// serial order; elsewhere the association differs (rounding only).
 template <int D>
-__global__ void cov_carry(const double* __restrict__ agg, int64_t nch, int nchains,
-                          double* __restrict__ phat) {
+__device__ __forceinline__ void cov_map_apply(const double* __restrict__ ag, double (&Ph)[D][D]) {
+  double Gm[D][D], T[D][D], U[D][D];
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) Gm[i][q] = ag[D * D + i * D + q];
+  mat_mul(Gm, Ph, T);
+  mat_mul_bt(T, Gm, U);
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) Ph[i][q] = ag[i * D + q] + U[i][q];
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void cov_group_local(const double* __restrict__ agg, int64_t nch,
+                                                       int GS, int64_t ng, int nchains,
+                                                       double* __restrict__ gagg) {
+  const int64_t gi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (gi >= ng) return;
+  const int64_t j0 = gi * GS, j1 = (j0 + GS < nch) ? j0 + GS : nch;
+  double S[D][D], Gm[D][D];
+  mat_zero(S);
+  mat_eye(Gm);
+  for (int64_t j = j1 - 1; j >= j0; --j) {   // F <- f_j o F
+    const double* ag = agg + ((int64_t)b * nch + j) * (2 * D * D);
+    double Gj[D][D], T[D][D], U[D][D];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) Gj[i][q] = ag[D * D + i * D + q];
+    mat_mul(Gj, S, T);
+    mat_mul_bt(T, Gj, U);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) S[i][q] = ag[i * D + q] + U[i][q];
+    mat_mul(Gj, Gm, T);
+    mat_copy(T, Gm);
+  }
+  double* o = gagg + ((int64_t)b * ng + gi) * (2 * D * D);
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      o[i * D + q] = S[i][q];
+      o[D * D + i * D + q] = Gm[i][q];
+    }
+}
+
+template <int D>
+__global__ __launch_bounds__(64) void cov_group_scan(const double* __restrict__ gagg, int64_t ng,
+                                                     int nchains, double* __restrict__ gin) {
   const int b = blockIdx.x * blockDim.x + threadIdx.x;
   if (b >= nchains) return;
   double Ph[D][D];
   mat_zero(Ph);
-  for (int64_t j = nch - 1; j >= 0; --j) {
+  for (int64_t g = ng - 1; g >= 0; --g) {
+    double* o = gin + ((int64_t)b * ng + g) * (D * D);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) o[i * D + q] = Ph[i][q];
+    cov_map_apply<D>(gagg + ((int64_t)b * ng + g) * (2 * D * D), Ph);
+  }
+}
+
+template <int D>
+__global__ __launch_bounds__(256) void cov_group_apply(const double* __restrict__ agg,
+                                                       const double* __restrict__ gin, int64_t nch,
+                                                       int GS, int64_t ng, int nchains,
+                                                       double* __restrict__ phat) {
+  const int64_t gi = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (gi >= ng) return;
+  const int64_t j0 = gi * GS, j1 = (j0 + GS < nch) ? j0 + GS : nch;
+  double Ph[D][D];
+  const double* gp = gin + ((int64_t)b * ng + gi) * (D * D);
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) Ph[i][q] = gp[i * D + q];
+  for (int64_t j = j1 - 1; j >= j0; --j) {
     double* o = phat + ((int64_t)b * nch + j) * (D * D);
 #pragma unroll
     for (int i = 0; i < D; ++i)
 #pragma unroll
       for (int q = 0; q < D; ++q) o[i * D + q] = Ph[i][q];
-    const double* ag = agg + ((int64_t)b * nch + j) * (2 * D * D);
-    double Gm[D][D], T[D][D], U[D][D];
-#pragma unroll
-    for (int i = 0; i < D; ++i)
-#pragma unroll
-      for (int q = 0; q < D; ++q) Gm[i][q] = ag[D * D + i * D + q];
-    mat_mul(Gm, Ph, T);
-    mat_mul_bt(T, Gm, U);
-#pragma unroll
-    for (int i = 0; i < D; ++i)
-#pragma unroll
-      for (int q = 0; q < D; ++q) Ph[i][q] = ag[i * D + q] + U[i][q];
+    cov_map_apply<D>(agg + ((int64_t)b * nch + j) * (2 * D * D), Ph);
   }
 }
 
@@ -2414,6 +2543,11 @@ void launch_adjoint_local(hipStream_t st, int sdim, double* X, int64_t ldx, int6
                           const double* rec, const double* g, const double* cin, int64_t mc,
                           int64_t n, int L, int64_t nch, double* bend, int nchains,
                           int64_t xstride, int64_t sstride) {
+  if (ncols == 1 && ldx == 1 && mc == 1) {   // one column per chain: a lane per chunk
+    dim3 gc((unsigned)((nch + 255) / 256), (unsigned)nchains);
+    GPAR_DISPATCH_D(sdim, adjoint_local_col<DD><<<gc, 256, 0, st>>>(X, rec, g, cin, n, L, nch, bend, xstride, sstride));
+    return;
+  }
   dim3 grid((unsigned)nch, (unsigned)((ncols + 63) / 64), (unsigned)nchains);
   GPAR_DISPATCH_D(sdim, adjoint_local<DD><<<grid, 64, 0, st>>>(X, ldx, ncols, rec, g, cin, mc, n, L, bend, xstride, sstride));
 }
@@ -2440,16 +2574,28 @@ void launch_smooth_mean(hipStream_t st, int sdim, const double* u, const double*
   GPAR_DISPATCH_D(sdim, smooth_mean<DD><<<grid, 256, 0, st>>>(u, h, chat, sstride, y, ldy, noise, reinterpret_cast<const ChainParams*>(cps), n, L, mean, ldm));
 }
 
+int64_t cov_carry_scratch_doubles(int sdim, int64_t nch, int nchains) {
+  const int64_t ng = (nch + carry_group_size(nch) - 1) / carry_group_size(nch);
+  return (int64_t)nchains * ng * 3 * sdim * sdim;
+}
+
 void launch_cov_smooth(hipStream_t st, int sdim, const double* t, const double* rec,
                        const double* pf, const ChainParamsHost* cps, int64_t n, int L,
                        int64_t nch, int nchains, double* vloc, double* gam, double* agg,
-                       double* phat, double* var, int64_t ldv) {
+                       double* phat, double* var, int64_t ldv, double* scratch) {
   dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
   dim3 gout((unsigned)((n + 255) / 256), (unsigned)nchains);
   const ChainParams* c = reinterpret_cast<const ChainParams*>(cps);
+  const int GS = carry_group_size(nch);
+  const int64_t ng = (nch + GS - 1) / GS;
+  dim3 gg((unsigned)((ng + 255) / 256), (unsigned)nchains);
   GPAR_DISPATCH_D(sdim, {
+    double* gagg = scratch;
+    double* gin = scratch + (int64_t)nchains * ng * 2 * DD * DD;
     cov_local<DD><<<grid, 256, 0, st>>>(t, rec, pf, c, n, L, nch, vloc, gam, agg);
-    cov_carry<DD><<<(nchains + 63) / 64, 64, 0, st>>>(agg, nch, nchains, phat);
+    cov_group_local<DD><<<gg, 256, 0, st>>>(agg, nch, GS, ng, nchains, gagg);
+    cov_group_scan<DD><<<(nchains + 63) / 64, 64, 0, st>>>(gagg, ng, nchains, gin);
+    cov_group_apply<DD><<<gg, 256, 0, st>>>(agg, gin, nch, GS, ng, nchains, phat);
     cov_out<DD><<<gout, 256, 0, st>>>(vloc, gam, phat, n, L, nch, var, ldv);
   });
 }

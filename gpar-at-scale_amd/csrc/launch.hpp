@@ -181,10 +181,12 @@ void launch_smooth_mean(hipStream_t st, int sdim, const double* u, const double*
                         const double* noise, const ChainParamsHost* cps, int64_t n, int L,
                         int nchains, double* mean, int64_t ldm);
 // vloc/var: nchains * n; gam: nchains * n * 4; agg: nchains * nch * 2 sdim^2; phat: nchains * nch * sdim^2
+// scratch: cov_carry_scratch_doubles(sdim, nch, nchains) doubles (the carry's group maps)
+int64_t cov_carry_scratch_doubles(int sdim, int64_t nch, int nchains);
 void launch_cov_smooth(hipStream_t st, int sdim, const double* t, const double* rec,
                        const double* pf, const ChainParamsHost* cps, int64_t n, int L,
                        int64_t nch, int nchains, double* vloc, double* gam, double* agg,
-                       double* phat, double* var, int64_t ldv);
+                       double* phat, double* var, int64_t ldv, double* scratch);
 int64_t vec_fix_blocks(int64_t n);
 void launch_vec_fix(hipStream_t st, int sdim, double* alpha, int64_t lda, const double* g,
                     int64_t gstride, const double* cin, int64_t sstride, int64_t mc,

@@ -184,10 +184,11 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *                   cache cannot hold all at once: each sub-batch computes its distances once
  *                   and every evaluation reads them, instead of the outputs left uncached
  *                   recomputing theirs every evaluation.  -1 (default) = auto: fits too large
- *                   to pipeline (beta > 8 GB: the N = 1e7, M = 1024 stress config) whose outputs
- *                   all have D >= 17, in sub-batches of as many outputs as the free memory (or
- *                   an explicit gpar_ctx_set_dist_cache budget) holds; 0 = one batch; k >= 1 =
- *                   sub-batches of k.  Not for gpar_fit_predict / gpar_fit_posterior.  Each
+ *                   to pipeline (beta > 8 GB: the N = 1e7, M = 1024 stress config): the outputs
+ *                   with D < 17 (fused whitening, never cached) as one sub-batch, the others in
+ *                   sub-batches of as many outputs as the free memory (or an explicit
+ *                   gpar_ctx_set_dist_cache budget) holds; 0 = one batch; k >= 1 = sub-batches
+ *                   of k consecutive outputs.  Not for gpar_fit_predict / gpar_fit_posterior.  Each
  *                   output's fit is independent of its batch, so a sub-batched fit equals the
  *                   one-batch fit with every output cached bit for bit
  * The environment variable GPAR_<KNOB> (upper case) sets a knob at context creation.

@@ -249,3 +249,37 @@ def test_fit_chunks_equal_one_fully_cached_batch():
         np.testing.assert_array_equal(res[k].theta, res[0].theta)
         np.testing.assert_array_equal(res[k].nlml, res[0].nlml)
         np.testing.assert_array_equal(res[k].evals, res[0].evals)
+
+
+def test_fit_chunks_auto_keeps_narrow_outputs_apart():
+    """The auto rule where the fit is not pipelined (here: two lanes; in the stress config: an
+    82 GB beta) and the cache budget holds fewer wide outputs than the batch has: the outputs
+    with D < 17 (never cached) run as one sub-batch, the cacheable ones two at a time (the budget),
+    and the fit equals one batch with every wide output cached, bit for bit."""
+    t, Y = O.synthetic_gpar(12_000, 45, seed=53, noise=0.3)
+    probs, keep = [], []
+    dims = (4, 20, 40, 9, 18, 30)
+    for D in dims:
+        V = np.ascontiguousarray(Y[:, :D].T)
+        Z = O.pick_pseudo_inputs(V, 64, D)
+        pr, k = G.make_problem(V, Z, t, Y[:, D], "matern52", "matern52")
+        probs.append(pr)
+        keep.append(k)
+    ctx = G.context(0)
+    x0 = np.tile(X0, (len(probs), 1))
+    two = 2 * 12_000 * 128 * 8 + (1 << 20)          # the distances of two outputs of Mp = 128
+    try:
+        ctx.set_lanes(2)
+        ctx.set_schedule("fit_chunks", 0)
+        whole = G.fit_batch(probs, x0, max_evals=12, g_tol=-1.0)
+        assert ctx.dist_cache_stats()[0] == 4
+        ctx.set_schedule("fit_chunks", -1)
+        ctx.set_dist_cache(two)
+        auto = G.fit_batch(probs, x0, max_evals=12, g_tol=-1.0)
+        assert ctx.dist_cache_stats()[0] == 2          # the last sub-batch: two wide outputs
+    finally:
+        ctx.set_lanes(1)
+        ctx.set_dist_cache(-1)
+        ctx.set_schedule("fit_chunks", -1)
+    np.testing.assert_array_equal(auto.theta, whole.theta)
+    np.testing.assert_array_equal(auto.nlml, whole.nlml)
