@@ -451,6 +451,17 @@ void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* lo
       return;
     }
   }
+  // the cache lives for this fit call only, unless the caller keeps it (gpar_ctx_set_dist_cache_keep)
+  struct CacheRelease {
+    gpar_ctx* c;
+    ~CacheRelease() {
+      if (c->dist_cache_keep) return;
+      try {
+        release_dist_cache(c);
+      } catch (...) {
+      }
+    }
+  } release_{ctx};
   const std::vector<DevProblem> P =
       attach_dist_cache(ctx, P0, fit_ws_estimate(ctx, P0) + later_bytes);
   const int nprob = (int)P.size();
