@@ -425,13 +425,25 @@ void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* lo
   if (!keep) {   // (the kept Grams are named by batch index: one batch when they are wanted)
     const std::vector<std::vector<int>> chunks = cache_chunks(ctx, P0, later_bytes);
     if (!chunks.empty()) {
-      const int saved = ctx->fit_chunks;
-      ctx->fit_chunks = 0;   // each sub-batch is one batch
+      // each sub-batch is one batch, and the cache buffers pass from one sub-batch to the next
+      // (re-allocating tens of GB per sub-batch costs seconds: fresh VRAM is cleared); released at
+      // the end unless the caller keeps them
       struct Restore {
         gpar_ctx* c;
-        int v;
-        ~Restore() { c->fit_chunks = v; }
-      } restore_{ctx, saved};
+        int chunks;
+        bool keep;
+        ~Restore() {
+          c->fit_chunks = chunks;
+          c->dist_cache_keep = keep;
+          if (keep) return;
+          try {
+            release_dist_cache(c);
+          } catch (...) {
+          }
+        }
+      } restore_{ctx, ctx->fit_chunks, ctx->dist_cache_keep};
+      ctx->fit_chunks = 0;
+      ctx->dist_cache_keep = true;
       for (const auto& idx : chunks) {
         const size_t k = idx.size();
         std::vector<DevProblem> sub;
