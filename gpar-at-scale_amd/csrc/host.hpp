@@ -108,10 +108,6 @@ struct gpar_ctx {
   bool serialize = false;
   // own_s: s_w, s_g, s_g2 and s_d (the round overlap's dense tails and gains, on the whitening CUs)
   hipStream_t own_side = nullptr, own_s[4] = {nullptr, nullptr, nullptr, nullptr};
-  // two more whole-chip streams (created on first use, ensure_aux): the pipelined grouped Gram's
-  // whitenings run there while the previous group's Gram runs on the context stream
-  hipStream_t own_aux[2] = {nullptr, nullptr}, aux[2] = {nullptr, nullptr};
-  hipEvent_t ev_gg[2] = {nullptr, nullptr};   // grouped Gram of buffer set 0 / 1 done
   std::string ws_suffix;          // appended to workspace names (a prediction lane's own buffers)
   std::vector<hipEvent_t> ev_grp;   // fit_overlapped: a group's values are in (one per group)
   std::vector<hipEvent_t> ev_gn;    // fit_overlapped: a group's gains are done
@@ -197,7 +193,6 @@ struct Timed {
   }
 };
 void flush_stats(gpar_ctx* c);
-void ensure_aux(gpar_ctx* c);   // creates (and routes) the aux streams and ev_gg
 
 inline bool is_cache_buf(const std::string& name) { return name.rfind("distcache", 0) == 0; }
 void sync_all(gpar_ctx* c);

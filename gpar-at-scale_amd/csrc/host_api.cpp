@@ -26,8 +26,6 @@ int fail(gpar_ctx* c, int code, const char* what) {
   (void)hipStreamSynchronize(c->own_side);
   for (hipStream_t st : c->own_s)
     if (st) (void)hipStreamSynchronize(st);
-  for (hipStream_t st : c->own_aux)
-    if (st) (void)hipStreamSynchronize(st);
   (void)hipGetLastError();
   return code;
 }
@@ -35,17 +33,8 @@ int fail(gpar_ctx* c, int code, const char* what) {
 // The stream handles launches use: the created streams, or all `main` when serialized.
 static void route_streams(gpar_ctx* c) {
   c->side = c->serialize ? c->main : c->own_side;
-  for (int i = 0; i < 2; ++i) c->aux[i] = (c->serialize && c->own_aux[i]) ? c->main : c->own_aux[i];
   hipStream_t* act[4] = {&c->s_w, &c->s_g, &c->s_g2, &c->s_d};
   for (int i = 0; i < 4; ++i) *act[i] = (c->serialize && c->own_s[i]) ? c->main : c->own_s[i];
-}
-
-void ensure_aux(gpar_ctx* c) {
-  for (int i = 0; i < 2; ++i) {
-    if (!c->own_aux[i]) HIPCHECK(hipStreamCreateWithFlags(&c->own_aux[i], hipStreamNonBlocking));
-    if (!c->ev_gg[i]) HIPCHECK(hipEventCreateWithFlags(&c->ev_gg[i], hipEventDisableTiming));
-  }
-  route_streams(c);
 }
 
 // CU split of the pipelined fit (gpar_ctx_set_cu_split): CU-masked streams for the whitening
@@ -139,8 +128,6 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
     (void)hipStreamSynchronize(c->main);
     (void)hipStreamSynchronize(c->own_side);
     for (hipStream_t st : c->own_s)
-      if (st) (void)hipStreamSynchronize(st);
-    for (hipStream_t st : c->own_aux)
       if (st) (void)hipStreamSynchronize(st);
     c->serialize = v != 0;
     route_streams(c);
@@ -237,13 +224,6 @@ int32_t gpar_ctx_destroy(gpar_ctx* ctx) {
         if (ev) (void)hipEventDestroy(ev);
     for (auto& s : ctx->stage)
       if (s.host) (void)hipHostFree(s.host);
-    for (int i = 0; i < 2; ++i) {
-      if (ctx->own_aux[i]) {
-        (void)hipStreamSynchronize(ctx->own_aux[i]);
-        (void)hipStreamDestroy(ctx->own_aux[i]);
-      }
-      if (ctx->ev_gg[i]) (void)hipEventDestroy(ctx->ev_gg[i]);
-    }
   }
   (void)hipStreamDestroy(ctx->own_side);
   (void)hipStreamDestroy(ctx->main);

@@ -73,7 +73,7 @@ static StageBufs stage_bufs_grp(gpar_ctx* c, int lane, int slot, int64_t n, int6
 // items come from several outputs with 1/g of the time splits each.
 constexpr double kGramGroupMaxWork = 5e10;
 constexpr int kGramGroupAuto = 16;
-constexpr int64_t kGramGroupMaxBytes = (int64_t)24 << 30;   // one buffer set's beta (two sets)
+constexpr int64_t kGramGroupMaxBytes = (int64_t)24 << 30;   // the group's beta buffers
 static int gram_group_size(gpar_ctx* c, const std::vector<DevProblem>& P, int64_t n,
                            int64_t mpmax, bool fix_beta, int nlanes, bool split_pipe) {
   const int np = (int)P.size();
@@ -335,25 +335,18 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
   }
   const int gsz = gram_group_size(c, P, n, mpmax, fix_beta, nlanes, split_pipe);
   if (gsz >= 2) {
-    // Grouped Gram: per group of gsz outputs, their whitenings and short chains alternate over two
-    // whole-chip streams (aux) into buffers of their own, then one set of Gram launches covers the
+    // Grouped Gram: per group of gsz outputs, their whitenings and short chains alternate over the
+    // context and side streams into buffers of their own, then one set of Gram launches covers the
     // whole group (grid y = output, GramGroupPtrs table), its plan sized for 1/gsz of the chip per
     // output.  A different split plan than the per-output Gram's: G moves within rounding.
-    // Pipelined (r06): two buffer sets, so group g + 1's (memory-bound) whitenings run on the aux
-    // streams while group g's (MFMA-bound) Gram runs on the context stream; a set is rewritten only
-    // after the Gram two groups back has read it (ev_gg).  Before, every group's whitenings waited
-    // for the previous Gram (eeg config: 0.85 s of a 2.56 s job off the Gram).
     const hipStream_t base = c->stream;
-    ensure_aux(c);
     const int ngroups = (np + gsz - 1) / gsz;
-    const int nsets = ngroups > 1 ? 2 : 1;
     auto* tab = ws<GramGroupPtrs>(c, "gram_grp_tab", (size_t)ngroups * gsz);
     auto plan_of = [&](int cnt) {
       const int cus = std::max(256 / cnt, 8);
       return gram_plan(n, mpmax, false, cus, cus);
     };
-    // the partials, sized once for every group's plan (no buffer may move under a running launch);
-    // one set: the Grams run in order on the context stream
+    // the partials, sized once for every group's plan (no buffer may move under a running launch)
     int64_t pd = 0, rd = 0;
     for (int cnt : {gsz, np % gsz})
       if (cnt > 0) {
@@ -363,22 +356,20 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
       }
     double* part = ws<double>(c, "gram_part_grp", (size_t)gsz * pd);
     double* rpart = ws<double>(c, "gram_rpart_grp", (size_t)gsz * rd);
-    // both whitening streams start after everything queued so far (inputs, the gains)
-    HIPCHECK(hipEventRecord(c->ev_fork, base));
-    for (hipStream_t st : c->aux) HIPCHECK(hipStreamWaitEvent(st, c->ev_fork, 0));
     for (int g0 = 0, gi = 0; g0 < np; g0 += gsz, ++gi) {
       const int cnt = std::min(gsz, np - g0);
-      const int set = gi % nsets;
       const GramPlan plan = plan_of(cnt);
-      if (gi >= 2)   // this set's buffers: read by the Gram two groups back
-        for (hipStream_t st : c->aux) HIPCHECK(hipStreamWaitEvent(st, c->ev_gg[set], 0));
+      // the side lane starts after everything queued so far (the gains, the previous group's Gram,
+      // which still reads the buffers this group overwrites)
+      HIPCHECK(hipEventRecord(c->ev_fork, base));
+      HIPCHECK(hipStreamWaitEvent(c->side, c->ev_fork, 0));
       std::vector<StageBufs> gb(cnt);
       std::vector<GramGroupPtrs> th_tab(cnt);
       double work = 0.0;
       for (int k = 0; k < cnt; ++k) {
         const int i = g0 + k, lane = k & 1;
-        gb[k] = stage_bufs_grp(c, lane, set * gsz + k, n, mpmax);
-        OnStream on_(c, c->aux[lane]);
+        gb[k] = stage_bufs_grp(c, lane, k, n, mpmax);
+        OnStream on_(c, lane ? c->side : base);
         const StageJob& j = job(i, gb[k]);
         stage_whiten(c, j, gb[k]);
         stage_post(c, j, gb[k], false);
@@ -387,10 +378,8 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
                      j.G, j.r};
         work += (double)P[i].n * (double)P[i].m * (double)(P[i].m + 1);
       }
-      for (int l = 0; l < 2; ++l) {
-        HIPCHECK(hipEventRecord(c->ev_pc[l], c->aux[l]));
-        HIPCHECK(hipStreamWaitEvent(base, c->ev_pc[l], 0));
-      }
+      HIPCHECK(hipEventRecord(c->ev_join, c->side));
+      HIPCHECK(hipStreamWaitEvent(base, c->ev_join, 0));
       GramGroupPtrs* dtab = tab + (size_t)gi * gsz;
       h2d(c, dtab, th_tab.data(), (size_t)cnt);
       {
@@ -399,7 +388,6 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
                             c->side, c->ev_fork, c->ev_join);
       }
       check_launch("gram (grouped)");
-      HIPCHECK(hipEventRecord(c->ev_gg[set], base));
     }
     return o;
   }

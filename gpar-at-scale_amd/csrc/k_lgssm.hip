@@ -1051,7 +1051,11 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
   constexpr int VS = DP + 2;      // V tile row stride: conflict-free A-fragment reads
   constexpr int NKS = DP / 4;
   __shared__ __attribute__((aligned(16))) double vs[kMT * VS];
-  __shared__ __attribute__((aligned(16))) double xt[4][kMT][65];
+  // rows of 66 doubles (528 B, 16-byte aligned): the flush reads a lane's column pair as one
+  // ds_read_b128, conflict-free; with 65 the pair was two ds_read_b64 whose lanes l and l + 16
+  // hit one bank (2-way; 16 % of the kernel's LDS cycles were bank conflicts, r05q PMC)
+  constexpr int XS = 66;
+  __shared__ __attribute__((aligned(16))) double xt[4][kMT][XS];
   // the sub-tile's step rows {A_k (SD x SD), K_k (SD), rs_k, g_k (SD)}, 16 doubles each (fmac_row)
   constexpr int RK = SD * SD, RR = SD * SD + SD, RG = SD * SD + SD + 1;
   static_assert(RG + SD <= 16, "step row");
@@ -1141,10 +1145,8 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     if (cw0 < mp && ntp == kMT) {   // all LDS reads first, then the 8 stores (no per-row branch)
       double2 v2[kMT / 2];
 #pragma unroll
-      for (int i = 0; i < kMT / 2; ++i) {
-        v2[i].x = xt[wave][2 * i + fh][fc2];
-        v2[i].y = xt[wave][2 * i + fh][fc2 + 1];
-      }
+      for (int i = 0; i < kMT / 2; ++i)
+        v2[i] = *reinterpret_cast<const double2*>(&xt[wave][2 * i + fh][fc2]);
 #pragma unroll
       for (int i = 0; i < kMT / 2; ++i)
         *reinterpret_cast<double2*>(beta + (ktp + 2 * i + fh) * ldb + cw0 + fc2) = v2[i];
@@ -1153,9 +1155,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
       for (int i = 0; i < kMT / 2; ++i) {
         const int kk = 2 * i + fh;
         if (kk < ntp) {
-          double2 v2;
-          v2.x = xt[wave][kk][fc2];
-          v2.y = xt[wave][kk][fc2 + 1];
+          const double2 v2 = *reinterpret_cast<const double2*>(&xt[wave][kk][fc2]);
           *reinterpret_cast<double2*>(beta + (ktp + kk) * ldb + cw0 + fc2) = v2;
         }
       }
