@@ -16,7 +16,16 @@ void chains_logpdf(gpar_ctx* c, const std::vector<const double*>& ys, int64_t n,
     ARGCHECK(l > 0 && pv > 0 && ns > 0, "theta entries must be positive");
     cps[i] = {1.0 / l, l, pv * pv, ns * ns};
   }
-  const int64_t nch = (n + kChunk - 1) / kChunk;
+  // Chunk length: each chunk is one lane's sequential recursion, and with few chains the 256-step
+  // chunks leave the chip nearly idle (ssm config: 16 chains x 1e6 steps = 62.5 k lanes, under one
+  // wave per SIMD, so every dependent fp64 step waits out its full latency).  Shorter chunks give
+  // the lanes to hide it, at the price of a longer chunk scan (phase 2, the carry).
+  int L = kChunk;
+  const char* el = std::getenv("GPAR_CHAIN_L");
+  if (el) L = std::atoi(el);
+  else
+    while (L > 64 && (double)nchains * (double)n / L < 4.0 * 1024 * 64) L /= 2;
+  const int64_t nch = (n + L - 1) / L;
   // one pass: the gains recursion filters each chain's y from zero per chunk and keeps, per chunk,
   // sum log S_k and the moments of the chunk-local alpha against the fix-up rows (no per-step
   // record, fix-up row or alpha reaches HBM: t and y are read, 32 + 96 bytes per chunk written);
@@ -28,7 +37,7 @@ void chains_logpdf(gpar_ctx* c, const std::vector<const double*>& ys, int64_t n,
   double* mom = ws<double>(c, "chain_mom", (size_t)nchains * nch * kGainsMomStride);
   double* dl = ws<double>(c, "chain_lml", nchains);
   GainsPlan gp = plan_gains(c, sdim, t, n, cps, nullptr, false, "chain", &ys, nullptr, send, false,
-                            mom);
+                            mom, L);
   {
     Timed tm_(c, "chains_logpdf", 8.0 * (double)n * (1.0 + nchains));
     gp.launch(c->stream, 0, nchains);
