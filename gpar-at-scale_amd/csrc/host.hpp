@@ -326,14 +326,13 @@ struct GainsPlan {
   bool ys_aligned16 = false;   // every ys[i] 16-byte aligned (the fast gains path's LDS-DMA)
   double *alpha_loc = nullptr, *asend = nullptr;
   double* moments = nullptr;   // chains_logpdf: per-chunk data moments instead of records
-  int L = kChunk;       // steps per chunk (shorter only for chains_logpdf, see there)
   void launch(hipStream_t st, int first, int count) const;
 };
 GainsPlan plan_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                      const std::vector<ChainParamsHost>& cps, const double* noise, bool want_pf,
                      const std::string& tag, const std::vector<const double*>* ys = nullptr,
                      double* alpha_loc = nullptr, double* asend = nullptr, bool compact = false,
-                     double* moments = nullptr, int L = kChunk);
+                     double* moments = nullptr);
 GainsOut run_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                           const std::vector<ChainParamsHost>& cps, const double* noise,
                           bool want_pf, const std::string& tag,

@@ -282,17 +282,14 @@ std::vector<DevProblem> prepare_batch(gpar_ctx* c, const gpar_problem* probs, in
 GainsPlan plan_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
                      const std::vector<ChainParamsHost>& cps, const double* noise, bool want_pf,
                      const std::string& tag, const std::vector<const double*>* ys,
-                     double* alpha_loc, double* asend, bool compact, double* moments, int L) {
-  ARGCHECK(L == kChunk || (moments && L >= 16 && (L & (L - 1)) == 0),
-           "gains: chunks other than kChunk only for the moments form");
+                     double* alpha_loc, double* asend, bool compact, double* moments) {
   GainsPlan gp;
   gp.c = c;
   gp.sdim = sdim;
   gp.t = t;
   gp.n = n;
-  gp.L = L;
   gp.nchains = (int)cps.size();
-  gp.nch = (n + L - 1) / L;
+  gp.nch = (n + kChunk - 1) / kChunk;
   gp.noise = noise;
   const int nchains = gp.nchains;
   const int64_t nch = gp.nch;
@@ -333,7 +330,7 @@ void GainsPlan::launch(hipStream_t st, int first, int count) const {
   const int d2 = sdim * sdim;
   OnStream on_(c, st);
   Timed tm_(c, "gains");
-  launch_gains(st, sdim, t, n, L, nch, count, dcps + first, noise,
+  launch_gains(st, sdim, t, n, kChunk, nch, count, dcps + first, noise,
                agg + (size_t)first * nch * 3 * d2, pst + (size_t)first * nch * d2,
                o.rec ? o.rec + (size_t)first * o.recstride : nullptr,
                o.g ? o.g + (size_t)first * o.gstride : nullptr,

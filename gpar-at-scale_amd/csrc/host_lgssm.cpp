@@ -16,16 +16,7 @@ void chains_logpdf(gpar_ctx* c, const std::vector<const double*>& ys, int64_t n,
     ARGCHECK(l > 0 && pv > 0 && ns > 0, "theta entries must be positive");
     cps[i] = {1.0 / l, l, pv * pv, ns * ns};
   }
-  // Chunk length: each chunk is one lane's sequential recursion, and with few chains the 256-step
-  // chunks leave the chip nearly idle (ssm config: 16 chains x 1e6 steps = 62.5 k lanes, under one
-  // wave per SIMD, so every dependent fp64 step waits out its full latency).  Shorter chunks give
-  // the lanes to hide it, at the price of a longer chunk scan (phase 2, the carry).
-  int L = kChunk;
-  const char* el = std::getenv("GPAR_CHAIN_L");
-  if (el) L = std::atoi(el);
-  else
-    while (L > 64 && (double)nchains * (double)n / L < 4.0 * 1024 * 64) L /= 2;
-  const int64_t nch = (n + L - 1) / L;
+  const int64_t nch = (n + kChunk - 1) / kChunk;
   // one pass: the gains recursion filters each chain's y from zero per chunk and keeps, per chunk,
   // sum log S_k and the moments of the chunk-local alpha against the fix-up rows (no per-step
   // record, fix-up row or alpha reaches HBM: t and y are read, 32 + 96 bytes per chunk written);
@@ -37,7 +28,7 @@ void chains_logpdf(gpar_ctx* c, const std::vector<const double*>& ys, int64_t n,
   double* mom = ws<double>(c, "chain_mom", (size_t)nchains * nch * kGainsMomStride);
   double* dl = ws<double>(c, "chain_lml", nchains);
   GainsPlan gp = plan_gains(c, sdim, t, n, cps, nullptr, false, "chain", &ys, nullptr, send, false,
-                            mom, L);
+                            mom);
   {
     Timed tm_(c, "chains_logpdf", 8.0 * (double)n * (1.0 + nchains));
     gp.launch(c->stream, 0, nchains);
@@ -73,21 +64,21 @@ void chains_smooth(gpar_ctx* c, int nchains, int64_t n, const double* t, const d
   launch_whiten_vec(c->stream, sdim, g.rec, g.recstride, y, ldy, n, kChunk, nch, nchains, u, n,
                     send, ss, 1, 0);
   run_carry(c, sdim, g.phi, g.phistride, send, cin, ss, nch, 1, 1, nchains, "smf");
-  launch_gains_adjoint(c->stream, sdim, g.rec, n, kChunk, nch, nchains, h);
-  launch_adjoint_local(c->stream, sdim, u, 1, 1, g.rec, g.g, cin, 1, n, kChunk, nch, bend, nchains,
-                       n, ss);
-  run_carry(c, sdim, g.phi, g.phistride, bend, chat, ss, nch, 1, 1, nchains, "smb", true);
   auto* dcps = ws<ChainParamsHost>(c, "sm_cps2", nchains);
   h2d(c, dcps, cps.data(), nchains);
-  launch_smooth_mean(c->stream, sdim, u, h, chat, ss, y, ldy, noise, dcps, n, kChunk, nchains, mean,
-                     ldo);
   double* vloc = ws<double>(c, "sm_vloc", (size_t)nchains * n);
   double* gam = ws<double>(c, "sm_gam", (size_t)nchains * n * 4);
   double* agg = ws<double>(c, "sm_agg", (size_t)nchains * nch * 2 * sdim * sdim);
   double* phat = ws<double>(c, "sm_phat", (size_t)nchains * nch * sdim * sdim);
+  // the backward pass in one launch (r06; gains_adjoint + adjoint_local + cov_local before)
+  launch_smooth_back(c->stream, sdim, g.rec, g.g, g.pf, dcps, cin, u, h, vloc, gam, agg, bend, n,
+                     kChunk, nch, nchains, n, ss);
+  run_carry(c, sdim, g.phi, g.phistride, bend, chat, ss, nch, 1, 1, nchains, "smb", true);
+  launch_smooth_mean(c->stream, sdim, u, h, chat, ss, y, ldy, noise, dcps, n, kChunk, nchains, mean,
+                     ldo);
   double* cscr = ws<double>(c, "sm_covscan", (size_t)cov_carry_scratch_doubles(sdim, nch, nchains));
   launch_cov_smooth(c->stream, sdim, t, g.rec, g.pf, dcps, n, kChunk, nch, nchains, vloc, gam, agg,
-                    phat, var, ldo, cscr);
+                    phat, var, ldo, cscr, /*local_done=*/true);
   check_launch("chains_smooth");
 }
 

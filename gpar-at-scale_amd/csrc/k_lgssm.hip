@@ -2001,6 +2001,172 @@ __global__ __launch_bounds__(256) void cov_local(const double* __restrict__ t,
     }
 }
 
+// The temporal chains' backward smoothing pass in one kernel, one lane per (chunk, chain): per
+// step the three chunk-local backward recursions that gains_adjoint (h_k), adjoint_local_col
+// (u_k, the chunk's adjoint end state) and cov_local (the local smoothed variance and Gamma row)
+// ran as three launches, each re-reading the step's gains record (r06: 1.12 + 1.03 + 1.74 ms at
+// the ssm config's 16 chains x 2e6 steps, latency-bound at two waves per SIMD).  The same
+// arithmetic in the same order per recursion, so the results are bit-identical to the three
+// kernels; interleaved, the three independent dependency chains hide each other's latency and the
+// record, fix-up row and filtered covariance are read once.
+template <int D>
+__global__ __launch_bounds__(256) void smooth_back(const double* __restrict__ rec,
+                                                   const double* __restrict__ g,
+                                                   const double* __restrict__ pf,
+                                                   const ChainParams* __restrict__ cps,
+                                                   const double* __restrict__ cin,
+                                                   double* __restrict__ X, double* __restrict__ h,
+                                                   double* __restrict__ vloc,
+                                                   double* __restrict__ gam,
+                                                   double* __restrict__ agg,
+                                                   double* __restrict__ bend, int64_t n, int L,
+                                                   int64_t nch, int64_t xstride, int64_t sstride) {
+  constexpr int RS = Rec<D>::size;
+  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int b = blockIdx.y;
+  if (j >= nch) return;
+  const ChainParams cp = cps[b];
+  rec += (int64_t)b * n * RS;
+  g += (int64_t)b * n * kGStride;
+  pf += (int64_t)b * n * D * D;
+  X += (int64_t)b * xstride;
+  h += (int64_t)b * n * kGStride;
+  vloc += (int64_t)b * n;
+  gam += (int64_t)b * n * kGStride;
+  cin += (int64_t)b * sstride;
+  bend += (int64_t)b * sstride;
+  const int64_t k0 = j * L;
+  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  double cf[D], lam[D], Ga[D][D], Ps[D][D], Gm[D][D], A1[D][D], Pinf[D][D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+    cf[i] = cin[j * kSStride + i];
+    lam[i] = 0.0;
+  }
+  mat_eye(Ga);
+  mat_zero(Ps);
+  mat_eye(Gm);
+  sde_pinf<D>(cp.s, Pinf);
+  if (k1 < n) {   // A_{k1}: the transition into the next chunk's first step
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) A1[i][q] = rec[k1 * RS + i * D + q];
+  } else {
+    mat_zero(A1);
+  }
+  for (int64_t k = k1 - 1; k >= k0; --k) {
+    const double* r = rec + k * RS;
+    double A[D][D], K[D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) {
+      K[i] = r[D * D + i];
+#pragma unroll
+      for (int q = 0; q < D; ++q) A[i][q] = r[i * D + q];
+    }
+    const double rs = r[D * D + D];
+    // ---- gains_adjoint: h_k = Gamma^T K, Gamma <- Abar^T Gamma
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      double acc = 0.0;
+#pragma unroll
+      for (int i = 0; i < D; ++i) acc = fma(Ga[i][q], K[i], acc);
+      h[k * kGStride + q] = acc;
+    }
+    {
+      double Ab[D][D], T[D][D];
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) Ab[i][q] = A[i][q] - K[i] * A[0][q];
+      mat_mul_at(Ab, Ga, T);
+      mat_copy(T, Ga);
+    }
+    // ---- adjoint_local_col: u_k and lambda
+    {
+      const double* gk = g + k * kGStride;
+      double w = X[k];
+#pragma unroll
+      for (int i = 0; i < D; ++i) w = fma(gk[i], cf[i], w);
+      double u = w * rs;
+#pragma unroll
+      for (int i = 0; i < D; ++i) u = fma(K[i], lam[i], u);
+      lam[0] -= u;
+      double nl[D];
+#pragma unroll
+      for (int q = 0; q < D; ++q) {
+        double acc = 0.0;
+#pragma unroll
+        for (int i = 0; i < D; ++i) acc = fma(A[i][q], lam[i], acc);
+        nl[q] = acc;
+      }
+#pragma unroll
+      for (int i = 0; i < D; ++i) lam[i] = nl[i];
+      X[k] = u;
+    }
+    // ---- cov_local: the local smoothed covariance and Gamma's first row
+    {
+      double P[D][D];
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) P[i][q] = pf[k * D * D + i * D + q];
+      double G[D][D], C[D][D];
+      if (k == n - 1) {
+        mat_zero(G);
+        mat_copy(P, C);
+      } else {
+        double Q1[D][D], T[D][D], Pm[D][D], Pmi[D][D];
+        mat_mul(A1, Pinf, T);
+        mat_mul_bt(T, A1, Q1);
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+          for (int q = 0; q < D; ++q) Q1[i][q] = Pinf[i][q] - Q1[i][q];
+        mat_mul(A1, P, T);
+        mat_mul_bt(T, A1, Pm);
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+          for (int q = 0; q < D; ++q) Pm[i][q] += Q1[i][q];
+        mat_inv(Pm, Pmi);
+        mat_mul_bt(P, A1, T);
+        mat_mul(T, Pmi, G);
+        double GP[D][D], GPG[D][D];
+        mat_mul(G, Pm, GP);
+        mat_mul_bt(GP, G, GPG);
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+          for (int q = 0; q < D; ++q) C[i][q] = P[i][q] - GPG[i][q];
+      }
+      double T[D][D], U[D][D];
+      mat_mul(G, Ps, T);
+      mat_mul_bt(T, G, U);
+#pragma unroll
+      for (int i = 0; i < D; ++i)
+#pragma unroll
+        for (int q = 0; q < D; ++q) Ps[i][q] = U[i][q] + C[i][q];
+      mat_mul(G, Gm, T);
+      mat_copy(T, Gm);
+      vloc[k] = Ps[0][0];
+#pragma unroll
+      for (int q = 0; q < D; ++q) gam[k * kGStride + q] = Gm[0][q];
+    }
+    mat_copy(A, A1);
+  }
+#pragma unroll
+  for (int i = 0; i < D; ++i) bend[j * kSStride + i] = lam[i];
+  double* ag = agg + ((int64_t)b * nch + j) * (2 * D * D);
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int q = 0; q < D; ++q) {
+      ag[i * D + q] = Ps[i][q];
+      ag[D * D + i * D + q] = Gm[i][q];
+    }
+}
+
 // Backward carry over chunks: Phat_{J-1} = 0, Phat_{j-1} = f_j(Phat_j) = S_j + Gamma_j Phat_j
 // Gamma_j^T with S_j = the chunk's local smoothed covariance at its start and Gamma_j its
 // transfer (agg).  The maps compose, (S_a, Gamma_a) o (S_b, Gamma_b) = (S_a + Gamma_a S_b
@@ -2579,10 +2745,19 @@ int64_t cov_carry_scratch_doubles(int sdim, int64_t nch, int nchains) {
   return (int64_t)nchains * ng * 3 * sdim * sdim;
 }
 
+void launch_smooth_back(hipStream_t st, int sdim, const double* rec, const double* g,
+                        const double* pf, const ChainParamsHost* cps, const double* cin, double* X,
+                        double* h, double* vloc, double* gam, double* agg, double* bend, int64_t n,
+                        int L, int64_t nch, int nchains, int64_t xstride, int64_t sstride) {
+  dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
+  const ChainParams* c = reinterpret_cast<const ChainParams*>(cps);
+  GPAR_DISPATCH_D(sdim, smooth_back<DD><<<grid, 256, 0, st>>>(rec, g, pf, c, cin, X, h, vloc, gam, agg, bend, n, L, nch, xstride, sstride));
+}
+
 void launch_cov_smooth(hipStream_t st, int sdim, const double* t, const double* rec,
                        const double* pf, const ChainParamsHost* cps, int64_t n, int L,
                        int64_t nch, int nchains, double* vloc, double* gam, double* agg,
-                       double* phat, double* var, int64_t ldv, double* scratch) {
+                       double* phat, double* var, int64_t ldv, double* scratch, bool local_done) {
   dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
   dim3 gout((unsigned)((n + 255) / 256), (unsigned)nchains);
   const ChainParams* c = reinterpret_cast<const ChainParams*>(cps);
@@ -2592,7 +2767,7 @@ void launch_cov_smooth(hipStream_t st, int sdim, const double* t, const double* 
   GPAR_DISPATCH_D(sdim, {
     double* gagg = scratch;
     double* gin = scratch + (int64_t)nchains * ng * 2 * DD * DD;
-    cov_local<DD><<<grid, 256, 0, st>>>(t, rec, pf, c, n, L, nch, vloc, gam, agg);
+    if (!local_done) cov_local<DD><<<grid, 256, 0, st>>>(t, rec, pf, c, n, L, nch, vloc, gam, agg);
     cov_group_local<DD><<<gg, 256, 0, st>>>(agg, nch, GS, ng, nchains, gagg);
     cov_group_scan<DD><<<(nchains + 63) / 64, 64, 0, st>>>(gagg, ng, nchains, gin);
     cov_group_apply<DD><<<gg, 256, 0, st>>>(agg, gin, nch, GS, ng, nchains, phat);

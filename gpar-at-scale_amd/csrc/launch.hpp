@@ -186,7 +186,14 @@ int64_t cov_carry_scratch_doubles(int sdim, int64_t nch, int nchains);
 void launch_cov_smooth(hipStream_t st, int sdim, const double* t, const double* rec,
                        const double* pf, const ChainParamsHost* cps, int64_t n, int L,
                        int64_t nch, int nchains, double* vloc, double* gam, double* agg,
-                       double* phat, double* var, int64_t ldv, double* scratch);
+                       double* phat, double* var, int64_t ldv, double* scratch,
+                       bool local_done = false);
+// the chains' backward pass (h, u in place of X, bend; vloc, gam, agg) in one launch: what
+// launch_gains_adjoint + launch_adjoint_local (one column) + cov_local compute, bit for bit
+void launch_smooth_back(hipStream_t st, int sdim, const double* rec, const double* g,
+                        const double* pf, const ChainParamsHost* cps, const double* cin, double* X,
+                        double* h, double* vloc, double* gam, double* agg, double* bend, int64_t n,
+                        int L, int64_t nch, int nchains, int64_t xstride, int64_t sstride);
 int64_t vec_fix_blocks(int64_t n);
 void launch_vec_fix(hipStream_t st, int sdim, double* alpha, int64_t lda, const double* g,
                     int64_t gstride, const double* cin, int64_t sstride, int64_t mc,

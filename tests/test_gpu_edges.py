@@ -162,9 +162,6 @@ def test_gains_fast_path_bit_identical_to_general(kind, monkeypatch):
     chunk counts inside one block and across blocks, with short last chunks, large time gaps
     (negative stale steps) and short length scales."""
     rng = np.random.default_rng(11)
-    # the chains' logpdf at 256-step chunks (with few chains it picks shorter ones, which the fast
-    # kernel does not take)
-    monkeypatch.setenv("GPAR_CHAIN_L", "256")
     # 256 * 300 + 8: an even n, so every chain's row of Y (ldy = n) is 16-byte aligned and the
     # multi-block case really takes the fast kernel with data (an odd n misaligns row 1 and the
     # library falls back to the general kernel for both settings; ADVICE r05)

@@ -1,4 +1,4 @@
-# Bit-identity of the in-tree library against gpar-at-scale_amd/ab_old/ (a saved earlier build) on
+# Bit-identity of the in-tree library against gpar-at-scale_amd/ab_old/ (a saved earlier build; AB_OLD=<dir> for another) on
 # tools/lib_bitcheck.py's workload, then the GPU suite subset given as arguments and the default
 # bench line.   bash tools/gpu_bitcheck.sh <tag> [tests ...]
 # BITCHECK_TOLS="key_prefix=rtol ..." lets named outputs move within rounding (lib_bitcheck.py).
@@ -9,7 +9,7 @@ TAG=${1:?tag}
 shift
 OUT=gpurun_out/$TAG
 mkdir -p $OUT
-GPAR_HIP_LIB=$PWD/gpar-at-scale_amd/ab_old/libgparhip.so timeout -k 10 300 python tools/lib_bitcheck.py run $OUT/old.npz > $OUT/bit_old.txt 2>&1 || { echo OLD RUN FAILED; tail -20 $OUT/bit_old.txt; exit 1; }
+GPAR_HIP_LIB=${AB_OLD:-$PWD/gpar-at-scale_amd/ab_old}/libgparhip.so timeout -k 10 300 python tools/lib_bitcheck.py run $OUT/old.npz > $OUT/bit_old.txt 2>&1 || { echo OLD RUN FAILED; tail -20 $OUT/bit_old.txt; exit 1; }
 timeout -k 10 300 python tools/lib_bitcheck.py run $OUT/new.npz > $OUT/bit_new.txt 2>&1 || { echo NEW RUN FAILED; tail -20 $OUT/bit_new.txt; exit 1; }
 python tools/lib_bitcheck.py compare $OUT/old.npz $OUT/new.npz $BITCHECK_TOLS | tee $OUT/bitcheck.txt
 if [ $# -gt 0 ]; then
