@@ -580,7 +580,19 @@ void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<T
   int64_t mpmax = 0;
   for (const auto& p : P) mpmax = std::max(mpmax, p.mp);
   const bool early = c->dense_early && fit_pipelined(c, P) && split_active(c, P[0].n, mpmax);
+  // Unsplit batched rounds (the dtc / eeg configs, a rank's eeg shard): the same G-independent
+  // half on the dense stream (s_d), beside the round's gains, whitenings and Grams instead of
+  // after the last Gram -- a chain of latency-bound 64 x 64 launches (eeg shard 0/8, r06d trace:
+  // 2.2 ms of a 5.3 ms round boundary was the dense tail)
+  const bool early_side = !early && c->dense_early && P.size() > 1 && c->s_d != nullptr;
   DenseOut dn{};
+  if (early_side) {
+    HIPCHECK(hipEventRecord(c->ev_dn, c->stream));
+    HIPCHECK(hipStreamWaitEvent(c->s_d, c->ev_dn, 0));
+    OnStream on_(c, c->s_d);
+    dn = run_dense_pre(c, P, th, mpmax, false);
+    HIPCHECK(hipEventRecord(c->ev_dn, c->s_d));
+  }
   if (early) {
     // the Gram stream first follows everything queued on the context stream (host inputs' uploads,
     // the pseudo-input centres, the distance cache), then factors Kuu beside the round's gains
@@ -593,7 +605,8 @@ void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<T
   }
   GramOut go = run_gram_stage(c, P, th);
   if (gram_out) *gram_out = go;
-  if (!early) dn = run_dense_pre(c, P, th, go.ldg, false);
+  if (early_side) HIPCHECK(hipStreamWaitEvent(c->stream, c->ev_dn, 0));
+  else if (!early) dn = run_dense_pre(c, P, th, go.ldg, false);
   run_dense_post(c, P, go, dn);
   const int64_t nch = P[0].nch;
   std::vector<Finish2JobHost> fj(np);
