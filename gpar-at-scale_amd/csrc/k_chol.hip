@@ -122,6 +122,14 @@ __device__ __forceinline__ double rcp_pos(double p) {
   return fma(r, e, r);
 }
 
+// x of lane l, in every lane (two v_readlane_b32)
+__device__ __forceinline__ double bcast_lane(double x, int l) {
+  const long long v = __double_as_longlong(x);
+  const int lo = __builtin_amdgcn_readlane((int)v, l);
+  const int hi = __builtin_amdgcn_readlane((int)(v >> 32), l);
+  return __hiloint2double(hi, lo);
+}
+
 __global__ __launch_bounds__(256) void potrf_diag(const CholJob2* __restrict__ jobs, int64_t ld,
                                                   int kb, int want_t) {
   const CholJob2 jb = jobs[blockIdx.x];
@@ -130,37 +138,30 @@ __global__ __launch_bounds__(256) void potrf_diag(const CholJob2* __restrict__ j
   __shared__ double Ti[kNB * kSD];
   __shared__ double dinv[kNB], dkk[kNB];
   double* Ablk = jb.A + (int64_t)kb * kNB * ld + (int64_t)kb * kNB;
-  const int i = tid & 63, cls = tid >> 6;
-  double rv[16];
-#pragma unroll
-  for (int u = 0; u < 16; ++u) rv[u] = Ablk[(int64_t)i * ld + cls + 4 * u];
-  if (cls == 0) S[i * kSD] = rv[0];   // column 0 is final from the start
-  __syncthreads();
+  const int i = tid & 63;
   bool bad = false;
-  for (int k = 0; k < kNB - 1; ++k) {
-    double piv = S[k * kSD + k];
-    if (!(piv > 0.0)) { bad = true; piv = 1.0; }
-    const double c = (i > k) ? S[i * kSD + k] * rcp_pos(piv) : 0.0;
-    // loads unconditional (in bounds) and the predicate a select: a load inside the branch
-    // would be waited on one at a time
-    double sk[16];
+  // The elimination in one wave, lane i holding row i in registers: step k broadcasts the pivot
+  // and column k from their lanes (v_readlane, no LDS round trip, no workgroup barrier) and every
+  // lane updates its row.  The same operations in the same order as the r05 form (four waves,
+  // row i's 64 entries split over them, column k + 1 published through LDS behind a barrier per
+  // step: 63 barriers, 73 us per 64 x 64 block at the eeg shard, r06d trace), so L is unchanged
+  // bit for bit.  Entries above the diagonal take the updates too (never read).
+  if (tid < 64) {
+    double a[kNB];
 #pragma unroll
-    for (int u = 0; u < 16; ++u) sk[u] = S[(cls + 4 * u) * kSD + k];
+    for (int c = 0; c < kNB; ++c) a[c] = c <= i ? Ablk[(int64_t)i * ld + c] : 0.0;
 #pragma unroll
-    for (int u = 0; u < 16; ++u) {
-      const int j = cls + 4 * u;
-      const double nv = fma(-c, sk[u], rv[u]);
-      rv[u] = (j > k && j <= i) ? nv : rv[u];
+    for (int k = 0; k < kNB - 1; ++k) {
+      double piv = bcast_lane(a[k], k);
+      if (!(piv > 0.0)) { bad = true; piv = 1.0; }
+      const double c = (i > k) ? a[k] * rcp_pos(piv) : 0.0;
+#pragma unroll
+      for (int j = k + 1; j < kNB; ++j) a[j] = fma(-c, bcast_lane(a[k], j), a[j]);
     }
-    {
-      const int u1 = (k + 1) >> 2;   // publish column k + 1 (owner class (k + 1) & 3)
-      double v1 = rv[0];
 #pragma unroll
-      for (int u = 1; u < 16; ++u) v1 = (u == u1) ? rv[u] : v1;
-      if (cls == ((k + 1) & 3) && i >= k + 1) S[i * kSD + k + 1] = v1;
-    }
-    __syncthreads();
+    for (int c = 0; c < kNB; ++c) S[i * kSD + c] = a[c];
   }
+  __syncthreads();
   if (!(S[(kNB - 1) * kSD + kNB - 1] > 0.0)) bad = true;
   // scale: L_kk = sqrt(piv_k), L_ik = A_ik / L_kk
   if (tid < kNB) {
