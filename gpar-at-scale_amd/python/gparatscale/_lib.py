@@ -146,6 +146,8 @@ def load(path: str | None = None):
             "gpar_nm_result": (i32, [vp, dp, C.POINTER(C.c_double), C.POINTER(i32), C.POINTER(i32)]),
         })
         for name, (res, args) in sig.items():
+            if name == "gpar_debug_counter" and not hasattr(lib, name):
+                continue   # a diagnostic only: older builds (library A/B runs) lack it
             f = getattr(lib, name)
             f.restype = res
             f.argtypes = args
