@@ -208,18 +208,43 @@ __device__ __forceinline__ void elem_load(const double* __restrict__ p, Elem<D>&
 }
 
 // ---------------------------------------------------------------------------- phase 1
+// The chunk's aggregate element.  SUB lanes per chunk (SUB = 4 where the chains are too few to
+// fill the chip with one lane per chunk: a rank's 8-output eeg shard has 49 waves, the ssm
+// config's 16 chains one wave per SIMD, and each lane's 256 dependent steps then run at the
+// latency of its fp64 chain): lane q folds steps [q L / SUB, (q + 1) L / SUB) of the chunk and the
+// SUB partial elements are combined in time order through lane shuffles, (e0 e1)(e2 e3).
 template <int D>
+__device__ __forceinline__ void elem_shfl_down(const Elem<D>& e, int off, Elem<D>& o) {
+#pragma unroll
+  for (int i = 0; i < D; ++i)
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+      o.A[i][j] = __shfl_down(e.A[i][j], off, 64);
+      o.C[i][j] = __shfl_down(e.C[i][j], off, 64);
+      o.J[i][j] = __shfl_down(e.J[i][j], off, 64);
+    }
+}
+
+template <int D, int SUB>
 __global__ __launch_bounds__(256) void gains_phase1(const double* __restrict__ t, int64_t n,
                                                     int L, int64_t nch,
                                                     const ChainParams* __restrict__ cps,
                                                     const double* __restrict__ noise,
                                                     double* __restrict__ agg) {
-  const int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  static_assert(SUB == 1 || SUB == 4, "sub-lanes per chunk");
+  const int64_t gl = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+  const int64_t j = gl / SUB;
+  const int q = (int)(gl % SUB);
   const int p = blockIdx.y;
-  if (j >= nch) return;
+  if (SUB == 1 && j >= nch) return;
+  const bool live = j < nch;   // SUB > 1: every lane stays for the shuffles
   const ChainParams cp = cps[p];
-  const int64_t k0 = j * L;
-  const int64_t k1 = (k0 + L < n) ? k0 + L : n;
+  const int64_t jc = live ? j : 0;
+  const int64_t c0 = jc * L;
+  const int64_t c1 = (c0 + L < n) ? c0 + L : n;
+  const int64_t Ls = L / SUB;
+  const int64_t k0 = live ? (c0 + q * Ls < c1 ? c0 + q * Ls : c1) : c1;
+  const int64_t k1 = (SUB == 1) ? c1 : (k0 + Ls < c1 ? k0 + Ls : c1);
   Elem<D> acc, e;
   elem_identity(acc);   // identity (x) e == e exactly: one code path for every step
   double tprev = k0 > 0 ? t[k0 - 1] : 0.0;
@@ -233,6 +258,15 @@ __global__ __launch_bounds__(256) void gains_phase1(const double* __restrict__ t
     const double R = noise ? (rk < 0.0 ? cp.r : rk) : cp.r;
     step_elem_tau<D>(tau, k == 0, cp, R, e);
     elem_combine<D>(acc, e, acc);
+  }
+  if constexpr (SUB > 1) {
+#pragma unroll
+    for (int off = 1; off < SUB; off <<= 1) {
+      Elem<D> o;
+      elem_shfl_down(acc, off, o);
+      if ((q & (2 * off - 1)) == 0) elem_combine<D>(acc, o, acc);
+    }
+    if (q != 0 || !live) return;
   }
   elem_store<D>(agg + ((int64_t)p * nch + j) * (3 * D * D), acc);
 }
@@ -1051,11 +1085,7 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
   constexpr int VS = DP + 2;      // V tile row stride: conflict-free A-fragment reads
   constexpr int NKS = DP / 4;
   __shared__ __attribute__((aligned(16))) double vs[kMT * VS];
-  // rows of 66 doubles (528 B, 16-byte aligned): the flush reads a lane's column pair as one
-  // ds_read_b128, conflict-free; with 65 the pair was two ds_read_b64 whose lanes l and l + 16
-  // hit one bank (2-way; 16 % of the kernel's LDS cycles were bank conflicts, r05q PMC)
-  constexpr int XS = 66;
-  __shared__ __attribute__((aligned(16))) double xt[4][kMT][XS];
+  __shared__ __attribute__((aligned(16))) double xt[4][kMT][65];
   // the sub-tile's step rows {A_k (SD x SD), K_k (SD), rs_k, g_k (SD)}, 16 doubles each (fmac_row)
   constexpr int RK = SD * SD, RR = SD * SD + SD, RG = SD * SD + SD + 1;
   static_assert(RG + SD <= 16, "step row");
@@ -1145,8 +1175,10 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
     if (cw0 < mp && ntp == kMT) {   // all LDS reads first, then the 8 stores (no per-row branch)
       double2 v2[kMT / 2];
 #pragma unroll
-      for (int i = 0; i < kMT / 2; ++i)
-        v2[i] = *reinterpret_cast<const double2*>(&xt[wave][2 * i + fh][fc2]);
+      for (int i = 0; i < kMT / 2; ++i) {
+        v2[i].x = xt[wave][2 * i + fh][fc2];
+        v2[i].y = xt[wave][2 * i + fh][fc2 + 1];
+      }
 #pragma unroll
       for (int i = 0; i < kMT / 2; ++i)
         *reinterpret_cast<double2*>(beta + (ktp + 2 * i + fh) * ldb + cw0 + fc2) = v2[i];
@@ -1155,7 +1187,9 @@ __global__ __launch_bounds__(256, 2) void whiten_kfu_mfma(
       for (int i = 0; i < kMT / 2; ++i) {
         const int kk = 2 * i + fh;
         if (kk < ntp) {
-          const double2 v2 = *reinterpret_cast<const double2*>(&xt[wave][kk][fc2]);
+          double2 v2;
+          v2.x = xt[wave][kk][fc2];
+          v2.y = xt[wave][kk][fc2 + 1];
           *reinterpret_cast<double2*>(beta + (ktp + kk) * ldb + cw0 + fc2) = v2;
         }
       }
@@ -2537,7 +2571,13 @@ void launch_gains(hipStream_t st, int sdim, const double* t, int64_t n, int L, i
   const ChainParams* cps = reinterpret_cast<const ChainParams*>(cps_dev);
   dim3 grid((unsigned)((nch + 255) / 256), (unsigned)nchains);
   GPAR_DISPATCH_D(sdim, {
-    gains_phase1<DD><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, agg);
+    // four lanes per chunk below ~four waves per SIMD of chunks (gains_phase1)
+    if ((int64_t)nchains * nch < 4 * 1024 * 64) {
+      dim3 g4((unsigned)((4 * nch + 255) / 256), (unsigned)nchains);
+      gains_phase1<DD, 4><<<g4, 256, 0, st>>>(t, n, L, nch, cps, noise, agg);
+    } else {
+      gains_phase1<DD, 1><<<grid, 256, 0, st>>>(t, n, L, nch, cps, noise, agg);
+    }
     gains_phase2<DD><<<nchains, 256, 0, st>>>(nch, agg, pstart);
     // the fast phase 3 stages its inputs by 16-byte LDS-DMA: every input array 16-byte aligned
     // (GPAR_GAINS_FAST=0: the general kernel everywhere, for the fast path's bit-identity test)

@@ -11,7 +11,13 @@ import json
 import sys
 from collections import defaultdict
 
-N, M, D = 1_000_000, 512, 32
+import os
+
+# the probe's sizes (tools/pmc_passes.sh: the north shape; PMC_N / PMC_M / PMC_D for another, e.g.
+# the stress config's N = 1e7, M = 1024, tools/pmc_stress.sh)
+N = int(os.environ.get("PMC_N", 1_000_000))
+M = int(os.environ.get("PMC_M", 512))
+D = int(os.environ.get("PMC_D", 32))
 SIMDS = 1024
 
 
