@@ -52,15 +52,17 @@ StageBufs stage_bufs(gpar_ctx* c, int l, int64_t n, int64_t mpmax) {
 
 // The grouped Gram's per-output stage buffers: slot `slot` of a group, carry tags of stream lane
 // `lane` (its carry workspaces are reused output after output on that lane).
-static StageBufs stage_bufs_grp(gpar_ctx* c, int lane, int slot, int64_t n, int64_t mpmax) {
+static StageBufs stage_bufs_grp(gpar_ctx* c, int lane, int slot, int64_t n, int64_t mpmax,
+                                double* send = nullptr, double* cin = nullptr) {
   const int64_t nch = (n + kChunk - 1) / kChunk;
   const std::string sfx = "_g" + std::to_string(slot);
   StageBufs b;
   b.idx = lane;
   b.beta = ws<double>(c, "beta" + sfx, (size_t)(n + 16) * mpmax);
   b.alpha = ws<double>(c, "alpha" + sfx, (size_t)n);
-  b.send = ws<double>(c, "send" + sfx, (size_t)nch * (mpmax + 1) * 4);
-  b.cin = ws<double>(c, "cin" + sfx, (size_t)nch * (mpmax + 1) * 4);
+  // the carry's input / output: the group's shared arrays when its carries run batched
+  b.send = send ? send : ws<double>(c, "send" + sfx, (size_t)nch * (mpmax + 1) * 4);
+  b.cin = cin ? cin : ws<double>(c, "cin" + sfx, (size_t)nch * (mpmax + 1) * 4);
   b.hsum = ws<double>(c, "hsum" + sfx, (size_t)nch * (mpmax + 1) * 4);
   b.qv = ws<double>(c, "qv" + sfx, (size_t)nch * 4);
   return b;
@@ -117,8 +119,9 @@ void stage_whiten(gpar_ctx* c, const StageJob& j, const StageBufs& b) {
 
 // The short chain between a whitening and its Gram, on c->stream: alpha's chunk end states, the
 // chunk carry, vec_fix (alpha fix-up, the Gram's correction E_j = H_j + W_j C_j / 2 and q_j), the
-// beta tail (and the beta fix-up pass when fix_beta).
-void stage_post(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_beta) {
+// beta tail (and the beta fix-up pass when fix_beta).  In three parts so that the grouped Gram can
+// run the carries of a whole group in one batched launch set (stage_post_head / _tail).
+static void stage_post_head(gpar_ctx* c, const StageJob& j, const StageBufs& b) {
   const DevProblem& p = *j.p;
   const int64_t n = p.n, nch = p.nch;
   if (j.asend) {   // alpha's chunk end states -> column mp of the carry input
@@ -130,9 +133,11 @@ void stage_post(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_bet
                       0, p.mc, p.mp);
   }
   check_launch("whiten_vec");
-  run_carry(c, p.sdim, j.gi.phi, 0, b.send, b.cin, 0, nch, p.mc, p.mc, 1,
-            b.idx ? "fitc_1" : "fitc");
-  check_launch("carry");
+}
+
+static void stage_post_tail(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_beta) {
+  const DevProblem& p = *j.p;
+  const int64_t n = p.n;
   launch_vec_fix(c->stream, p.sdim, j.alpha, 0, j.gi.g, 0, b.cin, 0, p.mc, p.mp, n, kChunk, 1,
                  j.a2part, fix_beta ? nullptr : b.hsum, p.mp, b.qv);
   check_launch("vec_fix");
@@ -141,6 +146,15 @@ void stage_post(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_bet
     check_launch("beta_fix");
   }
   HIPCHECK(hipMemsetAsync(b.beta + (size_t)n * p.mp, 0, (size_t)16 * p.mp * sizeof(double), c->stream));
+}
+
+void stage_post(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_beta) {
+  const DevProblem& p = *j.p;
+  stage_post_head(c, j, b);
+  run_carry(c, p.sdim, j.gi.phi, 0, b.send, b.cin, 0, p.nch, p.mc, p.mc, 1,
+            b.idx ? "fitc_1" : "fitc");
+  check_launch("carry");
+  stage_post_tail(c, j, b, fix_beta);
 }
 
 // G = beta^T beta, r = beta^T alpha of j on c->stream, which may use `cus` CUs; side: the stream of
@@ -356,6 +370,13 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
       }
     double* part = ws<double>(c, "gram_part_grp", (size_t)gsz * pd);
     double* rpart = ws<double>(c, "gram_rpart_grp", (size_t)gsz * rd);
+    // shared gains (one grid; the outputs' transfers phi strided in one array): the group's chunk
+    // carries run as one batched launch set after its whitenings (r06: three small latency-bound
+    // launches per output were 0.8 ms of a rank's eeg round boundary, r06d trace)
+    const bool batch_post = shared;
+    const int64_t sstr = nch * (mpmax + 1) * 4;
+    double* send_grp = batch_post ? ws<double>(c, "send_grp", (size_t)gsz * sstr) : nullptr;
+    double* cin_grp = batch_post ? ws<double>(c, "cin_grp", (size_t)gsz * sstr) : nullptr;
     for (int g0 = 0, gi = 0; g0 < np; g0 += gsz, ++gi) {
       const int cnt = std::min(gsz, np - g0);
       const GramPlan plan = plan_of(cnt);
@@ -368,11 +389,13 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
       double work = 0.0;
       for (int k = 0; k < cnt; ++k) {
         const int i = g0 + k, lane = k & 1;
-        gb[k] = stage_bufs_grp(c, lane, k, n, mpmax);
+        gb[k] = batch_post ? stage_bufs_grp(c, lane, k, n, mpmax, send_grp + (size_t)k * sstr,
+                                            cin_grp + (size_t)k * sstr)
+                           : stage_bufs_grp(c, lane, k, n, mpmax);
         OnStream on_(c, lane ? c->side : base);
         const StageJob& j = job(i, gb[k]);
         stage_whiten(c, j, gb[k]);
-        stage_post(c, j, gb[k], false);
+        if (!batch_post) stage_post(c, j, gb[k], false);
         th_tab[k] = {gb[k].beta, j.alpha, gb[k].hsum, gb[k].cin, gb[k].qv,
                      part + (size_t)k * pd, rpart + (size_t)k * rd,
                      j.G, j.r};
@@ -380,6 +403,13 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
       }
       HIPCHECK(hipEventRecord(c->ev_join, c->side));
       HIPCHECK(hipStreamWaitEvent(base, c->ev_join, 0));
+      if (batch_post) {   // on the context stream, after both lanes' whitenings
+        for (int k = 0; k < cnt; ++k) stage_post_head(c, jobs[g0 + k], gb[k]);
+        run_carry(c, P[g0].sdim, gains[g0].phi, gplan.o.phistride, send_grp, cin_grp, sstr, nch,
+                  P[g0].mc, P[g0].mc, cnt, "fitc_grp");
+        check_launch("carry (grouped)");
+        for (int k = 0; k < cnt; ++k) stage_post_tail(c, jobs[g0 + k], gb[k], false);
+      }
       GramGroupPtrs* dtab = tab + (size_t)gi * gsz;
       h2d(c, dtab, th_tab.data(), (size_t)cnt);
       {
