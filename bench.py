@@ -58,8 +58,23 @@ CONFIGS = {
 # (SQ_VALU_MFMA_BUSY_CYCLES / SQ_INSTS_MFMA = 64, profiles/) x 2.4 GHz = 78.6 TF/s (AMD spec value)
 FP64_MFMA_PEAK_TFLOPS = 78.6
 HBM_PEAK_GBS = 8000.0
-# HBM bytes per launch from the PMC passes of this round's sources (tools/pmc_passes.sh, D = 32)
-PMC_FILE = "pmc_gram_whiten_r05.json"
+# HBM bytes per launch from the PMC passes of this round's sources (tools/pmc_passes.sh, D = 32),
+# else the newest earlier round's (the line names the file it used: roofline.traffic_source)
+PMC_FILE = "pmc_gram_whiten_r06.json"
+PMC_FALLBACK = "pmc_gram_whiten_r05.json"
+# the stress config's Gram traffic (tools/pmc_stress.sh: N = 1e7, M = 1024)
+PMC_STRESS_FILE = "pmc_gram_whiten_stress_r06.json"
+
+
+def pmc_traffic(names):
+    """(Gram bytes, whitening bytes, file) per launch from the first profiles/ PMC summary found."""
+    for name in names:
+        f = os.path.join(ROOT, "profiles", name)
+        if os.path.exists(f):
+            with open(f) as fh:
+                pj = json.load(fh)
+            return pj.get("hbm_bytes_per_launch"), pj.get("whiten_hbm_bytes_per_launch"), name
+    return None, None, None
 
 
 def log(*a):
@@ -703,13 +718,9 @@ def main():
         flops = float(n_eff) * M * (M + 1)       # N*M*(M+1) per Gram launch
         avg = gram_ms / max(gram_n, 1)
         achieved = gram_work / (gram_ms * 1e-3) / 1e12 if gram_n else None
-        traffic = wtraffic = None
-        pmc = os.path.join(ROOT, "profiles", PMC_FILE)   # tools/pmc_passes.sh at the north config
-        if args.config == "north" and os.path.exists(pmc):
-            with open(pmc) as f:
-                pj = json.load(f)
-            traffic = pj.get("hbm_bytes_per_launch")
-            wtraffic = pj.get("whiten_hbm_bytes_per_launch")
+        traffic = wtraffic = tsrc = None
+        if args.config == "north":   # tools/pmc_passes.sh at the north config
+            traffic, wtraffic, tsrc = pmc_traffic([PMC_FILE, PMC_FALLBACK])
         out = {
             # BASELINE.json's metric string (north), the same wording at the other configs' sizes
             "metric": "GPAR fit+predict wall-clock (ms) and pts\u00b7outputs/sec, "
@@ -744,7 +755,8 @@ def main():
                if args.rehearse else {}),
             "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": (achieved / FP64_MFMA_PEAK_TFLOPS) if achieved else None,
-                         "traffic": traffic, "kernel": "Gram beta^T beta + beta^T alpha, fp64 MFMA (v3: gram3_off + gram3_dg + gram3_corr + gram3_reduce per launch; lanes=2: gram2)",
+                         "traffic": traffic, "traffic_source": tsrc,
+                         "kernel": "Gram beta^T beta + beta^T alpha, fp64 MFMA (v3: gram3_off + gram3_dg + gram3_corr + gram3_reduce per launch; lanes=2: gram2)",
                          "note": "avg_ms spans one Gram launch (HIP events): gram3_off_kernel, then "
                                  "gram3_dg_kernel and gram3_reduce; gram3_corr_slim_kernel runs "
                                  "concurrently with gram3_off_kernel on a second stream (and with "
@@ -1021,6 +1033,7 @@ def stress_main(args):
         per_eval_ms = el / max(evals_rank, 1)
         # the whole stress job (every GPAR output, 50 evaluations each) projected from this rank's
         # per-evaluation time and the LPT loads of the sized cost model
+        stress_traffic, _, stress_tsrc = pmc_traffic([PMC_STRESS_FILE])
         loads = [sum(cost(p) for p in sh if p >= 2) for sh in shards]
         mine_load = loads[r_]
         proj_s = (el / 1e3) * (50.0 / EV) * max(loads) / mine_load if mine_load else None
@@ -1043,7 +1056,8 @@ def stress_main(args):
             "evaluations_per_step": evals_rank,
             "roofline": {"bound": "mfma", "achieved": gach, "peak": FP64_MFMA_PEAK_TFLOPS,
                          "unit": "TFLOP/s", "frac": gach / FP64_MFMA_PEAK_TFLOPS if gach else None,
-                         "traffic": None, "launches": gn, "avg_ms": gms / gn if gn else None,
+                         "traffic": stress_traffic, "traffic_source": stress_tsrc,
+                         "launches": gn, "avg_ms": gms / gn if gn else None,
                          "flops_per_launch": float(N) * M * (M + 1),
                          "kernel": "Gram beta^T beta + beta^T alpha, fp64 MFMA (gram3_off + gram3_dg "
                                    "+ gram3_corr + gram3_reduce), HIP events per launch"},

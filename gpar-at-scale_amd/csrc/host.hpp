@@ -90,6 +90,9 @@ struct gpar_ctx {
   // "gram_group": outputs per grouped Gram launch set in an unsplit batched fit of small problems
   // (run_gram_stage): 0 = off, >= 2 that many, 1 = off, -1 = auto (kGramGroupAuto below)
   int gram_group = -1;
+  // set by eval_dtc when the round's dense prefix runs on s_d: the round's first Gram waits for it
+  // (beside a Gram the latency-bound 64 x 64 launches slowed it 4.4 -> 5.3 ms at the eeg shard)
+  hipEvent_t gram_after = nullptr;
   // "fit_chunks": outputs per consecutive sub-batch of a gpar_fit whose distances the cache
   // cannot all hold at once (fit_impl): -1 = auto (unpipelined fits of outputs with D >= 17, the
   // stress config), 0 = off (one batch), k >= 1 = sub-batches of k outputs

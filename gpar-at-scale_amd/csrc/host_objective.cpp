@@ -164,6 +164,10 @@ void stage_gram(gpar_ctx* c, const StageJob& j, const StageBufs& b, bool fix_bet
                        bool one_per_cu, const std::string& part_sfx, hipStream_t side, int cus,
                        hipStream_t st_w, hipEvent_t ev_w, int w_frac32, int dg_rows_w) {
   const DevProblem& p = *j.p;
+  if (c->gram_after) {   // the round's dense prefix (eval_dtc) first
+    HIPCHECK(hipStreamWaitEvent(c->stream, c->gram_after, 0));
+    c->gram_after = nullptr;
+  }
   GramPlan plan = gram_plan(p.n, p.mp, one_per_cu, cus, st_w ? 256 : cus);
   const int w_items = st_w ? plan.ndg * plan.sdg * w_frac32 / 32 : 0;
   // dg_rows_w: the DG time splits that run on the whitening CUs take that many percent more rows
@@ -412,6 +416,10 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
       }
       GramGroupPtrs* dtab = tab + (size_t)gi * gsz;
       h2d(c, dtab, th_tab.data(), (size_t)cnt);
+      if (c->gram_after) {   // the round's dense prefix (eval_dtc) first
+        HIPCHECK(hipStreamWaitEvent(base, c->gram_after, 0));
+        c->gram_after = nullptr;
+      }
       {
         Timed tm_(c, "gram", work);   // flops of every beta^T beta of the group
         launch_gram_grouped(base, P[g0].sdim, plan, dtab, cnt, mpmax, n, P[g0].mc, kChunk, mpmax,
@@ -622,6 +630,7 @@ void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<T
     OnStream on_(c, c->s_d);
     dn = run_dense_pre(c, P, th, mpmax, false);
     HIPCHECK(hipEventRecord(c->ev_dn, c->s_d));
+    c->gram_after = c->ev_dn;
   }
   if (early) {
     // the Gram stream first follows everything queued on the context stream (host inputs' uploads,
@@ -635,7 +644,10 @@ void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<T
   }
   GramOut go = run_gram_stage(c, P, th);
   if (gram_out) *gram_out = go;
-  if (early_side) HIPCHECK(hipStreamWaitEvent(c->stream, c->ev_dn, 0));
+  if (early_side) {
+    c->gram_after = nullptr;   // (consumed by the first Gram; cleared if there was none)
+    HIPCHECK(hipStreamWaitEvent(c->stream, c->ev_dn, 0));
+  }
   else if (!early) dn = run_dense_pre(c, P, th, go.ldg, false);
   run_dense_post(c, P, go, dn);
   const int64_t nch = P[0].nch;

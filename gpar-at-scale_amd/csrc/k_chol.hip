@@ -135,7 +135,6 @@ __global__ __launch_bounds__(256) void potrf_diag(const CholJob2* __restrict__ j
   const CholJob2 jb = jobs[blockIdx.x];
   const int tid = threadIdx.x;
   __shared__ double S[kNB * kSD];
-  __shared__ double Ti[kNB * kSD];
   __shared__ double dinv[kNB], dkk[kNB];
   double* Ablk = jb.A + (int64_t)kb * kNB * ld + (int64_t)kb * kNB;
   const int i = tid & 63;
@@ -180,32 +179,36 @@ __global__ __launch_bounds__(256) void potrf_diag(const CholJob2* __restrict__ j
     if (c <= r) S[r * kSD + c] = v;
   }
   __syncthreads();
-  // T = L^-1 column by column: column j by the 4 lanes 4j..4j+3 of one wave (k-split dot
-  // products); only wave-level ordering is needed (a column never leaves its wave).
-  {
-    const int j = tid >> 2, q = tid & 3;
-    if (q == 0) Ti[j * kSD + j] = dinv[j];
-    __builtin_amdgcn_s_waitcnt(0xc07f);
-    __builtin_amdgcn_wave_barrier();
-    for (int r = 1; r < kNB; ++r) {
-      double acc = 0.0;
-      if (r > j)
-        for (int k = j + q; k < r; k += 4) acc = fma(S[r * kSD + k], Ti[k * kSD + j], acc);
-      acc += __shfl_xor(acc, 1, 64);
-      acc += __shfl_xor(acc, 2, 64);
-      if (r > j && q == 0) Ti[r * kSD + j] = -acc * dinv[r];
-      __builtin_amdgcn_s_waitcnt(0xc07f);
-      __builtin_amdgcn_wave_barrier();
+  // T = L^-1 by forward substitution in one wave, lane c holding column c in registers:
+  // T_rc = -(sum_{k<r} L_rk T_kc) / L_rr, the L_rk broadcast from LDS.  The dot product is split
+  // into four partial sums over k = c + q (mod 4), combined as (p0 + p1) + (p2 + p3) -- the r05
+  // form's four lanes per column and their two shuffles, so T is unchanged bit for bit -- but
+  // kept by k mod 4 (static registers; T_kc = 0 for k < c adds nothing) and relabelled per lane
+  // at the end of each row.  (r05: one row per step behind a wave barrier, each step's k loop a
+  // chain of dependent LDS reads: ~45 us of the 64 x 64 block.)
+  if (tid < kNB) {
+    const int c = tid, cr = c & 3;
+    double tc[kNB];
+#pragma unroll
+    for (int r = 0; r < kNB; ++r) {
+      double b4[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+      for (int k = 0; k < r; ++k) b4[k & 3] = fma(S[r * kSD + k], tc[k], b4[k & 3]);
+      // p_q = b4[(q + c) & 3]
+      const double p0 = cr == 0 ? b4[0] : cr == 1 ? b4[1] : cr == 2 ? b4[2] : b4[3];
+      const double p1 = cr == 0 ? b4[1] : cr == 1 ? b4[2] : cr == 2 ? b4[3] : b4[0];
+      const double p2 = cr == 0 ? b4[2] : cr == 1 ? b4[3] : cr == 2 ? b4[0] : b4[1];
+      const double p3 = cr == 0 ? b4[3] : cr == 1 ? b4[0] : cr == 2 ? b4[1] : b4[2];
+      const double acc = (p0 + p1) + (p2 + p3);
+      tc[r] = r > c ? -acc * dinv[r] : (r == c ? dinv[r] : 0.0);
     }
-  }
-  __syncthreads();
-  double* Td = jb.Td + (int64_t)kb * kNB * kNB;
-  double* Tb = want_t ? jb.T + (int64_t)kb * kNB * ld + (int64_t)kb * kNB : nullptr;
-  for (int e = tid; e < kNB * kNB; e += 256) {
-    const int r = e >> 6, c = e & 63;
-    const double v = (c <= r) ? Ti[r * kSD + c] : 0.0;
-    Td[e] = v;
-    if (Tb) Tb[(int64_t)r * ld + c] = v;
+    double* Td = jb.Td + (int64_t)kb * kNB * kNB;
+    double* Tb = want_t ? jb.T + (int64_t)kb * kNB * ld + (int64_t)kb * kNB : nullptr;
+#pragma unroll
+    for (int r = 0; r < kNB; ++r) {
+      Td[r * kNB + c] = tc[r];
+      if (Tb) Tb[(int64_t)r * ld + c] = tc[r];
+    }
   }
   if (bad && tid == 0) *jb.status = 1;
 }
