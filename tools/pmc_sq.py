@@ -73,7 +73,8 @@ def load(d):
 
 
 def main(root):
-    res = {"source": "tools/pmc_passes.sh: rocprofv3 --pmc passes over tools/gram_probe.py "
+    res = {"source": os.environ.get("PMC_SOURCE") or
+                     "tools/pmc_passes.sh: rocprofv3 --pmc passes over tools/gram_probe.py "
                      f"--fit --evals 4 --batch 3 (N={N}, M={M}, D={D}; the batched fit's CU-split "
                      "Gram stage; the whitening reads the fit's distance cache: whiten_kfu_d2x2); "
                      "per-launch values: counters summed over every dispatch of the family, divided "

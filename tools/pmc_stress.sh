@@ -14,4 +14,4 @@ run() {  # name, counters...
 run sq1 SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_MFMA SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_VALU GRBM_GUI_ACTIVE
 run fetch FETCH_SIZE
 run write WRITE_SIZE
-PMC_N=10000000 PMC_M=1024 PMC_D=8 python3 tools/pmc_sq.py $OUT > $OUT/summary.json && cat $OUT/summary.json
+PMC_SOURCE="tools/pmc_stress.sh: rocprofv3 --pmc passes over tools/gram_probe.py --n 10000000 --m 1024 --d 8 --evals 2 (two objective evaluations of one output at the stress config's N and M, whole chip; the whitening is the fused kernel at D = 8, its algorithmic bytes below assume the cached form); " PMC_N=10000000 PMC_M=1024 PMC_D=8 python3 tools/pmc_sq.py $OUT > $OUT/summary.json && cat $OUT/summary.json
