@@ -139,23 +139,26 @@ __global__ __launch_bounds__(256) void potrf_diag(const CholJob2* __restrict__ j
   double* Ablk = jb.A + (int64_t)kb * kNB * ld + (int64_t)kb * kNB;
   const int i = tid & 63;
   bool bad = false;
-  // The elimination in one wave, lane i holding row i in registers: step k broadcasts the pivot
-  // and column k from their lanes (v_readlane, no LDS round trip, no workgroup barrier) and every
-  // lane updates its row.  The same operations in the same order as the r05 form (four waves,
-  // row i's 64 entries split over them, column k + 1 published through LDS behind a barrier per
-  // step: 63 barriers, 73 us per 64 x 64 block at the eeg shard, r06d trace), so L is unchanged
-  // bit for bit.  Entries above the diagonal take the updates too (never read).
+  // The elimination in one wave, lane i holding row i in registers: at step k every lane
+  // publishes its column-k entry to LDS (one contiguous ds_write) and reads the pivot and the
+  // column back as broadcasts -- a wave's LDS operations complete in order, so no barrier -- and
+  // updates its row.  The same operations in the same order as the r05 form (four waves, row i's
+  // 64 entries split over them, column k + 1 published through LDS behind a workgroup barrier
+  // per step: 63 barriers, 71 us per 64 x 64 block, r06l probe; v_readlane broadcasts, 50 us),
+  // so L is unchanged bit for bit.  Entries above the diagonal take the updates too (never read).
+  __shared__ double colk[kNB];
   if (tid < 64) {
     double a[kNB];
 #pragma unroll
     for (int c = 0; c < kNB; ++c) a[c] = c <= i ? Ablk[(int64_t)i * ld + c] : 0.0;
 #pragma unroll
     for (int k = 0; k < kNB - 1; ++k) {
-      double piv = bcast_lane(a[k], k);
+      colk[i] = a[k];
+      double piv = colk[k];
       if (!(piv > 0.0)) { bad = true; piv = 1.0; }
       const double c = (i > k) ? a[k] * rcp_pos(piv) : 0.0;
 #pragma unroll
-      for (int j = k + 1; j < kNB; ++j) a[j] = fma(-c, bcast_lane(a[k], j), a[j]);
+      for (int j = k + 1; j < kNB; ++j) a[j] = fma(-c, colk[j], a[j]);
     }
 #pragma unroll
     for (int c = 0; c < kNB; ++c) S[i * kSD + c] = a[c];
@@ -379,30 +382,63 @@ __global__ __launch_bounds__(256) void finish2_kernel(const Finish2Job* __restri
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int mp = nb * kNB;
   __shared__ double b[2048], w[2048], red[4][4];
-  for (int row = wave; row < mp; row += 4) {
-    double s = 0.0;
-    for (int k = lane; k <= row; k += 64) s = fma(jb.Tu[(int64_t)row * ld + k], jb.r[k], s);
-    s = wave_sum(s);
-    if (lane == 0) b[row] = s;
+  // b = T_u r: groups of 16 rows per wave, lanes along k, 16 independent loads in flight per lane
+  // (one row at a time, each row's loads then its reduction, was a chain of HBM latencies)
+  for (int g = wave; g < mp / 16; g += 4) {
+    double s16[16];
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) s16[rr] = 0.0;
+    const int kcn = (16 * g + 15) / kNB + 1;
+    for (int kc = 0; kc < kcn; ++kc) {
+      const int k = kc * kNB + lane;
+      const double rk = jb.r[k];
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) {
+        const int row = 16 * g + rr;
+        const double tv = jb.Tu[(int64_t)row * ld + k];
+        s16[rr] = fma(k <= row ? tv : 0.0, rk, s16[rr]);
+      }
+    }
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) {
+      const double v = wave_sum(s16[rr]);
+      if (lane == 0) b[16 * g + rr] = v;
+    }
   }
   __syncthreads();
   __shared__ double part[kNB];
   __shared__ double Tds[kNB * kSD];
+  __shared__ double partq[4][64];
+  // Forward solve L_lam w = b block by block: part = b_I - sum_{J<I} L_IJ w_J, then w_I = Td_I part.
+  // Each wave takes 16 of the block's rows with its lanes along k (coalesced 512-byte row segments,
+  // 16 independent loads in flight per lane) and reduces them across the lanes; Td_I's product
+  // splits k over the four waves.  (r05: four threads per row walked k with stride 4, each step a
+  // dependent global load: 0.31 ms per round of 8 outputs at the eeg shard, r06i trace.)
   for (int I = 0; I < nb; ++I) {
     const int row = tid & 63, q = tid >> 6;
-    double s = 0.0;
-    for (int k = q; k < I * kNB; k += 4) s = fma(jb.Llam[(int64_t)(I * kNB + row) * ld + k], w[k], s);
-    __shared__ double partq[4][64];
-    partq[q][row] = s;
-    __syncthreads();
-    if (q == 0) part[row] = b[I * kNB + row] - (partq[0][row] + partq[1][row] + partq[2][row] + partq[3][row]);
-    __syncthreads();
-    if (q == 0) {
-      double acc = 0.0;
-      const double* Td = jb.Tdl + (int64_t)I * kNB * kNB;
-      for (int k = 0; k <= row; ++k) acc = fma(Td[row * kNB + k], part[k], acc);
-      w[I * kNB + row] = acc;
+    const double* Td = jb.Tdl + (int64_t)I * kNB * kNB;
+    for (int e = tid; e < kNB * kNB; e += 256) Tds[(e >> 6) * kSD + (e & 63)] = Td[e];
+    double s16[16];
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) s16[rr] = 0.0;
+    const double* L0 = jb.Llam + (int64_t)(I * kNB + 16 * wave) * ld;
+    for (int kc = 0; kc < I; ++kc) {
+      const int k = kc * kNB + lane;
+      const double wk = w[k];
+#pragma unroll
+      for (int rr = 0; rr < 16; ++rr) s16[rr] = fma(L0[(int64_t)rr * ld + k], wk, s16[rr]);
     }
+#pragma unroll
+    for (int rr = 0; rr < 16; ++rr) {
+      const double v = wave_sum(s16[rr]);
+      if (lane == 0) part[16 * wave + rr] = b[I * kNB + 16 * wave + rr] - v;
+    }
+    __syncthreads();
+    double acc = 0.0;
+    for (int k = q; k <= row; k += 4) acc = fma(Tds[row * kSD + k], part[k], acc);
+    partq[q][row] = acc;
+    __syncthreads();
+    if (q == 0) w[I * kNB + row] = (partq[0][row] + partq[1][row]) + (partq[2][row] + partq[3][row]);
     __syncthreads();
   }
   if (jb.me) {
