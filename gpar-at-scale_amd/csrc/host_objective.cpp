@@ -360,8 +360,11 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     const hipStream_t base = c->stream;
     const int ngroups = (np + gsz - 1) / gsz;
     auto* tab = ws<GramGroupPtrs>(c, "gram_grp_tab", (size_t)ngroups * gsz);
+    // (A/B hook, r06: GPAR_GRP_CUS_PCT scales the per-output CU share of the plan)
+    const char* ep = std::getenv("GPAR_GRP_CUS_PCT");
+    const int pct = ep ? std::atoi(ep) : 100;
     auto plan_of = [&](int cnt) {
-      const int cus = std::max(256 / cnt, 8);
+      const int cus = std::max(256 * pct / 100 / cnt, 8);
       return gram_plan(n, mpmax, false, cus, cus);
     };
     // the partials, sized once for every group's plan (no buffer may move under a running launch)
