@@ -72,10 +72,13 @@ static StageBufs stage_bufs_grp(gpar_ctx* c, int lane, int slot, int64_t n, int6
 // Gram (N Mp^2 <= kGramGroupMaxWork) has too few (group, split) items to fill the chip without
 // splitting time so finely that its partial sums and chunk correction cost as much as the GEMM
 // (N = 1e5, M = 256: 0.22 ms per launch against 0.084 ms of MFMA work, r05i); grouped, the same
-// items come from several outputs with 1/g of the time splits each.
+// items come from several outputs with 1/g of the time splits each.  Groups of 8 (r06, eeg at
+// N = 1e5, M = 512, 64 outputs, one box: g = 4 2413, 6 3366, 8 2411, 12 2883, 16 2533 ms per job;
+// sizes that leave noff * soff off a multiple of 8 lose the XCD deal's balance).
 constexpr double kGramGroupMaxWork = 5e10;
-constexpr int kGramGroupAuto = 16;
+constexpr int kGramGroupAuto = 8;
 constexpr int64_t kGramGroupMaxBytes = (int64_t)24 << 30;   // the group's beta buffers
+constexpr int64_t kGrpMinRows = 4096;   // rows per OFF workgroup below which the share stays 1/cnt
 static int gram_group_size(gpar_ctx* c, const std::vector<DevProblem>& P, int64_t n,
                            int64_t mpmax, bool fix_beta, int nlanes, bool split_pipe) {
   const int np = (int)P.size();
@@ -360,11 +363,14 @@ GramOut run_gram_stage(gpar_ctx* c, const std::vector<DevProblem>& P,
     const hipStream_t base = c->stream;
     const int ngroups = (np + gsz - 1) / gsz;
     auto* tab = ws<GramGroupPtrs>(c, "gram_grp_tab", (size_t)ngroups * gsz);
-    // (A/B hook, r06: GPAR_GRP_CUS_PCT scales the per-output CU share of the plan)
-    const char* ep = std::getenv("GPAR_GRP_CUS_PCT");
-    const int pct = ep ? std::atoi(ep) : 100;
+    // The per-output CU share: 256 / cnt, doubled while the OFF workgroups keep >= kGrpMinRows
+    // rows each (twice the split workgroups: the eeg shard's group of 8 at N = 1e5, M = 512 went
+    // 4.46 -> 3.81 ms per Gram, OFF 10000 -> 4762 rows; dtc's 1563-row OFF slices lose 13 % when
+    // halved again: per-workgroup prologue and more partials to reduce)
     auto plan_of = [&](int cnt) {
-      const int cus = std::max(256 * pct / 100 / cnt, 8);
+      const int cus = std::max(256 / cnt, 8);
+      const GramPlan p2 = gram_plan(n, mpmax, false, 2 * cus, 2 * cus);
+      if (p2.noff > 0 && p2.rows_off >= kGrpMinRows) return p2;
       return gram_plan(n, mpmax, false, cus, cus);
     };
     // the partials, sized once for every group's plan (no buffer may move under a running launch)

@@ -178,7 +178,7 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *   "gram_group"    outputs per grouped Gram of an unsplit batched fit: the group's outputs whiten
  *                   over two streams into buffers of their own and one set of Gram launches covers
  *                   them all (grid y = output), each with 1/g of the time splits; -1 (default) =
- *                   auto: groups of 16 when one output's N Mp^2 <= 5e10 (the dtc / eeg configs),
+ *                   auto: groups of 8 when one output's N Mp^2 <= 5e10 (the dtc / eeg configs),
  *                   0 = per-output Grams; a plan like dg_rows_w (G's summation grouping: last bits)
  *   "fit_chunks"    outputs per consecutive sub-batch of a gpar_fit whose outputs' distances the
  *                   cache cannot hold all at once: each sub-batch computes its distances once
