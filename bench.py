@@ -897,7 +897,7 @@ def main():
             if "roofline" in out and out["roofline"]:
                 out["roofline"].update(
                     kernel="chains_logpdf: gains_phase1 + gains_phase2 + gains_phase3 (moments) + "
-                           "the carry + chain_lml_mom, one HIP-event span per NM round",
+                           "chain_carry_lml (the carry and the value), one HIP-event span per NM round",
                     bytes="8 N (t) + 8 N per active chain (y) per launch; the per-chunk outputs "
                           "(~0.7 B per step and chain) not counted")
             if out.get("roofline_smooth"):

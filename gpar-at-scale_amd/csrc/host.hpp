@@ -23,6 +23,7 @@
 
 #include "launch.hpp"
 #include "nelder_mead.hpp"
+#include "nm_dev.hpp"
 
 namespace gpar {
 struct PredPrep;
@@ -97,6 +98,10 @@ struct gpar_ctx {
   // cannot all hold at once (fit_impl): -1 = auto (unpipelined fits of outputs with D >= 17, the
   // stress config), 0 = off (one batch), k >= 1 = sub-batches of k outputs
   int fit_chunks = -1;
+  // "device_nm": the chains fit (gpar_sde_predictions) steps its Nelder-Mead machines on the
+  // device between rounds (1), or on the host after each round's values come back (0; also any
+  // fit with a wall-clock time limit)
+  int device_nm = 1;
   // "dg_rows_w": percent more rows per DG split on the whitening CUs (fewer on the Gram CUs);
   // kDgRowsAuto: +40 in the round-by-round fit, where the whitening side (3.19 ms whitening since
   // the DPP step rows, r05r) has time to spare and the Gram CUs' side sets the span (north, same

@@ -86,7 +86,8 @@ static int set_cu_split(gpar_ctx* c, int w, bool forced) {
 static constexpr const char* kScheduleKnobs[] = {"overlap", "overlap_group", "predict_fused",
                                                   "qu_batch", "dense_early", "predict_lanes",
                                                   "serialize", "post_gram", "compact_rec",
-                                                  "dg_rows_w", "gram_group", "fit_chunks"};
+                                                  "dg_rows_w", "gram_group", "fit_chunks",
+                                                  "device_nm"};
 
 // gpar_ctx_set_schedule / gpar_ctx_get_schedule (GPAR_ERR_ARG: unknown knob or value).
 static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
@@ -115,6 +116,10 @@ static int set_schedule(gpar_ctx* c, const std::string& k, int v) {
   else if (k == "fit_chunks") {
     if (v < -1 || v > 4096) return GPAR_ERR_ARG;
     c->fit_chunks = v;
+  }
+  else if (k == "device_nm") {
+    if (v < 0 || v > 1) return GPAR_ERR_ARG;
+    c->device_nm = v;
   }
   else if (k == "post_gram") {
     if (v < -1 || v > 1) return GPAR_ERR_ARG;
@@ -148,6 +153,7 @@ static int get_schedule(const gpar_ctx* c, const std::string& k, int32_t* v) {
   else if (k == "dg_rows_w") *v = c->dg_rows_w;
   else if (k == "gram_group") *v = c->gram_group;
   else if (k == "fit_chunks") *v = c->fit_chunks;
+  else if (k == "device_nm") *v = c->device_nm;
   else if (k == "predict_lanes") *v = c->predict_lanes;
   else if (k == "serialize") *v = c->serialize;
   else return GPAR_ERR_ARG;

@@ -7,6 +7,46 @@ namespace gpar {
 // logpdf of independent LGSSM chains sharing t (device pointers; ys: each chain's data vector).
 // Timed "chains_logpdf": algorithmic bytes 8 n (t, once) + 8 n per chain (y); the per-chunk
 // outputs (about 0.7 bytes per step and chain) are not counted.
+// One pass: the gains recursion filters each chain's y from zero per chunk and keeps, per chunk,
+// sum log S_k and the moments of the chunk-local alpha against the fix-up rows (no per-step
+// record, fix-up row or alpha reaches HBM: t and y are read, 32 + 96 bytes per chunk written);
+// the carry gives each chunk's incoming state and sum alpha_k^2 follows from the moments (r05;
+// before, the gains wrote 160 bytes per step and chain and whiten_vec / vec_fix read them back).
+// The plan uploads the chain parameters and sets up the workspace; each launch is one round into
+// dl (device, one value per chain).
+struct ChainsLml {
+  GainsPlan gp;
+  double *send = nullptr, *mom = nullptr, *dl = nullptr;
+  int sdim = 0, nchains = 0;
+  int64_t n = 0, nch = 0;
+};
+
+static ChainsLml plan_chains_lml(gpar_ctx* c, const std::vector<const double*>& ys, int64_t n,
+                                 const double* t, int sdim,
+                                 const std::vector<ChainParamsHost>& cps) {
+  ChainsLml q;
+  q.sdim = sdim;
+  q.nchains = (int)ys.size();
+  q.n = n;
+  q.nch = (n + kChunk - 1) / kChunk;
+  q.send = ws<double>(c, "chain_send", (size_t)q.nchains * q.nch * 4);
+  q.mom = ws<double>(c, "chain_mom", (size_t)q.nchains * q.nch * kGainsMomStride);
+  q.dl = ws<double>(c, "chain_lml", q.nchains);
+  q.gp = plan_gains(c, sdim, t, n, cps, nullptr, false, "chain", &ys, nullptr, q.send, false,
+                    q.mom);
+  return q;
+}
+
+static void launch_chains_lml(gpar_ctx* c, const ChainsLml& q, NmDev<3>* nm = nullptr,
+                              int* active = nullptr) {
+  Timed tm_(c, "chains_logpdf", 8.0 * (double)q.n * (1.0 + q.nchains));
+  q.gp.launch(c->stream, 0, q.nchains);
+  const GainsOut& g = q.gp.o;
+  launch_chain_carry_lml(c->stream, q.sdim, g.phi, g.phistride, q.send, q.nch * kSStride, g.logs,
+                         q.mom, q.nch, q.n, q.nchains, q.dl, nm, q.gp.dcps, active);
+  check_launch("chains_logpdf");
+}
+
 void chains_logpdf(gpar_ctx* c, const std::vector<const double*>& ys, int64_t n, const double* t,
                    int sdim, const double* theta, double* lml) {
   const int nchains = (int)ys.size();
@@ -16,31 +56,109 @@ void chains_logpdf(gpar_ctx* c, const std::vector<const double*>& ys, int64_t n,
     ARGCHECK(l > 0 && pv > 0 && ns > 0, "theta entries must be positive");
     cps[i] = {1.0 / l, l, pv * pv, ns * ns};
   }
-  const int64_t nch = (n + kChunk - 1) / kChunk;
-  // one pass: the gains recursion filters each chain's y from zero per chunk and keeps, per chunk,
-  // sum log S_k and the moments of the chunk-local alpha against the fix-up rows (no per-step
-  // record, fix-up row or alpha reaches HBM: t and y are read, 32 + 96 bytes per chunk written);
-  // the carry gives each chunk's incoming state and sum alpha_k^2 follows from the moments
-  // (r05; before, the gains wrote 160 bytes per step and chain and whiten_vec / vec_fix read them
-  // back)
-  double* send = ws<double>(c, "chain_send", (size_t)nchains * nch * 4);
-  double* cin = ws<double>(c, "chain_cin", (size_t)nchains * nch * 4);
-  double* mom = ws<double>(c, "chain_mom", (size_t)nchains * nch * kGainsMomStride);
-  double* dl = ws<double>(c, "chain_lml", nchains);
-  GainsPlan gp = plan_gains(c, sdim, t, n, cps, nullptr, false, "chain", &ys, nullptr, send, false,
-                            mom);
-  {
-    Timed tm_(c, "chains_logpdf", 8.0 * (double)n * (1.0 + nchains));
-    gp.launch(c->stream, 0, nchains);
-    const GainsOut& g = gp.o;
-    run_carry(c, sdim, g.phi, g.phistride, send, cin, nch * 4, nch, 1, 1, nchains, "chainc");
-    launch_chain_lml_mom(c->stream, sdim, g.logs, mom, cin, nch, n, nchains, dl);
-    check_launch("chains_logpdf");
-  }
-  d2h(c, lml, dl, nchains);
+  const ChainsLml q = plan_chains_lml(c, ys, n, t, sdim, cps);
+  launch_chains_lml(c, q);
+  d2h(c, lml, q.dl, nchains);
   sync(c);
 }
 
+// The chains' Nelder-Mead fit with the machines on the device (nm_dev.hpp): every round's logpdf
+// launches queue on the stream in batches of kNmBatch rounds, the last of them (chain_carry_lml)
+// stepping each chain's machine; the host reads one batch behind which machines still run (the last batch
+// of a fit that ends on g_tol or its iteration cap is evaluated and discarded).  The rounds
+// evaluate every chain (the host loop packs the running ones): a finished machine ignores its
+// values.  log_theta0 / theta: nchains x 3 (packed, then unpacked, as the host loop).
+constexpr int kNmBatch = 8;
+
+static void fit_chains_device(gpar_ctx* c, int nchains, int64_t n, const double* t,
+                              const double* y, int64_t ldy, int sdim, const double* log_theta0,
+                              const gpar_fit_options& o, double* theta) {
+  std::vector<NmDev<3>> hs(nchains);
+  bool any = false;
+  for (int i = 0; i < nchains; ++i) {
+    nm_init(hs[i], log_theta0 + 3 * i, o.max_evals, o.max_iterations, o.g_tol);
+    any = any || hs[i].st != NmDev<3>::Done;
+  }
+  if (any) {
+    // round 0's parameters as the host loop sets them
+    std::vector<ChainParamsHost> cps(nchains);
+    std::vector<const double*> ys(nchains);
+    for (int i = 0; i < nchains; ++i) {
+      const double l = unpack(hs[i].pending[0]), pv = unpack(hs[i].pending[1]),
+                   ns = unpack(hs[i].pending[2]);
+      cps[i] = {1.0 / l, l, pv * pv, ns * ns};
+      ys[i] = y + (size_t)i * ldy;
+    }
+    const ChainsLml q = plan_chains_lml(c, ys, n, t, sdim, cps);
+    auto* dnm = ws<NmDev<3>>(c, "nm_dev", nchains);
+    h2d(c, dnm, hs.data(), nchains);
+    int* dact = ws<int>(c, "nm_active", nchains);
+    int* hact = nullptr;
+    HIPCHECK(hipHostMalloc((void**)&hact, 2 * (size_t)nchains * sizeof(int), hipHostMallocDefault));
+    std::unique_ptr<int, void (*)(int*)> hact_(hact, [](int* p) { (void)hipHostFree(p); });
+    hipEvent_t ev[2];
+    HIPCHECK(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming));
+    HIPCHECK(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming));
+    struct Evs {
+      hipEvent_t* e;
+      ~Evs() { (void)hipEventDestroy(e[0]); (void)hipEventDestroy(e[1]); }
+    } evs_{ev};
+    const int64_t cap = o.max_evals > 0 ? (int64_t)o.max_evals : INT64_MAX;
+    int64_t r = 0;
+    for (int k = 0; r < cap; ++k) {
+      const int64_t nb = std::min<int64_t>(kNmBatch, cap - r);
+      for (int64_t b = 0; b < nb; ++b) launch_chains_lml(c, q, dnm, dact);
+      r += nb;
+      HIPCHECK(hipMemcpyAsync(hact + (k & 1) * nchains, dact, nchains * sizeof(int),
+                              hipMemcpyDeviceToHost, c->stream));
+      HIPCHECK(hipEventRecord(ev[k & 1], c->stream));
+      if (k >= 1) {
+        HIPCHECK(hipEventSynchronize(ev[(k - 1) & 1]));
+        const int* a = hact + ((k - 1) & 1) * nchains;
+        if (std::none_of(a, a + nchains, [](int x) { return x != 0; })) break;
+      }
+    }
+    d2h(c, hs.data(), dnm, nchains);
+    sync(c);
+  }
+  for (int i = 0; i < nchains; ++i)
+    for (int q = 0; q < 3; ++q) theta[3 * i + q] = unpack(hs[i].x_min[q]);
+}
+
+// The same fit with the machines on the host (NelderMead), one round trip per round: the running
+// chains' values come back, each machine steps, the next round's parameters go up.
+static void fit_chains_host(gpar_ctx* c, int nchains, int64_t n, const double* t, const double* y,
+                            int64_t ldy, int sdim, const double* log_theta0,
+                            const gpar_fit_options& o, double* theta) {
+  std::vector<NelderMead> nm;
+  nm.reserve(nchains);
+  for (int i = 0; i < nchains; ++i)
+    nm.emplace_back(std::vector<double>(log_theta0 + 3 * i, log_theta0 + 3 * i + 3), o.max_evals,
+                    o.max_iterations, o.g_tol, o.time_limit);
+  while (true) {
+    std::vector<int> act;
+    for (int i = 0; i < nchains; ++i)
+      if (!nm[i].done()) act.push_back(i);
+    if (act.empty()) break;
+    // the active chains' own data columns (no copy into a packed block)
+    std::vector<double> th(3 * act.size());
+    std::vector<const double*> ys(act.size());
+    for (size_t a = 0; a < act.size(); ++a) {
+      const auto& x = nm[act[a]].ask();
+      for (int q = 0; q < 3; ++q) th[3 * a + q] = unpack(x[q]);
+      ys[a] = y + (size_t)act[a] * ldy;
+    }
+    std::vector<double> lml(act.size());
+    chains_logpdf(c, ys, n, t, sdim, th.data(), lml.data());
+    for (size_t a = 0; a < act.size(); ++a) {
+      double f = -lml[a];
+      if (!std::isfinite(f)) f = INFINITY;
+      nm[act[a]].tell(f);
+    }
+  }
+  for (int i = 0; i < nchains; ++i)
+    for (int q = 0; q < 3; ++q) theta[3 * i + q] = unpack(nm[i].x_min()[q]);
+}
 
 // --------------------------------------------------------------------------- temporal chains: smoothing
 // Smoothed marginals of f for chains sharing the grid t (device pointers): mean = y - R Sigma^-1 y,
@@ -191,35 +309,12 @@ int32_t gpar_sde_predictions(gpar_ctx* ctx, int32_t nchains, int64_t n, const do
     dt = tt; dy = yy; dts = ts; ldyd = n;
   }
   // ---- NM fit of (l, process_var, noise_sigma) per chain on -logpdf (temporal_gp_inference.jl:69-82)
-  std::vector<NelderMead> nm;
-  nm.reserve(nchains);
-  for (int i = 0; i < nchains; ++i)
-    nm.emplace_back(std::vector<double>(log_theta0 + 3 * i, log_theta0 + 3 * i + 3), o.max_evals,
-                    o.max_iterations, o.g_tol, o.time_limit);
-  while (true) {
-    std::vector<int> act;
-    for (int i = 0; i < nchains; ++i)
-      if (!nm[i].done()) act.push_back(i);
-    if (act.empty()) break;
-    // the active chains' own data columns (no copy into a packed block)
-    std::vector<double> th(3 * act.size());
-    std::vector<const double*> ys(act.size());
-    for (size_t a = 0; a < act.size(); ++a) {
-      const auto& x = nm[act[a]].ask();
-      for (int q = 0; q < 3; ++q) th[3 * a + q] = unpack(x[q]);
-      ys[a] = dy + (size_t)act[a] * ldyd;
-    }
-    std::vector<double> lml(act.size());
-    chains_logpdf(ctx, ys, n, dt, sdim, th.data(), lml.data());
-    for (size_t a = 0; a < act.size(); ++a) {
-      double f = -lml[a];
-      if (!std::isfinite(f)) f = INFINITY;
-      nm[act[a]].tell(f);
-    }
-  }
   std::vector<double> theta(3 * nchains);
-  for (int i = 0; i < nchains; ++i)
-    for (int q = 0; q < 3; ++q) theta[3 * i + q] = theta_out[3 * i + q] = unpack(nm[i].x_min()[q]);
+  if (ctx->device_nm && !(o.time_limit > 0))
+    fit_chains_device(ctx, nchains, n, dt, dy, ldyd, sdim, log_theta0, o, theta.data());
+  else
+    fit_chains_host(ctx, nchains, n, dt, dy, ldyd, sdim, log_theta0, o, theta.data());
+  for (int i = 0; i < 3 * nchains; ++i) theta_out[i] = theta[i];
   // ---- merged grid: y* = y (train) / 0 (test), R = sigma_c^2 (train, -1 flag) / 1e10 (test)
   const int64_t nt = n + n_star;
   double* tm = ws<double>(ctx, "sp_tm", nt);

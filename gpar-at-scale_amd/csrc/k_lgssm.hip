@@ -18,6 +18,7 @@
 //    (carry_kernel), and alpha_k(true) = alpha_k(local) + g_k . c_chunk (applied by the
 //    consumer: vec_fix_kernel here, the Gram loader in k_gram.hip).
 #include "device_common.hpp"
+#include "nm_dev.hpp"
 
 #include <atomic>
 #include <cstdlib>
@@ -275,6 +276,8 @@ __global__ __launch_bounds__(256) void gains_phase1(const double* __restrict__ t
 // One workgroup per chain: exclusive scan over chunk aggregates; writes the filtered
 // covariance at the end of chunk j-1 into pstart[j] (j >= 1).
 template <int D>
+constexpr int kP2B = D == 3 ? 4 : 8;   // aggregates per batch of loads (3 D^2 doubles each)
+template <int D>
 __global__ __launch_bounds__(256) void gains_phase2(int64_t nch, const double* __restrict__ agg,
                                                     double* __restrict__ pstart) {
   constexpr int E = 3 * D * D;
@@ -285,11 +288,19 @@ __global__ __launch_bounds__(256) void gains_phase2(int64_t nch, const double* _
   const int64_t j0 = tid * per;
   const int64_t j1 = (j0 + per < nch) ? j0 + per : nch;
   const double* a = agg + (int64_t)p * nch * E;
-  Elem<D> loc, e;
+  // a thread's run is read kP2B aggregates at a time, every load issued before the first combine
+  // (one memory latency per batch instead of one per aggregate: 33 -> ~10 us at 3907 chunks)
+  constexpr int KB = kP2B<D>;
+  Elem<D> loc;
   elem_identity(loc);
-  for (int64_t j = j0; j < j1; ++j) {
-    elem_load<D>(a + j * E, e);
-    elem_combine<D>(loc, e, loc);
+  for (int64_t jb = j0; jb < j1; jb += KB) {
+    Elem<D> eb[KB];
+#pragma unroll
+    for (int u = 0; u < KB; ++u)
+      if (jb + u < j1) elem_load<D>(a + (jb + u) * E, eb[u]);
+#pragma unroll
+    for (int u = 0; u < KB; ++u)
+      if (jb + u < j1) elem_combine<D>(loc, eb[u], loc);
   }
   elem_store<D>(&buf[0][tid * E], loc);
   __syncthreads();
@@ -313,13 +324,22 @@ __global__ __launch_bounds__(256) void gains_phase2(int64_t nch, const double* _
     elem_load<D>(&buf[cur][(tid - 1) * E], pre);
   }
   double* ps = pstart + (int64_t)p * nch * (D * D);
-  for (int64_t j = j0; j < j1; ++j) {
+  for (int64_t jb = j0; jb < j1; jb += KB) {
+    Elem<D> eb[KB];
 #pragma unroll
-    for (int i = 0; i < D; ++i)
+    for (int u = 0; u < KB; ++u)
+      if (jb + u < j1) elem_load<D>(a + (jb + u) * E, eb[u]);
 #pragma unroll
-      for (int q = 0; q < D; ++q) ps[j * D * D + i * D + q] = pre.C[i][q];
-    elem_load<D>(a + j * E, e);
-    elem_combine<D>(pre, e, pre);
+    for (int u = 0; u < KB; ++u) {
+      const int64_t j = jb + u;
+      if (j < j1) {
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+          for (int q = 0; q < D; ++q) ps[j * D * D + i * D + q] = pre.C[i][q];
+        elem_combine<D>(pre, eb[u], pre);
+      }
+    }
   }
 }
 
@@ -2435,39 +2455,189 @@ __global__ void chain_lml(const double* __restrict__ logs, int64_t nch,
   if (threadIdx.x == 0) lml[b] = -0.5 * ((double)n * kLog2Pi + red[0][0] + red[1][0]);
 }
 
-// lml[b] from the phase-3 moments (MOM): -0.5 (n log 2pi + sum_j [logS_j + s0_j + 2 c_j . s1_j +
-// c_j^T s2_j c_j]), c_j = the chunk's incoming state from the carry; partials summed in a fixed
-// order.
-template <int D>
-__global__ void chain_lml_mom(const double* __restrict__ logs, const double* __restrict__ mom,
-                              const double* __restrict__ cin, int64_t nch, int64_t n,
-                              double* __restrict__ lml) {
-  const int b = blockIdx.x;
-  __shared__ double red[256];
-  double s = 0.0;
-  for (int64_t j = threadIdx.x; j < nch; j += 256) {
-    const double* m = mom + ((int64_t)b * nch + j) * kMomStride;
-    const double* c = cin + ((int64_t)b * nch + j) * kSStride;
-    double v = logs[(int64_t)b * nch + j] + m[0];
-    int e = 1 + D;
-#pragma unroll
-    for (int i = 0; i < D; ++i) {
-      v = fma(2.0 * c[i], m[1 + i], v);
-#pragma unroll
-      for (int q = i; q < D; ++q) {
-        v = fma((q == i ? 1.0 : 2.0) * c[i] * c[q], m[e], v);
-        ++e;
+// The chains fit on the device (nm_dev.hpp): chain b's machine takes -v, and its next point's
+// parameters go where the next round's gains read them.  Called by the whole workgroup; the
+// record is staged in LDS (one coalesced copy each way) so the machine's dependent accesses are
+// LDS reads, not HBM round trips.
+__device__ void nm_chain_step(NmDev<3>* __restrict__ nm, ChainParams* __restrict__ cps,
+                              int* __restrict__ active, int b, double v) {
+  constexpr int kW = (int)(sizeof(NmDev<3>) / sizeof(int));
+  static_assert(sizeof(NmDev<3>) % sizeof(int) == 0, "NmDev<3> in whole words");
+  __shared__ NmDev<3> ls;
+  int* lw = reinterpret_cast<int*>(&ls);
+  const int* gw = reinterpret_cast<const int*>(nm + b);
+  for (int w = threadIdx.x; w < kW; w += blockDim.x) lw[w] = gw[w];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    if (ls.st != NmDev<3>::Done) {
+      double f = -v;
+      if (!isfinite(f)) f = INFINITY;
+      nm_tell(ls, f);
+      if (ls.st != NmDev<3>::Done) {
+        // unpack() (host.hpp: exp(p) + 1e-3) and chains_logpdf's parameters
+        const double l = exp(ls.pending[0]) + 1e-3, pv = exp(ls.pending[1]) + 1e-3,
+                     ns = exp(ls.pending[2]) + 1e-3;
+        cps[b] = ChainParams{1.0 / l, l, pv * pv, ns * ns};
+        run = 1;
       }
     }
-    s += v;
+    active[b] = run;
   }
-  red[threadIdx.x] = s;
+  __syncthreads();
+  int* ow = reinterpret_cast<int*>(nm + b);
+  for (int w = threadIdx.x; w < kW; w += blockDim.x) ow[w] = lw[w];
+}
+
+// A chain's logpdf from the phase-3 moments (MOM) in one workgroup per chain, its chunk carry
+// included: lml = -0.5 (n log 2pi + sum_j [logS_j + s0_j + 2 c_j . s1_j + c_j^T s2_j c_j]), c_j
+// the state entering chunk j (c_0 = 0, c_{j+1} = Phi_j c_j + send_j).  Thread t owns a run of
+// consecutive chunks: it composes its run's affine map, a workgroup scan of the 256 maps gives
+// each run's incoming state, and the run is walked once more for the chunk terms, its loads
+// issued KB chunks at a time.  (r06: the three-launch group carry and a separate reduction took
+// 40 us per round at 3907 chunks, this 35 us; staging segments of 1024 chunks through LDS with
+// coalesced loads measured 63 us -- four segments' scans and barriers.)  nm (optional): the
+// device Nelder-Mead step after the value (nm_chain_step).
+template <int D>
+__global__ __launch_bounds__(256) void chain_carry_lml(
+    const double* __restrict__ phi, int64_t phistride, const double* __restrict__ send,
+    int64_t sstride, const double* __restrict__ logs, const double* __restrict__ mom, int64_t nch,
+    int64_t n, double* __restrict__ lml, NmDev<3>* __restrict__ nm, ChainParams* __restrict__ cps,
+    int* __restrict__ active) {
+  const int b = blockIdx.x;
+  const int t = threadIdx.x;
+  const double* ph = phi + (int64_t)b * phistride;
+  const double* sp = send + (int64_t)b * sstride;
+  const int64_t run = (nch + 255) / 256;
+  const int64_t j0 = (int64_t)t * run < nch ? (int64_t)t * run : nch;
+  const int64_t j1 = j0 + run < nch ? j0 + run : nch;
+  constexpr int KB = D == 3 ? 4 : 8;
+  // the run's map x -> A x + c
+  double A[D][D], c[D];
+  mat_eye(A);
+#pragma unroll
+  for (int i = 0; i < D; ++i) c[i] = 0.0;
+  for (int64_t jb = j0; jb < j1; jb += KB) {
+    double Fb[KB][D * D], Sb[KB][D];
+#pragma unroll
+    for (int u = 0; u < KB; ++u)
+      if (jb + u < j1) {
+#pragma unroll
+        for (int e = 0; e < D * D; ++e) Fb[u][e] = ph[(jb + u) * D * D + e];
+#pragma unroll
+        for (int i = 0; i < D; ++i) Sb[u][i] = sp[(jb + u) * kSStride + i];
+      }
+#pragma unroll
+    for (int u = 0; u < KB; ++u)
+      if (jb + u < j1) {
+        double F[D][D], X[D][D], y[D];
+#pragma unroll
+        for (int i = 0; i < D; ++i)
+#pragma unroll
+          for (int q = 0; q < D; ++q) F[i][q] = Fb[u][i * D + q];
+        mat_mul(F, A, X);
+        mat_copy(X, A);
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          double acc = Sb[u][i];
+#pragma unroll
+          for (int q = 0; q < D; ++q) acc = fma(F[i][q], c[q], acc);
+          y[i] = acc;
+        }
+#pragma unroll
+        for (int i = 0; i < D; ++i) c[i] = y[i];
+      }
+  }
+  // inclusive scan of the runs' maps (Hillis-Steele, composition: later after earlier)
+  constexpr int E = D * D + D;
+  __shared__ double sm[2][256 * E];
+  int cur = 0;
+#pragma unroll
+  for (int i = 0; i < D; ++i) {
+#pragma unroll
+    for (int q = 0; q < D; ++q) sm[0][t * E + i * D + q] = A[i][q];
+    sm[0][t * E + D * D + i] = c[i];
+  }
+  __syncthreads();
+  for (int off = 1; off < 256; off <<= 1) {
+    const double* src = sm[cur];
+    double* dst = sm[cur ^ 1];
+    if (t >= off) {
+      // (A_t, c_t) o (A_{t-off}, c_{t-off}) = (A_t A_{t-off}, A_t c_{t-off} + c_t)
+      const double* e = src + (t - off) * E;
+      const double* f = src + t * E;
+#pragma unroll
+      for (int i = 0; i < D; ++i) {
+#pragma unroll
+        for (int q = 0; q < D; ++q) {
+          double acc = 0.0;
+#pragma unroll
+          for (int k = 0; k < D; ++k) acc = fma(f[i * D + k], e[k * D + q], acc);
+          dst[t * E + i * D + q] = acc;
+        }
+        double acc = f[D * D + i];
+#pragma unroll
+        for (int k = 0; k < D; ++k) acc = fma(f[i * D + k], e[D * D + k], acc);
+        dst[t * E + D * D + i] = acc;
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < E; ++e) dst[t * E + e] = src[t * E + e];
+    }
+    __syncthreads();
+    cur ^= 1;
+  }
+  // the run's incoming state: the inclusive prefix of the runs before it, applied to 0
+  double x[D];
+#pragma unroll
+  for (int i = 0; i < D; ++i) x[i] = t > 0 ? sm[cur][(t - 1) * E + D * D + i] : 0.0;
+  double s = 0.0;
+  constexpr int NM = 1 + D + D * (D + 1) / 2;   // moments used per chunk
+  for (int64_t jb = j0; jb < j1; jb += KB) {
+    double Fb[KB][D * D], Sb[KB][D], Mb[KB][NM], Lb[KB];
+#pragma unroll
+    for (int u = 0; u < KB; ++u)
+      if (jb + u < j1) {
+        const int64_t j = jb + u;
+#pragma unroll
+        for (int e = 0; e < D * D; ++e) Fb[u][e] = ph[j * D * D + e];
+#pragma unroll
+        for (int i = 0; i < D; ++i) Sb[u][i] = sp[j * kSStride + i];
+        const double* m = mom + ((int64_t)b * nch + j) * kMomStride;
+#pragma unroll
+        for (int e = 0; e < NM; ++e) Mb[u][e] = m[e];
+        Lb[u] = logs[(int64_t)b * nch + j];
+      }
+#pragma unroll
+    for (int u = 0; u < KB; ++u)
+      if (jb + u < j1) {
+        const double* m = Mb[u];
+        double v = Lb[u] + m[0];
+        int e = 1 + D;
+#pragma unroll
+        for (int i = 0; i < D; ++i) {
+          v = fma(2.0 * x[i], m[1 + i], v);
+#pragma unroll
+          for (int q = i; q < D; ++q) {
+            v = fma((q == i ? 1.0 : 2.0) * x[i] * x[q], m[e], v);
+            ++e;
+          }
+        }
+        s += v;
+        carry_step<D, false>(Fb[u], 0, Sb[u], x);
+      }
+  }
+  __syncthreads();   // sm is reused for the reduction
+  double* red = sm[0];
+  red[t] = s;
   __syncthreads();
   for (int off = 128; off > 0; off >>= 1) {
-    if (threadIdx.x < off) red[threadIdx.x] += red[threadIdx.x + off];
+    if (t < off) red[t] += red[t + off];
     __syncthreads();
   }
-  if (threadIdx.x == 0) lml[b] = -0.5 * ((double)n * kLog2Pi + red[0]);
+  const double v = -0.5 * ((double)n * kLog2Pi + red[0]);
+  if (t == 0) lml[b] = v;
+  if (nm) nm_chain_step(nm, cps, active, b, v);
 }
 
 }  // namespace gpar
@@ -2734,9 +2904,13 @@ void launch_carry(hipStream_t st, int sdim, const double* phi, int64_t phistride
 #undef GPAR_CARRY_LAUNCH
 }
 
-void launch_chain_lml_mom(hipStream_t st, int sdim, const double* logs, const double* mom,
-                          const double* cin, int64_t nch, int64_t n, int nchains, double* lml) {
-  GPAR_DISPATCH_D(sdim, chain_lml_mom<DD><<<nchains, 256, 0, st>>>(logs, mom, cin, nch, n, lml));
+void launch_chain_carry_lml(hipStream_t st, int sdim, const double* phi, int64_t phistride,
+                            const double* send, int64_t sstride, const double* logs,
+                            const double* mom, int64_t nch, int64_t n, int nchains, double* lml,
+                            NmDev<3>* nm, ChainParamsHost* cps, int* active) {
+  GPAR_DISPATCH_D(sdim, chain_carry_lml<DD><<<nchains, 256, 0, st>>>(
+                            phi, phistride, send, sstride, logs, mom, nch, n, lml, nm,
+                            reinterpret_cast<ChainParams*>(cps), active));
 }
 
 void launch_gains_adjoint(hipStream_t st, int sdim, const double* rec, int64_t n, int L,

@@ -114,8 +114,17 @@ void launch_gains(hipStream_t st, int sdim, const double* t, int64_t n, int L, i
 // the chains' logpdf from the gains' moments (moments != null in launch_gains; kMomStride doubles
 // per chunk) and the carried chunk states cin [nchains][nch][4]
 constexpr int kGainsMomStride = 12;
-void launch_chain_lml_mom(hipStream_t st, int sdim, const double* logs, const double* mom,
-                          const double* cin, int64_t nch, int64_t n, int nchains, double* lml);
+// a chain's logpdf from the phase-3 moments, its chunk carry included (one workgroup per chain);
+// nm (optional): the chains fit on the device (nm_dev.hpp) -- each chain's Nelder-Mead machine
+// takes the value and writes the next round's parameters into cps; active[chain] = 1 while its
+// machine runs
+template <int N>
+struct NmDev;
+void launch_chain_carry_lml(hipStream_t st, int sdim, const double* phi, int64_t phistride,
+                            const double* send, int64_t sstride, const double* logs,
+                            const double* mom, int64_t nch, int64_t n, int nchains, double* lml,
+                            NmDev<3>* nm = nullptr, ChainParamsHost* cps = nullptr,
+                            int* active = nullptr);
 // compact gains records {K, rs, pad} (gains_phase3<D, true>): doubles per step
 inline int crec_size(int sdim) { return sdim == 1 ? 2 : 4; }
 int dp_bucket(int d);

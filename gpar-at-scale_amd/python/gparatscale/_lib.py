@@ -283,9 +283,10 @@ class Context:
 
     def set_schedule(self, knob, value):
         """A schedule knob (gpar_ctx_set_schedule: overlap, overlap_group, qu_batch, dense_early,
-        post_gram, compact_rec, predict_lanes, serialize, predict_fused, dg_rows_w; the header
-        lists their values); results are bit-identical with any setting except the plan knobs
-        predict_fused and dg_rows_w (last bits)."""
+        post_gram, compact_rec, predict_lanes, serialize, predict_fused, dg_rows_w, gram_group,
+        fit_chunks, device_nm; the header lists their values); results are bit-identical with
+        any setting except the plan knobs predict_fused, dg_rows_w and gram_group (last bits)
+        and device_nm (the device's exp() in the chains fit's parameters)."""
         self.check(load().gpar_ctx_set_schedule(self.h, knob.encode(), int(value)))
 
     def schedule(self, knob):

@@ -191,6 +191,12 @@ int32_t gpar_ctx_set_predict_fused(gpar_ctx* ctx, int32_t on);
  *                   of k consecutive outputs.  Not for gpar_fit_predict / gpar_fit_posterior.  Each
  *                   output's fit is independent of its batch, so a sub-batched fit equals the
  *                   one-batch fit with every output cached bit for bit
+ *   "device_nm"     the chains fit of gpar_sde_predictions steps its Nelder-Mead machines on
+ *                   the device after each evaluation round (1, default: rounds queue back to
+ *                   back, the host reads the running count one batch of 8 rounds behind) or on
+ *                   the host after each round's values come back (0).  A fit with a wall-clock
+ *                   time limit always runs on the host.  The same steps; the device's exp() in
+ *                   the chain parameters may move a value in its last bit
  * The environment variable GPAR_<KNOB> (upper case) sets a knob at context creation.
  * GPAR_ERR_ARG for an unknown knob or value.  Every non-default value is a supported schedule
  * mode; the A/B-only knobs of round 4 (split_head, dg_share, tail_cus, predict_d2, dense_early 2)

@@ -47,7 +47,8 @@ SETTINGS = [
 PLAN = {"dg_rows_w": 10}
 DEFAULTS = {"serialize": 0, "overlap": 1, "overlap_group": 0, "dense_early": 1, "post_gram": -1,
             "compact_rec": -1, "dg_rows_w": -100, "qu_batch": 1, "predict_lanes": 2,
-            "predict_fused": 1, "gram_group": -1, "fit_chunks": -1}
+            "predict_fused": 1, "gram_group": -1, "fit_chunks": -1,
+            "device_nm": 1}
 DELETED = ["split_head", "dg_share", "tail_cus", "predict_d2"]
 
 
