@@ -498,8 +498,18 @@ DenseOut run_dense(gpar_ctx* c, const std::vector<DevProblem>& P,
 Finish2JobHost finish_job(const DenseOut& dn, const GramOut& go, const DevProblem& p, int i,
                                  int64_t nch, double* out, double* me);
 std::vector<Theta> thetas_from(const double* theta, int np);
+// async (the unsplit round overlap, fit_overlapped_unsplit): the values and Cholesky status
+// flags go to pinned host memory by async copies, `done` is recorded after them and eval_dtc
+// returns without waiting (out / status_out untouched)
+bool grouped_gram_eligible(gpar_ctx* c, const std::vector<DevProblem>& P);
+struct EvalAsync {
+  double* hout = nullptr;   // pinned, one value per problem
+  int* hstat = nullptr;     // pinned, two flags per problem
+  hipEvent_t done = nullptr;
+};
 void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<Theta>& th,
-                     double* out, std::vector<int>& status_out, GramOut* gram_out = nullptr);
+                     double* out, std::vector<int>& status_out, GramOut* gram_out = nullptr,
+                     const EvalAsync* async = nullptr);
 
 
 struct QuOut {

@@ -353,6 +353,177 @@ static void fit_overlapped(gpar_ctx* c, const std::vector<DevProblem>& P,
   sp.join(c->main);
 }
 
+// ---------------------------------------------------------------- unsplit round overlap
+// The same idea for the batched fits that do not take the CU split (N Mp^2 < 1e11: the dtc and eeg
+// configs, one rank's eeg shard), whose rounds run eval_dtc's unsplit schedule with the grouped
+// Gram.  There a round is one grouped Gram (3.8 ms for a rank's 8 eeg outputs) and a boundary of
+// about as long of latency-bound work -- the dense tail's 64 x 64 launches, the host's simplex
+// step, the next round's gains, whitenings and chunk carries (profiles/trace_eeg_shard0of8_r06m_gaps.txt).
+// The outputs are dealt round-robin into K groups (2, or groups of overlap_group outputs); each
+// group's rounds run on streams of their own (group 0: the context's main / side / dense streams,
+// the others three each) with workspaces of their own (ws_suffix; the distance cache is shared and
+// only read) and pinned upload arenas, and eval_dtc returns as soon as a round is queued (its values
+// land in pinned memory behind an event).  The host takes the groups in turn: wait for a group's
+// values, step its simplices, queue its next round -- which then runs beside the other groups'
+// rounds, one group's boundary under another's Gram.  Every output evaluates the points its own
+// simplex asks for with the same kernels; only its group's grouped-Gram plan (sized for the
+// group's outputs) differs from the one-group round, so the fit matches the round-by-round one
+// within rounding, and bit for bit its serialized twin (every group on the main stream).
+// Measured (r06ov1/2, one box): a rank's eeg shard (8 outputs, M = 512) 407 / 410 -> 393 / 397 ms
+// per step with two groups of 4 -- the groups' Grams slow 1.75 -> 2.7 ms beside the other group's
+// whitenings (the fp64 pipe they share), which eats most of the boundary they hide; four groups of
+// 2: 576 ms, three: 554 ms (every group pays the boundary's launch chains); the 1-GPU eeg job (two
+// groups of 32) 2398 -> 2350 / 2414 ms (noise); dtc (M = 256, its Gram a third of its round)
+// 167 -> 172 ms.  So: two groups, calls of 4..16 outputs with Mp >= 512 (or any overlap_group).
+constexpr int kOverlapUnsplitMax = 16;
+constexpr int64_t kOverlapUnsplitMinMp = 512;
+
+static void fit_overlapped_unsplit(gpar_ctx* c, const std::vector<DevProblem>& P,
+                                   std::vector<NelderMead>& nm, const AcceptFn& accept) {
+  const int np = (int)P.size();
+  const int K = c->overlap_group > 0 ? std::max(2, (np + c->overlap_group - 1) / c->overlap_group) : 2;
+  struct UGroup {
+    int id = 0;
+    std::vector<int> members, act;
+    std::vector<Theta> th;
+    std::vector<DevProblem> sub;
+    GramOut go{};
+    hipStream_t st[3] = {nullptr, nullptr, nullptr};   // main, side, dense
+    double* hout = nullptr;
+    int* hstat = nullptr;
+    hipEvent_t done = nullptr;
+    size_t res_bytes = 0;
+    bool in_flight = false;
+  };
+  std::vector<UGroup> grp(K);
+  for (int i = 0; i < np; ++i) grp[i % K].members.push_back(i);
+  // streams and events made here are released on every exit, after their work
+  struct Owned {
+    std::vector<hipStream_t> st;
+    std::vector<hipEvent_t> ev;
+    ~Owned() {
+      for (hipStream_t s : st) {
+        (void)hipStreamSynchronize(s);
+        (void)hipStreamDestroy(s);
+      }
+      for (hipEvent_t e : ev) (void)hipEventDestroy(e);
+    }
+  } own;
+  auto make_stream = [&]() {
+    if (c->serialize) return c->main;   // the order-free twin: every group on the main stream
+    hipStream_t s;
+    HIPCHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    own.st.push_back(s);
+    return s;
+  };
+  if ((int)c->stage.size() < K) c->stage.resize(K);   // no arena is in use between calls
+  HIPCHECK(hipEventRecord(c->ev_fork, c->main));   // the inputs and the distance cache, on main
+  for (int g = 0; g < K; ++g) {
+    UGroup& G = grp[g];
+    G.id = g;
+    if (g == 0) {
+      G.st[0] = c->main;
+      G.st[1] = c->side;
+      G.st[2] = c->s_d;
+    } else {
+      for (hipStream_t& s : G.st) {
+        s = make_stream();
+        HIPCHECK(hipStreamWaitEvent(s, c->ev_fork, 0));
+      }
+    }
+    HIPCHECK(hipEventCreateWithFlags(&G.done, hipEventDisableTiming));
+    own.ev.push_back(G.done);
+    const size_t cap = G.members.size();
+    gpar_ctx::Staging& a = c->stage[g];
+    const size_t vbytes = (cap * sizeof(double) + 255) & ~(size_t)255;
+    G.res_bytes = vbytes + ((2 * cap * sizeof(int) + 255) & ~(size_t)255);
+    const size_t need = G.res_bytes + ((size_t)1 << 20) + cap * 4096;
+    if (a.cap < need) {
+      if (a.host) HIPCHECK(hipHostFree(a.host));
+      a.host = nullptr;
+      a.cap = 0;
+      HIPCHECK(hipHostMalloc((void**)&a.host, need, hipHostMallocDefault));
+      a.cap = need;
+    }
+    G.hout = reinterpret_cast<double*>(a.host);
+    G.hstat = reinterpret_cast<int*>(a.host + vbytes);
+  }
+  // a group's streams, workspaces and upload arena, for the scope of its launches
+  struct GroupScope {
+    gpar_ctx* c;
+    hipStream_t saved[4];
+    std::string sfx;
+    GroupScope(gpar_ctx* c_, const UGroup& G) : c(c_) {
+      saved[0] = c->stream;
+      saved[1] = c->main;
+      saved[2] = c->side;
+      saved[3] = c->s_d;
+      c->stream = c->main = G.st[0];
+      c->side = G.st[1];
+      c->s_d = G.st[2];
+      sfx = c->ws_suffix;
+      if (G.id > 0) c->ws_suffix = sfx + "~ov" + std::to_string(G.id);
+      c->staging = &c->stage[G.id];
+    }
+    ~GroupScope() {
+      c->stream = saved[0];
+      c->main = saved[1];
+      c->side = saved[2];
+      c->s_d = saved[3];
+      c->ws_suffix = sfx;
+      c->staging = nullptr;
+    }
+  };
+  auto issue = [&](UGroup& G) {
+    G.act.clear();
+    for (int i : G.members)
+      if (!nm[i].done()) G.act.push_back(i);
+    if (G.act.empty()) return;
+    G.th.clear();
+    G.sub.clear();
+    for (int i : G.act) {
+      const auto& x = nm[i].ask();
+      G.th.push_back({unpack(x[0]), unpack(x[1]), unpack(x[2]), unpack(x[3]), unpack(x[4])});
+      G.sub.push_back(P[i]);
+    }
+    c->stage[G.id].used = G.res_bytes;   // the previous round's uploads have been consumed
+    GroupScope gs_(c, G);
+    const EvalAsync as{G.hout, G.hstat, G.done};
+    std::vector<int> unused;
+    eval_dtc(c, G.sub, G.th, nullptr, unused, &G.go, &as);
+    G.in_flight = true;
+  };
+  auto finish = [&](UGroup& G) {
+    HIPCHECK(hipEventSynchronize(G.done));
+    OnStream on_(c, G.st[0]);   // a kept point's Gram copy, ahead of the group's next round
+    const size_t sq = (size_t)G.go.ldg * G.go.ldg;
+    for (size_t a = 0; a < G.act.size(); ++a) {
+      double f = -G.hout[a];
+      if (G.hstat[2 * a] || G.hstat[2 * a + 1] || !std::isfinite(f)) f = INFINITY;
+      accept(G.act[a], f, G.go.G + a * sq, G.go.r + a * G.go.ldg, G.go.ldg);
+    }
+    G.in_flight = false;
+  };
+  for (auto& G : grp) issue(G);
+  auto any_in_flight = [&]() {
+    for (const auto& G : grp)
+      if (G.in_flight) return true;
+    return false;
+  };
+  for (int g = 0; any_in_flight(); g = (g + 1) % K) {
+    if (!grp[g].in_flight) continue;
+    finish(grp[g]);
+    issue(grp[g]);
+  }
+  // the context's stream follows every group's work (kept Grams, the streams released above)
+  for (int g = 1; g < K; ++g)
+    for (hipStream_t s : grp[g].st)
+      if (s != c->main) {
+        HIPCHECK(hipEventRecord(c->ev_join, s));
+        HIPCHECK(hipStreamWaitEvent(c->main, c->ev_join, 0));
+      }
+}
+
 // Cache-resident sub-batches.  The batched fit evaluates every output once per Nelder-Mead round,
 // so an output's cached distances are only reused if the cache holds the whole batch; where it
 // cannot (BASELINE config 5: N = 1e7, M = 1024, 82 GB of distances per output, 32 outputs per
@@ -515,6 +686,12 @@ void fit_impl(gpar_ctx* ctx, const std::vector<DevProblem>& P0, const double* lo
       fit_pipelined(ctx, P) &&
       split_active(ctx, P[0].n, mpmax))
     fit_overlapped(ctx, P, nm, accept);
+  else if (ctx->overlap && nprob >= 4 &&
+           ((nprob <= kOverlapUnsplitMax && mpmax >= kOverlapUnsplitMinMp) ||
+            ctx->overlap_group > 0) &&
+           fit_pipelined(ctx, P) && !split_active(ctx, P[0].n, mpmax) &&
+           grouped_gram_eligible(ctx, P))
+    fit_overlapped_unsplit(ctx, P, nm, accept);
   std::vector<double> vals;
   while (true) {
     std::vector<int> act;

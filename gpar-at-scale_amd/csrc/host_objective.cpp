@@ -99,6 +99,13 @@ static int gram_group_size(gpar_ctx* c, const std::vector<DevProblem>& P, int64_
   return g >= 2 ? g : 0;
 }
 
+// an unsplit batched round of these problems would run the grouped Gram
+bool grouped_gram_eligible(gpar_ctx* c, const std::vector<DevProblem>& P) {
+  int64_t mpmax = 0;
+  for (const auto& p : P) mpmax = std::max(mpmax, p.mp);
+  return gram_group_size(c, P, P[0].n, mpmax, false, 1, false) >= 2;
+}
+
 // Kfu assembly + chunk-local whitening of j's output into b.beta, on c->stream.
 void stage_whiten(gpar_ctx* c, const StageJob& j, const StageBufs& b) {
   const DevProblem& p = *j.p;
@@ -585,7 +592,8 @@ std::vector<Theta> thetas_from(const double* theta, int np) {
 
 // DTC objective for all problems; status_out[i] = 1 if a Cholesky failed for problem i.
 void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<Theta>& th,
-                     double* out, std::vector<int>& status_out, GramOut* gram_out) {
+                     double* out, std::vector<int>& status_out, GramOut* gram_out,
+                     const EvalAsync* async) {
   const int np = (int)P.size();
   // one Nelder-Mead round of a batched fit, entry to values (the bench's round overhead: this
   // span less the round's Gram spans is what does not overlap a Gram)
@@ -667,6 +675,15 @@ void eval_dtc(gpar_ctx* c, const std::vector<DevProblem>& P, const std::vector<T
   h2d(c, dfj, fj.data(), np);
   launch_finish2(c->stream, dfj, np, dn.ld, dn.nb);
   check_launch("finish");
+  if (async) {
+    HIPCHECK(hipMemcpyAsync(async->hout, dout, np * sizeof(double), hipMemcpyDeviceToHost,
+                            c->stream));
+    HIPCHECK(hipMemcpyAsync(async->hstat, dn.status, 2 * np * sizeof(int), hipMemcpyDeviceToHost,
+                            c->stream));
+    if (!seq.ev.empty()) HIPCHECK(hipEventRecord(seq.ev.back(), c->stream));
+    HIPCHECK(hipEventRecord(async->done, c->stream));
+    return;
+  }
   std::vector<int> st(2 * np);
   d2h(c, out, dout, np);
   d2h(c, st.data(), dn.status, 2 * np);
