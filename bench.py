@@ -888,6 +888,10 @@ def main():
             out.pop("roofline_whiten", None)
             for fam, key in (("chains_logpdf", "roofline"), ("chains_smooth", "roofline_smooth")):
                 (fn, fms), w = chain_stats[fam]
+                if fn and fam == "chains_logpdf":
+                    # the device-stepped fit times batches of rounds: count NM rounds by their
+                    # algorithmic bytes (8 N (1 + chains) per round)
+                    fn = max(fn, int(round(w / (8.0 * t_d.numel() * (1 + len(mine))))))
                 if fn:
                     ga = w / (fms * 1e-3) / 1e9
                     out[key] = {"bound": "hbm", "achieved": ga, "peak": HBM_PEAK_GBS, "unit": "GB/s",
@@ -897,7 +901,8 @@ def main():
             if "roofline" in out and out["roofline"]:
                 out["roofline"].update(
                     kernel="chains_logpdf: gains_phase1 + gains_phase2 + gains_phase3 (moments) + "
-                           "chain_carry_lml (the carry and the value), one HIP-event span per NM round",
+                           "chain_carry_lml (the carry, the value and the device Nelder-Mead step), HIP-event "
+                           "spans around batches of 8 NM rounds, reported per round",
                     bytes="8 N (t) + 8 N per active chain (y) per launch; the per-chunk outputs "
                           "(~0.7 B per step and chain) not counted")
             if out.get("roofline_smooth"):

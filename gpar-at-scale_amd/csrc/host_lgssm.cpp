@@ -37,9 +37,14 @@ static ChainsLml plan_chains_lml(gpar_ctx* c, const std::vector<const double*>& 
   return q;
 }
 
+static double chains_lml_bytes(const ChainsLml& q) { return 8.0 * (double)q.n * (1.0 + q.nchains); }
+
+// one round's launches; timed: one "chains_logpdf" span around them (the device-stepped fit times
+// whole batches of rounds instead: two event records per round were a third of its 15 us boundary)
 static void launch_chains_lml(gpar_ctx* c, const ChainsLml& q, NmDev<3>* nm = nullptr,
-                              int* active = nullptr) {
-  Timed tm_(c, "chains_logpdf", 8.0 * (double)q.n * (1.0 + q.nchains));
+                              int* active = nullptr, bool timed = true) {
+  std::optional<Timed> tm_;
+  if (timed) tm_.emplace(c, "chains_logpdf", chains_lml_bytes(q));
   q.gp.launch(c->stream, 0, q.nchains);
   const GainsOut& g = q.gp.o;
   launch_chain_carry_lml(c->stream, q.sdim, g.phi, g.phistride, q.send, q.nch * kSStride, g.logs,
@@ -107,7 +112,10 @@ static void fit_chains_device(gpar_ctx* c, int nchains, int64_t n, const double*
     int64_t r = 0;
     for (int k = 0; r < cap; ++k) {
       const int64_t nb = std::min<int64_t>(kNmBatch, cap - r);
-      for (int64_t b = 0; b < nb; ++b) launch_chains_lml(c, q, dnm, dact);
+      {
+        Timed tm_(c, "chains_logpdf", chains_lml_bytes(q) * (double)nb);
+        for (int64_t b = 0; b < nb; ++b) launch_chains_lml(c, q, dnm, dact, /*timed=*/false);
+      }
       r += nb;
       HIPCHECK(hipMemcpyAsync(hact + (k & 1) * nchains, dact, nchains * sizeof(int),
                               hipMemcpyDeviceToHost, c->stream));
