@@ -326,6 +326,7 @@ struct GainsPlan {
   int sdim = 0, nchains = 0;
   const double* t = nullptr;
   int64_t n = 0, nch = 0;
+  int64_t nchs = 0;   // per-chunk output slots per chain (nch; moments: 256 ceil(nch / 256))
   const double* noise = nullptr;
   ChainParamsHost* dcps = nullptr;
   double *agg = nullptr, *pst = nullptr;

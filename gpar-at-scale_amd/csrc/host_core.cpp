@@ -297,17 +297,22 @@ GainsPlan plan_gains(gpar_ctx* c, int sdim, const double* t, int64_t n,
   const int d2 = sdim * sdim;
   gp.dcps = ws<ChainParamsHost>(c, tag + "_cps", nchains);
   h2d(c, gp.dcps, cps.data(), nchains);
-  gp.agg = ws<double>(c, tag + "_agg", (size_t)nchains * nch * 3 * d2);
+  // the chunk aggregates in gains_phase2's run-slot order: 256 ceil(nch / 256) slots per chain
+  gp.agg = ws<double>(c, tag + "_agg", (size_t)nchains * 256 * ((nch + 255) / 256) * 3 * d2);
   gp.pst = ws<double>(c, tag + "_pstart", (size_t)nchains * nch * d2);
   GainsOut& o = gp.o;
   o.recstride = n * rs;
   o.gstride = n * 4;
-  o.phistride = nch * d2;
+  // moments: the per-chunk outputs in chain_carry_lml's slot order (k_lgssm.hip mom_slot), 256
+  // ceil(nch / 256) slots per chain
+  gp.nchs = moments ? 256 * ((nch + 255) / 256) : nch;
+  const int64_t nchs = gp.nchs;
+  o.phistride = nchs * d2;
   // moments (the chains' logpdf): no per-step record or fix-up row is written
   o.rec = moments ? nullptr : ws<double>(c, tag + "_rec", (size_t)nchains * n * rs);
   o.g = moments ? nullptr : ws<double>(c, tag + "_g", (size_t)nchains * n * 4);
-  o.phi = ws<double>(c, tag + "_phi", (size_t)nchains * nch * d2);
-  o.logs = ws<double>(c, tag + "_logs", (size_t)nchains * nch);
+  o.phi = ws<double>(c, tag + "_phi", (size_t)nchains * nchs * d2);
+  o.logs = ws<double>(c, tag + "_logs", (size_t)nchains * nchs);
   o.pf = want_pf ? ws<double>(c, tag + "_pf", (size_t)nchains * n * d2) : nullptr;
   o.compact = compact;
   o.t = t;
@@ -331,14 +336,15 @@ void GainsPlan::launch(hipStream_t st, int first, int count) const {
   OnStream on_(c, st);
   Timed tm_(c, "gains");
   launch_gains(st, sdim, t, n, kChunk, nch, count, dcps + first, noise,
-               agg + (size_t)first * nch * 3 * d2, pst + (size_t)first * nch * d2,
+               agg + (size_t)first * 256 * ((nch + 255) / 256) * 3 * d2,
+               pst + (size_t)first * nch * d2,
                o.rec ? o.rec + (size_t)first * o.recstride : nullptr,
                o.g ? o.g + (size_t)first * o.gstride : nullptr,
-               o.phi + (size_t)first * o.phistride, o.logs + (size_t)first * nch,
+               o.phi + (size_t)first * o.phistride, o.logs + (size_t)first * nchs,
                o.pf ? o.pf + (size_t)first * n * d2 : nullptr, dys ? dys + first : nullptr,
                alpha_loc ? alpha_loc + (size_t)first * n : nullptr,
-               asend ? asend + (size_t)first * nch * kSStride : nullptr, o.compact, ys_aligned16,
-               moments ? moments + (size_t)first * nch * kGainsMomStride : nullptr);
+               asend ? asend + (size_t)first * nchs * kSStride : nullptr, o.compact, ys_aligned16,
+               moments ? moments + (size_t)first * nchs * kGainsMomStride : nullptr);
   check_launch("gains");
 }
 

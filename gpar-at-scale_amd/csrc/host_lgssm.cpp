@@ -29,8 +29,9 @@ static ChainsLml plan_chains_lml(gpar_ctx* c, const std::vector<const double*>& 
   q.nchains = (int)ys.size();
   q.n = n;
   q.nch = (n + kChunk - 1) / kChunk;
-  q.send = ws<double>(c, "chain_send", (size_t)q.nchains * q.nch * 4);
-  q.mom = ws<double>(c, "chain_mom", (size_t)q.nchains * q.nch * kGainsMomStride);
+  const int64_t nchs = 256 * ((q.nch + 255) / 256);   // GainsPlan::nchs of a moments plan
+  q.send = ws<double>(c, "chain_send", (size_t)q.nchains * nchs * kSStride);
+  q.mom = ws<double>(c, "chain_mom", (size_t)q.nchains * nchs * kGainsMomStride);
   q.dl = ws<double>(c, "chain_lml", q.nchains);
   q.gp = plan_gains(c, sdim, t, n, cps, nullptr, false, "chain", &ys, nullptr, q.send, false,
                     q.mom);
@@ -47,7 +48,7 @@ static void launch_chains_lml(gpar_ctx* c, const ChainsLml& q, NmDev<3>* nm = nu
   if (timed) tm_.emplace(c, "chains_logpdf", chains_lml_bytes(q));
   q.gp.launch(c->stream, 0, q.nchains);
   const GainsOut& g = q.gp.o;
-  launch_chain_carry_lml(c->stream, q.sdim, g.phi, g.phistride, q.send, q.nch * kSStride, g.logs,
+  launch_chain_carry_lml(c->stream, q.sdim, g.phi, g.phistride, q.send, q.gp.nchs * kSStride, g.logs,
                          q.mom, q.nch, q.n, q.nchains, q.dl, nm, q.gp.dcps, active);
   check_launch("chains_logpdf");
 }

@@ -226,6 +226,18 @@ __device__ __forceinline__ void elem_shfl_down(const Elem<D>& e, int off, Elem<D
     }
 }
 
+// Per-chunk values read by a one-workgroup-per-chain scan (gains_phase2: the aggregates;
+// chain_carry_lml: MOM's per-chunk outputs) are stored in "run slot" order: chunk j of chain p at
+// p 256 run + (j % run) 256 + j / run, run = ceil(nch / 256).  The scan's thread t walks chunks
+// t run .. t run + run - 1, so its u-th chunk sits at u 256 + t and each of its loads is
+// contiguous across the wave (in chunk order each load touched 64 lines: 35 us per scan at 16
+// chains x 3907 chunks, 20 us in slot order).
+__host__ __device__ __forceinline__ int64_t run_len(int64_t nch) { return (nch + 255) / 256; }
+__device__ __forceinline__ int64_t run_slot(int p, int64_t j, int64_t nch) {
+  const int64_t r = run_len(nch);
+  return (int64_t)p * 256 * r + (j % r) * 256 + j / r;
+}
+
 template <int D, int SUB>
 __global__ __launch_bounds__(256) void gains_phase1(const double* __restrict__ t, int64_t n,
                                                     int L, int64_t nch,
@@ -269,7 +281,7 @@ __global__ __launch_bounds__(256) void gains_phase1(const double* __restrict__ t
     }
     if (q != 0 || !live) return;
   }
-  elem_store<D>(agg + ((int64_t)p * nch + j) * (3 * D * D), acc);
+  elem_store<D>(agg + run_slot(p, j, nch) * (3 * D * D), acc);
 }
 
 // ---------------------------------------------------------------------------- phase 2
@@ -284,10 +296,12 @@ __global__ __launch_bounds__(256) void gains_phase2(int64_t nch, const double* _
   __shared__ double buf[2][256 * E];
   const int p = blockIdx.x;
   const int tid = threadIdx.x;
-  const int64_t per = (nch + 255) / 256;
+  const int64_t per = run_len(nch);
   const int64_t j0 = tid * per;
   const int64_t j1 = (j0 + per < nch) ? j0 + per : nch;
-  const double* a = agg + (int64_t)p * nch * E;
+  // the aggregates in run-slot order: chunk j0 + u at u 256 + tid
+  const double* a = agg + (int64_t)p * 256 * per * E + (int64_t)tid * E;
+  auto at = [&](int64_t j) __attribute__((always_inline)) { return a + (j - j0) * 256 * E; };
   // a thread's run is read kP2B aggregates at a time, every load issued before the first combine
   // (one memory latency per batch instead of one per aggregate: 33 -> ~10 us at 3907 chunks)
   constexpr int KB = kP2B<D>;
@@ -297,7 +311,7 @@ __global__ __launch_bounds__(256) void gains_phase2(int64_t nch, const double* _
     Elem<D> eb[KB];
 #pragma unroll
     for (int u = 0; u < KB; ++u)
-      if (jb + u < j1) elem_load<D>(a + (jb + u) * E, eb[u]);
+      if (jb + u < j1) elem_load<D>(at(jb + u), eb[u]);
 #pragma unroll
     for (int u = 0; u < KB; ++u)
       if (jb + u < j1) elem_combine<D>(loc, eb[u], loc);
@@ -328,7 +342,7 @@ __global__ __launch_bounds__(256) void gains_phase2(int64_t nch, const double* _
     Elem<D> eb[KB];
 #pragma unroll
     for (int u = 0; u < KB; ++u)
-      if (jb + u < j1) elem_load<D>(a + (jb + u) * E, eb[u]);
+      if (jb + u < j1) elem_load<D>(at(jb + u), eb[u]);
 #pragma unroll
     for (int u = 0; u < KB; ++u) {
       const int64_t j = jb + u;
@@ -374,6 +388,7 @@ constexpr int kGainsPF = 4;
 // from which sum_k alpha_k^2 = sum_j s0 + 2 c_j . s1 + c_j^T s2 c_j once the carry has given the
 // chunks' incoming states c_j (alpha_k = alpha_loc,k + g_k . c_j, as vec_fix applies it).
 constexpr int kMomStride = 12;   // >= 1 + D + D (D + 1) / 2 for D <= 3
+// MOM's per-chunk outputs (phi, logS, the end state, the moments) go to run_slot order (above)
 
 template <int D, bool COMPACT, bool HAS_Y, bool HAS_NOISE, bool HAS_PF, bool MASKED, bool MOM>
 __global__ __launch_bounds__(256, 2) void gains_phase3(int64_t blk0, const double* __restrict__ t,
@@ -620,19 +635,20 @@ __global__ __launch_bounds__(256, 2) void gains_phase3(int64_t blk0, const doubl
     }
   }
   if (!jv) return;
-  double* ph = phi + ((int64_t)p * nch + j) * (D * D);
+  const int64_t jo = MOM ? run_slot(p, j, nch) : (int64_t)p * nch + j;
+  double* ph = phi + jo * (D * D);
 #pragma unroll
   for (int i = 0; i < D; ++i)
 #pragma unroll
     for (int q = 0; q < D; ++q) ph[i * D + q] = Phi[i][q];
-  logs[(int64_t)p * nch + j] = lsum;
+  logs[jo] = lsum;
   if constexpr (HAS_Y) {
-    double* sp = asend + ((int64_t)p * nch + j) * kSStride;
+    double* sp = asend + jo * kSStride;
 #pragma unroll
     for (int i = 0; i < kSStride; ++i) sp[i] = i < D ? ma[i] : 0.0;
   }
   if constexpr (MOM) {
-    double* mp_ = mom + ((int64_t)p * nch + j) * kMomStride;
+    double* mp_ = mom + jo * kMomStride;
 #pragma unroll
     for (int e = 0; e < kMomStride; ++e) mp_[e] = ms[e];
   }
@@ -951,19 +967,20 @@ __device__ __forceinline__ void g3_body(
   }
   asm volatile("s_waitcnt vmcnt(0)" : : : "memory");   // the ring's last DMAs land before exit
   if (!jv) return;
-  double* ph = phi + ((int64_t)p * nch + j) * (D * D);
+  const int64_t jo = MOM ? run_slot(p, j, nch) : (int64_t)p * nch + j;
+  double* ph = phi + jo * (D * D);
 #pragma unroll
   for (int i = 0; i < D; ++i)
 #pragma unroll
     for (int q = 0; q < D; ++q) ph[i * D + q] = Phi[i][q];
-  logs[(int64_t)p * nch + j] = lsum;
+  logs[jo] = lsum;
   if constexpr (HAS_Y) {
-    double* sp = asend + ((int64_t)p * nch + j) * kSStride;
+    double* sp = asend + jo * kSStride;
 #pragma unroll
     for (int i = 0; i < kSStride; ++i) sp[i] = i < D ? ma[i] : 0.0;
   }
   if constexpr (MOM) {
-    double* mp_ = mom + ((int64_t)p * nch + j) * kMomStride;
+    double* mp_ = mom + jo * kMomStride;
 #pragma unroll
     for (int e = 0; e < kMomStride; ++e) mp_[e] = ms[e];
   }
@@ -2508,9 +2525,13 @@ __global__ __launch_bounds__(256) void chain_carry_lml(
   const int t = threadIdx.x;
   const double* ph = phi + (int64_t)b * phistride;
   const double* sp = send + (int64_t)b * sstride;
-  const int64_t run = (nch + 255) / 256;
+  const int64_t run = run_len(nch);
   const int64_t j0 = (int64_t)t * run < nch ? (int64_t)t * run : nch;
   const int64_t j1 = j0 + run < nch ? j0 + run : nch;
+  // chunk j = j0 + u of this thread's run sits at slot u 256 + t (mom_slot)
+  auto slot = [&](int64_t j) __attribute__((always_inline)) { return (j - j0) * 256 + t; };
+  const double* lgb = logs + (int64_t)b * 256 * run;
+  const double* mob = mom + (int64_t)b * 256 * run * kMomStride;
   constexpr int KB = D == 3 ? 4 : 8;
   // the run's map x -> A x + c
   double A[D][D], c[D];
@@ -2523,9 +2544,9 @@ __global__ __launch_bounds__(256) void chain_carry_lml(
     for (int u = 0; u < KB; ++u)
       if (jb + u < j1) {
 #pragma unroll
-        for (int e = 0; e < D * D; ++e) Fb[u][e] = ph[(jb + u) * D * D + e];
+        for (int e = 0; e < D * D; ++e) Fb[u][e] = ph[slot(jb + u) * D * D + e];
 #pragma unroll
-        for (int i = 0; i < D; ++i) Sb[u][i] = sp[(jb + u) * kSStride + i];
+        for (int i = 0; i < D; ++i) Sb[u][i] = sp[slot(jb + u) * kSStride + i];
       }
 #pragma unroll
     for (int u = 0; u < KB; ++u)
@@ -2598,15 +2619,15 @@ __global__ __launch_bounds__(256) void chain_carry_lml(
 #pragma unroll
     for (int u = 0; u < KB; ++u)
       if (jb + u < j1) {
-        const int64_t j = jb + u;
+        const int64_t so = slot(jb + u);
 #pragma unroll
-        for (int e = 0; e < D * D; ++e) Fb[u][e] = ph[j * D * D + e];
+        for (int e = 0; e < D * D; ++e) Fb[u][e] = ph[so * D * D + e];
 #pragma unroll
-        for (int i = 0; i < D; ++i) Sb[u][i] = sp[j * kSStride + i];
-        const double* m = mom + ((int64_t)b * nch + j) * kMomStride;
+        for (int i = 0; i < D; ++i) Sb[u][i] = sp[so * kSStride + i];
+        const double* m = mob + so * kMomStride;
 #pragma unroll
         for (int e = 0; e < NM; ++e) Mb[u][e] = m[e];
-        Lb[u] = logs[(int64_t)b * nch + j];
+        Lb[u] = lgb[so];
       }
 #pragma unroll
     for (int u = 0; u < KB; ++u)
