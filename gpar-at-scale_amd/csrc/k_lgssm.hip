@@ -238,6 +238,8 @@ __device__ __forceinline__ int64_t run_slot(int p, int64_t j, int64_t nch) {
   return (int64_t)p * 256 * r + (j % r) * 256 + j / r;
 }
 
+constexpr int kP1B = 2;   // gains_phase1: steps per input block
+
 template <int D, int SUB>
 __global__ __launch_bounds__(256) void gains_phase1(const double* __restrict__ t, int64_t n,
                                                     int L, int64_t nch,
@@ -261,16 +263,36 @@ __global__ __launch_bounds__(256) void gains_phase1(const double* __restrict__ t
   Elem<D> acc, e;
   elem_identity(acc);   // identity (x) e == e exactly: one code path for every step
   double tprev = k0 > 0 ? t[k0 - 1] : 0.0;
-  StepPipe sp;
-  sp.init(t, noise, nullptr, k0, k1);
-  for (int64_t k = k0; k < k1; ++k) {
-    double tk, rk, yk;
-    sp.next(k, tk, rk, yk);
+  // the step inputs in two static register blocks of kP1B steps, one block fetched while the other
+  // is consumed (a rotating prefetch queue -- StepPipe -- moves pending loads between registers,
+  // and each move waits for its load)
+  constexpr int PB = kP1B;
+  double tb[2][PB], rb[2][PB];
+  auto fetch = [&](int buf, int64_t kb) __attribute__((always_inline)) {
+#pragma unroll
+    for (int u = 0; u < PB; ++u) {
+      const int64_t kk = kb + u < k1 ? kb + u : k1 - 1;
+      tb[buf][u] = t[kk];
+      rb[buf][u] = noise ? noise[kk] : 0.0;
+    }
+  };
+  auto step = [&](int64_t k, double tk, double rk) __attribute__((always_inline)) {
     const double tau = (k == 0) ? 1.0 : (tk - tprev) / cp.l;
     tprev = tk;
     const double R = noise ? (rk < 0.0 ? cp.r : rk) : cp.r;
     step_elem_tau<D>(tau, k == 0, cp, R, e);
     elem_combine<D>(acc, e, acc);
+  };
+  if (k0 < k1) fetch(0, k0);
+  for (int64_t kb = k0; kb < k1; kb += 2 * PB) {
+    fetch(1, kb + PB);
+#pragma unroll
+    for (int u = 0; u < PB; ++u)
+      if (kb + u < k1) step(kb + u, tb[0][u], rb[0][u]);
+    fetch(0, kb + 2 * PB);
+#pragma unroll
+    for (int u = 0; u < PB; ++u)
+      if (kb + PB + u < k1) step(kb + PB + u, tb[1][u], rb[1][u]);
   }
   if constexpr (SUB > 1) {
 #pragma unroll
