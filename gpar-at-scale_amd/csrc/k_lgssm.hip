@@ -2148,16 +2148,33 @@ __global__ __launch_bounds__(256) void smooth_back(const double* __restrict__ re
   } else {
     mat_zero(A1);
   }
-  for (int64_t k = k1 - 1; k >= k0; --k) {
+  // a step's inputs (its record, fix-up row, adjoint input and filtered covariance), fetched one
+  // step ahead into the other of two static register sets while the current step computes (in
+  // step order each step waited out its loads, at about two waves per SIMD)
+  struct In {
+    double A[D][D], K[D], rs, gk[D], x, P[D][D];
+  };
+  auto fetch = [&](In& in, int64_t k) __attribute__((always_inline)) {
     const double* r = rec + k * RS;
-    double A[D][D], K[D];
 #pragma unroll
     for (int i = 0; i < D; ++i) {
-      K[i] = r[D * D + i];
+      in.K[i] = r[D * D + i];
 #pragma unroll
-      for (int q = 0; q < D; ++q) A[i][q] = r[i * D + q];
+      for (int q = 0; q < D; ++q) in.A[i][q] = r[i * D + q];
     }
-    const double rs = r[D * D + D];
+    in.rs = r[D * D + D];
+#pragma unroll
+    for (int i = 0; i < D; ++i) in.gk[i] = g[k * kGStride + i];
+    in.x = X[k];
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) in.P[i][q] = pf[k * D * D + i * D + q];
+  };
+  auto step = [&](const In& in, int64_t k) __attribute__((always_inline)) {
+    const double(&A)[D][D] = in.A;
+    const double(&K)[D] = in.K;
+    const double rs = in.rs;
     // ---- gains_adjoint: h_k = Gamma^T K, Gamma <- Abar^T Gamma
 #pragma unroll
     for (int q = 0; q < D; ++q) {
@@ -2177,10 +2194,9 @@ __global__ __launch_bounds__(256) void smooth_back(const double* __restrict__ re
     }
     // ---- adjoint_local_col: u_k and lambda
     {
-      const double* gk = g + k * kGStride;
-      double w = X[k];
+      double w = in.x;
 #pragma unroll
-      for (int i = 0; i < D; ++i) w = fma(gk[i], cf[i], w);
+      for (int i = 0; i < D; ++i) w = fma(in.gk[i], cf[i], w);
       double u = w * rs;
 #pragma unroll
       for (int i = 0; i < D; ++i) u = fma(K[i], lam[i], u);
@@ -2199,11 +2215,7 @@ __global__ __launch_bounds__(256) void smooth_back(const double* __restrict__ re
     }
     // ---- cov_local: the local smoothed covariance and Gamma's first row
     {
-      double P[D][D];
-#pragma unroll
-      for (int i = 0; i < D; ++i)
-#pragma unroll
-        for (int q = 0; q < D; ++q) P[i][q] = pf[k * D * D + i * D + q];
+      const double(&P)[D][D] = in.P;
       double G[D][D], C[D][D];
       if (k == n - 1) {
         mat_zero(G);
@@ -2246,7 +2258,19 @@ __global__ __launch_bounds__(256) void smooth_back(const double* __restrict__ re
 #pragma unroll
       for (int q = 0; q < D; ++q) gam[k * kGStride + q] = Gm[0][q];
     }
-    mat_copy(A, A1);
+#pragma unroll
+    for (int i = 0; i < D; ++i)
+#pragma unroll
+      for (int q = 0; q < D; ++q) A1[i][q] = A[i][q];
+  };
+  In b0, b1;
+  if (k1 - 1 >= k0) fetch(b0, k1 - 1);
+  for (int64_t k = k1 - 1; k >= k0; k -= 2) {
+    if (k - 1 >= k0) fetch(b1, k - 1);
+    step(b0, k);
+    if (k - 1 < k0) break;
+    if (k - 2 >= k0) fetch(b0, k - 2);
+    step(b1, k - 1);
   }
 #pragma unroll
   for (int i = 0; i < D; ++i) bend[j * kSStride + i] = lam[i];
