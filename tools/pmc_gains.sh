@@ -8,7 +8,7 @@ CFG=${CFG:-north}
 EVALS=${EVALS:-2}
 OUT=gpurun_out/${TAG:-pmcg}
 mkdir -p $OUT
-KRE="gains_phase|chain_lml"
+KRE="gains_phase|chain_carry_lml"
 run() {  # name, counters...
   local name=$1; shift
   timeout -s KILL 240 rocprofv3 --pmc "$@" --kernel-include-regex "$KRE" -d $OUT/$name -o run --output-format csv -- python3 bench.py --config $CFG --steps 1 --warmup 0 --evals $EVALS --no-cpu-baseline --h2h-steps 0 > $OUT/$name.log 2>&1 || { echo "pass $name failed"; tail -5 $OUT/$name.log; exit 1; }
